@@ -1,0 +1,141 @@
+"""ctypes binding of the in-tree HIP library libgr_hip.so (C ABI declared in include/gr_hip.h).
+
+This is the Python side of the drop-in boundary: it replaces the reference's pybind11 module
+(src/bindings.cpp) and the pure-torch math of python/torch_renderer.py with calls into hand-written
+gfx950 kernels.  There is no fallback: if the library is missing or cannot be loaded, importing the
+renderer raises, so a GPU test can never pass on a silent CPU/eager path.
+
+torch is imported first on purpose: the wheel ships its own libamdhip64.so (SONAME libamdhip64.so.7),
+and loading it before libgr_hip.so makes our library bind to the same HIP runtime instance as torch,
+so torch device pointers and streams are valid inside our calls.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load; see module docstring)
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GR_HIP_LIB", os.path.join(_PKG_DIR, "libgr_hip.so"))
+
+TILE = 16
+
+GR_OK = 0
+GR_ERR_INVALID_ARGUMENT = 1
+GR_ERR_HIP = 2
+GR_ERR_WORKSPACE = 3
+GR_ERR_OVERFLOW = 4
+
+
+class GrView(ctypes.Structure):
+    """gr_view (include/gr_hip.h)."""
+
+    _fields_ = [
+        ("width", ctypes.c_int),
+        ("height", ctypes.c_int),
+        ("view", ctypes.c_float * 16),
+        ("proj", ctypes.c_float * 16),
+        ("background", ctypes.c_float * 3),
+        ("cam_pos", ctypes.c_float * 3),
+        ("cutoff", ctypes.c_float),
+    ]
+
+
+class GrRenderParams(ctypes.Structure):
+    """gr_render_params (include/gr_hip.h); same field order as gr::RenderParams
+    (include/gr/gaussian_types.h:24-46)."""
+
+    _fields_ = [
+        ("width", ctypes.c_int),
+        ("height", ctypes.c_int),
+        ("view", ctypes.c_float * 16),
+        ("proj", ctypes.c_float * 16),
+        ("background", ctypes.c_float * 3),
+        ("enable_depth_sort", ctypes.c_int),
+        ("depth_slices", ctypes.c_int),
+        ("force_cpu", ctypes.c_int),
+    ]
+
+
+class NativeLibraryError(ImportError):
+    pass
+
+
+_lib = None
+
+_P = ctypes.c_void_p
+_VP = ctypes.POINTER(GrView)
+_SIG = {
+    "gr_geom_bytes": (ctypes.c_size_t, [ctypes.c_int]),
+    "gr_fwd_prepare": (ctypes.c_int, [_VP, ctypes.c_int, _P, _P, _P, ctypes.c_int, _P, _P, ctypes.c_size_t,
+                                      ctypes.POINTER(ctypes.c_int64), _P]),
+    "gr_bins_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, ctypes.c_int64]),
+    "gr_saved_floats": (ctypes.c_size_t, [_VP]),
+    "gr_fwd_render": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int64, _P, _P, ctypes.c_size_t, _P, _P, _P, _P, _P]),
+    "gr_bwd_bytes": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int64]),
+    "gr_bwd": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int64, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P,
+                              _P, _P, _P, _P, _P, ctypes.c_size_t, _P]),
+    "gr_render_u8": (ctypes.c_int, [ctypes.POINTER(GrRenderParams), ctypes.c_int, _P, _P, _P, _P, _P]),
+    "gr_geom_layout": (None, [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
+    "gr_bins_layout": (None, [_VP, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_size_t)]),
+    "gr_last_error": (ctypes.c_char_p, []),
+    "gr_version": (ctypes.c_char_p, []),
+}
+
+
+def lib() -> ctypes.CDLL:
+    """Load libgr_hip.so (once).  Raises NativeLibraryError when it is absent: no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(
+            f"HIP extension {LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(or `make -C 3dgaussian_amd/csrc`) first")
+    try:
+        handle = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the box
+        raise NativeLibraryError(f"cannot load HIP extension {LIB_PATH}: {e}") from e
+    for name, (res, args) in _SIG.items():
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = handle
+    return _lib
+
+
+def check(status: int, what: str = "") -> None:
+    """Map a gr_status to the reference's exception types (bindings.cpp raises RuntimeError,
+    torch_renderer.py raises ValueError for argument errors)."""
+    if status == GR_OK:
+        return
+    msg = lib().gr_last_error().decode("utf-8", "replace")
+    if what:
+        msg = f"{what}: {msg}"
+    if status == GR_ERR_INVALID_ARGUMENT:
+        raise ValueError(msg)
+    raise RuntimeError(msg)
+
+
+def ptr(t) -> ctypes.c_void_p:
+    """Device/host pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return ctypes.c_void_p(0)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def version() -> str:
+    return lib().gr_version().decode()
+
+
+def geom_layout(n: int):
+    out = (ctypes.c_size_t * 6)()
+    lib().gr_geom_layout(int(n), out)
+    return list(out)
+
+
+def bins_layout(gv: GrView, n: int, num_pairs: int):
+    out = (ctypes.c_size_t * 3)()
+    lib().gr_bins_layout(ctypes.byref(gv), int(n), int(num_pairs), out)
+    return list(out)

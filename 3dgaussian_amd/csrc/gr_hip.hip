@@ -1,0 +1,993 @@
+// gr_hip.hip — MI355X (gfx950, CDNA4) differentiable Gaussian rasterizer: HIP kernels + C ABI.
+//
+// Replaces src/renderer.cu (4 CUDA kernels, forward only, uint8, static buffers) and the math of
+// python/torch_renderer.py:109-203 (+ its autograd backward) with a tile-binned forward/backward:
+//
+//   k_preprocess   per Gaussian: project (torch_renderer.py:57-78), colour (:81-106,:144),
+//                  sigma (:146-150), cutoff*sigma box -> 16x16 tile rectangle, pair count.
+//   hipcub scan    pair offsets (exclusive), K = total pairs.
+//   k_emit         (tile, gaussian) pairs in Gaussian-index order.
+//   hipcub sort    stable LSD radix sort by tile id -> per-tile lists in Gaussian-index order.
+//   k_ranges       per-tile [start, end) of the sorted list.
+//   k_raster_fwd   one workgroup per tile; Gaussian records staged through LDS in batches of 256;
+//                  one lane per pixel accumulates W, C, D (order-independent weighted average,
+//                  torch_renderer.py:184-203); writes out/alpha/depth + 5 floats of saved state.
+//   k_raster_bwd   one workgroup per tile; per-pixel upstream vector U = (dC, dW, dD) built in LDS
+//                  from the saved state, then one lane per Gaussian walks the tile's 256 pixels
+//                  (LDS broadcast reads) and writes 9 partial sums to the pair's slot.
+//   k_reduce_bwd   one lane per Gaussian sums its pair partials in a fixed order (deterministic,
+//                  no float atomics) and applies the chain rule back to means/scales/colours/opacity.
+//
+// The legacy uint8 surface (gr_render_u8, renderer_cpu.cpp semantics) reuses the binning with a
+// 3-sigma box, and adds exact depth-sorted front-to-back compositing (enable_depth_sort=1).
+//
+// Built with -ffp-contract=off: the preprocess float sequence must match oracle/gr_oracle.c
+// bit-for-bit (tile rectangles are integers derived from it); hot loops use explicit fmaf.
+
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/gr_hip.h"
+
+#define GR_VERSION_STR "gr_hip 0.1.0 (gfx950)"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+gr_status set_error(gr_status st, const std::string& msg) {
+  g_last_error = msg;
+  return st;
+}
+
+#define GR_HIP_TRY(expr)                                                                          \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess)                                                                         \
+      return set_error(GR_ERR_HIP, std::string("HIP error: ") + hipGetErrorString(e_) + " (" +   \
+                                       std::to_string((int)e_) + ") at " __FILE__ ":" +           \
+                                       std::to_string(__LINE__) + " in " #expr);                  \
+  } while (0)
+
+constexpr int T = GR_TILE;        // tile edge
+constexpr int TP = GR_TILE * GR_TILE;  // pixels per tile (256)
+constexpr float LOG2E = 1.4426950408889634f;
+
+inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+inline int tiles_x_of(int w) { return (w + T - 1) / T; }
+inline int tiles_y_of(int h) { return (h + T - 1) / T; }
+
+int bits_for(uint32_t maxval) {
+  int b = 1;
+  while (b < 32 && (1u << b) <= maxval) ++b;
+  return b;
+}
+
+// Kernel parameter block (by value): matrices etc.
+struct ViewK {
+  int W, H, tiles_x, tiles_y;
+  float V[16], P[16];
+  float bg[3];
+  float cam[3];
+  float cutoff;
+};
+
+ViewK make_viewk(const gr_view* v) {
+  ViewK k;
+  k.W = v->width;
+  k.H = v->height;
+  k.tiles_x = tiles_x_of(v->width);
+  k.tiles_y = tiles_y_of(v->height);
+  std::memcpy(k.V, v->view, sizeof(k.V));
+  std::memcpy(k.P, v->proj, sizeof(k.P));
+  std::memcpy(k.bg, v->background, sizeof(k.bg));
+  std::memcpy(k.cam, v->cam_pos, sizeof(k.cam));
+  k.cutoff = v->cutoff > 0.0f ? v->cutoff : 6.0f;
+  return k;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Projection (torch_renderer.py:57-78, 146-150).  Same float32 sequence as oracle/gr_oracle.c.
+// ------------------------------------------------------------------------------------------------
+struct Proj {
+  float pc[4], clip[4];
+  float ws, px, py, za, sxr, syr, sx, sy;
+  bool valid;
+};
+
+__device__ __forceinline__ void project(const ViewK& v, float x, float y, float z, float s0, float s1, Proj& o) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o.pc[i] = ((v.V[i * 4 + 0] * x + v.V[i * 4 + 1] * y) + v.V[i * 4 + 2] * z) + v.V[i * 4 + 3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    o.clip[i] = ((v.P[i * 4 + 0] * o.pc[0] + v.P[i * 4 + 1] * o.pc[1]) + v.P[i * 4 + 2] * o.pc[2]) + v.P[i * 4 + 3] * o.pc[3];
+  const float w = o.clip[3];
+  o.ws = (fabsf(w) < 1e-8f) ? 1.0f : w;
+  const float nx = o.clip[0] / o.ws, ny = o.clip[1] / o.ws, nz = o.clip[2] / o.ws;
+  o.px = (nx * 0.5f + 0.5f) * (float)(v.W - 1);
+  o.py = (1.0f - (ny * 0.5f + 0.5f)) * (float)(v.H - 1);
+  o.valid = (nz >= -1.0f) && (nz <= 1.0f) && (w != 0.0f);
+  const float az = fabsf(o.pc[2]);
+  o.za = az < 1e-6f ? 1e-6f : az;
+  const float fx = fabsf(v.P[0]), fy = fabsf(v.P[5]);
+  o.sxr = fabsf(s0) * 0.5f * (float)v.W * fx / o.za;
+  o.syr = fabsf(s1) * 0.5f * (float)v.H * fy / o.za;
+  o.sx = o.sxr < 1.0f ? 1.0f : o.sxr;
+  o.sy = o.syr < 1.0f ? 1.0f : o.syr;
+}
+
+// Colour before clamp (torch_renderer.py:86-106).
+template <int CD>
+__device__ __forceinline__ void eval_color(const ViewK& v, float mx, float my, float mz, const float* col, float out[3]) {
+  if constexpr (CD == 3) {
+    out[0] = col[0];
+    out[1] = col[1];
+    out[2] = col[2];
+  } else {
+    float d0 = v.cam[0] - mx, d1 = v.cam[1] - my, d2 = v.cam[2] - mz;
+    const float nrm = sqrtf(d0 * d0 + d1 * d1 + d2 * d2) + 1e-8f;
+    d0 /= nrm;
+    d1 /= nrm;
+    d2 /= nrm;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) out[k] = ((col[k] + col[3 + k] * d0) + col[6 + k] * d1) + col[9 + k] * d2;
+  }
+}
+
+__device__ __forceinline__ float clamp01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
+
+// Tile rectangle of the cutoff*sigma box (oracle/gr_oracle.c tile_rect, bit-exact).
+__device__ __forceinline__ int tile_rect(const ViewK& v, const Proj& p, float op, int4& r) {
+  r = make_int4(0, 0, -1, -1);
+  if (!p.valid || !(op >= 0.0f)) return 0;
+  const float R = v.cutoff;
+  const float rx = R * p.sx, ry = R * p.sy;
+  const float lox = p.px - rx, hix = p.px + rx, loy = p.py - ry, hiy = p.py + ry;
+  const float wm1 = (float)(v.W - 1), hm1 = (float)(v.H - 1);
+  if (!(hix >= 0.0f) || !(lox <= wm1) || !(hiy >= 0.0f) || !(loy <= hm1)) return 0;
+  const int x0 = (lox <= 0.0f) ? 0 : (int)floorf(lox);
+  const int x1 = (hix >= wm1) ? (v.W - 1) : (int)ceilf(hix);
+  const int y0 = (loy <= 0.0f) ? 0 : (int)floorf(loy);
+  const int y1 = (hiy >= hm1) ? (v.H - 1) : (int)ceilf(hiy);
+  r = make_int4(x0 / T, y0 / T, x1 / T, y1 / T);
+  return (r.z - r.x + 1) * (r.w - r.y + 1);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Geometry buffer layout.
+// ------------------------------------------------------------------------------------------------
+struct Geom {
+  float4* recA;  // px, py, qx, qy  (q = -0.5*log2(e)/sigma^2)
+  float4* recB;  // o, r, g, b (clamped)
+  float* recZ;   // z_abs
+  int4* rect;    // tile rectangle
+  int* counts;   // n+1
+  int* offsets;  // n+1 (exclusive scan)
+  void* scan_tmp;
+  size_t scan_tmp_bytes;
+};
+
+size_t geom_fixed(int n, size_t off[6]) {
+  size_t o = 0;
+  const size_t nn = (size_t)(n > 0 ? n : 1);
+  off[0] = o; o = align_up(o + nn * sizeof(float4));
+  off[1] = o; o = align_up(o + nn * sizeof(float4));
+  off[2] = o; o = align_up(o + nn * sizeof(float));
+  off[3] = o; o = align_up(o + nn * sizeof(int4));
+  off[4] = o; o = align_up(o + (nn + 1) * sizeof(int));
+  off[5] = o; o = align_up(o + (nn + 1) * sizeof(int));
+  return o;
+}
+
+size_t scan_tmp_bytes(int n) {
+  size_t tmp = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (int*)nullptr, (int*)nullptr, n + 1, (hipStream_t)0);
+  return tmp;
+}
+
+Geom geom_view(void* base, int n) {
+  size_t off[6];
+  const size_t fixed = geom_fixed(n, off);
+  char* b = (char*)base;
+  Geom g;
+  g.recA = (float4*)(b + off[0]);
+  g.recB = (float4*)(b + off[1]);
+  g.recZ = (float*)(b + off[2]);
+  g.rect = (int4*)(b + off[3]);
+  g.counts = (int*)(b + off[4]);
+  g.offsets = (int*)(b + off[5]);
+  g.scan_tmp = b + fixed;
+  g.scan_tmp_bytes = 0;
+  return g;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Bins buffer layout.
+// ------------------------------------------------------------------------------------------------
+struct Bins {
+  uint32_t* keys;      // sorted keys (K)
+  int* ids;            // sorted gaussian ids (K)
+  int2* ranges;        // tiles
+  uint32_t* keys_in;   // K
+  int* ids_in;         // K
+  void* sort_tmp;
+};
+
+size_t bins_fixed(int tiles, int64_t K, size_t off[5]) {
+  const size_t kk = (size_t)(K > 0 ? K : 1);
+  size_t o = 0;
+  off[0] = o; o = align_up(o + kk * sizeof(uint32_t));
+  off[1] = o; o = align_up(o + kk * sizeof(int));
+  off[2] = o; o = align_up(o + (size_t)tiles * sizeof(int2));
+  off[3] = o; o = align_up(o + kk * sizeof(uint32_t));
+  off[4] = o; o = align_up(o + kk * sizeof(int));
+  return o;
+}
+
+template <typename KeyT>
+size_t sort_tmp_bytes(int64_t K, int bits) {
+  size_t tmp = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (KeyT*)nullptr, (KeyT*)nullptr, (int*)nullptr, (int*)nullptr,
+                                     (int)(K > 0 ? K : 1), 0, bits, (hipStream_t)0);
+  return tmp;
+}
+
+Bins bins_view(void* base, int tiles, int64_t K) {
+  size_t off[5];
+  const size_t fixed = bins_fixed(tiles, K, off);
+  char* b = (char*)base;
+  Bins r;
+  r.keys = (uint32_t*)(b + off[0]);
+  r.ids = (int*)(b + off[1]);
+  r.ranges = (int2*)(b + off[2]);
+  r.keys_in = (uint32_t*)(b + off[3]);
+  r.ids_in = (int*)(b + off[4]);
+  r.sort_tmp = b + fixed;
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Kernels: binning.
+// ------------------------------------------------------------------------------------------------
+template <int CD>
+__global__ __launch_bounds__(256) void k_preprocess(ViewK v, int n, const float* __restrict__ means,
+                                                    const float* __restrict__ scales, const float* __restrict__ colors,
+                                                    const float* __restrict__ opac, Geom g) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == n) g.counts[n] = 0;
+  if (i >= n) return;
+  const float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
+  Proj p;
+  project(v, mx, my, mz, scales[3 * i], scales[3 * i + 1], p);
+  float c[3];
+  eval_color<CD>(v, mx, my, mz, colors + (size_t)CD * i, c);
+  const float op = opac[i];
+  int4 r;
+  const int cnt = tile_rect(v, p, op, r);
+  const float qx = (-0.5f * LOG2E) / (p.sx * p.sx);
+  const float qy = (-0.5f * LOG2E) / (p.sy * p.sy);
+  g.recA[i] = make_float4(p.px, p.py, qx, qy);
+  g.recB[i] = make_float4(op < 0.0f ? 0.0f : op, clamp01(c[0]), clamp01(c[1]), clamp01(c[2]));
+  g.recZ[i] = p.za;
+  g.rect[i] = r;
+  g.counts[i] = cnt;
+}
+
+template <typename KeyT>
+__global__ __launch_bounds__(256) void k_emit(int n, int tiles_x, const int4* __restrict__ rect,
+                                              const int* __restrict__ counts, const int* __restrict__ offsets,
+                                              const KeyT* __restrict__ low_keys, KeyT* keys, int* ids) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || counts[i] == 0) return;
+  const int4 r = rect[i];
+  int k = offsets[i];
+  const KeyT low = low_keys ? low_keys[i] : (KeyT)0;
+  for (int ty = r.y; ty <= r.w; ++ty)
+    for (int tx = r.x; tx <= r.z; ++tx) {
+      const KeyT t = (KeyT)(ty * tiles_x + tx);
+      if constexpr (sizeof(KeyT) == 8)
+        keys[k] = (t << 32) | low;
+      else
+        keys[k] = t;
+      ids[k] = i;
+      ++k;
+    }
+}
+
+template <typename KeyT>
+__global__ __launch_bounds__(256) void k_ranges(int64_t K, const KeyT* __restrict__ keys, int2* ranges) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  const int shift = sizeof(KeyT) == 8 ? 32 : 0;
+  const int t = (int)(keys[k] >> shift);
+  if (k == 0 || (int)(keys[k - 1] >> shift) != t) ranges[t].x = (int)k;
+  if (k == K - 1 || (int)(keys[k + 1] >> shift) != t) ranges[t].y = (int)(k + 1);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Forward splat.  One 256-lane workgroup per 16x16 tile, one lane per pixel.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_raster_fwd(ViewK v, const int2* __restrict__ ranges, const int* __restrict__ ids,
+                                                    const float4* __restrict__ recA, const float4* __restrict__ recB,
+                                                    const float* __restrict__ recZ, float* __restrict__ out_rgb,
+                                                    float* __restrict__ out_alpha, float* __restrict__ out_depth,
+                                                    float4* __restrict__ saved4, float* __restrict__ savedD) {
+  __shared__ float4 sA[TP];
+  __shared__ float4 sB[TP];
+  __shared__ float sZ[TP];
+  const int tile = blockIdx.x;
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  const int tid = threadIdx.x;
+  const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
+  const float xc = (float)x + 0.5f, yc = (float)y + 0.5f;
+  const int2 rg = ranges[tile];
+  float aW = 0.f, aR = 0.f, aG = 0.f, aB = 0.f, aD = 0.f;
+  for (int base = rg.x; base < rg.y; base += TP) {
+    const int cnt = min(TP, rg.y - base);
+    __syncthreads();
+    if (tid < cnt) {
+      const int g = ids[base + tid];
+      sA[tid] = recA[g];
+      sB[tid] = recB[g];
+      sZ[tid] = recZ[g];
+    }
+    __syncthreads();
+    for (int j = 0; j < cnt; ++j) {
+      const float4 a = sA[j];
+      const float4 b = sB[j];
+      const float z = sZ[j];
+      const float dx = xc - a.x, dy = yc - a.y;
+      const float e = fmaf(dx * a.z, dx, dy * a.w * dy);
+      const float E = __builtin_amdgcn_exp2f(e);
+      const float w = b.x * E;
+      aW += w;
+      aR = fmaf(w, b.y, aR);
+      aG = fmaf(w, b.z, aG);
+      aB = fmaf(w, b.w, aB);
+      aD = fmaf(w, z, aD);
+    }
+  }
+  if (x >= v.W || y >= v.H) return;
+  const int p = y * v.W + x;
+  const float den = 1.0f + aW;
+  out_rgb[3 * p + 0] = clamp01((v.bg[0] + aR) / den);
+  out_rgb[3 * p + 1] = clamp01((v.bg[1] + aG) / den);
+  out_rgb[3 * p + 2] = clamp01((v.bg[2] + aB) / den);
+  if (out_alpha) out_alpha[p] = clamp01(aW / den);
+  if (out_depth) {
+    const float d = aD / (aW + 1e-6f);
+    out_depth[p] = d < 0.0f ? 0.0f : d;
+  }
+  saved4[p] = make_float4(aW, aR, aG, aB);
+  savedD[p] = aD;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Backward splat.  Prologue: per-pixel U = (dC_r, dC_g, dC_b, dW) and dD into LDS.
+// Main: one lane per (Gaussian, this tile) pair, walking the 256 pixels with broadcast LDS reads.
+// Partials per pair (9 floats, slot = Gaussian's offset + tile index inside its rectangle):
+//   [0..2] sum w*dC_k   [3] sum w*dD   [4] sum gw*E   [5] sum gw*E*dx  [6] sum gw*E*dy
+//   [7] sum gw*E*dx^2   [8] sum gw*E*dy^2            (gw = dW + dC.c + dD*za; ge = o*gw*E)
+// ------------------------------------------------------------------------------------------------
+constexpr int NPART = 9;
+
+__global__ __launch_bounds__(256) void k_raster_bwd(ViewK v, const int2* __restrict__ ranges, const int* __restrict__ ids,
+                                                    const float4* __restrict__ recA, const float4* __restrict__ recB,
+                                                    const float* __restrict__ recZ, const int4* __restrict__ rect,
+                                                    const int* __restrict__ offsets, const float4* __restrict__ saved4,
+                                                    const float* __restrict__ savedD, const float* __restrict__ g_rgb,
+                                                    const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
+                                                    float* __restrict__ partials) {
+  __shared__ float4 sU[TP];
+  __shared__ float sUd[TP];
+  const int tile = blockIdx.x;
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  const int tid = threadIdx.x;
+  const int2 rg = ranges[tile];
+  if (rg.y <= rg.x) return;  // uniform per block
+  {
+    const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
+    float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+    float ud = 0.f;
+    if (x < v.W && y < v.H) {
+      const int p = y * v.W + x;
+      const float4 s = saved4[p];
+      const float Dp = savedD[p];
+      const float den = 1.0f + s.x, dden = s.x + 1e-6f;
+      float gW = 0.f;
+      float gc[3];
+      const float C[3] = {s.y, s.z, s.w};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float r = (v.bg[k] + C[k]) / den;
+        const float go = (r >= 0.0f && r <= 1.0f) ? g_rgb[3 * p + k] : 0.0f;
+        gc[k] = go / den;
+        gW -= go * r / den;
+      }
+      if (g_alpha) {
+        const float al = s.x / den;
+        if (al >= 0.0f && al <= 1.0f) gW += g_alpha[p] / (den * den);
+      }
+      if (g_depth) {
+        const float d = Dp / dden;
+        if (d >= 0.0f) {
+          const float gd = g_depth[p];
+          gW -= gd * Dp / (dden * dden);
+          ud = gd / dden;
+        }
+      }
+      u = make_float4(gc[0], gc[1], gc[2], gW);
+    }
+    sU[tid] = u;
+    sUd[tid] = ud;
+  }
+  __syncthreads();
+  const float x0 = (float)(tx * T) + 0.5f, y0 = (float)(ty * T) + 0.5f;
+  for (int k = rg.x + tid; k < rg.y; k += TP) {
+    const int g = ids[k];
+    const float4 a = recA[g];
+    const float4 b = recB[g];
+    const float z = recZ[g];
+    float Sc0 = 0.f, Sc1 = 0.f, Sc2 = 0.f, Sz = 0.f, So = 0.f, Sdx = 0.f, Sdy = 0.f, Sdx2 = 0.f, Sdy2 = 0.f;
+    for (int py = 0; py < T; ++py) {
+      const float dy = (y0 + (float)py) - a.y;
+      const float ey = dy * a.w * dy;
+      float rowT = 0.f;
+#pragma unroll
+      for (int px = 0; px < T; ++px) {
+        const float dx = (x0 + (float)px) - a.x;
+        const float E = __builtin_amdgcn_exp2f(fmaf(dx * a.z, dx, ey));
+        const float4 u = sU[py * T + px];
+        const float ud = sUd[py * T + px];
+        const float w = b.x * E;
+        const float gw = fmaf(ud, z, fmaf(u.z, b.w, fmaf(u.y, b.z, fmaf(u.x, b.y, u.w))));
+        Sc0 = fmaf(w, u.x, Sc0);
+        Sc1 = fmaf(w, u.y, Sc1);
+        Sc2 = fmaf(w, u.z, Sc2);
+        Sz = fmaf(w, ud, Sz);
+        const float Tv = gw * E;
+        rowT += Tv;
+        const float Tx = Tv * dx;
+        Sdx += Tx;
+        Sdx2 = fmaf(Tx, dx, Sdx2);
+      }
+      So += rowT;
+      const float Ty = rowT * dy;
+      Sdy += Ty;
+      Sdy2 = fmaf(Ty, dy, Sdy2);
+    }
+    const int4 r = rect[g];
+    const int slot = offsets[g] + (ty - r.y) * (r.z - r.x + 1) + (tx - r.x);
+    float* dst = partials + (size_t)slot * NPART;
+    dst[0] = Sc0;
+    dst[1] = Sc1;
+    dst[2] = Sc2;
+    dst[3] = Sz;
+    dst[4] = So;
+    dst[5] = Sdx;
+    dst[6] = Sdy;
+    dst[7] = Sdx2;
+    dst[8] = Sdy2;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Per-Gaussian reduction of pair partials + chain rule.  Deterministic.
+// ------------------------------------------------------------------------------------------------
+template <int CD>
+__global__ __launch_bounds__(256) void k_reduce_bwd(ViewK v, int n, const float* __restrict__ means,
+                                                    const float* __restrict__ scales, const float* __restrict__ colors,
+                                                    const float* __restrict__ opac, const int* __restrict__ counts,
+                                                    const int* __restrict__ offsets, const float* __restrict__ partials,
+                                                    float* __restrict__ d_means, float* __restrict__ d_scales,
+                                                    float* __restrict__ d_colors, float* __restrict__ d_opac) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double S[NPART];
+#pragma unroll
+  for (int q = 0; q < NPART; ++q) S[q] = 0.0;
+  const int cnt = counts[i];
+  const float* src = partials + (size_t)offsets[i] * NPART;
+  for (int j = 0; j < cnt; ++j) {
+#pragma unroll
+    for (int q = 0; q < NPART; ++q) S[q] += (double)src[j * NPART + q];
+  }
+  const float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
+  const float s0 = scales[3 * i], s1 = scales[3 * i + 1];
+  const float op = opac[i];
+  const float* col = colors + (size_t)CD * i;
+  float* dc = d_colors + (size_t)CD * i;
+  if (cnt == 0) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      d_means[3 * i + q] = 0.f;
+      d_scales[3 * i + q] = 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < CD; ++q) dc[q] = 0.f;
+    d_opac[i] = 0.f;
+    return;
+  }
+  Proj p;
+  project(v, mx, my, mz, s0, s1, p);
+  const double o = op < 0.0f ? 0.0 : (double)op;
+  const double sx = p.sx, sy = p.sy;
+  // ge = o * gw * E  ->  sums over ge carry a factor o.
+  const double dpx = o * S[5] / (sx * sx), dpy = o * S[6] / (sy * sy);
+  double dsx = o * S[7] / (sx * sx * sx), dsy = o * S[8] / (sy * sy * sy);
+  if (!(p.sxr >= 1.0f)) dsx = 0.0;
+  if (!(p.syr >= 1.0f)) dsy = 0.0;
+  const double fx = fabs((double)v.P[0]), fy = fabs((double)v.P[5]);
+  const double kx = 0.5 * v.W * fx / p.za, ky = 0.5 * v.H * fy / p.za;
+  const double sgx = s0 > 0.f ? 1.0 : (s0 < 0.f ? -1.0 : 0.0);
+  const double sgy = s1 > 0.f ? 1.0 : (s1 < 0.f ? -1.0 : 0.0);
+  d_scales[3 * i + 0] = (float)(dsx * kx * sgx);
+  d_scales[3 * i + 1] = (float)(dsy * ky * sgy);
+  d_scales[3 * i + 2] = 0.f;
+  const double dza = S[3] - dsx * p.sxr / p.za - dsy * p.syr / p.za;
+  double dpc[4] = {0.0, 0.0, 0.0, 0.0};
+  if (fabsf(p.pc[2]) >= 1e-6f) dpc[2] += dza * (p.pc[2] > 0.f ? 1.0 : (p.pc[2] < 0.f ? -1.0 : 0.0));
+  const double dndx = dpx * 0.5 * (v.W - 1);
+  const double dndy = -dpy * 0.5 * (v.H - 1);
+  double dclip[4];
+  dclip[0] = dndx / p.ws;
+  dclip[1] = dndy / p.ws;
+  dclip[2] = 0.0;
+  dclip[3] = (fabsf(p.clip[3]) < 1e-8f) ? 0.0 : -(dndx * p.clip[0] + dndy * p.clip[1]) / ((double)p.ws * p.ws);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dpc[j] += (double)v.P[r * 4 + j] * dclip[r];
+  double dm[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    dm[j] = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dm[j] += (double)v.V[r * 4 + j] * dpc[r];
+  }
+  d_opac[i] = (float)((op >= 0.0f) ? S[4] : 0.0);
+  float cpre[3];
+  eval_color<CD>(v, mx, my, mz, col, cpre);
+  double dcol[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) dcol[k] = (cpre[k] >= 0.0f && cpre[k] <= 1.0f) ? S[k] : 0.0;
+  if constexpr (CD == 3) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) dc[k] = (float)dcol[k];
+  } else {
+    const double vv[3] = {(double)v.cam[0] - mx, (double)v.cam[1] - my, (double)v.cam[2] - mz};
+    const double nn = sqrt(vv[0] * vv[0] + vv[1] * vv[1] + vv[2] * vv[2]);
+    const double ne = nn + 1e-8;
+    const double d[3] = {vv[0] / ne, vv[1] / ne, vv[2] / ne};
+    double gd[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      dc[k] = (float)dcol[k];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        dc[(1 + j) * 3 + k] = (float)(dcol[k] * d[j]);
+        gd[j] += dcol[k] * (double)col[(1 + j) * 3 + k];
+      }
+    }
+    if (nn > 0.0) {
+      const double vg = vv[0] * gd[0] + vv[1] * gd[1] + vv[2] * gd[2];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) dm[j] -= gd[j] / ne - vv[j] * vg / (nn * ne * ne);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) d_means[3 * i + j] = (float)dm[j];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Legacy uint8 surface (renderer_cpu.cpp:34-260 semantics).
+// ------------------------------------------------------------------------------------------------
+struct LegacyRec {
+  float4* a;   // px, py, 1/sx^2, 1/sy^2
+  float4* c;   // r, g, b, opacity (unclamped, as the reference)
+  int4* box;   // xmin, xmax, ymin, ymax (3-sigma, inclusive)
+  int4* rect;  // tile rectangle
+  int* counts;
+  int* offsets;
+  uint32_t* depth_key;  // descending camera z -> ascending key
+};
+
+__global__ __launch_bounds__(256) void k_preprocess_u8(ViewK v, int n, const float* __restrict__ means,
+                                                       const float* __restrict__ scales, const float* __restrict__ colors,
+                                                       const float* __restrict__ opac, LegacyRec g) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == n) g.counts[n] = 0;
+  if (i >= n) return;
+  const float x = means[3 * i], y = means[3 * i + 1], z = means[3 * i + 2];
+  float pc[4], cl[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) pc[r] = v.V[r * 4 + 0] * x + v.V[r * 4 + 1] * y + v.V[r * 4 + 2] * z + v.V[r * 4 + 3] * 1.0f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) cl[r] = v.P[r * 4 + 0] * pc[0] + v.P[r * 4 + 1] * pc[1] + v.P[r * 4 + 2] * pc[2] + v.P[r * 4 + 3] * pc[3];
+  // depth key: larger camera z first (renderer_cpu.cpp:144-146); -0 folded onto +0.
+  uint32_t zb = __float_as_uint(pc[2] + 0.0f);
+  zb = (zb & 0x80000000u) ? ~zb : (zb | 0x80000000u);
+  g.depth_key[i] = ~zb;
+  g.counts[i] = 0;
+  g.rect[i] = make_int4(0, 0, -1, -1);
+  const float z_abs = fabsf(pc[2]) + 1e-6f;
+  if (cl[3] == 0.0f) return;
+  const float inv_w = 1.0f / cl[3];
+  const float nx = cl[0] * inv_w, ny = cl[1] * inv_w, nz = cl[2] * inv_w;
+  if (nz < -1.0f || nz > 1.0f) return;
+  const float px = (nx * 0.5f + 0.5f) * (float)(v.W - 1);
+  const float py = (1.0f - (ny * 0.5f + 0.5f)) * (float)(v.H - 1);
+  float sx = scales[3 * i] * 0.5f * (float)v.W * fabsf(v.P[0]) / z_abs;
+  float sy = scales[3 * i + 1] * 0.5f * (float)v.H * fabsf(v.P[5]) / z_abs;
+  sx = sx > 1.0f ? sx : 1.0f;
+  sy = sy > 1.0f ? sy : 1.0f;
+  const float rx = 3.0f * sx, ry = 3.0f * sy;
+  if (!(px + rx >= 0.0f) || !(px - rx <= (float)(v.W - 1)) || !(py + ry >= 0.0f) || !(py - ry <= (float)(v.H - 1))) return;
+  const int xmin = (px - rx <= 0.0f) ? 0 : (int)floorf(px - rx);
+  const int xmax = (px + rx >= (float)(v.W - 1)) ? v.W - 1 : (int)ceilf(px + rx);
+  const int ymin = (py - ry <= 0.0f) ? 0 : (int)floorf(py - ry);
+  const int ymax = (py + ry >= (float)(v.H - 1)) ? v.H - 1 : (int)ceilf(py + ry);
+  g.a[i] = make_float4(px, py, 1.0f / (sx * sx), 1.0f / (sy * sy));
+  g.c[i] = make_float4(colors[3 * i], colors[3 * i + 1], colors[3 * i + 2], opac[i]);
+  g.box[i] = make_int4(xmin, xmax, ymin, ymax);
+  const int4 r = make_int4(xmin / T, ymin / T, xmax / T, ymax / T);
+  g.rect[i] = r;
+  g.counts[i] = (r.z - r.x + 1) * (r.w - r.y + 1);
+}
+
+template <bool SORTED>
+__global__ __launch_bounds__(256) void k_raster_u8(ViewK v, const int2* __restrict__ ranges, const int* __restrict__ ids,
+                                                   const float4* __restrict__ ga, const float4* __restrict__ gc,
+                                                   const int4* __restrict__ gbox, uint8_t* __restrict__ rgba) {
+  __shared__ float4 sA[TP];
+  __shared__ float4 sC[TP];
+  __shared__ int4 sBox[TP];
+  const int tile = blockIdx.x;
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  const int tid = threadIdx.x;
+  const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
+  const float xc = (float)x + 0.5f, yc = (float)y + 0.5f;
+  const int2 rg = ranges[tile];
+  float r = 0.f, g = 0.f, b = 0.f, a = 0.f;
+  bool done = !(x < v.W && y < v.H);
+  for (int base = rg.x; base < rg.y; base += TP) {
+    if (SORTED) {
+      if (__syncthreads_and(done)) break;  // front-to-back: every pixel of the tile saturated
+    } else {
+      __syncthreads();
+    }
+    const int cnt = min(TP, rg.y - base);
+    if (tid < cnt) {
+      const int id = ids[base + tid];
+      sA[tid] = ga[id];
+      sC[tid] = gc[id];
+      sBox[tid] = gbox[id];
+    }
+    __syncthreads();
+    for (int j = 0; j < cnt; ++j) {
+      const int4 bx = sBox[j];
+      if (x < bx.x || x > bx.y || y < bx.z || y > bx.w) continue;
+      const float4 ga_ = sA[j];
+      const float4 gc_ = sC[j];
+      const float dx = xc - ga_.x, dy = yc - ga_.y;
+      const float e = -0.5f * (dx * dx * ga_.z + dy * dy * ga_.w);
+      float w = gc_.w * expf(e);
+      if (w < 1e-5f) continue;
+      if (!SORTED) {
+        r += w * gc_.x;
+        g += w * gc_.y;
+        b += w * gc_.z;
+        a += w;
+      } else {
+        w = clamp01(w);
+        const float contrib = (1.0f - a) * w;
+        if (contrib <= 0.0f) continue;
+        r += contrib * gc_.x;
+        g += contrib * gc_.y;
+        b += contrib * gc_.z;
+        a += contrib;
+        if (a >= 1.0f) done = true;
+      }
+    }
+  }
+  if (!(x < v.W && y < v.H)) return;
+  float rr, gg, bb;
+  if (!SORTED) {
+    const float den = 1.0f + a;
+    rr = (v.bg[0] + r) / den;
+    gg = (v.bg[1] + g) / den;
+    bb = (v.bg[2] + b) / den;
+  } else {
+    const float al = clamp01(a);
+    rr = r + (1.0f - al) * v.bg[0];
+    gg = g + (1.0f - al) * v.bg[1];
+    bb = b + (1.0f - al) * v.bg[2];
+  }
+  const int p = y * v.W + x;
+  uchar4 o;
+  o.x = (uint8_t)(clamp01(rr) * 255.0f + 0.5f);
+  o.y = (uint8_t)(clamp01(gg) * 255.0f + 0.5f);
+  o.z = (uint8_t)(clamp01(bb) * 255.0f + 0.5f);
+  o.w = 255;
+  reinterpret_cast<uchar4*>(rgba)[p] = o;
+}
+
+// Sorted mode: OR each pair's Gaussian depth key into the low 32 bits of its 64-bit key.
+__global__ __launch_bounds__(256) void k_patch_depth(int64_t K, uint64_t* keys, const int* __restrict__ ids,
+                                                     const uint32_t* __restrict__ dk) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < K) keys[k] |= (uint64_t)dk[ids[k]];
+}
+
+inline int blocks_for(int64_t n, int bs = 256) { return (int)((n + bs - 1) / bs); }
+
+gr_status check_view(const gr_view* v) {
+  if (!v) return set_error(GR_ERR_INVALID_ARGUMENT, "view is null");
+  if (v->width <= 0 || v->height <= 0) return set_error(GR_ERR_INVALID_ARGUMENT, "width/height must be positive");
+  if ((int64_t)v->width * v->height > (1ll << 30)) return set_error(GR_ERR_INVALID_ARGUMENT, "image too large");
+  return GR_OK;
+}
+
+}  // namespace
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" {
+
+const char* gr_last_error(void) { return g_last_error.c_str(); }
+const char* gr_version(void) { return GR_VERSION_STR; }
+
+void gr_geom_layout(int n, size_t offsets_out[6]) { geom_fixed(n, offsets_out); }
+
+void gr_bins_layout(const gr_view* v, int n, int64_t num_pairs, size_t offsets_out[3]) {
+  (void)n;
+  size_t off[5];
+  bins_fixed(tiles_x_of(v->width) * tiles_y_of(v->height), num_pairs, off);
+  offsets_out[0] = off[0];
+  offsets_out[1] = off[1];
+  offsets_out[2] = off[2];
+}
+
+size_t gr_geom_bytes(int n) {
+  size_t off[6];
+  return geom_fixed(n, off) + align_up(scan_tmp_bytes(n > 0 ? n : 1));
+}
+
+size_t gr_saved_floats(const gr_view* v) { return (size_t)5 * v->width * v->height; }
+
+size_t gr_bins_bytes(const gr_view* v, int n, int64_t num_pairs) {
+  (void)n;
+  const int tiles = tiles_x_of(v->width) * tiles_y_of(v->height);
+  size_t off[5];
+  return bins_fixed(tiles, num_pairs, off) + align_up(sort_tmp_bytes<uint32_t>(num_pairs, bits_for((uint32_t)tiles)));
+}
+
+size_t gr_bwd_bytes(int n, int64_t num_pairs) {
+  (void)n;
+  return align_up((size_t)(num_pairs > 0 ? num_pairs : 1) * NPART * sizeof(float));
+}
+
+gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const float* scales, const float* colors,
+                         int color_dim, const float* opacities, void* geom, size_t geom_bytes, int64_t* num_pairs,
+                         void* stream) {
+  gr_status st = check_view(v);
+  if (st != GR_OK) return st;
+  if (n < 0) return set_error(GR_ERR_INVALID_ARGUMENT, "n must be >= 0");
+  if (color_dim != 3 && color_dim != 12) return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3)");
+  if (!num_pairs) return set_error(GR_ERR_INVALID_ARGUMENT, "num_pairs is null");
+  *num_pairs = 0;
+  if (n == 0) return GR_OK;
+  if (!means || !scales || !colors || !opacities || !geom) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+  if (geom_bytes < gr_geom_bytes(n)) return set_error(GR_ERR_WORKSPACE, "geom workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const ViewK vk = make_viewk(v);
+  Geom g = geom_view(geom, n);
+  if (color_dim == 3)
+    hipLaunchKernelGGL(k_preprocess<3>, dim3(blocks_for(n + 1)), dim3(256), 0, s, vk, n, means, scales, colors, opacities, g);
+  else
+    hipLaunchKernelGGL(k_preprocess<12>, dim3(blocks_for(n + 1)), dim3(256), 0, s, vk, n, means, scales, colors, opacities, g);
+  GR_HIP_TRY(hipGetLastError());
+  size_t tmp = scan_tmp_bytes(n);
+  GR_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(g.scan_tmp, tmp, g.counts, g.offsets, n + 1, s));
+  int total = 0;
+  GR_HIP_TRY(hipMemcpyAsync(&total, g.offsets + n, sizeof(int), hipMemcpyDeviceToHost, s));
+  GR_HIP_TRY(hipStreamSynchronize(s));
+  if (total < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
+  *num_pairs = total;
+  return GR_OK;
+}
+
+gr_status gr_fwd_render(const gr_view* v, int n, int64_t num_pairs, const void* geom, void* bins, size_t bins_bytes,
+                        float* out_rgb, float* out_alpha, float* out_depth, float* saved, void* stream) {
+  gr_status st = check_view(v);
+  if (st != GR_OK) return st;
+  if (!out_rgb || !saved) return set_error(GR_ERR_INVALID_ARGUMENT, "out_rgb and saved are required");
+  if (n > 0 && (!geom || !bins)) return set_error(GR_ERR_INVALID_ARGUMENT, "null workspace");
+  if (bins_bytes < gr_bins_bytes(v, n, num_pairs)) return set_error(GR_ERR_WORKSPACE, "bins workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const ViewK vk = make_viewk(v);
+  const int tiles = vk.tiles_x * vk.tiles_y;
+  Bins b = bins_view(bins, tiles, num_pairs);
+  GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * tiles, s));
+  if (n > 0 && num_pairs > 0) {
+    Geom g = geom_view((void*)geom, n);
+    hipLaunchKernelGGL(k_emit<uint32_t>, dim3(blocks_for(n)), dim3(256), 0, s, n, vk.tiles_x, g.rect, g.counts, g.offsets,
+                       (const uint32_t*)nullptr, b.keys_in, b.ids_in);
+    GR_HIP_TRY(hipGetLastError());
+    const int bits = bits_for((uint32_t)tiles);
+    size_t tmp = sort_tmp_bytes<uint32_t>(num_pairs, bits);
+    GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, tmp, b.keys_in, b.keys, b.ids_in, b.ids, (int)num_pairs, 0,
+                                                  bits, s));
+    hipLaunchKernelGGL(k_ranges<uint32_t>, dim3(blocks_for(num_pairs)), dim3(256), 0, s, num_pairs, b.keys, b.ranges);
+    GR_HIP_TRY(hipGetLastError());
+  }
+  Geom g = geom_view((void*)geom, n > 0 ? n : 1);
+  const size_t HW = (size_t)v->width * v->height;
+  hipLaunchKernelGGL(k_raster_fwd, dim3(tiles), dim3(256), 0, s, vk, b.ranges, b.ids, g.recA, g.recB, g.recZ, out_rgb,
+                     out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
+  GR_HIP_TRY(hipGetLastError());
+  return GR_OK;
+}
+
+gr_status gr_bwd(const gr_view* v, int n, int64_t num_pairs, const float* means, const float* scales, const float* colors,
+                 int color_dim, const float* opacities, const void* geom, const void* bins, const float* saved,
+                 const float* g_rgb, const float* g_alpha, const float* g_depth, float* d_means, float* d_scales,
+                 float* d_colors, float* d_opacities, void* ws, size_t ws_bytes, void* stream) {
+  gr_status st = check_view(v);
+  if (st != GR_OK) return st;
+  if (color_dim != 3 && color_dim != 12) return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3)");
+  if (n == 0) return GR_OK;
+  if (!g_rgb || !saved || !geom || !bins || !d_means || !d_scales || !d_colors || !d_opacities)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+  if (num_pairs > 0 && (!ws || ws_bytes < gr_bwd_bytes(n, num_pairs)))
+    return set_error(GR_ERR_WORKSPACE, "backward workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const ViewK vk = make_viewk(v);
+  const int tiles = vk.tiles_x * vk.tiles_y;
+  Geom g = geom_view((void*)geom, n);
+  Bins b = bins_view((void*)bins, tiles, num_pairs);
+  const size_t HW = (size_t)v->width * v->height;
+  float* partials = (float*)ws;
+  if (num_pairs > 0) {
+    hipLaunchKernelGGL(k_raster_bwd, dim3(tiles), dim3(256), 0, s, vk, b.ranges, b.ids, g.recA, g.recB, g.recZ, g.rect,
+                       g.offsets, (const float4*)saved, saved + 4 * HW, g_rgb, g_alpha, g_depth, partials);
+    GR_HIP_TRY(hipGetLastError());
+  }
+  if (color_dim == 3)
+    hipLaunchKernelGGL(k_reduce_bwd<3>, dim3(blocks_for(n)), dim3(256), 0, s, vk, n, means, scales, colors, opacities,
+                       g.counts, g.offsets, partials, d_means, d_scales, d_colors, d_opacities);
+  else
+    hipLaunchKernelGGL(k_reduce_bwd<12>, dim3(blocks_for(n)), dim3(256), 0, s, vk, n, means, scales, colors, opacities,
+                       g.counts, g.offsets, partials, d_means, d_scales, d_colors, d_opacities);
+  GR_HIP_TRY(hipGetLastError());
+  return GR_OK;
+}
+
+gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, const float* scales, const float* colors,
+                       const float* opacities, uint8_t* rgba) {
+  if (!p || !rgba) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+  if (p->width <= 0 || p->height <= 0) return set_error(GR_ERR_INVALID_ARGUMENT, "width/height must be positive");
+  const size_t HW = (size_t)p->width * p->height;
+  if (n <= 0) {  // renderer.cu:279-281
+    std::memset(rgba, 0, HW * 4);
+    return GR_OK;
+  }
+  if (!means || !scales || !colors || !opacities) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+  gr_view gv;
+  gv.width = p->width;
+  gv.height = p->height;
+  std::memcpy(gv.view, p->view, sizeof(gv.view));
+  std::memcpy(gv.proj, p->proj, sizeof(gv.proj));
+  std::memcpy(gv.background, p->background, sizeof(gv.background));
+  gv.cam_pos[0] = gv.cam_pos[1] = gv.cam_pos[2] = 0.f;
+  gv.cutoff = 3.0f;
+  const ViewK vk = make_viewk(&gv);
+  const int tiles = vk.tiles_x * vk.tiles_y;
+  const bool sorted = p->enable_depth_sort != 0;
+  // One device allocation per call: reentrant (no function-static buffers as renderer.cu:349).
+  const size_t nn = (size_t)n;
+  size_t o = 0;
+  const size_t o_in = o; o = align_up(o + nn * 10 * sizeof(float));
+  const size_t o_a = o; o = align_up(o + nn * sizeof(float4));
+  const size_t o_c = o; o = align_up(o + nn * sizeof(float4));
+  const size_t o_box = o; o = align_up(o + nn * sizeof(int4));
+  const size_t o_rect = o; o = align_up(o + nn * sizeof(int4));
+  const size_t o_cnt = o; o = align_up(o + (nn + 1) * sizeof(int));
+  const size_t o_off = o; o = align_up(o + (nn + 1) * sizeof(int));
+  const size_t o_dk = o; o = align_up(o + nn * sizeof(uint32_t));
+  const size_t o_img = o; o = align_up(o + HW * 4);
+  const size_t o_scan = o; o = align_up(o + scan_tmp_bytes(n));
+  const size_t fixed = o;
+  char* d = nullptr;
+  GR_HIP_TRY(hipMalloc(&d, fixed));
+  struct Guard {
+    void* p;
+    ~Guard() { if (p) (void)hipFree(p); }
+  } guard{d};
+  hipStream_t s = nullptr;
+  float* din = (float*)(d + o_in);
+  GR_HIP_TRY(hipMemcpy(din, means, nn * 3 * sizeof(float), hipMemcpyHostToDevice));
+  GR_HIP_TRY(hipMemcpy(din + 3 * nn, scales, nn * 3 * sizeof(float), hipMemcpyHostToDevice));
+  GR_HIP_TRY(hipMemcpy(din + 6 * nn, colors, nn * 3 * sizeof(float), hipMemcpyHostToDevice));
+  GR_HIP_TRY(hipMemcpy(din + 9 * nn, opacities, nn * sizeof(float), hipMemcpyHostToDevice));
+  LegacyRec lr;
+  lr.a = (float4*)(d + o_a);
+  lr.c = (float4*)(d + o_c);
+  lr.box = (int4*)(d + o_box);
+  lr.rect = (int4*)(d + o_rect);
+  lr.counts = (int*)(d + o_cnt);
+  lr.offsets = (int*)(d + o_off);
+  lr.depth_key = (uint32_t*)(d + o_dk);
+  hipLaunchKernelGGL(k_preprocess_u8, dim3(blocks_for(n + 1)), dim3(256), 0, s, vk, n, din, din + 3 * nn, din + 6 * nn,
+                     din + 9 * nn, lr);
+  GR_HIP_TRY(hipGetLastError());
+  size_t tmp = scan_tmp_bytes(n);
+  GR_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(d + o_scan, tmp, lr.counts, lr.offsets, n + 1, s));
+  int K = 0;
+  GR_HIP_TRY(hipMemcpy(&K, lr.offsets + n, sizeof(int), hipMemcpyDeviceToHost));
+  if (K < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
+  // bins: keys_in/out (u32 or u64), ids_in/out, ranges, sort tmp
+  const size_t kk = (size_t)(K > 0 ? K : 1);
+  const size_t ksz = sorted ? sizeof(uint64_t) : sizeof(uint32_t);
+  const int bits = sorted ? 32 + bits_for((uint32_t)tiles) : bits_for((uint32_t)tiles);
+  const size_t stmp = sorted ? sort_tmp_bytes<uint64_t>(K, bits) : sort_tmp_bytes<uint32_t>(K, bits);
+  size_t q = 0;
+  const size_t q_kin = q; q = align_up(q + kk * ksz);
+  const size_t q_kout = q; q = align_up(q + kk * ksz);
+  const size_t q_iin = q; q = align_up(q + kk * sizeof(int));
+  const size_t q_iout = q; q = align_up(q + kk * sizeof(int));
+  const size_t q_rg = q; q = align_up(q + (size_t)tiles * sizeof(int2));
+  const size_t q_tmp = q; q = align_up(q + stmp);
+  char* e = nullptr;
+  GR_HIP_TRY(hipMalloc(&e, q));
+  Guard guard2{e};
+  int2* ranges = (int2*)(e + q_rg);
+  GR_HIP_TRY(hipMemsetAsync(ranges, 0, sizeof(int2) * tiles, s));
+  if (K > 0) {
+    size_t t2 = stmp;
+    if (sorted) {
+      uint64_t* kin = (uint64_t*)(e + q_kin);
+      uint64_t* kout = (uint64_t*)(e + q_kout);
+      // low 32 bits = depth key; high bits = tile
+      hipLaunchKernelGGL(k_emit<uint64_t>, dim3(blocks_for(n)), dim3(256), 0, s, n, vk.tiles_x, lr.rect, lr.counts,
+                         lr.offsets, (const uint64_t*)nullptr, kin, (int*)(e + q_iin));
+      GR_HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_patch_depth, dim3(blocks_for(K)), dim3(256), 0, s, (int64_t)K, kin, (const int*)(e + q_iin),
+                         (const uint32_t*)lr.depth_key);
+      GR_HIP_TRY(hipGetLastError());
+      GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e + q_tmp, t2, kin, kout, (int*)(e + q_iin), (int*)(e + q_iout), K, 0,
+                                                    bits, s));
+      hipLaunchKernelGGL(k_ranges<uint64_t>, dim3(blocks_for(K)), dim3(256), 0, s, (int64_t)K, (const uint64_t*)kout, ranges);
+    } else {
+      uint32_t* kin = (uint32_t*)(e + q_kin);
+      uint32_t* kout = (uint32_t*)(e + q_kout);
+      hipLaunchKernelGGL(k_emit<uint32_t>, dim3(blocks_for(n)), dim3(256), 0, s, n, vk.tiles_x, lr.rect, lr.counts,
+                         lr.offsets, (const uint32_t*)nullptr, kin, (int*)(e + q_iin));
+      GR_HIP_TRY(hipGetLastError());
+      GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e + q_tmp, t2, kin, kout, (int*)(e + q_iin), (int*)(e + q_iout), K, 0,
+                                                    bits, s));
+      hipLaunchKernelGGL(k_ranges<uint32_t>, dim3(blocks_for(K)), dim3(256), 0, s, (int64_t)K, (const uint32_t*)kout, ranges);
+    }
+    GR_HIP_TRY(hipGetLastError());
+  }
+  uint8_t* img = (uint8_t*)(d + o_img);
+  if (sorted)
+    hipLaunchKernelGGL(k_raster_u8<true>, dim3(tiles), dim3(256), 0, s, vk, ranges, (const int*)(e + q_iout), lr.a, lr.c,
+                       lr.box, img);
+  else
+    hipLaunchKernelGGL(k_raster_u8<false>, dim3(tiles), dim3(256), 0, s, vk, ranges, (const int*)(e + q_iout), lr.a, lr.c,
+                       lr.box, img);
+  GR_HIP_TRY(hipGetLastError());
+  GR_HIP_TRY(hipMemcpy(rgba, img, HW * 4, hipMemcpyDeviceToHost));
+  return GR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,140 @@
+/*
+ * gr_hip.h — C ABI of the MI355X (gfx950) differentiable Gaussian rasterizer.
+ *
+ * This is the drop-in boundary for the render op of Kirkice/3DGaussian:
+ *
+ *   reference surface (file:line)                          replaced by
+ *   ------------------------------------------------------ ------------------------------------
+ *   python/torch_renderer.py:109-203 render_gaussians_torch gr_fwd_prepare + gr_fwd_render (fwd)
+ *     (autograd backward at fit_multiview_stub.py:310)      gr_bwd                         (bwd)
+ *   include/gr/renderer.h:33-39 gr::render_gaussians        gr_render_u8
+ *   include/gr/renderer.h:10-30 render_gaussians_{cpu,cuda} gr_render_u8 (HIP only)
+ *   src/renderer_dispatch.cpp:5-21 (force_cpu / CUDA)       gr_render_u8 (HIP-only dispatch)
+ *   src/bindings.cpp:27-100 (pybind11 module)               3dgaussian_amd/gaussian_renderer.py
+ *   include/gr/cuda_utils.cuh:10-18 GR_CUDA_CHECK throw     gr_status codes + gr_last_error()
+ *   include/gr/gaussian_types.h:24-46 RenderParams          gr_render_params (same field order)
+ *
+ * Conventions
+ *   - Plain C: no C++ or torch types in any signature.  All matrices are 4x4 row-major float32,
+ *     exactly as RenderParams::view/proj (gaussian_types.h:28-30).
+ *   - The differentiable entry points (gr_fwd_*, gr_bwd) take DEVICE pointers owned by the caller
+ *     and a hipStream_t passed as void*.  They allocate nothing and keep no global state, so they
+ *     are reentrant and stream-ordered (unlike renderer.cu:349's function-static buffers).
+ *     Workspace sizes come from the *_bytes() queries.
+ *   - gr_fwd_prepare is the one call that synchronises its stream: it returns the number of
+ *     (Gaussian, tile) pairs, which sizes the binning workspace.
+ *   - gr_render_u8 takes HOST pointers (as gr::render_gaussians does) and is synchronous.
+ *   - Every function returns GR_OK or an error code; gr_last_error() gives a thread-local message.
+ */
+#ifndef GR_HIP_H_
+#define GR_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GR_TILE 16 /* screen tile edge in pixels (16x16 = 256 pixels per tile) */
+
+typedef enum gr_status {
+  GR_OK = 0,
+  GR_ERR_INVALID_ARGUMENT = 1, /* shapes / sizes / null pointers (python: ValueError/RuntimeError) */
+  GR_ERR_HIP = 2,              /* a HIP runtime call failed (reference: GR_CUDA_CHECK throw)      */
+  GR_ERR_WORKSPACE = 3,        /* caller-provided workspace too small                              */
+  GR_ERR_OVERFLOW = 4          /* pair count does not fit int32                                    */
+} gr_status;
+
+/* Mirrors gr::RenderParams (include/gr/gaussian_types.h:24-46), same field order and defaults
+ * (width 800, height 600, zero matrices, black background, enable_depth_sort 0, depth_slices 16,
+ * force_cpu 0).  Used by the legacy uint8 surface. */
+typedef struct gr_render_params {
+  int width;
+  int height;
+  float view[16];
+  float proj[16];
+  float background[3];
+  int enable_depth_sort; /* 0: OIT weighted average, 1: exact depth-sorted "over" compositing */
+  int depth_slices;      /* accepted for ABI compatibility; the HIP path sorts exactly       */
+  int force_cpu;         /* accepted for ABI compatibility; the HIP path is the only path    */
+} gr_render_params;
+
+/* One camera view for the differentiable path (torch_renderer.py:109-121 arguments). */
+typedef struct gr_view {
+  int width;
+  int height;
+  float view[16];      /* Camera.view, row-major                                          */
+  float proj[16];      /* Camera.proj, row-major                                          */
+  float background[3]; /* background colour (torch_renderer.py:128-130)                    */
+  float cam_pos[3];    /* inv(view)[:3,3] (torch_renderer.py:81-83); used by SH colours    */
+  float cutoff;        /* screen footprint half-width in sigmas used for binning (def. 5)  */
+} gr_view;
+
+/* ------------------------------------------------------------------------------------------ */
+/* Differentiable path (device pointers).                                                     */
+/*   means (N,3), scales (N,3), colors (N,3) [color_dim 3] or SH deg-1 (N,4,3) [color_dim 12], */
+/*   opacities (N,), all float32 contiguous.                                                   */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Per-Gaussian projection records, tile rectangles, pair counts and offsets. */
+size_t gr_geom_bytes(int n);
+
+/* Project + cull + count tiles + prefix-scan.  Writes *num_pairs (synchronises `stream`). */
+gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const float* scales,
+                         const float* colors, int color_dim, const float* opacities, void* geom,
+                         size_t geom_bytes, int64_t* num_pairs, void* stream);
+
+/* Tile-sorted (tile, Gaussian) pair lists and per-tile ranges. */
+size_t gr_bins_bytes(const gr_view* v, int n, int64_t num_pairs);
+
+/* Per-pixel state saved for the backward pass: 5 floats per pixel. */
+size_t gr_saved_floats(const gr_view* v);
+
+/* Emit pairs + sort by tile + tile ranges + forward splat.  Outputs:
+ *   out_rgb (H,W,3) clamp((bg+C)/(1+W),0,1); out_alpha (H,W) (may be NULL); out_depth (H,W)
+ *   (may be NULL); saved (5*H*W floats) accumulators kept for gr_bwd. */
+gr_status gr_fwd_render(const gr_view* v, int n, int64_t num_pairs, const void* geom, void* bins,
+                        size_t bins_bytes, float* out_rgb, float* out_alpha, float* out_depth,
+                        float* saved, void* stream);
+
+/* Backward workspace (per-pair gradient partials). */
+size_t gr_bwd_bytes(int n, int64_t num_pairs);
+
+/* Backward of gr_fwd_render.  g_rgb (H,W,3) required; g_alpha, g_depth may be NULL (zero).
+ * Writes (overwrites) d_means (N,3), d_scales (N,3) (column 2 is always 0),
+ * d_colors (N,3) or (N,4,3), d_opacities (N,). */
+gr_status gr_bwd(const gr_view* v, int n, int64_t num_pairs, const float* means,
+                 const float* scales, const float* colors, int color_dim, const float* opacities,
+                 const void* geom, const void* bins, const float* saved, const float* g_rgb,
+                 const float* g_alpha, const float* g_depth, float* d_means, float* d_scales,
+                 float* d_colors, float* d_opacities, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Legacy uint8 surface (host pointers), replaces gr::render_gaussians (renderer.h:33-39).    */
+/* Semantics of renderer_cpu.cpp: 3-sigma box, w < 1e-5 skip, uint8 round-half-up, A = 255.  */
+/* enable_depth_sort = 1 gives exact per-pixel front-to-back compositing in camera-z order.   */
+/* rgba must hold width*height*4 bytes.                                                       */
+/* ------------------------------------------------------------------------------------------ */
+gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, const float* scales,
+                       const float* colors, const float* opacities, uint8_t* rgba);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Introspection (host-only, no GPU needed).                                                  */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Byte offsets of the sub-buffers inside geom / bins, for debugging and bit-exact tests.
+ *   geom: [0] rec_a float4[n] (px,py,qx,qy)  [1] rec_b float4[n] (o,r,g,b)  [2] rec_z float[n]
+ *         [3] rect int4[n] (tx0,ty0,tx1,ty1) [4] counts int[n+1] [5] offsets int[n+1]
+ *   bins: [0] keys uint32[K] [1] gaussian ids int32[K] (tile-sorted) [2] ranges int2[tiles]  */
+void gr_geom_layout(int n, size_t offsets_out[6]);
+void gr_bins_layout(const gr_view* v, int n, int64_t num_pairs, size_t offsets_out[3]);
+
+const char* gr_last_error(void);
+const char* gr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GR_HIP_H_ */

@@ -1,0 +1,185 @@
+"""GPU parity tests: the HIP render op (through the C ABI) against the reference's golden vectors
+and the CPU oracle.  Bars (BASELINE.json north_star): relative L2 <= 1e-4 on outputs and every
+gradient, PSNR >= 60 dB, integer tile/bin data bit-exact against the oracle's binning.
+
+Tolerance note: for a few ill-conditioned tensors (e.g. the single opacity gradient of a one-Gaussian
+scene: a sum of large cancelling terms from d depth / d w = (z - depth)/(W + 1e-6)) the reference's
+own float32 result sits further than 1e-4 from the exact (float64 oracle) value.  Two float32
+implementations cannot agree to 1e-4 there, so for such tensors (reference error > 3e-5) the bar is
+on the distance to the exact value instead: relL2(hip, exact) <= max(1e-4, 3 x relL2(reference,
+exact)) — the HIP result is no worse than three times the reference's own rounding error.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, golden_names
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+GRAD_KEYS = ("d_means", "d_scales", "d_colors", "d_opacities")
+
+
+def _run_hip(pkg, d, device, cutoff=None):
+    tr = pkg.torch_renderer
+    W, H = int(d["width"]), int(d["height"])
+    t = {k: torch.from_numpy(np.ascontiguousarray(d[k])).to(device).requires_grad_(True)
+         for k in ("means", "scales", "colors", "opacities")}
+    cam = tr.Camera(view=torch.from_numpy(d["view"]).to(device), proj=torch.from_numpy(d["proj"]).to(device))
+    kw = {} if cutoff is None else {"cutoff": cutoff}
+    res = tr.render_gaussians_torch(t["means"], t["scales"], t["colors"], t["opacities"], cam, W, H,
+                                    background=torch.from_numpy(d["background"]).to(device),
+                                    max_gaussians=max(10000, d["means"].shape[0]), return_aux=True, **kw)
+    if d["means"].shape[0] == 0:
+        return {"out_rgb": res.cpu().numpy()}
+    out, alpha, depth = res
+    loss = ((out * torch.from_numpy(d["g_rgb"]).to(device)).sum() + (alpha * torch.from_numpy(d["g_alpha"]).to(device)).sum()
+            + (depth * torch.from_numpy(d["g_depth"]).to(device)).sum())
+    loss.backward()
+    r = {"out_rgb": out.detach().cpu().numpy(), "out_alpha": alpha.detach().cpu().numpy(), "out_depth": depth.detach().cpu().numpy()}
+    for k, name in zip(GRAD_KEYS, ("means", "scales", "colors", "opacities")):
+        r[k] = t[name].grad.cpu().numpy()
+    return r
+
+
+def _oracle(d, binned):
+    v = orc.make_view(d["view"], d["proj"], int(d["width"]), int(d["height"]), d["background"], cutoff=6.0)
+    sc = orc.Scene(d["means"], d["scales"], d["colors"], d["opacities"])
+    out, alpha, depth = orc.forward(v, sc, binned=binned)
+    dm, ds, dc, do = orc.backward(v, sc, d["g_rgb"], d["g_alpha"], d["g_depth"], binned=binned)
+    return {"out_rgb": out, "out_alpha": alpha, "out_depth": depth, "d_means": dm, "d_scales": ds, "d_colors": dc, "d_opacities": do}
+
+
+@pytest.mark.parametrize("name", golden_names("f1_") + golden_names("f2_"))
+def test_fwd_bwd_matches_reference_goldens(pkg, cuda, name):
+    d = golden(name)
+    hip = _run_hip(pkg, d, cuda)
+    if d["means"].shape[0] == 0:
+        np.testing.assert_array_equal(hip["out_rgb"], d["out_rgb"])
+        return
+    exact = _oracle(d, binned=False)
+    for k in ("out_rgb", "out_alpha", "out_depth") + GRAD_KEYS:
+        ref_err = orc.rel_l2(d[k], exact[k])  # the reference's own float32 error
+        if ref_err <= 3e-5:
+            err = orc.rel_l2(hip[k], d[k])
+            assert err <= 1e-4, f"{name} {k}: relL2 vs reference {err:.3e} > 1e-4"
+        else:
+            err = orc.rel_l2(hip[k], exact[k])
+            tol = max(1e-4, 3.0 * ref_err)
+            assert err <= tol, f"{name} {k}: relL2 vs exact {err:.3e} > {tol:.3e} (reference's own error {ref_err:.1e})"
+    assert orc.psnr(hip["out_rgb"], d["out_rgb"]) >= 60.0
+
+
+@pytest.mark.parametrize("name", golden_names("f1_n300") + golden_names("f2_c1_view0"))
+def test_fwd_bwd_matches_binned_oracle(pkg, cuda, name):
+    """Same semantics (6-sigma tile footprint) in float64 on the CPU: tighter bound."""
+    d = golden(name)
+    hip = _run_hip(pkg, d, cuda)
+    ora = _oracle(d, binned=True)
+    for k in ("out_rgb", "out_alpha", "out_depth"):
+        assert orc.rel_l2(hip[k], ora[k]) <= 2e-5, k
+    for k in GRAD_KEYS:
+        assert orc.rel_l2(hip[k], ora[k]) <= 1e-4, k
+
+
+def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=6.0):
+    tr = pkg.torch_renderer
+    nat = pkg._native
+    m, s, c, o = (torch.from_numpy(a).to(device) for a in scene.arrays())
+    gv = tr.make_view(view, proj, W, H, None, cutoff)
+    out, alpha, depth, st = tr.forward_native(m, s, c, o, gv)
+    torch.cuda.synchronize()
+    n = m.shape[0]
+    g_off = nat.geom_layout(n)
+    geom = st.geom.cpu().numpy()
+    recA = geom[g_off[0]: g_off[0] + 16 * n].view(np.float32).reshape(n, 4)
+    rect = geom[g_off[3]: g_off[3] + 16 * n].view(np.int32).reshape(n, 4)
+    counts = geom[g_off[4]: g_off[4] + 4 * n].view(np.int32)
+    offsets = geom[g_off[5]: g_off[5] + 4 * (n + 1)].view(np.int32)
+    b_off = nat.bins_layout(gv, n, st.num_pairs)
+    bins = st.bins.cpu().numpy()
+    K = st.num_pairs
+    tiles = ((W + 15) // 16) * ((H + 15) // 16)
+    keys = bins[b_off[0]: b_off[0] + 4 * K].view(np.uint32)
+    ids = bins[b_off[1]: b_off[1] + 4 * K].view(np.int32)
+    ranges = bins[b_off[2]: b_off[2] + 8 * tiles].view(np.int32).reshape(tiles, 2)
+    return dict(recA=recA, rect=rect, counts=counts, offsets=offsets, keys=keys, ids=ids, ranges=ranges, K=K)
+
+
+@pytest.mark.parametrize("case", ["f1_n300_64x48", "f2_c1_view1", "c2_100k_512", "edge_big_sigma"])
+def test_bins_bit_exact(pkg, cuda, case):
+    if case.startswith("f"):
+        d = golden(case)
+        scene = orc.Scene(d["means"], d["scales"], d["colors"], d["opacities"])
+        view, proj, W, H = d["view"], d["proj"], int(d["width"]), int(d["height"])
+    elif case == "c2_100k_512":
+        scene = orc.synthetic_scene(100_000, seed=3)
+        view, proj = orc.orbit_cameras(8, 512, 512)[5]
+        W = H = 512
+    else:
+        scene = orc.synthetic_scene(2000, seed=4, scale=0.4)  # huge footprints, many clipped rects
+        view, proj = orc.orbit_cameras(3, 200, 120)[1]
+        W, H = 200, 120
+    g = _native_bins(pkg, scene, view, proj, W, H, cuda)
+    v = orc.make_view(view, proj, W, H, None, cutoff=6.0)
+    rec, rect, counts = orc.preprocess(v, scene)
+    # projected centres are float32-identical (same operation sequence, no FMA contraction)
+    np.testing.assert_array_equal(g["recA"][:, 0].view(np.int32), rec[:, 0].view(np.int32))
+    np.testing.assert_array_equal(g["recA"][:, 1].view(np.int32), rec[:, 1].view(np.int32))
+    np.testing.assert_array_equal(g["counts"], counts)
+    np.testing.assert_array_equal(g["rect"], rect)
+    offsets, keys, vals, ranges = orc.bin_pairs(v, rect, counts)
+    np.testing.assert_array_equal(g["offsets"], offsets)
+    assert g["K"] == len(vals)
+    np.testing.assert_array_equal(g["keys"], keys)
+    np.testing.assert_array_equal(g["ids"], vals)
+    nonempty = ranges[:, 1] > ranges[:, 0]
+    np.testing.assert_array_equal(g["ranges"][nonempty], ranges[nonempty])
+    assert np.all(g["ranges"][~nonempty, 1] == g["ranges"][~nonempty, 0])
+
+
+def test_deterministic(pkg, cuda):
+    """No float atomics anywhere: two runs are bit-identical."""
+    d = golden("f2_c1_view2")
+    a = _run_hip(pkg, d, cuda)
+    b = _run_hip(pkg, d, cuda)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_c2_scale_vs_binned_oracle(pkg, cuda):
+    """100k Gaussians, 512x512 (config C2 size): forward and backward against the float64 oracle."""
+    scene = orc.synthetic_scene(100_000, seed=11)
+    view, proj = orc.orbit_cameras(8, 512, 512)[2]
+    rng = np.random.default_rng(5)
+    d = dict(width=np.int32(512), height=np.int32(512), view=view, proj=proj, background=np.zeros(3, np.float32),
+             means=scene.means, scales=scene.scales, colors=scene.colors, opacities=scene.opacities,
+             g_rgb=rng.standard_normal((512, 512, 3)).astype(np.float32),
+             g_alpha=rng.standard_normal((512, 512)).astype(np.float32),
+             g_depth=rng.standard_normal((512, 512)).astype(np.float32))
+    hip = _run_hip(pkg, d, cuda)
+    ora = _oracle(d, binned=True)
+    for k in ("out_rgb", "out_alpha", "out_depth"):
+        assert orc.rel_l2(hip[k], ora[k]) <= 2e-5, k
+    for k in GRAD_KEYS:
+        assert orc.rel_l2(hip[k], ora[k]) <= 1e-4, k
+    assert orc.psnr(hip["out_rgb"], ora["out_rgb"]) >= 60.0
+
+
+@pytest.mark.parametrize("name", golden_names("u8_"))
+def test_legacy_u8_matches_reference_cpu(pkg, cuda, name):
+    d = golden(name)
+    gr = pkg.gaussian_renderer
+    out = gr.render_gaussians(d["means"], d["scales"], d["colors"], d["opacities"], int(d["width"]), int(d["height"]),
+                              np.ascontiguousarray(d["view"]), np.ascontiguousarray(d["proj"]),
+                              np.ascontiguousarray(d["background"]), enable_depth_sort=int(d["sort"]))
+    if d["means"].shape[0] == 0:
+        # HIP path keeps renderer.cu's n<=0 contract (renderer.cu:279-281): all-zero RGBA
+        assert not out.any()
+        return
+    diff = np.abs(out.astype(np.int32) - d["rgba"].astype(np.int32))
+    assert diff.max() <= 1, f"{name}: max diff {diff.max()}"
+    assert (diff > 0).mean() < 0.01
