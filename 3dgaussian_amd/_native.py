@@ -73,7 +73,7 @@ _SIG = {
     "gr_bins_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, ctypes.c_int64]),
     "gr_saved_floats": (ctypes.c_size_t, [_VP]),
     "gr_fwd_render": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int64, _P, _P, ctypes.c_size_t, _P, _P, _P, _P, _P]),
-    "gr_bwd_bytes": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int64]),
+    "gr_bwd_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, ctypes.c_int64]),
     "gr_bwd": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int64, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, _P, _P, _P, ctypes.c_size_t, _P]),
     "gr_render_u8": (ctypes.c_int, [ctypes.POINTER(GrRenderParams), ctypes.c_int, _P, _P, _P, _P, _P]),

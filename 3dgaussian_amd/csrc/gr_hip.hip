@@ -30,6 +30,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -211,23 +212,37 @@ Geom geom_view(void* base, int n) {
 // ------------------------------------------------------------------------------------------------
 // Bins buffer layout.
 // ------------------------------------------------------------------------------------------------
+constexpr int CH = 1024;  // Gaussians per raster work item (one chunk of one tile's list)
+constexpr int NPART = 9;  // backward partial sums per (Gaussian, tile) pair
+
 struct Bins {
   uint32_t* keys;      // sorted keys (K)
   int* ids;            // sorted gaussian ids (K)
-  int2* ranges;        // tiles
+  int2* ranges;        // [tiles] pair range of each tile
+  int4* items;         // [cap] work items (tile, k0, k1, chunk)
+  int* num_items;      // [1]
+  int* tile_item0;     // [tiles] first work item of each tile
+  float* fwd_part;     // [cap][5][256] forward partial accumulators (tiles split over several items)
   uint32_t* keys_in;   // K
   int* ids_in;         // K
   void* sort_tmp;
 };
 
-size_t bins_fixed(int tiles, int64_t K, size_t off[5]) {
+inline int64_t item_cap(int tiles, int64_t K) { return (K + CH - 1) / CH + tiles; }
+
+size_t bins_fixed(int tiles, int64_t K, size_t off[9]) {
   const size_t kk = (size_t)(K > 0 ? K : 1);
+  const size_t cap = (size_t)item_cap(tiles, K);
   size_t o = 0;
   off[0] = o; o = align_up(o + kk * sizeof(uint32_t));
   off[1] = o; o = align_up(o + kk * sizeof(int));
   off[2] = o; o = align_up(o + (size_t)tiles * sizeof(int2));
-  off[3] = o; o = align_up(o + kk * sizeof(uint32_t));
-  off[4] = o; o = align_up(o + kk * sizeof(int));
+  off[3] = o; o = align_up(o + cap * sizeof(int4));
+  off[4] = o; o = align_up(o + sizeof(int));
+  off[5] = o; o = align_up(o + (size_t)tiles * sizeof(int));
+  off[6] = o; o = align_up(o + cap * 5 * TP * sizeof(float));
+  off[7] = o; o = align_up(o + kk * sizeof(uint32_t));
+  off[8] = o; o = align_up(o + kk * sizeof(int));
   return o;
 }
 
@@ -240,15 +255,19 @@ size_t sort_tmp_bytes(int64_t K, int bits) {
 }
 
 Bins bins_view(void* base, int tiles, int64_t K) {
-  size_t off[5];
+  size_t off[9];
   const size_t fixed = bins_fixed(tiles, K, off);
   char* b = (char*)base;
   Bins r;
   r.keys = (uint32_t*)(b + off[0]);
   r.ids = (int*)(b + off[1]);
   r.ranges = (int2*)(b + off[2]);
-  r.keys_in = (uint32_t*)(b + off[3]);
-  r.ids_in = (int*)(b + off[4]);
+  r.items = (int4*)(b + off[3]);
+  r.num_items = (int*)(b + off[4]);
+  r.tile_item0 = (int*)(b + off[5]);
+  r.fwd_part = (float*)(b + off[6]);
+  r.keys_in = (uint32_t*)(b + off[7]);
+  r.ids_in = (int*)(b + off[8]);
   r.sort_tmp = b + fixed;
   return r;
 }
@@ -312,169 +331,348 @@ __global__ __launch_bounds__(256) void k_ranges(int64_t K, const KeyT* __restric
 }
 
 // ------------------------------------------------------------------------------------------------
-// Forward splat.  One 256-lane workgroup per 16x16 tile, one lane per pixel.
+// MFMA formulation.  With axis-aligned footprints the weight is separable,
+//   w_g(x,y) = o_g * ex_g(x) * ey_g(y),  ex_g(x) = 2^(qx (x+.5-px)^2),  ey_g(y) likewise,
+// so the per-tile splat is a dense contraction over the tile's Gaussians g:
+//   forward   C_k[x][y] = sum_g (o_g v_gk ex_g(x)) * ey_g(y),  v = (1, r, g, b, z)
+//   backward  D_k,f[y][g] = sum_x U_k[x][y] * (f(x) ex_g(x)),  f in {1, dx, dx^2}
+// evaluated with v_mfma_f32_16x16x4_f32 (exact f32 fma chain, K = 4).  Lane l supplies
+// A[l&15][l>>4] and B[l>>4][l&15]; it receives C[4(l>>4)+r][l&15], r = 0..3.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_raster_fwd(ViewK v, const int2* __restrict__ ranges, const int* __restrict__ ids,
-                                                    const float4* __restrict__ recA, const float4* __restrict__ recB,
-                                                    const float* __restrict__ recZ, float* __restrict__ out_rgb,
-                                                    float* __restrict__ out_alpha, float* __restrict__ out_depth,
-                                                    float4* __restrict__ saved4, float* __restrict__ savedD) {
-  __shared__ float4 sA[TP];
-  __shared__ float4 sB[TP];
-  __shared__ float sZ[TP];
-  const int tile = blockIdx.x;
-  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
-  const int tid = threadIdx.x;
-  const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
-  const float xc = (float)x + 0.5f, yc = (float)y + 0.5f;
-  const int2 rg = ranges[tile];
-  float aW = 0.f, aR = 0.f, aG = 0.f, aB = 0.f, aD = 0.f;
-  for (int base = rg.x; base < rg.y; base += TP) {
-    const int cnt = min(TP, rg.y - base);
-    __syncthreads();
-    if (tid < cnt) {
-      const int g = ids[base + tid];
-      sA[tid] = recA[g];
-      sB[tid] = recB[g];
-      sZ[tid] = recZ[g];
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Work items: each non-empty tile's pair list is cut into chunks of CH Gaussians, so every
+// workgroup gets about the same amount of work however unevenly Gaussians fall on tiles.
+// One block; tiles are scanned in order, so items are ordered by (tile, chunk).
+__global__ __launch_bounds__(1024) void k_work_items(int tiles, const int2* __restrict__ ranges, int4* __restrict__ items,
+                                                     int* __restrict__ num_items, int* __restrict__ tile_item0) {
+  typedef hipcub::BlockScan<int, 1024> Scan;
+  __shared__ typename Scan::TempStorage tmp;
+  __shared__ int carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < tiles; base += 1024) {
+    const int t = base + (int)threadIdx.x;
+    int2 r = make_int2(0, 0);
+    if (t < tiles) r = ranges[t];
+    const int nch = (r.y - r.x + CH - 1) / CH;
+    int excl, total;
+    Scan(tmp).ExclusiveSum(nch, excl, total);
+    const int first = carry + excl;
+    if (t < tiles) {
+      tile_item0[t] = first;
+      for (int c = 0; c < nch; ++c) items[first + c] = make_int4(t, r.x + c * CH, min(r.y, r.x + (c + 1) * CH), c);
     }
     __syncthreads();
-    for (int j = 0; j < cnt; ++j) {
+    if (threadIdx.x == 0) carry += total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *num_items = carry;
+}
+
+// Gaussian records of one 256-wide batch, staged through registers (load early, write late).
+struct StageRec {
+  float4 a, b;
+  float z;
+  int g;
+};
+
+__device__ __forceinline__ StageRec stage_load(int k, int k1, const int* __restrict__ ids, const float4* __restrict__ recA,
+                                               const float4* __restrict__ recB, const float* __restrict__ recZ) {
+  StageRec r;
+  r.a = make_float4(0.f, 0.f, 0.f, 0.f);
+  r.b = r.a;
+  r.z = 0.f;
+  r.g = -1;
+  if (k < k1) {
+    r.g = ids[k];
+    r.a = recA[r.g];
+    r.b = recB[r.g];
+    r.z = recZ[r.g];
+  }
+  return r;
+}
+
+// Forward: one workgroup (4 waves) per work item.  Batches of 256 Gaussians go through LDS; wave w
+// takes Gaussians [64w, 64w+64) of each batch in steps of 4 (the MFMA K dimension).
+__global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, const int4* __restrict__ items,
+                                                         const int* __restrict__ num_items, const int2* __restrict__ ranges,
+                                                         const int* __restrict__ ids, const float4* __restrict__ recA,
+                                                         const float4* __restrict__ recB, const float* __restrict__ recZ,
+                                                         float* __restrict__ fwd_part, float* __restrict__ out_rgb,
+                                                         float* __restrict__ out_alpha, float* __restrict__ out_depth,
+                                                         float4* __restrict__ saved4, float* __restrict__ savedD) {
+  // LDS: staged records (9 KiB) during the loop, then the 4-wave reduction (20 KiB).
+  __shared__ __attribute__((aligned(16))) float smem[4 * 5 * TP];
+  float4* sA = reinterpret_cast<float4*>(smem);
+  float4* sB = sA + TP;
+  float* sZ = reinterpret_cast<float*>(sB + TP);
+  const int item = blockIdx.x;
+  if (item >= *num_items) return;
+  const int4 it = items[item];
+  const int tile = it.x, k0 = it.y, k1 = it.z;
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int li = lane & 15, gs = lane >> 4;
+  const float xc = (float)(tx * T + li) + 0.5f;  // A row = x
+  const float yc = (float)(ty * T + li) + 0.5f;  // B col = y
+  f32x4 cW = {0.f, 0.f, 0.f, 0.f}, cR = cW, cG = cW, cB = cW, cD = cW;
+  StageRec st = stage_load(k0 + tid, k1, ids, recA, recB, recZ);
+  for (int base = k0; base < k1; base += TP) {
+    __syncthreads();
+    sA[tid] = st.a;
+    sB[tid] = st.b;
+    sZ[tid] = st.z;
+    __syncthreads();
+    st = stage_load(base + TP + tid, k1, ids, recA, recB, recZ);
+    const int cnt = min(TP, k1 - base) - wave * 64;  // Gaussians of this batch for this wave
+    const int nst = cnt <= 0 ? 0 : min(16, (cnt + 3) >> 2);
+    for (int i = 0; i < nst; ++i) {
+      const int j = wave * 64 + 4 * i + gs;
       const float4 a = sA[j];
       const float4 b = sB[j];
       const float z = sZ[j];
       const float dx = xc - a.x, dy = yc - a.y;
-      const float e = fmaf(dx * a.z, dx, dy * a.w * dy);
-      const float E = __builtin_amdgcn_exp2f(e);
-      const float w = b.x * E;
-      aW += w;
-      aR = fmaf(w, b.y, aR);
-      aG = fmaf(w, b.z, aG);
-      aB = fmaf(w, b.w, aB);
-      aD = fmaf(w, z, aD);
+      const float ex = __builtin_amdgcn_exp2f(dx * a.z * dx);
+      const float ey = __builtin_amdgcn_exp2f(dy * a.w * dy);
+      const float oe = b.x * ex;
+      cW = mfma4(oe, ey, cW);
+      cR = mfma4(oe * b.y, ey, cR);
+      cG = mfma4(oe * b.z, ey, cG);
+      cB = mfma4(oe * b.w, ey, cB);
+      cD = mfma4(oe * z, ey, cD);
     }
-  }
-  if (x >= v.W || y >= v.H) return;
-  const int p = y * v.W + x;
-  const float den = 1.0f + aW;
-  out_rgb[3 * p + 0] = clamp01((v.bg[0] + aR) / den);
-  out_rgb[3 * p + 1] = clamp01((v.bg[1] + aG) / den);
-  out_rgb[3 * p + 2] = clamp01((v.bg[2] + aB) / den);
-  if (out_alpha) out_alpha[p] = clamp01(aW / den);
-  if (out_depth) {
-    const float d = aD / (aW + 1e-6f);
-    out_depth[p] = d < 0.0f ? 0.0f : d;
-  }
-  saved4[p] = make_float4(aW, aR, aG, aB);
-  savedD[p] = aD;
-}
-
-// ------------------------------------------------------------------------------------------------
-// Backward splat.  Prologue: per-pixel U = (dC_r, dC_g, dC_b, dW) and dD into LDS.
-// Main: one lane per (Gaussian, this tile) pair, walking the 256 pixels with broadcast LDS reads.
-// Partials per pair (9 floats, slot = Gaussian's offset + tile index inside its rectangle):
-//   [0..2] sum w*dC_k   [3] sum w*dD   [4] sum gw*E   [5] sum gw*E*dx  [6] sum gw*E*dy
-//   [7] sum gw*E*dx^2   [8] sum gw*E*dy^2            (gw = dW + dC.c + dD*za; ge = o*gw*E)
-// ------------------------------------------------------------------------------------------------
-constexpr int NPART = 9;
-
-__global__ __launch_bounds__(256) void k_raster_bwd(ViewK v, const int2* __restrict__ ranges, const int* __restrict__ ids,
-                                                    const float4* __restrict__ recA, const float4* __restrict__ recB,
-                                                    const float* __restrict__ recZ, const int4* __restrict__ rect,
-                                                    const int* __restrict__ offsets, const float4* __restrict__ saved4,
-                                                    const float* __restrict__ savedD, const float* __restrict__ g_rgb,
-                                                    const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
-                                                    float* __restrict__ partials) {
-  __shared__ float4 sU[TP];
-  __shared__ float sUd[TP];
-  const int tile = blockIdx.x;
-  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
-  const int tid = threadIdx.x;
-  const int2 rg = ranges[tile];
-  if (rg.y <= rg.x) return;  // uniform per block
-  {
-    const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
-    float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
-    float ud = 0.f;
-    if (x < v.W && y < v.H) {
-      const int p = y * v.W + x;
-      const float4 s = saved4[p];
-      const float Dp = savedD[p];
-      const float den = 1.0f + s.x, dden = s.x + 1e-6f;
-      float gW = 0.f;
-      float gc[3];
-      const float C[3] = {s.y, s.z, s.w};
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const float r = (v.bg[k] + C[k]) / den;
-        const float go = (r >= 0.0f && r <= 1.0f) ? g_rgb[3 * p + k] : 0.0f;
-        gc[k] = go / den;
-        gW -= go * r / den;
-      }
-      if (g_alpha) {
-        const float al = s.x / den;
-        if (al >= 0.0f && al <= 1.0f) gW += g_alpha[p] / (den * den);
-      }
-      if (g_depth) {
-        const float d = Dp / dden;
-        if (d >= 0.0f) {
-          const float gd = g_depth[p];
-          gW -= gd * Dp / (dden * dden);
-          ud = gd / dden;
-        }
-      }
-      u = make_float4(gc[0], gc[1], gc[2], gW);
-    }
-    sU[tid] = u;
-    sUd[tid] = ud;
   }
   __syncthreads();
-  const float x0 = (float)(tx * T) + 0.5f, y0 = (float)(ty * T) + 0.5f;
-  for (int k = rg.x + tid; k < rg.y; k += TP) {
-    const int g = ids[k];
-    const float4 a = recA[g];
-    const float4 b = recB[g];
-    const float z = recZ[g];
-    float Sc0 = 0.f, Sc1 = 0.f, Sc2 = 0.f, Sz = 0.f, So = 0.f, Sdx = 0.f, Sdy = 0.f, Sdx2 = 0.f, Sdy2 = 0.f;
-    for (int py = 0; py < T; ++py) {
-      const float dy = (y0 + (float)py) - a.y;
-      const float ey = dy * a.w * dy;
-      float rowT = 0.f;
+  {  // lane holds C[x = 4*gs + r][y = li]: pixel index y*16 + x, 4 consecutive x
+    float* rw = smem + wave * 5 * TP + li * T + 4 * gs;
+    *reinterpret_cast<f32x4*>(rw + 0 * TP) = cW;
+    *reinterpret_cast<f32x4*>(rw + 1 * TP) = cR;
+    *reinterpret_cast<f32x4*>(rw + 2 * TP) = cG;
+    *reinterpret_cast<f32x4*>(rw + 3 * TP) = cB;
+    *reinterpret_cast<f32x4*>(rw + 4 * TP) = cD;
+  }
+  __syncthreads();
+  float acc[5];
 #pragma unroll
-      for (int px = 0; px < T; ++px) {
-        const float dx = (x0 + (float)px) - a.x;
-        const float E = __builtin_amdgcn_exp2f(fmaf(dx * a.z, dx, ey));
-        const float4 u = sU[py * T + px];
-        const float ud = sUd[py * T + px];
-        const float w = b.x * E;
-        const float gw = fmaf(ud, z, fmaf(u.z, b.w, fmaf(u.y, b.z, fmaf(u.x, b.y, u.w))));
-        Sc0 = fmaf(w, u.x, Sc0);
-        Sc1 = fmaf(w, u.y, Sc1);
-        Sc2 = fmaf(w, u.z, Sc2);
-        Sz = fmaf(w, ud, Sz);
-        const float Tv = gw * E;
-        rowT += Tv;
-        const float Tx = Tv * dx;
-        Sdx += Tx;
-        Sdx2 = fmaf(Tx, dx, Sdx2);
-      }
-      So += rowT;
-      const float Ty = rowT * dy;
-      Sdy += Ty;
-      Sdy2 = fmaf(Ty, dy, Sdy2);
+  for (int c = 0; c < 5; ++c)
+    acc[c] = ((smem[0 * 5 * TP + c * TP + tid] + smem[1 * 5 * TP + c * TP + tid]) + smem[2 * 5 * TP + c * TP + tid]) +
+             smem[3 * 5 * TP + c * TP + tid];
+  const int2 rg = ranges[tile];
+  if (rg.y - rg.x > CH) {  // tile split over several items: combine in k_fwd_finalize
+    float* dst = fwd_part + (size_t)item * 5 * TP;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) dst[c * TP + tid] = acc[c];
+    return;
+  }
+  const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
+  if (x >= v.W || y >= v.H) return;
+  const int p = y * v.W + x;
+  const float aW = acc[0], den = 1.0f + aW;
+  out_rgb[3 * p + 0] = clamp01((v.bg[0] + acc[1]) / den);
+  out_rgb[3 * p + 1] = clamp01((v.bg[1] + acc[2]) / den);
+  out_rgb[3 * p + 2] = clamp01((v.bg[2] + acc[3]) / den);
+  if (out_alpha) out_alpha[p] = clamp01(aW / den);
+  if (out_depth) {
+    const float d = acc[4] / (aW + 1e-6f);
+    out_depth[p] = d < 0.0f ? 0.0f : d;
+  }
+  saved4[p] = make_float4(aW, acc[1], acc[2], acc[3]);
+  savedD[p] = acc[4];
+}
+
+// Tiles with no Gaussians (background) or split over several work items: sum the items' partial
+// accumulators in chunk order (deterministic) and write the outputs.
+__global__ __launch_bounds__(256) void k_fwd_finalize(ViewK v, const int2* __restrict__ ranges,
+                                                      const int* __restrict__ tile_item0, const float* __restrict__ fwd_part,
+                                                      float* __restrict__ out_rgb, float* __restrict__ out_alpha,
+                                                      float* __restrict__ out_depth, float4* __restrict__ saved4,
+                                                      float* __restrict__ savedD) {
+  const int tile = blockIdx.x, tid = threadIdx.x;
+  const int2 rg = ranges[tile];
+  const int nch = (rg.y - rg.x + CH - 1) / CH;
+  if (nch == 1) return;  // written by k_raster_fwd_mfma
+  float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  const float* src = fwd_part + (size_t)(nch > 0 ? tile_item0[tile] : 0) * 5 * TP;
+  for (int c = 0; c < nch; ++c)
+#pragma unroll
+    for (int q = 0; q < 5; ++q) acc[q] += src[(size_t)c * 5 * TP + q * TP + tid];
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
+  if (x >= v.W || y >= v.H) return;
+  const int p = y * v.W + x;
+  const float aW = acc[0], den = 1.0f + aW;
+  out_rgb[3 * p + 0] = clamp01((v.bg[0] + acc[1]) / den);
+  out_rgb[3 * p + 1] = clamp01((v.bg[1] + acc[2]) / den);
+  out_rgb[3 * p + 2] = clamp01((v.bg[2] + acc[3]) / den);
+  if (out_alpha) out_alpha[p] = clamp01(aW / den);
+  if (out_depth) {
+    const float d = acc[4] / (aW + 1e-6f);
+    out_depth[p] = d < 0.0f ? 0.0f : d;
+  }
+  saved4[p] = make_float4(aW, acc[1], acc[2], acc[3]);
+  savedD[p] = acc[4];
+}
+
+// Per-pixel upstream vector U = (dC_r, dC_g, dC_b, dW, dD) of the OIT finalize
+// (torch_renderer.py:192-203), laid out [tile][channel][256] for the backward work items.
+__global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __restrict__ saved4,
+                                                     const float* __restrict__ savedD, const float* __restrict__ g_rgb,
+                                                     const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
+                                                     float* __restrict__ U) {
+  const int tile = blockIdx.x, tid = threadIdx.x;
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
+  float u[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  if (x < v.W && y < v.H) {
+    const int p = y * v.W + x;
+    const float4 s = saved4[p];
+    const float Dp = savedD[p];
+    const float den = 1.0f + s.x, dden = s.x + 1e-6f;
+    float gW = 0.f;
+    const float C[3] = {s.y, s.z, s.w};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float r = (v.bg[k] + C[k]) / den;
+      const float go = (r >= 0.0f && r <= 1.0f) ? g_rgb[3 * p + k] : 0.0f;
+      u[k] = go / den;
+      gW -= go * r / den;
     }
-    const int4 r = rect[g];
-    const int slot = offsets[g] + (ty - r.y) * (r.z - r.x + 1) + (tx - r.x);
-    float* dst = partials + (size_t)slot * NPART;
-    dst[0] = Sc0;
-    dst[1] = Sc1;
-    dst[2] = Sc2;
-    dst[3] = Sz;
-    dst[4] = So;
-    dst[5] = Sdx;
-    dst[6] = Sdy;
-    dst[7] = Sdx2;
-    dst[8] = Sdy2;
+    if (g_alpha) {
+      const float al = s.x / den;
+      if (al >= 0.0f && al <= 1.0f) gW += g_alpha[p] / (den * den);
+    }
+    if (g_depth) {
+      const float d = Dp / dden;
+      if (d >= 0.0f) {
+        const float gd = g_depth[p];
+        gW -= gd * Dp / (dden * dden);
+        u[4] = gd / dden;
+      }
+    }
+    u[3] = gW;
+  }
+  float* dst = U + (size_t)tile * 5 * TP;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) dst[k * TP + tid] = u[k];
+}
+
+// Backward: one workgroup (4 waves) per work item.  A = U_k^T (tile-constant, 20 registers per
+// lane), B = f(x) ex_g(x) for 16 Gaussians on the MFMA columns; wave w takes groups [4w, 4w+4) of
+// each staged batch of 256 Gaussians.  Partials per pair (9 floats) go to the pair's slot
+// (Gaussian offset + tile index inside its rectangle), so k_reduce_bwd reads them contiguously.
+__global__ __launch_bounds__(256) void k_raster_bwd_mfma(ViewK v, const int4* __restrict__ items,
+                                                         const int* __restrict__ num_items, const int* __restrict__ ids,
+                                                         const float4* __restrict__ recA, const float4* __restrict__ recB,
+                                                         const float* __restrict__ recZ, const int4* __restrict__ rect,
+                                                         const int* __restrict__ offsets, const float* __restrict__ U,
+                                                         float* __restrict__ partials) {
+  __shared__ __attribute__((aligned(16))) float4 sA[TP];
+  __shared__ __attribute__((aligned(16))) float4 sB[TP];
+  __shared__ float sZ[TP];
+  __shared__ int sSlot[TP];
+  const int item = blockIdx.x;
+  if (item >= *num_items) return;
+  const int4 it = items[item];
+  const int tile = it.x, k0 = it.y, k1 = it.z;
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int li = lane & 15, xs = lane >> 4;
+  float A[5][4];
+  {
+    const float* Ut = U + (size_t)tile * 5 * TP;
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) A[k][s] = Ut[k * TP + li * T + 4 * s + xs];
+  }
+  const float x0 = (float)(tx * T) + 0.5f, y0 = (float)(ty * T) + 0.5f;
+  StageRec st = stage_load(k0 + tid, k1, ids, recA, recB, recZ);
+  int slot = -1;
+  if (st.g >= 0) {
+    const int4 r = rect[st.g];
+    slot = offsets[st.g] + (ty - r.y) * (r.z - r.x + 1) + (tx - r.x);
+  }
+  for (int base = k0; base < k1; base += TP) {
+    __syncthreads();
+    sA[tid] = st.a;
+    sB[tid] = st.b;
+    sZ[tid] = st.z;
+    sSlot[tid] = slot;
+    __syncthreads();
+    st = stage_load(base + TP + tid, k1, ids, recA, recB, recZ);
+    slot = -1;
+    if (st.g >= 0) {
+      const int4 r = rect[st.g];
+      slot = offsets[st.g] + (ty - r.y) * (r.z - r.x + 1) + (tx - r.x);
+    }
+    const int cnt = min(TP, k1 - base) - wave * 64;
+    const int ngr = cnt <= 0 ? 0 : min(4, (cnt + 15) >> 4);
+    for (int gi = 0; gi < ngr; ++gi) {
+      const int j = wave * 64 + gi * 16 + li;
+      const float4 a = sA[j];
+      const float4 b = sB[j];
+      const float z = sZ[j];
+      const int myslot = sSlot[j];
+      const bool valid = myslot >= 0;
+      const float vv[5] = {b.y, b.z, b.w, 1.0f, z};
+      f32x4 D1[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) D1[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 Ddx = {0.f, 0.f, 0.f, 0.f}, Ddx2 = Ddx;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const float dx = (x0 + (float)(4 * s + xs)) - a.x;
+        const float ex = valid ? __builtin_amdgcn_exp2f(dx * a.z * dx) : 0.0f;
+        const float edx = ex * dx, edx2 = edx * dx;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) D1[k] = mfma4(A[k][s], ex, D1[k]);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) Ddx = mfma4(A[k][s], vv[k] * edx, Ddx);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) Ddx2 = mfma4(A[k][s], vv[k] * edx2, Ddx2);
+      }
+      // lane holds D[y = 4*xs + r][g = li]
+      float S[NPART] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float dy = (y0 + (float)(4 * xs + r)) - a.y;
+        const float ey = __builtin_amdgcn_exp2f(dy * a.w * dy);
+        S[0] = fmaf(ey, D1[0][r], S[0]);
+        S[1] = fmaf(ey, D1[1][r], S[1]);
+        S[2] = fmaf(ey, D1[2][r], S[2]);
+        S[3] = fmaf(ey, D1[4][r], S[3]);
+        const float G1 = fmaf(z, D1[4][r], fmaf(vv[2], D1[2][r], fmaf(vv[1], D1[1][r], fmaf(vv[0], D1[0][r], D1[3][r]))));
+        const float t = ey * G1;
+        S[4] += t;
+        const float tdy = t * dy;
+        S[6] += tdy;
+        S[8] = fmaf(tdy, dy, S[8]);
+        S[5] = fmaf(ey, Ddx[r], S[5]);
+        S[7] = fmaf(ey, Ddx2[r], S[7]);
+      }
+#pragma unroll
+      for (int q = 0; q < NPART; ++q) {
+        S[q] += __shfl_xor(S[q], 16);
+        S[q] += __shfl_xor(S[q], 32);
+      }
+      if (valid && xs == 0) {
+        float* dst = partials + (size_t)myslot * NPART;
+        dst[0] = b.x * S[0];
+        dst[1] = b.x * S[1];
+        dst[2] = b.x * S[2];
+        dst[3] = b.x * S[3];
+        dst[4] = S[4];
+        dst[5] = S[5];
+        dst[6] = S[6];
+        dst[7] = S[7];
+        dst[8] = S[8];
+      }
+    }
   }
 }
 
@@ -749,7 +947,7 @@ void gr_geom_layout(int n, size_t offsets_out[6]) { geom_fixed(n, offsets_out); 
 
 void gr_bins_layout(const gr_view* v, int n, int64_t num_pairs, size_t offsets_out[3]) {
   (void)n;
-  size_t off[5];
+  size_t off[9];
   bins_fixed(tiles_x_of(v->width) * tiles_y_of(v->height), num_pairs, off);
   offsets_out[0] = off[0];
   offsets_out[1] = off[1];
@@ -766,13 +964,15 @@ size_t gr_saved_floats(const gr_view* v) { return (size_t)5 * v->width * v->heig
 size_t gr_bins_bytes(const gr_view* v, int n, int64_t num_pairs) {
   (void)n;
   const int tiles = tiles_x_of(v->width) * tiles_y_of(v->height);
-  size_t off[5];
+  size_t off[9];
   return bins_fixed(tiles, num_pairs, off) + align_up(sort_tmp_bytes<uint32_t>(num_pairs, bits_for((uint32_t)tiles)));
 }
 
-size_t gr_bwd_bytes(int n, int64_t num_pairs) {
+// Backward workspace: per-pair partials (K x 9 floats) + per-pixel upstream vectors (tiles x 5 x 256).
+size_t gr_bwd_bytes(const gr_view* v, int n, int64_t num_pairs) {
   (void)n;
-  return align_up((size_t)(num_pairs > 0 ? num_pairs : 1) * NPART * sizeof(float));
+  const size_t tiles = (size_t)tiles_x_of(v->width) * tiles_y_of(v->height);
+  return align_up((size_t)(num_pairs > 0 ? num_pairs : 1) * NPART * sizeof(float)) + align_up(tiles * 5 * TP * sizeof(float));
 }
 
 gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const float* scales, const float* colors,
@@ -831,8 +1031,18 @@ gr_status gr_fwd_render(const gr_view* v, int n, int64_t num_pairs, const void* 
   }
   Geom g = geom_view((void*)geom, n > 0 ? n : 1);
   const size_t HW = (size_t)v->width * v->height;
-  hipLaunchKernelGGL(k_raster_fwd, dim3(tiles), dim3(256), 0, s, vk, b.ranges, b.ids, g.recA, g.recB, g.recZ, out_rgb,
-                     out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
+  hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, tiles, (const int2*)b.ranges, b.items, b.num_items,
+                     b.tile_item0);
+  GR_HIP_TRY(hipGetLastError());
+  const int64_t cap = item_cap(tiles, num_pairs);
+  if (num_pairs > 0) {
+    hipLaunchKernelGGL(k_raster_fwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, (const int4*)b.items,
+                       (const int*)b.num_items, (const int2*)b.ranges, (const int*)b.ids, g.recA, g.recB, g.recZ,
+                       b.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
+    GR_HIP_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_fwd_finalize, dim3(tiles), dim3(256), 0, s, vk, (const int2*)b.ranges, (const int*)b.tile_item0,
+                     (const float*)b.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
   GR_HIP_TRY(hipGetLastError());
   return GR_OK;
 }
@@ -847,7 +1057,7 @@ gr_status gr_bwd(const gr_view* v, int n, int64_t num_pairs, const float* means,
   if (n == 0) return GR_OK;
   if (!g_rgb || !saved || !geom || !bins || !d_means || !d_scales || !d_colors || !d_opacities)
     return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
-  if (num_pairs > 0 && (!ws || ws_bytes < gr_bwd_bytes(n, num_pairs)))
+  if (num_pairs > 0 && (!ws || ws_bytes < gr_bwd_bytes(v, n, num_pairs)))
     return set_error(GR_ERR_WORKSPACE, "backward workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const ViewK vk = make_viewk(v);
@@ -857,8 +1067,14 @@ gr_status gr_bwd(const gr_view* v, int n, int64_t num_pairs, const float* means,
   const size_t HW = (size_t)v->width * v->height;
   float* partials = (float*)ws;
   if (num_pairs > 0) {
-    hipLaunchKernelGGL(k_raster_bwd, dim3(tiles), dim3(256), 0, s, vk, b.ranges, b.ids, g.recA, g.recB, g.recZ, g.rect,
-                       g.offsets, (const float4*)saved, saved + 4 * HW, g_rgb, g_alpha, g_depth, partials);
+    float* U = (float*)((char*)ws + align_up((size_t)num_pairs * NPART * sizeof(float)));
+    hipLaunchKernelGGL(k_pixel_grads, dim3(tiles), dim3(256), 0, s, vk, (const float4*)saved, saved + 4 * HW, g_rgb,
+                       g_alpha, g_depth, U);
+    GR_HIP_TRY(hipGetLastError());
+    const int64_t cap = item_cap(tiles, num_pairs);
+    hipLaunchKernelGGL(k_raster_bwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, (const int4*)b.items,
+                       (const int*)b.num_items, (const int*)b.ids, g.recA, g.recB, g.recZ, g.rect, g.offsets,
+                       (const float*)U, partials);
     GR_HIP_TRY(hipGetLastError());
   }
   if (color_dim == 3)

@@ -164,7 +164,7 @@ def backward_native(means, scales, colors, opacities, st: RenderState, g_out, g_
     L = _native.lib()
     dev = means.device
     cd = 3 if colors.dim() == 2 else 12
-    ws = torch.empty((int(L.gr_bwd_bytes(st.n, st.num_pairs)),), dtype=torch.uint8, device=dev)
+    ws = torch.empty((int(L.gr_bwd_bytes(ctypes.byref(st.gv), st.n, st.num_pairs)),), dtype=torch.uint8, device=dev)
     dm = torch.empty_like(means)
     ds = torch.empty_like(scales)
     dc = torch.empty_like(colors)

@@ -68,7 +68,7 @@ typedef struct gr_view {
   float proj[16];      /* Camera.proj, row-major                                          */
   float background[3]; /* background colour (torch_renderer.py:128-130)                    */
   float cam_pos[3];    /* inv(view)[:3,3] (torch_renderer.py:81-83); used by SH colours    */
-  float cutoff;        /* screen footprint half-width in sigmas used for binning (def. 5)  */
+  float cutoff;        /* screen footprint half-width in sigmas used for binning (def. 6)  */
 } gr_view;
 
 /* ------------------------------------------------------------------------------------------ */
@@ -98,8 +98,8 @@ gr_status gr_fwd_render(const gr_view* v, int n, int64_t num_pairs, const void* 
                         size_t bins_bytes, float* out_rgb, float* out_alpha, float* out_depth,
                         float* saved, void* stream);
 
-/* Backward workspace (per-pair gradient partials). */
-size_t gr_bwd_bytes(int n, int64_t num_pairs);
+/* Backward workspace: per-pair gradient partials + per-pixel upstream vectors. */
+size_t gr_bwd_bytes(const gr_view* v, int n, int64_t num_pairs);
 
 /* Backward of gr_fwd_render.  g_rgb (H,W,3) required; g_alpha, g_depth may be NULL (zero).
  * Writes (overwrites) d_means (N,3), d_scales (N,3) (column 2 is always 0),
