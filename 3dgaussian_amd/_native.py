@@ -72,13 +72,17 @@ _SIG = {
                                       ctypes.POINTER(ctypes.c_int64), _P]),
     "gr_bins_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, ctypes.c_int64]),
     "gr_saved_floats": (ctypes.c_size_t, [_VP]),
-    "gr_fwd_render": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int64, _P, _P, ctypes.c_size_t, _P, _P, _P, _P, _P]),
+    "gr_fwd_scratch_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, ctypes.c_int64]),
+    "gr_fwd_render": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int64, _P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P, _P,
+                                     _P, _P, _P]),
     "gr_bwd_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, ctypes.c_int64]),
     "gr_bwd": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int64, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, _P, _P, _P, ctypes.c_size_t, _P]),
     "gr_render_u8": (ctypes.c_int, [ctypes.POINTER(GrRenderParams), ctypes.c_int, _P, _P, _P, _P, _P]),
     "gr_geom_layout": (None, [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
     "gr_bins_layout": (None, [_VP, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_size_t)]),
+    "gr_profile_begin": (None, []),
+    "gr_profile_end": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
     "gr_last_error": (ctypes.c_char_p, []),
     "gr_version": (ctypes.c_char_p, []),
 }
@@ -123,6 +127,18 @@ def ptr(t) -> ctypes.c_void_p:
     if t is None:
         return ctypes.c_void_p(0)
     return ctypes.c_void_p(t.data_ptr())
+
+
+def profile_begin() -> None:
+    lib().gr_profile_begin()
+
+
+def profile_end():
+    """Returns {"raster_fwd": (total_ms, launches), "raster_bwd": (total_ms, launches)}."""
+    ms = (ctypes.c_double * 2)()
+    n = (ctypes.c_int * 2)()
+    check(lib().gr_profile_end(ms, n), "gr_profile_end")
+    return {"raster_fwd": (ms[0], n[0]), "raster_bwd": (ms[1], n[1])}
 
 
 def version() -> str:

@@ -32,7 +32,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/gr_hip.h"
 
@@ -215,22 +217,27 @@ Geom geom_view(void* base, int n) {
 constexpr int CH = 1024;  // Gaussians per raster work item (one chunk of one tile's list)
 constexpr int NPART = 9;  // backward partial sums per (Gaussian, tile) pair
 
+// Persistent binning state (kept from forward to backward).
 struct Bins {
-  uint32_t* keys;      // sorted keys (K)
-  int* ids;            // sorted gaussian ids (K)
+  uint32_t* keys;      // [K] sorted keys (tile id)
+  int* ids;            // [K] sorted gaussian ids
   int2* ranges;        // [tiles] pair range of each tile
   int4* items;         // [cap] work items (tile, k0, k1, chunk)
   int* num_items;      // [1]
   int* tile_item0;     // [tiles] first work item of each tile
-  float* fwd_part;     // [cap][5][256] forward partial accumulators (tiles split over several items)
-  uint32_t* keys_in;   // K
-  int* ids_in;         // K
+};
+
+// Forward-only scratch (freed by the caller after gr_fwd_render).
+struct Scratch {
+  uint32_t* keys_in;   // [K]
+  int* ids_in;         // [K]
+  float* fwd_part;     // [cap][5][256] partial accumulators of tiles split over several items
   void* sort_tmp;
 };
 
 inline int64_t item_cap(int tiles, int64_t K) { return (K + CH - 1) / CH + tiles; }
 
-size_t bins_fixed(int tiles, int64_t K, size_t off[9]) {
+size_t bins_fixed(int tiles, int64_t K, size_t off[6]) {
   const size_t kk = (size_t)(K > 0 ? K : 1);
   const size_t cap = (size_t)item_cap(tiles, K);
   size_t o = 0;
@@ -240,9 +247,16 @@ size_t bins_fixed(int tiles, int64_t K, size_t off[9]) {
   off[3] = o; o = align_up(o + cap * sizeof(int4));
   off[4] = o; o = align_up(o + sizeof(int));
   off[5] = o; o = align_up(o + (size_t)tiles * sizeof(int));
-  off[6] = o; o = align_up(o + cap * 5 * TP * sizeof(float));
-  off[7] = o; o = align_up(o + kk * sizeof(uint32_t));
-  off[8] = o; o = align_up(o + kk * sizeof(int));
+  return o;
+}
+
+size_t scratch_fixed(int tiles, int64_t K, size_t off[3]) {
+  const size_t kk = (size_t)(K > 0 ? K : 1);
+  const size_t cap = (size_t)item_cap(tiles, K);
+  size_t o = 0;
+  off[0] = o; o = align_up(o + kk * sizeof(uint32_t));
+  off[1] = o; o = align_up(o + kk * sizeof(int));
+  off[2] = o; o = align_up(o + cap * 5 * TP * sizeof(float));
   return o;
 }
 
@@ -255,8 +269,8 @@ size_t sort_tmp_bytes(int64_t K, int bits) {
 }
 
 Bins bins_view(void* base, int tiles, int64_t K) {
-  size_t off[9];
-  const size_t fixed = bins_fixed(tiles, K, off);
+  size_t off[6];
+  bins_fixed(tiles, K, off);
   char* b = (char*)base;
   Bins r;
   r.keys = (uint32_t*)(b + off[0]);
@@ -265,9 +279,17 @@ Bins bins_view(void* base, int tiles, int64_t K) {
   r.items = (int4*)(b + off[3]);
   r.num_items = (int*)(b + off[4]);
   r.tile_item0 = (int*)(b + off[5]);
-  r.fwd_part = (float*)(b + off[6]);
-  r.keys_in = (uint32_t*)(b + off[7]);
-  r.ids_in = (int*)(b + off[8]);
+  return r;
+}
+
+Scratch scratch_view(void* base, int tiles, int64_t K) {
+  size_t off[3];
+  const size_t fixed = scratch_fixed(tiles, K, off);
+  char* b = (char*)base;
+  Scratch r;
+  r.keys_in = (uint32_t*)(b + off[0]);
+  r.ids_in = (int*)(b + off[1]);
+  r.fwd_part = (float*)(b + off[2]);
   r.sort_tmp = b + fixed;
   return r;
 }
@@ -924,6 +946,29 @@ __global__ __launch_bounds__(256) void k_patch_depth(int64_t K, uint64_t* keys, 
   if (k < K) keys[k] |= (uint64_t)dk[ids[k]];
 }
 
+// Optional per-kernel timing with HIP events on the launch stream (gr_profile_begin/end), used by
+// bench.py to time the dominant kernels live.  Off by default; host-side state only.
+enum { PROF_RASTER_FWD = 0, PROF_RASTER_BWD = 1, PROF_SLOTS = 2 };
+struct ProfSlot {
+  std::vector<hipEvent_t> ev;
+  size_t used = 0;
+};
+std::mutex g_prof_mu;
+bool g_prof_on = false;
+ProfSlot g_prof[PROF_SLOTS];
+
+void prof_mark(int which, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  if (!g_prof_on) return;
+  ProfSlot& sl = g_prof[which];
+  if (sl.used == sl.ev.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    sl.ev.push_back(e);
+  }
+  (void)hipEventRecord(sl.ev[sl.used++], s);
+}
+
 inline int blocks_for(int64_t n, int bs = 256) { return (int)((n + bs - 1) / bs); }
 
 gr_status check_view(const gr_view* v) {
@@ -941,13 +986,40 @@ gr_status check_view(const gr_view* v) {
 extern "C" {
 
 const char* gr_last_error(void) { return g_last_error.c_str(); }
+
+void gr_profile_begin(void) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof_on = true;
+  for (auto& sl : g_prof) sl.used = 0;
+}
+
+gr_status gr_profile_end(double total_ms[2], int launches[2]) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof_on = false;
+  for (int k = 0; k < PROF_SLOTS; ++k) {
+    ProfSlot& sl = g_prof[k];
+    double tot = 0.0;
+    int cnt = 0;
+    for (size_t i = 0; i + 1 < sl.used; i += 2) {
+      GR_HIP_TRY(hipEventSynchronize(sl.ev[i + 1]));
+      float ms = 0.f;
+      GR_HIP_TRY(hipEventElapsedTime(&ms, sl.ev[i], sl.ev[i + 1]));
+      tot += ms;
+      ++cnt;
+    }
+    total_ms[k] = tot;
+    launches[k] = cnt;
+    sl.used = 0;
+  }
+  return GR_OK;
+}
 const char* gr_version(void) { return GR_VERSION_STR; }
 
 void gr_geom_layout(int n, size_t offsets_out[6]) { geom_fixed(n, offsets_out); }
 
 void gr_bins_layout(const gr_view* v, int n, int64_t num_pairs, size_t offsets_out[3]) {
   (void)n;
-  size_t off[9];
+  size_t off[6];
   bins_fixed(tiles_x_of(v->width) * tiles_y_of(v->height), num_pairs, off);
   offsets_out[0] = off[0];
   offsets_out[1] = off[1];
@@ -964,8 +1036,15 @@ size_t gr_saved_floats(const gr_view* v) { return (size_t)5 * v->width * v->heig
 size_t gr_bins_bytes(const gr_view* v, int n, int64_t num_pairs) {
   (void)n;
   const int tiles = tiles_x_of(v->width) * tiles_y_of(v->height);
-  size_t off[9];
-  return bins_fixed(tiles, num_pairs, off) + align_up(sort_tmp_bytes<uint32_t>(num_pairs, bits_for((uint32_t)tiles)));
+  size_t off[6];
+  return bins_fixed(tiles, num_pairs, off);
+}
+
+size_t gr_fwd_scratch_bytes(const gr_view* v, int n, int64_t num_pairs) {
+  (void)n;
+  const int tiles = tiles_x_of(v->width) * tiles_y_of(v->height);
+  size_t off[3];
+  return scratch_fixed(tiles, num_pairs, off) + align_up(sort_tmp_bytes<uint32_t>(num_pairs, bits_for((uint32_t)tiles)));
 }
 
 // Backward workspace: per-pair partials (K x 9 floats) + per-pixel upstream vectors (tiles x 5 x 256).
@@ -1006,25 +1085,29 @@ gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const floa
 }
 
 gr_status gr_fwd_render(const gr_view* v, int n, int64_t num_pairs, const void* geom, void* bins, size_t bins_bytes,
-                        float* out_rgb, float* out_alpha, float* out_depth, float* saved, void* stream) {
+                        void* scratch, size_t scratch_bytes, float* out_rgb, float* out_alpha, float* out_depth,
+                        float* saved, void* stream) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
   if (!out_rgb || !saved) return set_error(GR_ERR_INVALID_ARGUMENT, "out_rgb and saved are required");
   if (n > 0 && (!geom || !bins)) return set_error(GR_ERR_INVALID_ARGUMENT, "null workspace");
   if (bins_bytes < gr_bins_bytes(v, n, num_pairs)) return set_error(GR_ERR_WORKSPACE, "bins workspace too small");
+  if (scratch_bytes < gr_fwd_scratch_bytes(v, n, num_pairs) || !scratch)
+    return set_error(GR_ERR_WORKSPACE, "forward scratch workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const ViewK vk = make_viewk(v);
   const int tiles = vk.tiles_x * vk.tiles_y;
   Bins b = bins_view(bins, tiles, num_pairs);
+  Scratch sc = scratch_view(scratch, tiles, num_pairs);
   GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * tiles, s));
   if (n > 0 && num_pairs > 0) {
     Geom g = geom_view((void*)geom, n);
     hipLaunchKernelGGL(k_emit<uint32_t>, dim3(blocks_for(n)), dim3(256), 0, s, n, vk.tiles_x, g.rect, g.counts, g.offsets,
-                       (const uint32_t*)nullptr, b.keys_in, b.ids_in);
+                       (const uint32_t*)nullptr, sc.keys_in, sc.ids_in);
     GR_HIP_TRY(hipGetLastError());
     const int bits = bits_for((uint32_t)tiles);
     size_t tmp = sort_tmp_bytes<uint32_t>(num_pairs, bits);
-    GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, tmp, b.keys_in, b.keys, b.ids_in, b.ids, (int)num_pairs, 0,
+    GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp, tmp, sc.keys_in, b.keys, sc.ids_in, b.ids, (int)num_pairs, 0,
                                                   bits, s));
     hipLaunchKernelGGL(k_ranges<uint32_t>, dim3(blocks_for(num_pairs)), dim3(256), 0, s, num_pairs, b.keys, b.ranges);
     GR_HIP_TRY(hipGetLastError());
@@ -1036,13 +1119,15 @@ gr_status gr_fwd_render(const gr_view* v, int n, int64_t num_pairs, const void* 
   GR_HIP_TRY(hipGetLastError());
   const int64_t cap = item_cap(tiles, num_pairs);
   if (num_pairs > 0) {
+    prof_mark(PROF_RASTER_FWD, s);
     hipLaunchKernelGGL(k_raster_fwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, (const int4*)b.items,
                        (const int*)b.num_items, (const int2*)b.ranges, (const int*)b.ids, g.recA, g.recB, g.recZ,
-                       b.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
+                       sc.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
     GR_HIP_TRY(hipGetLastError());
+    prof_mark(PROF_RASTER_FWD, s);
   }
   hipLaunchKernelGGL(k_fwd_finalize, dim3(tiles), dim3(256), 0, s, vk, (const int2*)b.ranges, (const int*)b.tile_item0,
-                     (const float*)b.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
+                     (const float*)sc.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
   GR_HIP_TRY(hipGetLastError());
   return GR_OK;
 }
@@ -1072,10 +1157,12 @@ gr_status gr_bwd(const gr_view* v, int n, int64_t num_pairs, const float* means,
                        g_alpha, g_depth, U);
     GR_HIP_TRY(hipGetLastError());
     const int64_t cap = item_cap(tiles, num_pairs);
+    prof_mark(PROF_RASTER_BWD, s);
     hipLaunchKernelGGL(k_raster_bwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, (const int4*)b.items,
                        (const int*)b.num_items, (const int*)b.ids, g.recA, g.recB, g.recZ, g.rect, g.offsets,
                        (const float*)U, partials);
     GR_HIP_TRY(hipGetLastError());
+    prof_mark(PROF_RASTER_BWD, s);
   }
   if (color_dim == 3)
     hipLaunchKernelGGL(k_reduce_bwd<3>, dim3(blocks_for(n)), dim3(256), 0, s, vk, n, means, scales, colors, opacities,

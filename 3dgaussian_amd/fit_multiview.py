@@ -1,0 +1,335 @@
+"""View-sharded data-parallel multiview fitting on MI355X (one process per GPU, RCCL over xGMI).
+
+The math of one iteration is the reference fit loop's (python/fit_multiview_stub.py:265-325):
+activations (:268-275), per-view render + L1 / silhouette / depth losses (:277-305), loss =
+sum / V + regularisers (:307-308), backward (:310), Adam (:311), densify/prune every interval with
+an Adam reset (:318-325).  What changes is where it runs:
+
+* rank r renders views i = r, r+R, r+2R, ... (R ranks) with the HIP render op and computes
+  sum_{i in r} loss_i / V (the regulariser is added on rank 0 only);
+* one all_reduce(SUM) of a flat fp32 buffer of every parameter gradient (10 floats per Gaussian
+  RGB, 19 with SH degree 1) makes every rank hold the full-loss gradient, so the Adam steps are
+  identical on all ranks (up to summation order of the collective);
+* densify/prune is decided on rank 0 with the host RNG and broadcast, so parameters stay equal.
+
+Random initialisation and densify jitter are drawn from torch's CPU generator in the same order as
+the stub (torch.rand for means, then colours; torch.randn_like for jitter), so a seeded run
+reproduces the stub's parameters exactly before the first step.
+
+Run single-GPU:   python 3dgaussian_amd/fit_multiview.py --targets_dir DIR [stub flags]
+Run on 8 GPUs:    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+                      3dgaussian_amd/fit_multiview.py --targets_dir DIR [stub flags]
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import sys
+from pathlib import Path
+from typing import Callable, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+if __package__ in (None, ""):
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import torch_renderer as tr  # type: ignore
+else:
+    from . import torch_renderer as tr
+
+RenderFn = Callable[..., tuple]
+
+
+# ------------------------------------------------------------------------------------------------
+# Parameters (fit_multiview_stub.py:114-137) — CPU RNG, then moved to the device.
+# ------------------------------------------------------------------------------------------------
+def build_params(n: int, device: torch.device, use_sh: bool) -> dict:
+    means = (torch.rand((n, 3)) - 0.5) * 1.2
+    scales_raw = torch.full((n, 3), -2.2)
+    opacities_raw = torch.full((n,), -2.2)
+    params = {"means": means, "scales_raw": scales_raw, "opacities_raw": opacities_raw}
+    if use_sh:
+        sh = torch.zeros((n, 4, 3))
+        sh[:, 0, :] = 0.1 * torch.rand((n, 3))
+        params["sh_raw"] = sh
+    else:
+        params["colors_raw"] = 0.1 * torch.rand((n, 3))
+    return {k: torch.nn.Parameter(v.to(device)) for k, v in params.items()}
+
+
+def activations(params: dict):
+    """fit_multiview_stub.py:268-275."""
+    means = params["means"]
+    scales = torch.nn.functional.softplus(params["scales_raw"]) + 1e-3
+    opacities = torch.sigmoid(params["opacities_raw"])
+    colors = params["sh_raw"] if "sh_raw" in params else torch.sigmoid(params["colors_raw"])
+    return means, scales, colors, opacities
+
+
+def densify_and_prune(params: dict, max_gaussians: int, densify_ratio: float, prune_opacity: float) -> dict:
+    """fit_multiview_stub.py:140-197, evaluated on the host (CPU RNG for the jitter) so that every
+    rank that calls it with the same RNG state gets identical parameters."""
+    with torch.no_grad():
+        cpu = {k: v.detach().cpu() for k, v in params.items()}
+        means, scales_raw, op_raw = cpu["means"], cpu["scales_raw"], cpu["opacities_raw"]
+        op = torch.sigmoid(op_raw)
+        scales = torch.nn.functional.softplus(scales_raw) + 1e-3
+        keep = op > prune_opacity
+        if int(keep.sum()) < 64:
+            top_keep = torch.topk(op, k=min(64, op.shape[0]), largest=True).indices
+            keep = torch.zeros_like(keep, dtype=torch.bool)
+            keep[top_keep] = True
+        means, scales_raw, op_raw, scales = means[keep], scales_raw[keep], op_raw[keep], scales[keep]
+        op = torch.sigmoid(op_raw)
+        n = means.shape[0]
+        room = max(0, max_gaussians - n)
+        add_n = min(room, max(0, int(n * densify_ratio)))
+        if add_n > 0 and n > 0:
+            idx = torch.topk(op, k=min(n, add_n), largest=True).indices
+            jitter = 0.25 * scales[idx] * torch.randn_like(means[idx])
+            means = torch.cat([means, means[idx] + jitter], dim=0)
+            scales_raw = torch.cat([scales_raw, scales_raw[idx]], dim=0)
+            op_raw = torch.cat([op_raw, op_raw[idx] - 0.1], dim=0)
+        out = {"means": means, "scales_raw": scales_raw, "opacities_raw": op_raw}
+        key = "sh_raw" if "sh_raw" in cpu else "colors_raw"
+        col = cpu[key][keep]
+        if add_n > 0 and col.shape[0] > 0:
+            base_n = col.shape[0]
+            idx = torch.topk(torch.sigmoid(op_raw[:base_n]), k=min(base_n, add_n), largest=True).indices
+            col = torch.cat([col, col[idx]], dim=0)
+        out[key] = col
+    device = params["means"].device
+    return {k: torch.nn.Parameter(v.to(device)) for k, v in out.items()}
+
+
+def hip_render(means, scales, colors, opacities, cam, width, height, background):
+    return tr.render_gaussians_torch(means, scales, colors, opacities, cam, width=width, height=height,
+                                     background=background, max_gaussians=max(10000, int(means.shape[0])), return_aux=True)
+
+
+class ViewShardedFitter:
+    """One fit iteration = render own views, backward, one gradient all-reduce, Adam."""
+
+    def __init__(self, params: dict, cams: list, targets: list, width: int, height: int, lr: float = 0.02,
+                 masks: Optional[list] = None, depths: Optional[list] = None, silhouette_weight: float = 0.2,
+                 depth_weight: float = 0.05, reg_opacity: float = 1e-3, reg_scale: float = 1e-3,
+                 render_fn: RenderFn = hip_render, group=None):
+        self.params = params
+        self.cams, self.targets, self.masks, self.depths = cams, targets, masks, depths
+        self.width, self.height, self.lr = width, height, lr
+        self.w_sil, self.w_depth = silhouette_weight, depth_weight
+        self.reg_opacity, self.reg_scale = reg_opacity, reg_scale
+        self.render_fn = render_fn
+        self.group = group
+        self.distributed = dist.is_available() and dist.is_initialized()
+        self.rank = dist.get_rank(group) if self.distributed else 0
+        self.world = dist.get_world_size(group) if self.distributed else 1
+        self.my_views = list(range(self.rank, len(targets), self.world))
+        self.opt = torch.optim.Adam(list(self.params.values()), lr=lr)
+
+    def reset_optimizer(self) -> None:
+        self.opt = torch.optim.Adam(list(self.params.values()), lr=self.lr)
+
+    def view_loss(self, i: int, means, scales, colors, opacities) -> torch.Tensor:
+        device = means.device
+        pred, alpha, depth = self.render_fn(means, scales, colors, opacities, self.cams[i], self.width, self.height,
+                                            torch.zeros(3, device=device))
+        loss = torch.mean(torch.abs(pred - self.targets[i]))
+        if self.masks is not None and self.w_sil > 0.0:
+            loss = loss + self.w_sil * torch.mean(torch.abs(alpha - self.masks[i]))
+        if self.depths is not None and self.w_depth > 0.0:
+            d_pred = depth / (depth.max() + 1e-6)
+            loss = loss + self.w_depth * torch.mean(torch.abs(d_pred - self.depths[i]))
+        return loss
+
+    def step(self) -> torch.Tensor:
+        """One iteration; returns the full (all-rank) loss as a 0-d tensor on the device."""
+        self.opt.zero_grad(set_to_none=True)
+        means, scales, colors, opacities = activations(self.params)
+        device = means.device
+        total = torch.zeros((), device=device)
+        for i in self.my_views:
+            total = total + self.view_loss(i, means, scales, colors, opacities)
+        loss = total / len(self.targets)
+        if self.rank == 0:
+            loss = loss + self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean()
+        loss.backward()
+        plist = list(self.params.values())
+        for p in plist:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        if self.world > 1:
+            flat = torch.cat([p.grad.reshape(-1) for p in plist] + [loss.detach().reshape(1)])
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+            off = 0
+            for p in plist:
+                k = p.numel()
+                p.grad.copy_(flat[off:off + k].view_as(p))
+                off += k
+            loss_all = flat[off]
+        else:
+            loss_all = loss.detach()
+        self.opt.step()
+        return loss_all
+
+    def densify_and_prune(self, max_gaussians: int, densify_ratio: float, prune_opacity: float) -> None:
+        if self.world > 1:
+            # rank 0 decides (host RNG), everyone receives the new tensors
+            if self.rank == 0:
+                newp = densify_and_prune(self.params, max_gaussians, densify_ratio, prune_opacity)
+                n = torch.tensor([newp["means"].shape[0]], device=self.params["means"].device)
+            else:
+                n = torch.zeros(1, dtype=torch.int64, device=self.params["means"].device)
+            dist.broadcast(n, 0, group=self.group)
+            if self.rank != 0:
+                newp = {k: torch.nn.Parameter(torch.empty((int(n.item()),) + tuple(v.shape[1:]), device=v.device))
+                        for k, v in self.params.items()}
+            for k in sorted(newp):
+                dist.broadcast(newp[k].data, 0, group=self.group)
+            self.params = newp
+        else:
+            self.params = densify_and_prune(self.params, max_gaussians, densify_ratio, prune_opacity)
+        self.reset_optimizer()
+
+
+# ------------------------------------------------------------------------------------------------
+# CLI: same flags as fit_multiview_stub.py:200-229.
+# ------------------------------------------------------------------------------------------------
+def _load_image(path: Path, width: int, height: int, gray: bool = False) -> np.ndarray:
+    from PIL import Image
+
+    img = Image.open(path).convert("L" if gray else "RGB").resize((width, height), Image.Resampling.BILINEAR)
+    return np.asarray(img, dtype=np.float32) / 255.0
+
+
+def orbit_cameras(num_views: int, width: int, height: int, device) -> list:
+    """fit_multiview_stub.py:70-90."""
+    proj = tr.perspective(60.0, width / height, 0.01, 100.0, device=device)
+    target = torch.tensor([0.0, 0.0, 0.0], dtype=torch.float32, device=device)
+    up = torch.tensor([0.0, 1.0, 0.0], dtype=torch.float32, device=device)
+    cams = []
+    for i in range(num_views):
+        yaw = (2.0 * math.pi * i) / max(1, num_views)
+        eye = torch.tensor([2.5 * math.cos(0.2) * math.sin(yaw), 2.5 * math.sin(0.2), 2.5 * math.cos(0.2) * math.cos(yaw)],
+                           dtype=torch.float32, device=device)
+        cams.append(tr.Camera(view=tr.look_at(eye, target, up), proj=proj))
+    return cams
+
+
+def main(argv=None) -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--targets_dir", required=True)
+    ap.add_argument("--out_dir", default="outputs/fit_multiview_stub")
+    ap.add_argument("--camera_npz", default="")
+    ap.add_argument("--masks_dir", default="")
+    ap.add_argument("--depth_dir", default="")
+    ap.add_argument("--iters", type=int, default=300)
+    ap.add_argument("--lr", type=float, default=0.02)
+    ap.add_argument("--width", type=int, default=128)
+    ap.add_argument("--height", type=int, default=128)
+    ap.add_argument("--num_gaussians", type=int, default=800)
+    ap.add_argument("--max_gaussians", type=int, default=3000)
+    ap.add_argument("--use_sh", action="store_true")
+    ap.add_argument("--densify_interval", type=int, default=80)
+    ap.add_argument("--prune_interval", type=int, default=80)
+    ap.add_argument("--densify_ratio", type=float, default=0.15)
+    ap.add_argument("--prune_opacity", type=float, default=0.05)
+    ap.add_argument("--silhouette_weight", type=float, default=0.2)
+    ap.add_argument("--mask_thresh", type=float, default=0.06)
+    ap.add_argument("--depth_weight", type=float, default=0.05)
+    ap.add_argument("--reg_opacity", type=float, default=0.001)
+    ap.add_argument("--reg_scale", type=float, default=0.001)
+    ap.add_argument("--seed", type=int, default=None, help="torch.manual_seed before initialisation")
+    args = ap.parse_args(argv)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    rank = dist.get_rank() if world > 1 else 0
+    device = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    if args.seed is not None:
+        torch.manual_seed(args.seed)
+    if rank == 0:
+        print(f"Using device: {device} (ranks: {world})")
+
+    tdir = Path(args.targets_dir)
+    paths = sorted([*tdir.glob("*.png"), *tdir.glob("*.jpg"), *tdir.glob("*.jpeg")])
+    if not paths:
+        raise FileNotFoundError(f"No target images found in {tdir} (supported: png/jpg/jpeg)")
+    targets = [torch.from_numpy(_load_image(p, args.width, args.height)).to(device) for p in paths]
+    masks = None
+    if args.masks_dir:
+        cand = [Path(args.masks_dir) / f"{p.stem}.png" for p in paths]
+        if all(c.exists() for c in cand):
+            masks = [torch.from_numpy(_load_image(c, args.width, args.height, gray=True)).to(device) for c in cand]
+    if masks is None and args.silhouette_weight > 0.0:
+        masks = [(t.mean(dim=2) > args.mask_thresh).to(torch.float32) for t in targets]
+    depths = None
+    if args.depth_dir:
+        cand = [Path(args.depth_dir) / f"{p.stem}.png" for p in paths]
+        if all(c.exists() for c in cand):
+            depths = [torch.from_numpy(_load_image(c, args.width, args.height, gray=True)).to(device) for c in cand]
+    if args.camera_npz:
+        data = np.load(args.camera_npz)
+        if "view" not in data or "proj" not in data:
+            raise KeyError("camera npz must contain arrays: view (V,4,4), proj (V,4,4)")
+        views, projs = np.asarray(data["view"], np.float32), np.asarray(data["proj"], np.float32)
+        if views.shape[0] != len(targets) or projs.shape[0] != len(targets):
+            raise ValueError("camera count mismatch with number of target images")
+        cams = [tr.Camera(view=torch.from_numpy(views[i]).to(device), proj=torch.from_numpy(projs[i]).to(device))
+                for i in range(len(targets))]
+    else:
+        cams = orbit_cameras(len(targets), args.width, args.height, device)
+
+    params = build_params(args.num_gaussians, device, args.use_sh)
+    fitter = ViewShardedFitter(params, cams, targets, args.width, args.height, lr=args.lr, masks=masks, depths=depths,
+                               silhouette_weight=args.silhouette_weight, depth_weight=args.depth_weight,
+                               reg_opacity=args.reg_opacity, reg_scale=args.reg_scale)
+    loss_log = []
+    for it in range(args.iters):
+        lv = float(fitter.step())
+        loss_log.append(lv)
+        if rank == 0 and (it == 0 or (it + 1) % 25 == 0):
+            print(f"iter {it+1:4d}  loss={lv:.6f}  N={fitter.params['means'].shape[0]}")
+        if (it + 1) % args.prune_interval == 0 or (it + 1) % args.densify_interval == 0:
+            fitter.densify_and_prune(args.max_gaussians,
+                                     args.densify_ratio if (it + 1) % args.densify_interval == 0 else 0.0,
+                                     args.prune_opacity)
+    if rank == 0:
+        save_outputs(fitter, cams, args, Path(args.out_dir), loss_log)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def save_outputs(fitter: ViewShardedFitter, cams, args, out_dir: Path, loss_log) -> None:
+    """gaussians_fitted.npz / loss.txt / preview_view0.png exactly as fit_multiview_stub.py:327-380."""
+    from PIL import Image
+
+    out_dir.mkdir(parents=True, exist_ok=True)
+    p = fitter.params
+    means = p["means"]
+    scales = torch.nn.functional.softplus(p["scales_raw"]) + 1e-3
+    opacities = torch.sigmoid(p["opacities_raw"])
+    sh = p.get("sh_raw")
+    colors = sh[:, 0, :].clamp(0.0, 1.0) if sh is not None else torch.sigmoid(p["colors_raw"])
+    arrays = dict(means=means, scales=scales, colors=colors, opacities=opacities)
+    if sh is not None:
+        arrays["sh_coeffs"] = sh
+    np.savez(out_dir / "gaussians_fitted.npz", **{k: v.detach().cpu().numpy().astype(np.float32) for k, v in arrays.items()})
+    (out_dir / "loss.txt").write_text("\n".join(f"{v:.8f}" for v in loss_log), encoding="utf-8")
+    with torch.no_grad():
+        pred0 = tr.render_gaussians_torch(means, scales, sh if sh is not None else colors, opacities, cams[0],
+                                          width=args.width, height=args.height,
+                                          background=torch.tensor([0.0, 0.0, 0.0], device=means.device),
+                                          max_gaussians=max(args.max_gaussians, means.shape[0]), return_aux=False)
+        Image.fromarray((pred0.clamp(0, 1).cpu().numpy() * 255.0).astype(np.uint8), mode="RGB").save(out_dir / "preview_view0.png")
+    print(f"Done. Outputs written to: {out_dir}")
+
+
+if __name__ == "__main__":
+    main()

@@ -153,9 +153,12 @@ def forward_native(means, scales, colors, opacities, gv: _native.GrView):
     alpha = torch.empty((H, W), dtype=torch.float32, device=dev)
     depth = torch.empty((H, W), dtype=torch.float32, device=dev)
     saved = torch.empty((int(L.gr_saved_floats(ctypes.byref(gv))),), dtype=torch.float32, device=dev)
+    # scratch is released when this function returns; the caching allocator keeps it stream-ordered
+    scratch = torch.empty((int(L.gr_fwd_scratch_bytes(ctypes.byref(gv), n, num_pairs)),), dtype=torch.uint8, device=dev)
     _native.check(L.gr_fwd_render(ctypes.byref(gv), n, num_pairs, _native.ptr(geom), _native.ptr(bins), bins.numel(),
-                                  _native.ptr(out), _native.ptr(alpha), _native.ptr(depth), _native.ptr(saved), s),
-                  "gr_fwd_render")
+                                  _native.ptr(scratch), scratch.numel(), _native.ptr(out), _native.ptr(alpha),
+                                  _native.ptr(depth), _native.ptr(saved), s), "gr_fwd_render")
+    del scratch
     return out, alpha, depth, RenderState(gv, n, num_pairs, geom, bins, saved)
 
 

@@ -1,0 +1,186 @@
+"""Benchmark of the MI355X render op on BASELINE.json's headline workload.
+
+Metric: "Mpixels/sec fwd+bwd @1M Gaussians 800x800" (BASELINE.json).  Workload = config C4:
+1M Gaussians, 50 orbit views of 800x800, views sharded across ranks (rank r renders views
+r, r+R, ...), one RCCL all_reduce of the flat gradient buffer per step.
+
+One step = one fit iteration of fit_multiview_stub.py:265-311 over the 50 views: activations, HIP
+forward of this rank's views, L1 + silhouette losses, HIP backward, gradient all-reduce, Adam.
+value = 50 * 800 * 800 * steps / max-over-ranks wall time (whole job, Mpx/s); total work is fixed
+as N grows -> "scaling": "strong".
+
+Synthetic data (no network): means ~ U(-0.6,0.6)^3, opacity sigmoid(-2.2), colours sigmoid(0.1 U),
+density-matched scale 0.1061*(1200/N)^(1/3); targets are seeded random images.
+
+Also reported on rank 0:
+  roofline      the dominant kernel (k_raster_bwd_mfma), timed live with HIP events on its launch
+                stream: algorithmic FLOP per launch (MFMA formulation) / average
+                launch time, against the f32 MFMA dense peak; plus its HBM traffic from rocprofv3
+                PMC counters when profiles/pmc_traffic.json exists (tools/pmc_traffic.py).
+  cpu_baseline  the CPU oracle (oracle/gr_oracle.c, OpenMP) on one view of the same workload.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
+     --master-port P bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+pkg = importlib.import_module("3dgaussian_amd")
+tr = pkg.torch_renderer
+fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+
+F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 (f32-in MFMA) dense peak
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak (spec)
+FLOP_PER_PAIR_BWD = 60 / 16 * 2 * 16 * 16 * 4  # 60 MFMA 16x16x4 per 16 Gaussians per tile
+FLOP_PER_PAIR_FWD = 5 / 4 * 2 * 16 * 16 * 4  # 5 MFMA 16x16x4 per 4 Gaussians per tile
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--gaussians", type=int, default=1_000_000)
+    ap.add_argument("--views", type=int, default=50)
+    ap.add_argument("--res", type=int, default=800)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def synthetic_params(n: int, device) -> dict:
+    g = torch.Generator().manual_seed(0)
+    means = (torch.rand((n, 3), generator=g) - 0.5) * 1.2
+    scale = 0.1061 * (1200.0 / n) ** (1.0 / 3.0)
+    scales_raw = torch.full((n, 3), math.log(math.expm1(scale - 1e-3)))  # softplus^-1(scale - 1e-3)
+    op_raw = torch.full((n,), -2.2)
+    colors_raw = 0.1 * torch.rand((n, 3), generator=g)
+    p = {"means": means, "scales_raw": scales_raw, "opacities_raw": op_raw, "colors_raw": colors_raw}
+    return {k: torch.nn.Parameter(v.to(device)) for k, v in p.items()}
+
+
+def cpu_baseline(n: int, res: int, views: int) -> dict:
+    """Oracle port (float64 accumulation, OpenMP over the host cores) on ONE view of the workload."""
+    from oracle import oracle as orc
+
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    scene = orc.synthetic_scene(n, seed=0)
+    view, proj = orc.orbit_cameras(views, res, res)[0]
+    v = orc.make_view(view, proj, res, res, cutoff=tr.DEFAULT_CUTOFF)
+    g = np.random.default_rng(0).standard_normal((res, res, 3)).astype(np.float32)
+    t0 = time.perf_counter()
+    orc.forward(v, scene, binned=True)
+    orc.backward(v, scene, g, None, None, binned=True)
+    dt = time.perf_counter() - t0
+    return {"value": round(res * res / dt / 1e6, 5), "unit": "Mpixels/sec fwd+bwd", "cores": cores, "kind": "port",
+            "sample": f"1 view of the workload ({n} Gaussians, {res}x{res}), oracle/gr_oracle.c binned fwd+bwd, "
+                      f"OpenMP {cores} threads, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    n, V, R = args.gaussians, args.views, args.res
+
+    params = synthetic_params(n, device)
+    cams = fm.orbit_cameras(V, R, R, device)
+    g = torch.Generator(device=device).manual_seed(1)
+    targets = [torch.rand((R, R, 3), generator=g, device=device) for _ in range(V)]
+    masks = [(t.mean(dim=2) > 0.5).to(torch.float32) for t in targets]
+    fitter = fm.ViewShardedFitter(params, cams, targets, R, R, lr=0.02, masks=masks)
+
+    for _ in range(args.warmup):
+        fitter.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    pkg._native.profile_begin()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = fitter.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    prof = pkg._native.profile_end()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+
+    # pairs per view for the algorithmic FLOP count (same binning as the kernels)
+    pairs = []
+    with torch.no_grad():
+        means, scales, colors, opac = fm.activations(params)
+        for i in fitter.my_views:
+            gv = tr.make_view(cams[i].view, cams[i].proj, R, R, None, tr.DEFAULT_CUTOFF)
+            _, _, _, st = tr.forward_native(means.contiguous(), scales.contiguous(), colors.contiguous(), opac.contiguous(), gv)
+            pairs.append(st.num_pairs)
+    if rank == 0:
+        bwd_ms, bwd_n = prof["raster_bwd"]
+        fwd_ms, fwd_n = prof["raster_fwd"]
+        avg_pairs = float(np.mean(pairs))
+        bwd_avg_s = bwd_ms / max(bwd_n, 1) / 1e3
+        achieved = FLOP_PER_PAIR_BWD * avg_pairs / bwd_avg_s / 1e12
+        traffic = None
+        pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get("k_raster_bwd_mfma", {}).get("hbm_bytes_per_launch")
+        pixels = V * R * R * args.steps
+        value = pixels / elapsed / 1e6
+        out = {
+            "metric": "Mpixels/sec fwd+bwd @1M Gaussians 800x800",
+            "value": round(value, 2),
+            "unit": "Mpixels/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded Gaussians per SURVEY.md 8(d), random targets)",
+            "config": {"workload": f"C4: {n} Gaussians, {V} orbit views {R}x{R}, fwd+bwd+grad all-reduce+Adam per step",
+                       "gaussians": n, "views": V, "width": R, "height": R, "cutoff_sigma": tr.DEFAULT_CUTOFF,
+                       "scale": round(0.1061 * (1200.0 / n) ** (1.0 / 3.0), 5), "seed": 0,
+                       "parallelism": f"view-sharded dp{world}", "pairs_per_view": int(avg_pairs)},
+            "roofline": {"bound": "mfma", "kernel": "k_raster_bwd_mfma", "achieved": round(achieved, 2),
+                         "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
+                         "traffic": traffic, "avg_launch_us": round(bwd_avg_s * 1e6, 1), "launches": bwd_n,
+                         "fwd_kernel_avg_us": round(fwd_ms / max(fwd_n, 1) * 1e3, 1),
+                         "fwd_achieved_tflops": round(FLOP_PER_PAIR_FWD * avg_pairs / (fwd_ms / max(fwd_n, 1) / 1e3) / 1e12, 2)},
+            "loss": float(loss),
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(n, R, V)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

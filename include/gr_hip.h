@@ -88,6 +88,10 @@ gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const floa
 /* Tile-sorted (tile, Gaussian) pair lists and per-tile ranges. */
 size_t gr_bins_bytes(const gr_view* v, int n, int64_t num_pairs);
 
+/* Forward-only scratch (unsorted pairs, sort temporaries, split-tile partials); may be released
+ * as soon as gr_fwd_render has been enqueued (stream order keeps it alive for the kernels). */
+size_t gr_fwd_scratch_bytes(const gr_view* v, int n, int64_t num_pairs);
+
 /* Per-pixel state saved for the backward pass: 5 floats per pixel. */
 size_t gr_saved_floats(const gr_view* v);
 
@@ -95,8 +99,8 @@ size_t gr_saved_floats(const gr_view* v);
  *   out_rgb (H,W,3) clamp((bg+C)/(1+W),0,1); out_alpha (H,W) (may be NULL); out_depth (H,W)
  *   (may be NULL); saved (5*H*W floats) accumulators kept for gr_bwd. */
 gr_status gr_fwd_render(const gr_view* v, int n, int64_t num_pairs, const void* geom, void* bins,
-                        size_t bins_bytes, float* out_rgb, float* out_alpha, float* out_depth,
-                        float* saved, void* stream);
+                        size_t bins_bytes, void* scratch, size_t scratch_bytes, float* out_rgb,
+                        float* out_alpha, float* out_depth, float* saved, void* stream);
 
 /* Backward workspace: per-pair gradient partials + per-pixel upstream vectors. */
 size_t gr_bwd_bytes(const gr_view* v, int n, int64_t num_pairs);
@@ -129,6 +133,12 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
  *   bins: [0] keys uint32[K] [1] gaussian ids int32[K] (tile-sorted) [2] ranges int2[tiles]  */
 void gr_geom_layout(int n, size_t offsets_out[6]);
 void gr_bins_layout(const gr_view* v, int n, int64_t num_pairs, size_t offsets_out[3]);
+
+/* Live kernel timing with HIP events on the launch stream (bench.py).  Between begin and end,
+ * every raster launch is bracketed by two events; end() synchronises them and returns the summed
+ * device time and the launch count of [0] the forward splat and [1] the backward splat. */
+void gr_profile_begin(void);
+gr_status gr_profile_end(double total_ms[2], int launches[2]);
 
 const char* gr_last_error(void);
 const char* gr_version(void);
