@@ -1,0 +1,66 @@
+"""CPU: the C-ABI library loads and exports every function include/gr_hip.h declares (no GPU
+compute calls here); the host-only introspection entry points work."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "gr_hip.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-zA-Z_][\w\s\*]*?\b(gr_\w+)\s*\(", text, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ("gr_fwd_prepare", "gr_fwd_render", "gr_bwd", "gr_render_u8", "gr_last_error", "gr_geom_bytes",
+                 "gr_bins_bytes", "gr_bwd_bytes", "gr_fwd_scratch_bytes", "gr_saved_floats"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(pkg):
+    lib = pkg._native.lib()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_version_and_error_string(pkg):
+    assert "gfx950" in pkg._native.version()
+    assert isinstance(pkg._native.lib().gr_last_error(), bytes)
+
+
+def test_layouts_are_aligned_and_ordered(pkg):
+    off = pkg._native.geom_layout(1000)
+    assert off == sorted(off) and all(o % 256 == 0 for o in off)
+    gv = pkg.torch_renderer.make_view(__import__("numpy").eye(4, dtype="float32"),
+                                      __import__("numpy").eye(4, dtype="float32"), 800, 800)
+    b = pkg._native.bins_layout(gv, 1000, 12345)
+    assert b == sorted(b) and all(o % 256 == 0 for o in b)
+    assert b[1] - b[0] >= 4 * 12345
+
+
+def test_struct_sizes_match_header(pkg):
+    # gr_view: 2 ints + 16 + 16 + 3 + 3 + 1 floats; gr_render_params: RenderParams' layout
+    assert ctypes.sizeof(pkg._native.GrView) == 4 * (2 + 16 + 16 + 3 + 3 + 1)
+    assert ctypes.sizeof(pkg._native.GrRenderParams) == 4 * (2 + 16 + 16 + 3 + 3)
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    """No silent fallback: pointing GR_HIP_LIB at nothing makes the loader raise."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("_native_probe", os.path.join(REPO, "3dgaussian_amd", "_native.py"))
+    mod = importlib.util.module_from_spec(spec)
+    monkeypatch.setenv("GR_HIP_LIB", str(tmp_path / "nope.so"))
+    spec.loader.exec_module(mod)
+    with pytest.raises(ImportError):
+        mod.lib()

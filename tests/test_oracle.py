@@ -1,0 +1,96 @@
+"""CPU: pin the oracle (oracle/gr_oracle.c) against the reference's own golden vectors.
+
+Goldens (tests/golden/make_golden.py): F1 edge cases and F2 (the C1 scene) from the reference's
+python/torch_renderer.py (float32 forward + autograd backward); F3 uint8 from the reference's
+src/renderer_cpu.cpp compiled from source.  The oracle accumulates in float64, so for tensors
+where the reference's own float32 rounding exceeds 1e-4 (ill-conditioned sums) the bar is the
+larger of 1e-4 and 1.5 x what an independent float32 evaluation could be expected to deviate.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import golden, golden_names
+from oracle import oracle as orc
+
+FLOAT_GOLDENS = golden_names("f1_") + golden_names("f2_")
+KEYS = ("out_rgb", "out_alpha", "out_depth", "d_means", "d_scales", "d_colors", "d_opacities")
+
+
+def _run(d, binned, cutoff=6.0):
+    v = orc.make_view(d["view"], d["proj"], int(d["width"]), int(d["height"]), d["background"], cutoff=cutoff)
+    sc = orc.Scene(d["means"], d["scales"], d["colors"], d["opacities"])
+    out, a, dep = orc.forward(v, sc, binned=binned)
+    dm, ds, dc, do = orc.backward(v, sc, d["g_rgb"], d["g_alpha"], d["g_depth"], binned=binned)
+    return dict(zip(KEYS, (out, a, dep, dm, ds, dc, do)))
+
+
+@pytest.mark.parametrize("name", FLOAT_GOLDENS)
+def test_dense_oracle_matches_reference(name):
+    d = golden(name)
+    if d["means"].shape[0] == 0:
+        assert not d["out_rgb"].any()  # reference returns zeros for N == 0 (torch_renderer.py:135-136)
+        return
+    r = _run(d, binned=False)
+    for k in KEYS:
+        err = orc.rel_l2(r[k], d[k])
+        # f1_n1 d_opacities: one cancelling sum where float32 torch is 2.4e-4 from exact
+        tol = 3e-4 if (name == "f1_n1_17x13" and k == "d_opacities") else 1e-4
+        assert err <= tol, f"{name} {k}: {err:.3e}"
+
+
+@pytest.mark.parametrize("name", FLOAT_GOLDENS)
+def test_binned_6sigma_matches_reference(name):
+    """The product's semantics (6-sigma tile footprint) against the dense reference."""
+    d = golden(name)
+    if d["means"].shape[0] == 0:
+        return
+    r = _run(d, binned=True)
+    for k in KEYS:
+        err = orc.rel_l2(r[k], d[k])
+        tol = 3e-4 if (name == "f1_n1_17x13" and k == "d_opacities") else 1e-4
+        assert err <= tol, f"{name} {k}: {err:.3e}"
+    assert orc.psnr(r["out_rgb"], d["out_rgb"]) >= 60.0
+
+
+def test_5sigma_is_not_enough_with_depth_gradients():
+    """Why the default cutoff is 6 sigma: with upstream depth gradients, d depth/d w is amplified by
+    1/(W+1e-6) on near-empty pixels and the 5-sigma tails break the 1e-4 bar."""
+    d = golden("f2_c1_view3")
+    r5 = _run(d, binned=True, cutoff=5.0)
+    r6 = _run(d, binned=True, cutoff=6.0)
+    assert orc.rel_l2(r5["d_means"], d["d_means"]) > 1e-4
+    assert orc.rel_l2(r6["d_means"], d["d_means"]) < 1e-5
+
+
+@pytest.mark.parametrize("name", golden_names("u8_"))
+def test_u8_restatement_bit_exact(name):
+    d = golden(name)
+    sc = orc.Scene(d["means"], d["scales"], d["colors"], d["opacities"])
+    out = orc.render_u8(int(d["width"]), int(d["height"]), d["view"], d["proj"], sc, d["background"], int(d["sort"]))
+    np.testing.assert_array_equal(out, d["rgba"])
+
+
+def test_binning_is_stable_and_consistent():
+    sc = orc.synthetic_scene(3000, seed=9, scale=0.05)
+    view, proj = orc.orbit_cameras(5, 160, 96)[3]
+    v = orc.make_view(view, proj, 160, 96)
+    rec, rect, counts = orc.preprocess(v, sc)
+    offsets, keys, vals, ranges = orc.bin_pairs(v, rect, counts)
+    assert offsets[-1] == counts.sum() == len(vals)
+    assert np.all(np.diff(keys.astype(np.int64)) >= 0)  # tile-sorted
+    for t in range(ranges.shape[0]):
+        seg = vals[ranges[t, 0]:ranges[t, 1]]
+        assert np.all(np.diff(seg) > 0)  # Gaussian-index order inside a tile (stable)
+    # every pair's tile lies in its Gaussian's rectangle
+    r = rect[vals]
+    tx, ty = keys % 10, keys // 10
+    assert np.all((tx >= r[:, 0]) & (tx <= r[:, 2]) & (ty >= r[:, 1]) & (ty <= r[:, 3]))
+
+
+def test_camera_helpers_match_golden_views():
+    d = golden("f2_c1_view1")
+    view, proj = orc.orbit_cameras(4, 128, 128)[1]
+    np.testing.assert_array_equal(view, d["view"])
+    np.testing.assert_array_equal(proj, d["proj"])
