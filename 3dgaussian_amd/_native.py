@@ -58,6 +58,12 @@ class GrRenderParams(ctypes.Structure):
     ]
 
 
+class GrPlan(ctypes.Structure):
+    """gr_plan (include/gr_hip.h): sizes produced by gr_fwd_prepare."""
+
+    _fields_ = [("num_pairs", ctypes.c_int64), ("num_slots", ctypes.c_int64)]
+
+
 class NativeLibraryError(ImportError):
     pass
 
@@ -66,21 +72,20 @@ _lib = None
 
 _P = ctypes.c_void_p
 _VP = ctypes.POINTER(GrView)
+_PP = ctypes.POINTER(GrPlan)
 _SIG = {
     "gr_geom_bytes": (ctypes.c_size_t, [ctypes.c_int]),
-    "gr_fwd_prepare": (ctypes.c_int, [_VP, ctypes.c_int, _P, _P, _P, ctypes.c_int, _P, _P, ctypes.c_size_t,
-                                      ctypes.POINTER(ctypes.c_int64), _P]),
-    "gr_bins_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, ctypes.c_int64]),
+    "gr_fwd_prepare": (ctypes.c_int, [_VP, ctypes.c_int, _P, _P, _P, ctypes.c_int, _P, _P, ctypes.c_size_t, _PP, _P]),
+    "gr_bins_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
     "gr_saved_floats": (ctypes.c_size_t, [_VP]),
-    "gr_fwd_scratch_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, ctypes.c_int64]),
-    "gr_fwd_render": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int64, _P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P, _P,
-                                     _P, _P, _P]),
-    "gr_bwd_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, ctypes.c_int64]),
-    "gr_bwd": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int64, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P,
+    "gr_fwd_scratch_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
+    "gr_fwd_render": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P, _P, _P, _P, _P]),
+    "gr_bwd_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
+    "gr_bwd": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, _P, _P, _P, ctypes.c_size_t, _P]),
     "gr_render_u8": (ctypes.c_int, [ctypes.POINTER(GrRenderParams), ctypes.c_int, _P, _P, _P, _P, _P]),
     "gr_geom_layout": (None, [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
-    "gr_bins_layout": (None, [_VP, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_size_t)]),
+    "gr_bins_layout": (None, [_VP, ctypes.c_int, _PP, ctypes.POINTER(ctypes.c_size_t)]),
     "gr_profile_begin": (None, []),
     "gr_profile_end": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
     "gr_last_error": (ctypes.c_char_p, []),
@@ -133,12 +138,15 @@ def profile_begin() -> None:
     lib().gr_profile_begin()
 
 
+PROFILE_STAGES = ("raster_fwd", "raster_bwd", "reduce_bwd", "binning")
+
+
 def profile_end():
-    """Returns {"raster_fwd": (total_ms, launches), "raster_bwd": (total_ms, launches)}."""
-    ms = (ctypes.c_double * 2)()
-    n = (ctypes.c_int * 2)()
+    """Returns {stage: (total_ms, launches)} for PROFILE_STAGES."""
+    ms = (ctypes.c_double * 4)()
+    n = (ctypes.c_int * 4)()
     check(lib().gr_profile_end(ms, n), "gr_profile_end")
-    return {"raster_fwd": (ms[0], n[0]), "raster_bwd": (ms[1], n[1])}
+    return {k: (ms[i], n[i]) for i, k in enumerate(PROFILE_STAGES)}
 
 
 def version() -> str:
@@ -153,5 +161,6 @@ def geom_layout(n: int):
 
 def bins_layout(gv: GrView, n: int, num_pairs: int):
     out = (ctypes.c_size_t * 3)()
-    lib().gr_bins_layout(ctypes.byref(gv), int(n), int(num_pairs), out)
+    plan = GrPlan(int(num_pairs), 0)
+    lib().gr_bins_layout(ctypes.byref(gv), int(n), ctypes.byref(plan), out)
     return list(out)

@@ -92,7 +92,7 @@ ViewK make_viewk(const gr_view* v) {
   std::memcpy(k.P, v->proj, sizeof(k.P));
   std::memcpy(k.bg, v->background, sizeof(k.bg));
   std::memcpy(k.cam, v->cam_pos, sizeof(k.cam));
-  k.cutoff = v->cutoff > 0.0f ? v->cutoff : 6.0f;
+  k.cutoff = v->cutoff > 0.0f ? v->cutoff : 7.0f;
   return k;
 }
 
@@ -163,6 +163,29 @@ __device__ __forceinline__ int tile_rect(const ViewK& v, const Proj& p, float op
   return (r.z - r.x + 1) * (r.w - r.y + 1);
 }
 
+// Tile culling inside the rectangle (oracle/gr_oracle.c tile_pass, bit-exact): keep tile (tx,ty) iff
+// the Gaussian's largest weight over the tile's pixel centres (clipped to the image) is
+// >= o * exp(-cutoff^2/2).  q = -0.5 log2(e) / sigma^2 as stored in recA.
+__device__ __forceinline__ bool tile_pass(const ViewK& v, float px, float py, float qx, float qy, int tx, int ty) {
+  const float thr = (-0.5f * LOG2E) * (v.cutoff * v.cutoff);
+  const int xe = min(tx * T + T - 1, v.W - 1), ye = min(ty * T + T - 1, v.H - 1);
+  const float lox = (float)(tx * T) + 0.5f, hix = (float)xe + 0.5f;
+  const float loy = (float)(ty * T) + 0.5f, hiy = (float)ye + 0.5f;
+  const float cx = px < lox ? lox : (px > hix ? hix : px);
+  const float cy = py < loy ? loy : (py > hiy ? hiy : py);
+  const float dx = cx - px, dy = cy - py;
+  const float e = (dx * dx) * qx + (dy * dy) * qy;
+  return e >= thr;
+}
+
+__device__ __forceinline__ float qcoef(float s) { return (-0.5f * LOG2E) / (s * s); }
+
+// Partial-sum slot of pair (Gaussian, tile (tx,ty)): the Gaussian's first slot (high word of its
+// packed offset) + the tile's index inside its rectangle (culled tiles leave unused slots).
+__device__ __forceinline__ int pair_slot(unsigned long long off, const int4 r, int tx, int ty) {
+  return (int)(off >> 32) + (ty - r.y) * (r.z - r.x + 1) + (tx - r.x);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Geometry buffer layout.
 // ------------------------------------------------------------------------------------------------
@@ -171,8 +194,10 @@ struct Geom {
   float4* recB;  // o, r, g, b (clamped)
   float* recZ;   // z_abs
   int4* rect;    // tile rectangle
-  int* counts;   // n+1
-  int* offsets;  // n+1 (exclusive scan)
+  // packed (rect area << 32 | kept tiles): the exclusive scan gives, per Gaussian, the first pair
+  // index (low word) and the first partial-sum slot (high word; one slot per rectangle tile)
+  unsigned long long* counts;   // n+1
+  unsigned long long* offsets;  // n+1
   void* scan_tmp;
   size_t scan_tmp_bytes;
 };
@@ -184,16 +209,18 @@ size_t geom_fixed(int n, size_t off[6]) {
   off[1] = o; o = align_up(o + nn * sizeof(float4));
   off[2] = o; o = align_up(o + nn * sizeof(float));
   off[3] = o; o = align_up(o + nn * sizeof(int4));
-  off[4] = o; o = align_up(o + (nn + 1) * sizeof(int));
-  off[5] = o; o = align_up(o + (nn + 1) * sizeof(int));
+  off[4] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
+  off[5] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
   return o;
 }
 
-size_t scan_tmp_bytes(int n) {
+template <typename CountT>
+size_t scan_tmp_bytes_t(int n) {
   size_t tmp = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (int*)nullptr, (int*)nullptr, n + 1, (hipStream_t)0);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (CountT*)nullptr, (CountT*)nullptr, n + 1, (hipStream_t)0);
   return tmp;
 }
+size_t scan_tmp_bytes(int n) { return scan_tmp_bytes_t<unsigned long long>(n); }
 
 Geom geom_view(void* base, int n) {
   size_t off[6];
@@ -204,8 +231,8 @@ Geom geom_view(void* base, int n) {
   g.recB = (float4*)(b + off[1]);
   g.recZ = (float*)(b + off[2]);
   g.rect = (int4*)(b + off[3]);
-  g.counts = (int*)(b + off[4]);
-  g.offsets = (int*)(b + off[5]);
+  g.counts = (unsigned long long*)(b + off[4]);
+  g.offsets = (unsigned long long*)(b + off[5]);
   g.scan_tmp = b + fixed;
   g.scan_tmp_bytes = 0;
   return g;
@@ -311,35 +338,68 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, int n, const float*
   eval_color<CD>(v, mx, my, mz, colors + (size_t)CD * i, c);
   const float op = opac[i];
   int4 r;
-  const int cnt = tile_rect(v, p, op, r);
-  const float qx = (-0.5f * LOG2E) / (p.sx * p.sx);
-  const float qy = (-0.5f * LOG2E) / (p.sy * p.sy);
+  const float qx = qcoef(p.sx);
+  const float qy = qcoef(p.sy);
+  int cnt = 0;
+  const int area = tile_rect(v, p, op, r);
+  if (area > 0) {
+    for (int ty = r.y; ty <= r.w; ++ty)
+      for (int tx = r.x; tx <= r.z; ++tx) cnt += tile_pass(v, p.px, p.py, qx, qy, tx, ty) ? 1 : 0;
+  }
   g.recA[i] = make_float4(p.px, p.py, qx, qy);
   g.recB[i] = make_float4(op < 0.0f ? 0.0f : op, clamp01(c[0]), clamp01(c[1]), clamp01(c[2]));
   g.recZ[i] = p.za;
   g.rect[i] = r;
-  g.counts[i] = cnt;
+  g.counts[i] = cnt > 0 ? (((unsigned long long)area << 32) | (unsigned)cnt) : 0ull;
 }
 
-template <typename KeyT>
-__global__ __launch_bounds__(256) void k_emit(int n, int tiles_x, const int4* __restrict__ rect,
-                                              const int* __restrict__ counts, const int* __restrict__ offsets,
-                                              const KeyT* __restrict__ low_keys, KeyT* keys, int* ids) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || counts[i] == 0) return;
-  const int4 r = rect[i];
-  int k = offsets[i];
-  const KeyT low = low_keys ? low_keys[i] : (KeyT)0;
-  for (int ty = r.y; ty <= r.w; ++ty)
-    for (int tx = r.x; tx <= r.z; ++tx) {
-      const KeyT t = (KeyT)(ty * tiles_x + tx);
-      if constexpr (sizeof(KeyT) == 8)
-        keys[k] = (t << 32) | low;
-      else
-        keys[k] = t;
-      ids[k] = i;
-      ++k;
-    }
+constexpr int EWIN = 4096;  // pairs staged in LDS per emit block
+
+// Pairs of 256 consecutive Gaussians form one contiguous range; they are built in LDS and written
+// out with coalesced stores (direct scattered stores only when a block overflows the window).
+template <typename KeyT, typename OffT>
+__global__ __launch_bounds__(256) void k_emit(ViewK v, int n, const int4* __restrict__ rect,
+                                              const OffT* __restrict__ counts, const OffT* __restrict__ offsets,
+                                              const float4* __restrict__ recA, const KeyT* __restrict__ low_keys,
+                                              KeyT* keys, int* ids) {
+  // recA != nullptr: differentiable path, tiles culled by tile_pass; nullptr: legacy full rectangle
+  __shared__ KeyT sK[EWIN];
+  __shared__ int sI[EWIN];
+  const int g0 = blockIdx.x * 256;
+  const int i = g0 + (int)threadIdx.x;
+  const int gend = min(n, g0 + 256);
+  const int k0 = (int)(offsets[g0] & 0xffffffffu), k1 = (int)(offsets[gend] & 0xffffffffu);
+  const bool staged = (k1 - k0) <= EWIN;
+  if (i < n && counts[i] != 0) {
+    const int4 r = rect[i];
+    int k = (int)(offsets[i] & 0xffffffffu);  // pair index (low word when packed)
+    const KeyT low = low_keys ? low_keys[i] : (KeyT)0;
+    const float4 a = recA ? recA[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int ty = r.y; ty <= r.w; ++ty)
+      for (int tx = r.x; tx <= r.z; ++tx) {
+        if (recA && !tile_pass(v, a.x, a.y, a.z, a.w, tx, ty)) continue;
+        const KeyT t = (KeyT)(ty * v.tiles_x + tx);
+        KeyT key;
+        if constexpr (sizeof(KeyT) == 8)
+          key = (t << 32) | low;
+        else
+          key = t;
+        if (staged) {
+          sK[k - k0] = key;
+          sI[k - k0] = i;
+        } else {
+          keys[k] = key;
+          ids[k] = i;
+        }
+        ++k;
+      }
+  }
+  if (!staged) return;  // uniform per block
+  __syncthreads();
+  for (int e = (int)threadIdx.x; e < k1 - k0; e += 256) {
+    keys[k0 + e] = sK[e];
+    ids[k0 + e] = sI[e];
+  }
 }
 
 template <typename KeyT>
@@ -403,24 +463,45 @@ struct StageRec {
   int g;
 };
 
-__device__ __forceinline__ StageRec stage_load(int k, int k1, const int* __restrict__ ids, const float4* __restrict__ recA,
-                                               const float4* __restrict__ recB, const float* __restrict__ recZ) {
+// Staging pipeline for the 256-wide Gaussian batches of a work item: the Gaussian id of batch b+2
+// and the records of batch b+1 are in flight while batch b is computed, so neither the id load nor
+// the dependent record gathers sit on the critical path.
+__device__ __forceinline__ int stage_id(int k, int k1, const int* __restrict__ ids) { return k < k1 ? ids[k] : -1; }
+
+// Records of Gaussian g (g < 0: padding).  Padding has o = 0 and px = +huge, so every weight it
+// produces is exactly 0 (exp2(-inf) = 0) without a per-element select.
+__device__ __forceinline__ StageRec stage_rec(int g, const float4* __restrict__ recA, const float4* __restrict__ recB,
+                                             const float* __restrict__ recZ) {
   StageRec r;
-  r.a = make_float4(0.f, 0.f, 0.f, 0.f);
-  r.b = r.a;
-  r.z = 0.f;
-  r.g = -1;
-  if (k < k1) {
-    r.g = ids[k];
-    r.a = recA[r.g];
-    r.b = recB[r.g];
-    r.z = recZ[r.g];
+  r.g = g;
+  if (g >= 0) {
+    r.a = recA[g];
+    r.b = recB[g];
+    r.z = recZ[g];
+  } else {
+    r.a = make_float4(1e30f, 1e30f, -1.0f, -1.0f);
+    r.b = make_float4(0.f, 0.f, 0.f, 0.f);
+    r.z = 0.f;
   }
   return r;
 }
 
-// Forward: one workgroup (4 waves) per work item.  Batches of 256 Gaussians go through LDS; wave w
-// takes Gaussians [64w, 64w+64) of each batch in steps of 4 (the MFMA K dimension).
+// XCD-aware work-item order: the dispatcher deals workgroups round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md §Workgroup dispatch), so block b runs on XCD-group b % 8.  Give each XCD
+// group a contiguous run of items (= neighbouring tiles, which share most Gaussians) so their
+// records stay in that XCD's L2.  Bijective for any count (cdna_hip_programming.md §5 'XCD swizzle').
+// Speed only: any placement gives the same results.
+__device__ __forceinline__ int xcd_item(int b, int nwg) {
+#if defined(GR_NO_XCD_REMAP)
+  return b;
+#endif
+  const int q = nwg >> 3, r = nwg & 7, xcd = b & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+// Forward: one workgroup (4 waves) per work item.  Batches of 256 Gaussians go through a double-
+// buffered LDS stage; wave w takes Gaussians [64w, 64w+64) of each batch in blocks of 4 steps of 4
+// (the MFMA K dimension).  Padding entries are exact zeros, so whole blocks are processed.
 __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, const int4* __restrict__ items,
                                                          const int* __restrict__ num_items, const int2* __restrict__ ranges,
                                                          const int* __restrict__ ids, const float4* __restrict__ recA,
@@ -428,13 +509,11 @@ __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, const int4* __
                                                          float* __restrict__ fwd_part, float* __restrict__ out_rgb,
                                                          float* __restrict__ out_alpha, float* __restrict__ out_depth,
                                                          float4* __restrict__ saved4, float* __restrict__ savedD) {
-  // LDS: staged records (9 KiB) during the loop, then the 4-wave reduction (20 KiB).
+  // LDS: two staged record buffers (2 x 9 KiB) during the loop, then the 4-wave reduction (20 KiB).
   __shared__ __attribute__((aligned(16))) float smem[4 * 5 * TP];
-  float4* sA = reinterpret_cast<float4*>(smem);
-  float4* sB = sA + TP;
-  float* sZ = reinterpret_cast<float*>(sB + TP);
-  const int item = blockIdx.x;
-  if (item >= *num_items) return;
+  const int nitems = *num_items;
+  if ((int)blockIdx.x >= nitems) return;
+  const int item = xcd_item(blockIdx.x, nitems);
   const int4 it = items[item];
   const int tile = it.x, k0 = it.y, k1 = it.z;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
@@ -443,30 +522,47 @@ __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, const int4* __
   const float xc = (float)(tx * T + li) + 0.5f;  // A row = x
   const float yc = (float)(ty * T + li) + 0.5f;  // B col = y
   f32x4 cW = {0.f, 0.f, 0.f, 0.f}, cR = cW, cG = cW, cB = cW, cD = cW;
-  StageRec st = stage_load(k0 + tid, k1, ids, recA, recB, recZ);
-  for (int base = k0; base < k1; base += TP) {
-    __syncthreads();
+  StageRec st = stage_rec(stage_id(k0 + tid, k1, ids), recA, recB, recZ);
+  int idn = stage_id(k0 + TP + tid, k1, ids);
+  int buf = 0;
+  for (int base = k0; base < k1; base += TP, buf ^= 1) {
+    float4* sA = reinterpret_cast<float4*>(smem) + buf * (2 * TP + TP / 4);
+    float4* sB = sA + TP;
+    float* sZ = reinterpret_cast<float*>(sB + TP);
     sA[tid] = st.a;
     sB[tid] = st.b;
     sZ[tid] = st.z;
-    __syncthreads();
-    st = stage_load(base + TP + tid, k1, ids, recA, recB, recZ);
-    const int cnt = min(TP, k1 - base) - wave * 64;  // Gaussians of this batch for this wave
-    const int nst = cnt <= 0 ? 0 : min(16, (cnt + 3) >> 2);
-    for (int i = 0; i < nst; ++i) {
-      const int j = wave * 64 + 4 * i + gs;
-      const float4 a = sA[j];
-      const float4 b = sB[j];
-      const float z = sZ[j];
-      const float dx = xc - a.x, dy = yc - a.y;
-      const float ex = __builtin_amdgcn_exp2f(dx * a.z * dx);
-      const float ey = __builtin_amdgcn_exp2f(dy * a.w * dy);
-      const float oe = b.x * ex;
-      cW = mfma4(oe, ey, cW);
-      cR = mfma4(oe * b.y, ey, cR);
-      cG = mfma4(oe * b.z, ey, cG);
-      cB = mfma4(oe * b.w, ey, cB);
-      cD = mfma4(oe * z, ey, cD);
+    __syncthreads();  // the other buffer's readers (previous batch) are also past this point
+    st = stage_rec(idn, recA, recB, recZ);
+    idn = stage_id(base + 2 * TP + tid, k1, ids);
+    const int cnt = min(TP, k1 - base) - wave * 64;           // Gaussians of this batch for this wave
+    const int nblk = cnt <= 0 ? 0 : min(4, (cnt + 15) >> 4);  // blocks of 4 steps (16 Gaussians)
+    for (int blk = 0; blk < nblk; ++blk) {
+      float A0[4], A1[4], A2[4], A3[4], A4[4], Bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = wave * 64 + blk * 16 + 4 * u + gs;
+        const float4 a = sA[j];
+        const float4 b = sB[j];
+        const float z = sZ[j];
+        const float dx = xc - a.x, dy = yc - a.y;
+        const float ex = __builtin_amdgcn_exp2f(dx * a.z * dx);
+        Bv[u] = __builtin_amdgcn_exp2f(dy * a.w * dy);
+        const float oe = b.x * ex;
+        A0[u] = oe;
+        A1[u] = oe * b.y;
+        A2[u] = oe * b.z;
+        A3[u] = oe * b.w;
+        A4[u] = oe * z;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        cW = mfma4(A0[u], Bv[u], cW);
+        cR = mfma4(A1[u], Bv[u], cR);
+        cG = mfma4(A2[u], Bv[u], cG);
+        cB = mfma4(A3[u], Bv[u], cB);
+        cD = mfma4(A4[u], Bv[u], cD);
+      }
     }
   }
   __syncthreads();
@@ -586,19 +682,36 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
 // Backward: one workgroup (4 waves) per work item.  A = U_k^T (tile-constant, 20 registers per
 // lane), B = f(x) ex_g(x) for 16 Gaussians on the MFMA columns; wave w takes groups [4w, 4w+4) of
 // each staged batch of 256 Gaussians.  Partials per pair (9 floats) go to the pair's slot
-// (Gaussian offset + tile index inside its rectangle), so k_reduce_bwd reads them contiguously.
-__global__ __launch_bounds__(256) void k_raster_bwd_mfma(ViewK v, const int4* __restrict__ items,
-                                                         const int* __restrict__ num_items, const int* __restrict__ ids,
-                                                         const float4* __restrict__ recA, const float4* __restrict__ recB,
-                                                         const float* __restrict__ recZ, const int4* __restrict__ rect,
-                                                         const int* __restrict__ offsets, const float* __restrict__ U,
-                                                         float* __restrict__ partials) {
-  __shared__ __attribute__((aligned(16))) float4 sA[TP];
-  __shared__ __attribute__((aligned(16))) float4 sB[TP];
-  __shared__ float sZ[TP];
-  __shared__ int sSlot[TP];
-  const int item = blockIdx.x;
-  if (item >= *num_items) return;
+// (Gaussian's first slot + index of the tile inside its rectangle), so k_reduce_bwd reads each
+// Gaussian's partials contiguously and in a fixed order.
+#ifndef GR_BWD_WAVES
+#define GR_BWD_WAVES 4
+#endif
+
+// Sum over the 4 lane rows (lanes l, l+16, l+32, l+48) of a pair of values with one
+// v_permlane16_swap: returns rows {a01, b01, a23, b23} (row r of the result holds the named sum).
+__device__ __forceinline__ float pair16(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// Second level with v_permlane32_swap: rows {a, b, c, d} fully reduced from two pair16 results.
+__device__ __forceinline__ float pair32(float ab, float cd) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(ab), __float_as_uint(cd), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+__global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
+    ViewK v, const int4* __restrict__ items, const int* __restrict__ num_items, const int* __restrict__ ids,
+    const float4* __restrict__ recA, const float4* __restrict__ recB, const float* __restrict__ recZ,
+    const int4* __restrict__ rect, const unsigned long long* __restrict__ offsets, const float* __restrict__ U,
+    float* __restrict__ partials) {
+  __shared__ __attribute__((aligned(16))) float4 sA[2][TP];
+  __shared__ __attribute__((aligned(16))) float4 sB[2][TP];
+  __shared__ float sZ[2][TP];
+  __shared__ int sSlot[2][TP];
+  const int nitems = *num_items;
+  if ((int)blockIdx.x >= nitems) return;
+  const int item = xcd_item(blockIdx.x, nitems);
   const int4 it = items[item];
   const int tile = it.x, k0 = it.y, k1 = it.z;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
@@ -613,52 +726,48 @@ __global__ __launch_bounds__(256) void k_raster_bwd_mfma(ViewK v, const int4* __
       for (int s = 0; s < 4; ++s) A[k][s] = Ut[k * TP + li * T + 4 * s + xs];
   }
   const float x0 = (float)(tx * T) + 0.5f, y0 = (float)(ty * T) + 0.5f;
-  StageRec st = stage_load(k0 + tid, k1, ids, recA, recB, recZ);
-  int slot = -1;
-  if (st.g >= 0) {
-    const int4 r = rect[st.g];
-    slot = offsets[st.g] + (ty - r.y) * (r.z - r.x + 1) + (tx - r.x);
-  }
-  for (int base = k0; base < k1; base += TP) {
-    __syncthreads();
-    sA[tid] = st.a;
-    sB[tid] = st.b;
-    sZ[tid] = st.z;
-    sSlot[tid] = slot;
-    __syncthreads();
-    st = stage_load(base + TP + tid, k1, ids, recA, recB, recZ);
-    slot = -1;
-    if (st.g >= 0) {
-      const int4 r = rect[st.g];
-      slot = offsets[st.g] + (ty - r.y) * (r.z - r.x + 1) + (tx - r.x);
-    }
+  StageRec st = stage_rec(stage_id(k0 + tid, k1, ids), recA, recB, recZ);
+  int slot = st.g >= 0 ? pair_slot(offsets[st.g], rect[st.g], tx, ty) : -1;
+  int idn = stage_id(k0 + TP + tid, k1, ids);
+  int buf = 0;
+  for (int base = k0; base < k1; base += TP, buf ^= 1) {
+    sA[buf][tid] = st.a;
+    sB[buf][tid] = st.b;
+    sZ[buf][tid] = st.z;
+    sSlot[buf][tid] = slot;
+    __syncthreads();  // the other buffer's readers (previous batch) are also past this point
+    st = stage_rec(idn, recA, recB, recZ);
+    slot = st.g >= 0 ? pair_slot(offsets[st.g], rect[st.g], tx, ty) : -1;
+    idn = stage_id(base + 2 * TP + tid, k1, ids);
     const int cnt = min(TP, k1 - base) - wave * 64;
     const int ngr = cnt <= 0 ? 0 : min(4, (cnt + 15) >> 4);
     for (int gi = 0; gi < ngr; ++gi) {
       const int j = wave * 64 + gi * 16 + li;
-      const float4 a = sA[j];
-      const float4 b = sB[j];
-      const float z = sZ[j];
-      const int myslot = sSlot[j];
-      const bool valid = myslot >= 0;
+      const float4 a = sA[buf][j];
+      const float4 b = sB[buf][j];
+      const float z = sZ[buf][j];
+      const int myslot = sSlot[buf][j];
       const float vv[5] = {b.y, b.z, b.w, 1.0f, z};
       f32x4 D1[5];
 #pragma unroll
       for (int k = 0; k < 5; ++k) D1[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 Ddx = {0.f, 0.f, 0.f, 0.f}, Ddx2 = Ddx;
+      // dx / dx^2 contractions summed over the 5 channels, two accumulators each (no MFMA waits on
+      // the one before it: 16x16x4 f32 has a 32-cycle issue and a 40-cycle dependent latency)
+      f32x4 Ddx[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, Ddx2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const float dx = (x0 + (float)(4 * s + xs)) - a.x;
-        const float ex = valid ? __builtin_amdgcn_exp2f(dx * a.z * dx) : 0.0f;
+        const float ex = __builtin_amdgcn_exp2f(dx * a.z * dx);  // exactly 0 for padding
         const float edx = ex * dx, edx2 = edx * dx;
 #pragma unroll
-        for (int k = 0; k < 5; ++k) D1[k] = mfma4(A[k][s], ex, D1[k]);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) Ddx = mfma4(A[k][s], vv[k] * edx, Ddx);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) Ddx2 = mfma4(A[k][s], vv[k] * edx2, Ddx2);
+        for (int k = 0; k < 5; ++k) {
+          D1[k] = mfma4(A[k][s], ex, D1[k]);
+          Ddx[k & 1] = mfma4(A[k][s], vv[k] * edx, Ddx[k & 1]);
+          Ddx2[k & 1] = mfma4(A[k][s], vv[k] * edx2, Ddx2[k & 1]);
+        }
       }
-      // lane holds D[y = 4*xs + r][g = li]
+      const f32x4 Dx = Ddx[0] + Ddx[1], Dx2 = Ddx2[0] + Ddx2[1];
+      // lane holds D[y = 4*xs + r][g = li]; sum its 4 rows, then across the 4 lane rows
       float S[NPART] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -674,25 +783,18 @@ __global__ __launch_bounds__(256) void k_raster_bwd_mfma(ViewK v, const int4* __
         const float tdy = t * dy;
         S[6] += tdy;
         S[8] = fmaf(tdy, dy, S[8]);
-        S[5] = fmaf(ey, Ddx[r], S[5]);
-        S[7] = fmaf(ey, Ddx2[r], S[7]);
+        S[5] = fmaf(ey, Dx[r], S[5]);
+        S[7] = fmaf(ey, Dx2[r], S[7]);
       }
-#pragma unroll
-      for (int q = 0; q < NPART; ++q) {
-        S[q] += __shfl_xor(S[q], 16);
-        S[q] += __shfl_xor(S[q], 32);
-      }
-      if (valid && xs == 0) {
+      // row r of R03 holds the total of S_r, of R47 the total of S_{4+r}; rows 0 and 1 of R8 hold S8
+      const float R03 = pair32(pair16(S[0], S[1]), pair16(S[2], S[3]));
+      const float R47 = pair32(pair16(S[4], S[5]), pair16(S[6], S[7]));
+      const float R8 = pair32(pair16(S[8], S[8]), 0.0f);
+      if (myslot >= 0) {
         float* dst = partials + (size_t)myslot * NPART;
-        dst[0] = b.x * S[0];
-        dst[1] = b.x * S[1];
-        dst[2] = b.x * S[2];
-        dst[3] = b.x * S[3];
-        dst[4] = S[4];
-        dst[5] = S[5];
-        dst[6] = S[6];
-        dst[7] = S[7];
-        dst[8] = S[8];
+        dst[xs] = b.x * R03;  // colour / depth sums carry the opacity
+        dst[4 + xs] = R47;
+        if (xs == 0) dst[8] = R8;
       }
     }
   }
@@ -701,24 +803,103 @@ __global__ __launch_bounds__(256) void k_raster_bwd_mfma(ViewK v, const int4* __
 // ------------------------------------------------------------------------------------------------
 // Per-Gaussian reduction of pair partials + chain rule.  Deterministic.
 // ------------------------------------------------------------------------------------------------
+#ifndef GR_RG
+#define GR_RG 32
+#endif
+constexpr int RG = GR_RG;        // Gaussians per reduce block (4 lanes each)
+constexpr int RWIN = 18 * GR_RG;  // partial-sum slots staged in LDS per block (18 per Gaussian)
+
 template <int CD>
-__global__ __launch_bounds__(256) void k_reduce_bwd(ViewK v, int n, const float* __restrict__ means,
+__device__ void chain_rule(const ViewK& v, int i, const double* S, unsigned cnt, const float* __restrict__ means,
+                           const float* __restrict__ scales, const float* __restrict__ colors,
+                           const float* __restrict__ opac, float* __restrict__ d_means, float* __restrict__ d_scales,
+                           float* __restrict__ d_colors, float* __restrict__ d_opac);
+
+// Block of RG Gaussians: their partial slots are one contiguous range (slots are ordered by
+// Gaussian), staged into LDS with coalesced loads; lane q of each Gaussian's 4 sums the kept tiles
+// j = q (mod 4) of its rectangle in scan order, the 4 sums are combined in a fixed order
+// (deterministic, no atomics), and lane 0 applies the chain rule.
+template <int CD>
+__global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const float* __restrict__ means,
                                                     const float* __restrict__ scales, const float* __restrict__ colors,
-                                                    const float* __restrict__ opac, const int* __restrict__ counts,
-                                                    const int* __restrict__ offsets, const float* __restrict__ partials,
-                                                    float* __restrict__ d_means, float* __restrict__ d_scales,
-                                                    float* __restrict__ d_colors, float* __restrict__ d_opac) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+                                                    const float* __restrict__ opac, const float4* __restrict__ recA,
+                                                    const int4* __restrict__ rect,
+                                                    const unsigned long long* __restrict__ counts,
+                                                    const unsigned long long* __restrict__ offsets,
+                                                    const float* __restrict__ partials, float* __restrict__ d_means,
+                                                    float* __restrict__ d_scales, float* __restrict__ d_colors,
+                                                    float* __restrict__ d_opac) {
+  __shared__ __attribute__((aligned(16))) float sP[RWIN * NPART + 4];
+  const int g0 = blockIdx.x * RG;
+  const int tid = threadIdx.x, q4 = tid & 3;
+  const int i = g0 + (tid >> 2);
+  const int gend = min(n, g0 + RG);
+  const long long s0 = (long long)(offsets[g0] >> 32), s1 = (long long)(offsets[gend] >> 32);
+  const bool staged = (s1 - s0) <= RWIN;
+  // staged: LDS holds floats [fa, fe) of the partial array, fa rounded down to 16 B (float4 loads)
+  const long long fa = (s0 * NPART) & ~3ll;
+  if (staged) {
+    const long long fe = s1 * NPART;
+    const int nv = (int)((fe - fa + 3) >> 2);
+    const float4* src = reinterpret_cast<const float4*>(partials + fa);
+    float4* dst = reinterpret_cast<float4*>(sP);
+    int e = tid;
+    constexpr int NT = 4 * RG;
+    for (; e + 3 * NT < nv; e += 4 * NT) {  // 4 loads in flight per lane
+      const float4 x0 = src[e], x1 = src[e + NT], x2 = src[e + 2 * NT], x3 = src[e + 3 * NT];
+      dst[e] = x0;
+      dst[e + NT] = x1;
+      dst[e + 2 * NT] = x2;
+      dst[e + 3 * NT] = x3;
+    }
+    for (; e < nv; e += NT) dst[e] = src[e];
+  }
+  __syncthreads();
   double S[NPART];
 #pragma unroll
   for (int q = 0; q < NPART; ++q) S[q] = 0.0;
-  const int cnt = counts[i];
-  const float* src = partials + (size_t)offsets[i] * NPART;
-  for (int j = 0; j < cnt; ++j) {
+  unsigned cnt = 0;
+  if (i < n) {
+    cnt = (unsigned)(counts[i] & 0xffffffffu);
+    if (cnt > 0) {
+      const long long base = (long long)(offsets[i] >> 32);
+      const float* src = staged ? sP + (base * NPART - fa) : partials + base * NPART;
+      const int4 r = rect[i];
+      const float4 a = recA[i];
+      const int w = r.z - r.x + 1, area = w * (r.w - r.y + 1);
+      // tiles j = q4, q4+4, ... of the rectangle in scan order, stepped without division
+      int tx = r.x + q4, ty = r.y;
+      while (tx > r.z) {
+        tx -= w;
+        ++ty;
+      }
+      for (int j = q4; j < area; j += 4) {
+        if (tile_pass(v, a.x, a.y, a.z, a.w, tx, ty)) {
 #pragma unroll
-    for (int q = 0; q < NPART; ++q) S[q] += (double)src[j * NPART + q];
+          for (int q = 0; q < NPART; ++q) S[q] += (double)src[j * NPART + q];
+        }
+        tx += 4;
+        while (tx > r.z) {
+          tx -= w;
+          ++ty;
+        }
+      }
+    }
   }
+#pragma unroll
+  for (int q = 0; q < NPART; ++q) {
+    S[q] += __shfl_xor(S[q], 1);
+    S[q] += __shfl_xor(S[q], 2);
+  }
+  if (q4 != 0 || i >= n) return;
+  chain_rule<CD>(v, i, S, cnt, means, scales, colors, opac, d_means, d_scales, d_colors, d_opac);
+}
+
+template <int CD>
+__device__ void chain_rule(const ViewK& v, int i, const double* S, unsigned cnt, const float* __restrict__ means,
+                           const float* __restrict__ scales, const float* __restrict__ colors,
+                           const float* __restrict__ opac, float* __restrict__ d_means, float* __restrict__ d_scales,
+                           float* __restrict__ d_colors, float* __restrict__ d_opac) {
   const float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
   const float s0 = scales[3 * i], s1 = scales[3 * i + 1];
   const float op = opac[i];
@@ -948,7 +1129,7 @@ __global__ __launch_bounds__(256) void k_patch_depth(int64_t K, uint64_t* keys, 
 
 // Optional per-kernel timing with HIP events on the launch stream (gr_profile_begin/end), used by
 // bench.py to time the dominant kernels live.  Off by default; host-side state only.
-enum { PROF_RASTER_FWD = 0, PROF_RASTER_BWD = 1, PROF_SLOTS = 2 };
+enum { PROF_RASTER_FWD = 0, PROF_RASTER_BWD = 1, PROF_REDUCE = 2, PROF_BINNING = 3, PROF_SLOTS = 4 };
 struct ProfSlot {
   std::vector<hipEvent_t> ev;
   size_t used = 0;
@@ -993,7 +1174,7 @@ void gr_profile_begin(void) {
   for (auto& sl : g_prof) sl.used = 0;
 }
 
-gr_status gr_profile_end(double total_ms[2], int launches[2]) {
+gr_status gr_profile_end(double total_ms[4], int launches[4]) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
   g_prof_on = false;
   for (int k = 0; k < PROF_SLOTS; ++k) {
@@ -1017,10 +1198,10 @@ const char* gr_version(void) { return GR_VERSION_STR; }
 
 void gr_geom_layout(int n, size_t offsets_out[6]) { geom_fixed(n, offsets_out); }
 
-void gr_bins_layout(const gr_view* v, int n, int64_t num_pairs, size_t offsets_out[3]) {
+void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[3]) {
   (void)n;
   size_t off[6];
-  bins_fixed(tiles_x_of(v->width) * tiles_y_of(v->height), num_pairs, off);
+  bins_fixed(tiles_x_of(v->width) * tiles_y_of(v->height), plan ? plan->num_pairs : 0, off);
   offsets_out[0] = off[0];
   offsets_out[1] = off[1];
   offsets_out[2] = off[2];
@@ -1033,36 +1214,40 @@ size_t gr_geom_bytes(int n) {
 
 size_t gr_saved_floats(const gr_view* v) { return (size_t)5 * v->width * v->height; }
 
-size_t gr_bins_bytes(const gr_view* v, int n, int64_t num_pairs) {
+size_t gr_bins_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
   const int tiles = tiles_x_of(v->width) * tiles_y_of(v->height);
   size_t off[6];
-  return bins_fixed(tiles, num_pairs, off);
+  return bins_fixed(tiles, plan->num_pairs, off);
 }
 
-size_t gr_fwd_scratch_bytes(const gr_view* v, int n, int64_t num_pairs) {
+size_t gr_fwd_scratch_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
   const int tiles = tiles_x_of(v->width) * tiles_y_of(v->height);
   size_t off[3];
-  return scratch_fixed(tiles, num_pairs, off) + align_up(sort_tmp_bytes<uint32_t>(num_pairs, bits_for((uint32_t)tiles)));
+  return scratch_fixed(tiles, plan->num_pairs, off) +
+         align_up(sort_tmp_bytes<uint32_t>(plan->num_pairs, bits_for((uint32_t)tiles)));
 }
 
-// Backward workspace: per-pair partials (K x 9 floats) + per-pixel upstream vectors (tiles x 5 x 256).
-size_t gr_bwd_bytes(const gr_view* v, int n, int64_t num_pairs) {
+// Backward workspace: pair partials (one 9-float slot per rectangle tile) + per-pixel upstream
+// vectors (tiles x 5 x 256).
+size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
   const size_t tiles = (size_t)tiles_x_of(v->width) * tiles_y_of(v->height);
-  return align_up((size_t)(num_pairs > 0 ? num_pairs : 1) * NPART * sizeof(float)) + align_up(tiles * 5 * TP * sizeof(float));
+  return align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)) +
+         align_up(tiles * 5 * TP * sizeof(float));
 }
 
 gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const float* scales, const float* colors,
-                         int color_dim, const float* opacities, void* geom, size_t geom_bytes, int64_t* num_pairs,
+                         int color_dim, const float* opacities, void* geom, size_t geom_bytes, gr_plan* plan,
                          void* stream) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
   if (n < 0) return set_error(GR_ERR_INVALID_ARGUMENT, "n must be >= 0");
   if (color_dim != 3 && color_dim != 12) return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3)");
-  if (!num_pairs) return set_error(GR_ERR_INVALID_ARGUMENT, "num_pairs is null");
-  *num_pairs = 0;
+  if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
+  plan->num_pairs = 0;
+  plan->num_slots = 0;
   if (n == 0) return GR_OK;
   if (!means || !scales || !colors || !opacities || !geom) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
   if (geom_bytes < gr_geom_bytes(n)) return set_error(GR_ERR_WORKSPACE, "geom workspace too small");
@@ -1076,23 +1261,27 @@ gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const floa
   GR_HIP_TRY(hipGetLastError());
   size_t tmp = scan_tmp_bytes(n);
   GR_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(g.scan_tmp, tmp, g.counts, g.offsets, n + 1, s));
-  int total = 0;
-  GR_HIP_TRY(hipMemcpyAsync(&total, g.offsets + n, sizeof(int), hipMemcpyDeviceToHost, s));
+  unsigned long long total = 0;
+  GR_HIP_TRY(hipMemcpyAsync(&total, g.offsets + n, sizeof(total), hipMemcpyDeviceToHost, s));
   GR_HIP_TRY(hipStreamSynchronize(s));
-  if (total < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
-  *num_pairs = total;
+  const unsigned long long pairs = total & 0xffffffffull, slots = total >> 32;
+  if (pairs >= (1ull << 31) || slots >= (1ull << 31)) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
+  plan->num_pairs = (int64_t)pairs;
+  plan->num_slots = (int64_t)slots;
   return GR_OK;
 }
 
-gr_status gr_fwd_render(const gr_view* v, int n, int64_t num_pairs, const void* geom, void* bins, size_t bins_bytes,
+gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins, size_t bins_bytes,
                         void* scratch, size_t scratch_bytes, float* out_rgb, float* out_alpha, float* out_depth,
                         float* saved, void* stream) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
+  if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
   if (!out_rgb || !saved) return set_error(GR_ERR_INVALID_ARGUMENT, "out_rgb and saved are required");
   if (n > 0 && (!geom || !bins)) return set_error(GR_ERR_INVALID_ARGUMENT, "null workspace");
-  if (bins_bytes < gr_bins_bytes(v, n, num_pairs)) return set_error(GR_ERR_WORKSPACE, "bins workspace too small");
-  if (scratch_bytes < gr_fwd_scratch_bytes(v, n, num_pairs) || !scratch)
+  const int64_t num_pairs = plan->num_pairs;
+  if (bins_bytes < gr_bins_bytes(v, n, plan)) return set_error(GR_ERR_WORKSPACE, "bins workspace too small");
+  if (scratch_bytes < gr_fwd_scratch_bytes(v, n, plan) || !scratch)
     return set_error(GR_ERR_WORKSPACE, "forward scratch workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const ViewK vk = make_viewk(v);
@@ -1100,10 +1289,12 @@ gr_status gr_fwd_render(const gr_view* v, int n, int64_t num_pairs, const void* 
   Bins b = bins_view(bins, tiles, num_pairs);
   Scratch sc = scratch_view(scratch, tiles, num_pairs);
   GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * tiles, s));
+  prof_mark(PROF_BINNING, s);
   if (n > 0 && num_pairs > 0) {
     Geom g = geom_view((void*)geom, n);
-    hipLaunchKernelGGL(k_emit<uint32_t>, dim3(blocks_for(n)), dim3(256), 0, s, n, vk.tiles_x, g.rect, g.counts, g.offsets,
-                       (const uint32_t*)nullptr, sc.keys_in, sc.ids_in);
+    hipLaunchKernelGGL((k_emit<uint32_t, unsigned long long>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
+                       (const int4*)g.rect, (const unsigned long long*)g.counts, (const unsigned long long*)g.offsets,
+                       (const float4*)g.recA, (const uint32_t*)nullptr, sc.keys_in, sc.ids_in);
     GR_HIP_TRY(hipGetLastError());
     const int bits = bits_for((uint32_t)tiles);
     size_t tmp = sort_tmp_bytes<uint32_t>(num_pairs, bits);
@@ -1117,6 +1308,7 @@ gr_status gr_fwd_render(const gr_view* v, int n, int64_t num_pairs, const void* 
   hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, tiles, (const int2*)b.ranges, b.items, b.num_items,
                      b.tile_item0);
   GR_HIP_TRY(hipGetLastError());
+  prof_mark(PROF_BINNING, s);
   const int64_t cap = item_cap(tiles, num_pairs);
   if (num_pairs > 0) {
     prof_mark(PROF_RASTER_FWD, s);
@@ -1132,17 +1324,19 @@ gr_status gr_fwd_render(const gr_view* v, int n, int64_t num_pairs, const void* 
   return GR_OK;
 }
 
-gr_status gr_bwd(const gr_view* v, int n, int64_t num_pairs, const float* means, const float* scales, const float* colors,
-                 int color_dim, const float* opacities, const void* geom, const void* bins, const float* saved,
-                 const float* g_rgb, const float* g_alpha, const float* g_depth, float* d_means, float* d_scales,
-                 float* d_colors, float* d_opacities, void* ws, size_t ws_bytes, void* stream) {
+gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
+                 const float* colors, int color_dim, const float* opacities, const void* geom, const void* bins,
+                 const float* saved, const float* g_rgb, const float* g_alpha, const float* g_depth, float* d_means,
+                 float* d_scales, float* d_colors, float* d_opacities, void* ws, size_t ws_bytes, void* stream) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
+  if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
   if (color_dim != 3 && color_dim != 12) return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3)");
   if (n == 0) return GR_OK;
   if (!g_rgb || !saved || !geom || !bins || !d_means || !d_scales || !d_colors || !d_opacities)
     return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
-  if (num_pairs > 0 && (!ws || ws_bytes < gr_bwd_bytes(v, n, num_pairs)))
+  const int64_t num_pairs = plan->num_pairs;
+  if (num_pairs > 0 && (!ws || ws_bytes < gr_bwd_bytes(v, n, plan)))
     return set_error(GR_ERR_WORKSPACE, "backward workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const ViewK vk = make_viewk(v);
@@ -1152,25 +1346,31 @@ gr_status gr_bwd(const gr_view* v, int n, int64_t num_pairs, const float* means,
   const size_t HW = (size_t)v->width * v->height;
   float* partials = (float*)ws;
   if (num_pairs > 0) {
-    float* U = (float*)((char*)ws + align_up((size_t)num_pairs * NPART * sizeof(float)));
+    float* U = (float*)((char*)ws + align_up((size_t)plan->num_slots * NPART * sizeof(float)));
     hipLaunchKernelGGL(k_pixel_grads, dim3(tiles), dim3(256), 0, s, vk, (const float4*)saved, saved + 4 * HW, g_rgb,
                        g_alpha, g_depth, U);
     GR_HIP_TRY(hipGetLastError());
     const int64_t cap = item_cap(tiles, num_pairs);
     prof_mark(PROF_RASTER_BWD, s);
     hipLaunchKernelGGL(k_raster_bwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, (const int4*)b.items,
-                       (const int*)b.num_items, (const int*)b.ids, g.recA, g.recB, g.recZ, g.rect, g.offsets,
-                       (const float*)U, partials);
+                       (const int*)b.num_items, (const int*)b.ids, g.recA, g.recB, g.recZ, g.rect,
+                       (const unsigned long long*)g.offsets, (const float*)U, partials);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_BWD, s);
   }
+  prof_mark(PROF_REDUCE, s);
   if (color_dim == 3)
-    hipLaunchKernelGGL(k_reduce_bwd<3>, dim3(blocks_for(n)), dim3(256), 0, s, vk, n, means, scales, colors, opacities,
-                       g.counts, g.offsets, partials, d_means, d_scales, d_colors, d_opacities);
+    hipLaunchKernelGGL(k_reduce_bwd<3>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
+                       (const float4*)g.recA, (const int4*)g.rect, (const unsigned long long*)g.counts,
+                       (const unsigned long long*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
+                       d_opacities);
   else
-    hipLaunchKernelGGL(k_reduce_bwd<12>, dim3(blocks_for(n)), dim3(256), 0, s, vk, n, means, scales, colors, opacities,
-                       g.counts, g.offsets, partials, d_means, d_scales, d_colors, d_opacities);
+    hipLaunchKernelGGL(k_reduce_bwd<12>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
+                       (const float4*)g.recA, (const int4*)g.rect, (const unsigned long long*)g.counts,
+                       (const unsigned long long*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
+                       d_opacities);
   GR_HIP_TRY(hipGetLastError());
+  prof_mark(PROF_REDUCE, s);
   return GR_OK;
 }
 
@@ -1207,7 +1407,7 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
   const size_t o_off = o; o = align_up(o + (nn + 1) * sizeof(int));
   const size_t o_dk = o; o = align_up(o + nn * sizeof(uint32_t));
   const size_t o_img = o; o = align_up(o + HW * 4);
-  const size_t o_scan = o; o = align_up(o + scan_tmp_bytes(n));
+  const size_t o_scan = o; o = align_up(o + scan_tmp_bytes_t<int>(n));
   const size_t fixed = o;
   char* d = nullptr;
   GR_HIP_TRY(hipMalloc(&d, fixed));
@@ -1232,7 +1432,7 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
   hipLaunchKernelGGL(k_preprocess_u8, dim3(blocks_for(n + 1)), dim3(256), 0, s, vk, n, din, din + 3 * nn, din + 6 * nn,
                      din + 9 * nn, lr);
   GR_HIP_TRY(hipGetLastError());
-  size_t tmp = scan_tmp_bytes(n);
+  size_t tmp = scan_tmp_bytes_t<int>(n);
   GR_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(d + o_scan, tmp, lr.counts, lr.offsets, n + 1, s));
   int K = 0;
   GR_HIP_TRY(hipMemcpy(&K, lr.offsets + n, sizeof(int), hipMemcpyDeviceToHost));
@@ -1260,8 +1460,9 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
       uint64_t* kin = (uint64_t*)(e + q_kin);
       uint64_t* kout = (uint64_t*)(e + q_kout);
       // low 32 bits = depth key; high bits = tile
-      hipLaunchKernelGGL(k_emit<uint64_t>, dim3(blocks_for(n)), dim3(256), 0, s, n, vk.tiles_x, lr.rect, lr.counts,
-                         lr.offsets, (const uint64_t*)nullptr, kin, (int*)(e + q_iin));
+      hipLaunchKernelGGL((k_emit<uint64_t, int>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n, (const int4*)lr.rect,
+                         (const int*)lr.counts, (const int*)lr.offsets, (const float4*)nullptr, (const uint64_t*)nullptr,
+                         kin, (int*)(e + q_iin));
       GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_patch_depth, dim3(blocks_for(K)), dim3(256), 0, s, (int64_t)K, kin, (const int*)(e + q_iin),
                          (const uint32_t*)lr.depth_key);
@@ -1272,8 +1473,9 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
     } else {
       uint32_t* kin = (uint32_t*)(e + q_kin);
       uint32_t* kout = (uint32_t*)(e + q_kout);
-      hipLaunchKernelGGL(k_emit<uint32_t>, dim3(blocks_for(n)), dim3(256), 0, s, n, vk.tiles_x, lr.rect, lr.counts,
-                         lr.offsets, (const uint32_t*)nullptr, kin, (int*)(e + q_iin));
+      hipLaunchKernelGGL((k_emit<uint32_t, int>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n, (const int4*)lr.rect,
+                         (const int*)lr.counts, (const int*)lr.offsets, (const float4*)nullptr, (const uint32_t*)nullptr,
+                         kin, (int*)(e + q_iin));
       GR_HIP_TRY(hipGetLastError());
       GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e + q_tmp, t2, kin, kout, (int*)(e + q_iin), (int*)(e + q_iout), K, 0,
                                                     bits, s));

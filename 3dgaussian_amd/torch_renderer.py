@@ -7,8 +7,9 @@ exceptions.  The math is the reference's order-independent weighted average
 libgr_hip.so through a ``torch.autograd.Function`` — not by torch ops.  Differences that are by design
 (DESIGN.md §Semantics):
 
-* a Gaussian is evaluated on the 16x16 tiles its ``cutoff``*sigma box overlaps (default 6 sigma;
-  outputs and gradients agree with the dense reference to <=1e-6 relative L2 on its own fixtures);
+* a Gaussian is evaluated on the 16x16 tiles where its largest weight is >= o*exp(-cutoff^2/2)
+  (default cutoff 7: outputs and gradients agree with the dense reference to <=1e-5 relative L2 on
+  its own fixtures, including depth gradients on near-empty pixels);
 * ``chunk_size`` is accepted and ignored (no chunk loop);
 * gradients flow to means, scales, colours/SH, opacities and background; not to the camera matrices;
 * tensors must live on a HIP device: CPU tensors raise ``RuntimeError`` (there is no CPU fallback).
@@ -27,7 +28,7 @@ try:  # package import (3dgaussian_amd.torch_renderer) or flat import (drop-in o
 except ImportError:  # pragma: no cover
     import _native  # type: ignore
 
-DEFAULT_CUTOFF = 6.0
+DEFAULT_CUTOFF = 7.0
 
 
 @dataclass
@@ -129,10 +130,14 @@ def _stream(device: torch.device) -> ctypes.c_void_p:
 class RenderState:
     """Device workspaces produced by the forward pass and consumed by the backward pass."""
 
-    __slots__ = ("gv", "n", "num_pairs", "geom", "bins", "saved")
+    __slots__ = ("gv", "n", "plan", "geom", "bins", "saved")
 
-    def __init__(self, gv, n, num_pairs, geom, bins, saved):
-        self.gv, self.n, self.num_pairs, self.geom, self.bins, self.saved = gv, n, num_pairs, geom, bins, saved
+    def __init__(self, gv, n, plan, geom, bins, saved):
+        self.gv, self.n, self.plan, self.geom, self.bins, self.saved = gv, n, plan, geom, bins, saved
+
+    @property
+    def num_pairs(self) -> int:
+        return int(self.plan.num_pairs)
 
 
 def forward_native(means, scales, colors, opacities, gv: _native.GrView):
@@ -144,22 +149,23 @@ def forward_native(means, scales, colors, opacities, gv: _native.GrView):
     cd = 3 if colors.dim() == 2 else 12
     s = _stream(dev)
     geom = torch.empty((int(L.gr_geom_bytes(n)),), dtype=torch.uint8, device=dev)
-    K = ctypes.c_int64(0)
+    plan = _native.GrPlan()
     _native.check(L.gr_fwd_prepare(ctypes.byref(gv), n, _native.ptr(means), _native.ptr(scales), _native.ptr(colors), cd,
-                                   _native.ptr(opacities), _native.ptr(geom), geom.numel(), ctypes.byref(K), s), "gr_fwd_prepare")
-    num_pairs = int(K.value)
-    bins = torch.empty((int(L.gr_bins_bytes(ctypes.byref(gv), n, num_pairs)),), dtype=torch.uint8, device=dev)
+                                   _native.ptr(opacities), _native.ptr(geom), geom.numel(), ctypes.byref(plan), s),
+                  "gr_fwd_prepare")
+    bins = torch.empty((int(L.gr_bins_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8, device=dev)
     out = torch.empty((H, W, 3), dtype=torch.float32, device=dev)
     alpha = torch.empty((H, W), dtype=torch.float32, device=dev)
     depth = torch.empty((H, W), dtype=torch.float32, device=dev)
     saved = torch.empty((int(L.gr_saved_floats(ctypes.byref(gv))),), dtype=torch.float32, device=dev)
     # scratch is released when this function returns; the caching allocator keeps it stream-ordered
-    scratch = torch.empty((int(L.gr_fwd_scratch_bytes(ctypes.byref(gv), n, num_pairs)),), dtype=torch.uint8, device=dev)
-    _native.check(L.gr_fwd_render(ctypes.byref(gv), n, num_pairs, _native.ptr(geom), _native.ptr(bins), bins.numel(),
-                                  _native.ptr(scratch), scratch.numel(), _native.ptr(out), _native.ptr(alpha),
+    scratch = torch.empty((int(L.gr_fwd_scratch_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8,
+                          device=dev)
+    _native.check(L.gr_fwd_render(ctypes.byref(gv), n, ctypes.byref(plan), _native.ptr(geom), _native.ptr(bins),
+                                  bins.numel(), _native.ptr(scratch), scratch.numel(), _native.ptr(out), _native.ptr(alpha),
                                   _native.ptr(depth), _native.ptr(saved), s), "gr_fwd_render")
     del scratch
-    return out, alpha, depth, RenderState(gv, n, num_pairs, geom, bins, saved)
+    return out, alpha, depth, RenderState(gv, n, plan, geom, bins, saved)
 
 
 def backward_native(means, scales, colors, opacities, st: RenderState, g_out, g_alpha, g_depth):
@@ -167,12 +173,12 @@ def backward_native(means, scales, colors, opacities, st: RenderState, g_out, g_
     L = _native.lib()
     dev = means.device
     cd = 3 if colors.dim() == 2 else 12
-    ws = torch.empty((int(L.gr_bwd_bytes(ctypes.byref(st.gv), st.n, st.num_pairs)),), dtype=torch.uint8, device=dev)
+    ws = torch.empty((int(L.gr_bwd_bytes(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan))),), dtype=torch.uint8, device=dev)
     dm = torch.empty_like(means)
     ds = torch.empty_like(scales)
     dc = torch.empty_like(colors)
     do = torch.empty_like(opacities)
-    _native.check(L.gr_bwd(ctypes.byref(st.gv), st.n, st.num_pairs, _native.ptr(means), _native.ptr(scales),
+    _native.check(L.gr_bwd(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan), _native.ptr(means), _native.ptr(scales),
                            _native.ptr(colors), cd, _native.ptr(opacities), _native.ptr(st.geom), _native.ptr(st.bins),
                            _native.ptr(st.saved), _native.ptr(g_out), _native.ptr(g_alpha), _native.ptr(g_depth),
                            _native.ptr(dm), _native.ptr(ds), _native.ptr(dc), _native.ptr(do), _native.ptr(ws), ws.numel(),

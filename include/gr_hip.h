@@ -68,7 +68,7 @@ typedef struct gr_view {
   float proj[16];      /* Camera.proj, row-major                                          */
   float background[3]; /* background colour (torch_renderer.py:128-130)                    */
   float cam_pos[3];    /* inv(view)[:3,3] (torch_renderer.py:81-83); used by SH colours    */
-  float cutoff;        /* screen footprint half-width in sigmas used for binning (def. 6)  */
+  float cutoff;        /* footprint: tiles where max weight >= o*exp(-cutoff^2/2) (def. 7) */
 } gr_view;
 
 /* ------------------------------------------------------------------------------------------ */
@@ -77,20 +77,26 @@ typedef struct gr_view {
 /*   opacities (N,), all float32 contiguous.                                                   */
 /* ------------------------------------------------------------------------------------------ */
 
+/* Sizes produced by gr_fwd_prepare for one view. */
+typedef struct gr_plan {
+  int64_t num_pairs; /* kept (Gaussian, tile) pairs: the splat work                        */
+  int64_t num_slots; /* backward partial-sum slots: one per tile of each Gaussian's rectangle */
+} gr_plan;
+
 /* Per-Gaussian projection records, tile rectangles, pair counts and offsets. */
 size_t gr_geom_bytes(int n);
 
-/* Project + cull + count tiles + prefix-scan.  Writes *num_pairs (synchronises `stream`). */
+/* Project + cull + count tiles + prefix-scan.  Fills *plan (synchronises `stream`). */
 gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const float* scales,
                          const float* colors, int color_dim, const float* opacities, void* geom,
-                         size_t geom_bytes, int64_t* num_pairs, void* stream);
+                         size_t geom_bytes, gr_plan* plan, void* stream);
 
-/* Tile-sorted (tile, Gaussian) pair lists and per-tile ranges. */
-size_t gr_bins_bytes(const gr_view* v, int n, int64_t num_pairs);
+/* Tile-sorted (tile, Gaussian) pair lists, per-tile ranges and work items. */
+size_t gr_bins_bytes(const gr_view* v, int n, const gr_plan* plan);
 
 /* Forward-only scratch (unsorted pairs, sort temporaries, split-tile partials); may be released
  * as soon as gr_fwd_render has been enqueued (stream order keeps it alive for the kernels). */
-size_t gr_fwd_scratch_bytes(const gr_view* v, int n, int64_t num_pairs);
+size_t gr_fwd_scratch_bytes(const gr_view* v, int n, const gr_plan* plan);
 
 /* Per-pixel state saved for the backward pass: 5 floats per pixel. */
 size_t gr_saved_floats(const gr_view* v);
@@ -98,17 +104,17 @@ size_t gr_saved_floats(const gr_view* v);
 /* Emit pairs + sort by tile + tile ranges + forward splat.  Outputs:
  *   out_rgb (H,W,3) clamp((bg+C)/(1+W),0,1); out_alpha (H,W) (may be NULL); out_depth (H,W)
  *   (may be NULL); saved (5*H*W floats) accumulators kept for gr_bwd. */
-gr_status gr_fwd_render(const gr_view* v, int n, int64_t num_pairs, const void* geom, void* bins,
+gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins,
                         size_t bins_bytes, void* scratch, size_t scratch_bytes, float* out_rgb,
                         float* out_alpha, float* out_depth, float* saved, void* stream);
 
 /* Backward workspace: per-pair gradient partials + per-pixel upstream vectors. */
-size_t gr_bwd_bytes(const gr_view* v, int n, int64_t num_pairs);
+size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan);
 
 /* Backward of gr_fwd_render.  g_rgb (H,W,3) required; g_alpha, g_depth may be NULL (zero).
  * Writes (overwrites) d_means (N,3), d_scales (N,3) (column 2 is always 0),
  * d_colors (N,3) or (N,4,3), d_opacities (N,). */
-gr_status gr_bwd(const gr_view* v, int n, int64_t num_pairs, const float* means,
+gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* means,
                  const float* scales, const float* colors, int color_dim, const float* opacities,
                  const void* geom, const void* bins, const float* saved, const float* g_rgb,
                  const float* g_alpha, const float* g_depth, float* d_means, float* d_scales,
@@ -129,16 +135,19 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
 
 /* Byte offsets of the sub-buffers inside geom / bins, for debugging and bit-exact tests.
  *   geom: [0] rec_a float4[n] (px,py,qx,qy)  [1] rec_b float4[n] (o,r,g,b)  [2] rec_z float[n]
- *         [3] rect int4[n] (tx0,ty0,tx1,ty1) [4] counts int[n+1] [5] offsets int[n+1]
+ *         [3] rect int4[n] (tx0,ty0,tx1,ty1) [4] counts u64[n+1] [5] offsets u64[n+1]
+ *         (counts/offsets packed: rectangle area / first slot in the high word, kept tiles / first
+ *         pair in the low word)
  *   bins: [0] keys uint32[K] [1] gaussian ids int32[K] (tile-sorted) [2] ranges int2[tiles]  */
 void gr_geom_layout(int n, size_t offsets_out[6]);
-void gr_bins_layout(const gr_view* v, int n, int64_t num_pairs, size_t offsets_out[3]);
+void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[3]);
 
 /* Live kernel timing with HIP events on the launch stream (bench.py).  Between begin and end,
- * every raster launch is bracketed by two events; end() synchronises them and returns the summed
- * device time and the launch count of [0] the forward splat and [1] the backward splat. */
+ * the timed stages are bracketed by two events each; end() synchronises them and returns the
+ * summed device time and count of [0] the forward splat kernel, [1] the backward splat kernel,
+ * [2] the backward reduction kernel, [3] the binning stage (emit + sort + ranges + work items). */
 void gr_profile_begin(void);
-gr_status gr_profile_end(double total_ms[2], int launches[2]);
+gr_status gr_profile_end(double total_ms[4], int launches[4]);
 
 const char* gr_last_error(void);
 const char* gr_version(void);

@@ -71,7 +71,7 @@ def lib() -> ctypes.CDLL:
         _LIB = ctypes.CDLL(build())
         f = ctypes.c_void_p
         _LIB.gro_preprocess.argtypes = [ctypes.POINTER(GrView), ctypes.c_int, f, f, f, ctypes.c_int, f, f, f, f]
-        _LIB.gro_bin.argtypes = [ctypes.POINTER(GrView), ctypes.c_int] + [f] * 6
+        _LIB.gro_bin.argtypes = [ctypes.POINTER(GrView), ctypes.c_int] + [f] * 7
         _LIB.gro_bin.restype = ctypes.c_int64
         _LIB.gro_forward.argtypes = [ctypes.POINTER(GrView), ctypes.c_int, f, f, f, ctypes.c_int, f, ctypes.c_int] + [f] * 4
         _LIB.gro_backward.argtypes = [ctypes.POINTER(GrView), ctypes.c_int, f, f, f, ctypes.c_int, f, ctypes.c_int] + [f] * 7
@@ -132,17 +132,19 @@ def preprocess(v: GrView, scene: Scene):
     return rec, rect, counts
 
 
-def bin_pairs(v: GrView, rect: np.ndarray, counts: np.ndarray):
+def bin_pairs(v: GrView, rec: np.ndarray, rect: np.ndarray, counts: np.ndarray):
+    """Stable (tile, Gaussian) pair lists; rec/rect/counts from preprocess()."""
     n = counts.shape[0]
+    rec = np.ascontiguousarray(rec, np.float32)
     tiles = math.ceil(v.width / TILE) * math.ceil(v.height / TILE)
     offsets = np.zeros((n + 1,), np.int32)
     rect = np.ascontiguousarray(rect, np.int32)
     counts = np.ascontiguousarray(counts, np.int32)
-    K = lib().gro_bin(ctypes.byref(v), n, _p(rect), _p(counts), _p(offsets), None, None, None)
+    K = lib().gro_bin(ctypes.byref(v), n, _p(rec), _p(rect), _p(counts), _p(offsets), None, None, None)
     keys = np.zeros((max(K, 1),), np.uint32)
     vals = np.zeros((max(K, 1),), np.int32)
     ranges = np.zeros((tiles, 2), np.int32)
-    lib().gro_bin(ctypes.byref(v), n, _p(rect), _p(counts), _p(offsets), _p(keys), _p(vals), _p(ranges))
+    lib().gro_bin(ctypes.byref(v), n, _p(rec), _p(rect), _p(counts), _p(offsets), _p(keys), _p(vals), _p(ranges))
     return offsets, keys[:K], vals[:K], ranges
 
 

@@ -21,6 +21,7 @@ from oracle import oracle as orc
 pytestmark = pytest.mark.gpu
 
 GRAD_KEYS = ("d_means", "d_scales", "d_colors", "d_opacities")
+CUTOFF = 7.0  # product default (3dgaussian_amd/torch_renderer.py DEFAULT_CUTOFF)
 
 
 def _run_hip(pkg, d, device, cutoff=None):
@@ -46,7 +47,7 @@ def _run_hip(pkg, d, device, cutoff=None):
 
 
 def _oracle(d, binned):
-    v = orc.make_view(d["view"], d["proj"], int(d["width"]), int(d["height"]), d["background"], cutoff=6.0)
+    v = orc.make_view(d["view"], d["proj"], int(d["width"]), int(d["height"]), d["background"], cutoff=CUTOFF)
     sc = orc.Scene(d["means"], d["scales"], d["colors"], d["opacities"])
     out, alpha, depth = orc.forward(v, sc, binned=binned)
     dm, ds, dc, do = orc.backward(v, sc, d["g_rgb"], d["g_alpha"], d["g_depth"], binned=binned)
@@ -75,7 +76,7 @@ def test_fwd_bwd_matches_reference_goldens(pkg, cuda, name):
 
 @pytest.mark.parametrize("name", golden_names("f1_n300") + golden_names("f2_c1_view0"))
 def test_fwd_bwd_matches_binned_oracle(pkg, cuda, name):
-    """Same semantics (6-sigma tile footprint) in float64 on the CPU: tighter bound."""
+    """Same semantics (7-sigma elliptical tile footprint) in float64 on the CPU: tighter bound."""
     d = golden(name)
     hip = _run_hip(pkg, d, cuda)
     ora = _oracle(d, binned=True)
@@ -85,7 +86,7 @@ def test_fwd_bwd_matches_binned_oracle(pkg, cuda, name):
         assert orc.rel_l2(hip[k], ora[k]) <= 1e-4, k
 
 
-def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=6.0):
+def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=CUTOFF):
     tr = pkg.torch_renderer
     nat = pkg._native
     m, s, c, o = (torch.from_numpy(a).to(device) for a in scene.arrays())
@@ -97,8 +98,12 @@ def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=6.0):
     geom = st.geom.cpu().numpy()
     recA = geom[g_off[0]: g_off[0] + 16 * n].view(np.float32).reshape(n, 4)
     rect = geom[g_off[3]: g_off[3] + 16 * n].view(np.int32).reshape(n, 4)
-    counts = geom[g_off[4]: g_off[4] + 4 * n].view(np.int32)
-    offsets = geom[g_off[5]: g_off[5] + 4 * (n + 1)].view(np.int32)
+    # packed u64: low word = kept tiles / first pair, high word = rectangle area / first slot
+    counts64 = geom[g_off[4]: g_off[4] + 8 * n].view(np.uint64)
+    offsets64 = geom[g_off[5]: g_off[5] + 8 * (n + 1)].view(np.uint64)
+    counts = (counts64 & 0xFFFFFFFF).astype(np.int32)
+    offsets = (offsets64 & 0xFFFFFFFF).astype(np.int32)
+    areas = (counts64 >> 32).astype(np.int64)
     b_off = nat.bins_layout(gv, n, st.num_pairs)
     bins = st.bins.cpu().numpy()
     K = st.num_pairs
@@ -106,7 +111,8 @@ def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=6.0):
     keys = bins[b_off[0]: b_off[0] + 4 * K].view(np.uint32)
     ids = bins[b_off[1]: b_off[1] + 4 * K].view(np.int32)
     ranges = bins[b_off[2]: b_off[2] + 8 * tiles].view(np.int32).reshape(tiles, 2)
-    return dict(recA=recA, rect=rect, counts=counts, offsets=offsets, keys=keys, ids=ids, ranges=ranges, K=K)
+    return dict(recA=recA, rect=rect, counts=counts, offsets=offsets, keys=keys, ids=ids, ranges=ranges, K=K, areas=areas,
+                slots=int(st.plan.num_slots))
 
 
 @pytest.mark.parametrize("case", ["f1_n300_64x48", "f2_c1_view1", "c2_100k_512", "edge_big_sigma"])
@@ -124,14 +130,20 @@ def test_bins_bit_exact(pkg, cuda, case):
         view, proj = orc.orbit_cameras(3, 200, 120)[1]
         W, H = 200, 120
     g = _native_bins(pkg, scene, view, proj, W, H, cuda)
-    v = orc.make_view(view, proj, W, H, None, cutoff=6.0)
+    v = orc.make_view(view, proj, W, H, None, cutoff=CUTOFF)
     rec, rect, counts = orc.preprocess(v, scene)
     # projected centres are float32-identical (same operation sequence, no FMA contraction)
     np.testing.assert_array_equal(g["recA"][:, 0].view(np.int32), rec[:, 0].view(np.int32))
     np.testing.assert_array_equal(g["recA"][:, 1].view(np.int32), rec[:, 1].view(np.int32))
+    np.testing.assert_array_equal(g["recA"][:, 2].view(np.int32), rec[:, 9].view(np.int32))  # qx
+    np.testing.assert_array_equal(g["recA"][:, 3].view(np.int32), rec[:, 10].view(np.int32))  # qy
     np.testing.assert_array_equal(g["counts"], counts)
     np.testing.assert_array_equal(g["rect"], rect)
-    offsets, keys, vals, ranges = orc.bin_pairs(v, rect, counts)
+    kept = counts > 0
+    area = (rect[:, 2] - rect[:, 0] + 1) * (rect[:, 3] - rect[:, 1] + 1)
+    np.testing.assert_array_equal(g["areas"], np.where(kept, area, 0))
+    assert g["slots"] == int(np.where(kept, area, 0).sum())
+    offsets, keys, vals, ranges = orc.bin_pairs(v, rec, rect, counts)
     np.testing.assert_array_equal(g["offsets"], offsets)
     assert g["K"] == len(vals)
     np.testing.assert_array_equal(g["keys"], keys)

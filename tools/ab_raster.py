@@ -1,0 +1,27 @@
+"""A/B helper: average raster fwd/bwd kernel time (HIP events) for the library in $GR_HIP_LIB."""
+import importlib, os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from oracle import oracle as orc
+pkg = importlib.import_module("3dgaussian_amd")
+tr = pkg.torch_renderer
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+R = int(sys.argv[2]) if len(sys.argv) > 2 else 800
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 6
+dev = torch.device("cuda:0")
+scene = orc.synthetic_scene(N, seed=0)
+views = orc.orbit_cameras(50, R, R)
+t = [torch.from_numpy(a).to(dev).requires_grad_(True) for a in scene.arrays()]
+g = torch.randn(R, R, 3, device=dev)
+for i in range(2):
+    out, a, d = tr.rasterize(*t, *views[i], R, R)
+    (out * g).sum().backward()
+torch.cuda.synchronize()
+pkg._native.profile_begin()
+for i in range(reps):
+    out, a, d = tr.rasterize(*t, *views[i % 10], R, R)
+    (out * g).sum().backward()
+torch.cuda.synchronize()
+p = pkg._native.profile_end()
+lib = os.path.basename(os.environ.get("GR_HIP_LIB", "libgr_hip.so"))
+print(f"{lib:24s} " + "  ".join(f"{k} {1e3*v[0]/max(v[1],1):7.1f}us" for k, v in p.items()))
