@@ -26,6 +26,7 @@
 
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rocprim/rocprim.hpp>
 
 #include <cmath>
 #include <cstdint>
@@ -246,7 +247,7 @@ constexpr int NPART = 9;  // backward partial sums per (Gaussian, tile) pair
 
 // Persistent binning state (kept from forward to backward).
 struct Bins {
-  uint32_t* keys;      // [K] sorted keys (tile id)
+  uint32_t* keys;      // [K] sorted tile keys (radix-sort path only; the counting sort needs none)
   int* ids;            // [K] sorted gaussian ids
   int2* ranges;        // [tiles] pair range of each tile
   int4* items;         // [cap] work items (tile, k0, k1, chunk)
@@ -256,7 +257,7 @@ struct Bins {
 
 // Forward-only scratch (freed by the caller after gr_fwd_render).
 struct Scratch {
-  uint32_t* keys_in;   // [K]
+  uint32_t* keys_in;   // [K] tile key of each emitted pair (uint16_t when short_keys(tiles))
   int* ids_in;         // [K]
   float* fwd_part;     // [cap][5][256] partial accumulators of tiles split over several items
   void* sort_tmp;
@@ -285,6 +286,55 @@ size_t scratch_fixed(int tiles, int64_t K, size_t off[3]) {
   off[1] = o; o = align_up(o + kk * sizeof(int));
   off[2] = o; o = align_up(o + cap * 5 * TP * sizeof(float));
   return o;
+}
+
+// Pair order by tile.  Pairs leave k_emit in Gaussian order; the forward and backward need them
+// grouped by tile with ascending Gaussian ids inside a tile (a stable sort by tile).  Up to
+// TSORT_MAX_TILES tiles this is a stable counting sort over 16-bit tile keys (k_tile_count ..
+// k_tile_place below): the keys are read twice and the ids once, instead of a radix sort's
+// histogram + two scatter passes over keys and values.  Larger images use the hipcub radix sort on
+// 32-bit keys.
+constexpr int TSORT_MAX_TILES = 16384;
+
+inline bool short_keys(int tiles) { return tiles <= TSORT_MAX_TILES; }
+
+// Waves per column block: the per-wave tile counters (tiles ints per wave) stay within 64 KB LDS.
+inline int tsort_waves(int tiles) { return tiles <= 4096 ? 4 : tiles <= 8192 ? 2 : 1; }
+
+struct TSortPlan {
+  int waves, cw, cols;  // waves per column, pairs per column, columns
+  size_t cells;         // tiles * cols
+};
+
+// 2048 pairs per wave (k_tile_place's register-resident segment); more segments per wave only when
+// the count matrix would pass 2^28 cells.
+#ifndef GR_TSORT_NSEG
+#define GR_TSORT_NSEG 1
+#endif
+inline TSortPlan tsort_plan(int64_t K, int tiles) {
+  TSortPlan p;
+  p.waves = tsort_waves(tiles);
+  int64_t pw = 2048 * GR_TSORT_NSEG;
+  const int64_t kk = K > 0 ? K : 1;
+  while ((int64_t)tiles * ((kk + pw * p.waves - 1) / (pw * p.waves)) > (1ll << 28)) pw *= 2;
+  p.cw = (int)(pw * p.waves);
+  p.cols = (int)((kk + p.cw - 1) / p.cw);
+  p.cells = (size_t)tiles * p.cols;
+  return p;
+}
+
+// Scratch behind the fixed part: counting sort = count matrix M, its row scan S, tile totals T;
+// radix sort = its temp storage.
+size_t tile_sort_tmp_bytes(int64_t K, int tiles) {
+  if (short_keys(tiles)) {
+    const TSortPlan p = tsort_plan(K, tiles);
+    return 2 * align_up(p.cells * sizeof(int)) + align_up((size_t)tiles * sizeof(int));
+  }
+  size_t tmp = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const int*)nullptr,
+                                           (int*)nullptr, (int)(K > 0 ? K : 1), 0, bits_for((uint32_t)tiles),
+                                           (hipStream_t)0);
+  return tmp;
 }
 
 template <typename KeyT>
@@ -430,17 +480,31 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // Work items: each non-empty tile's pair list is cut into chunks of CH Gaussians, so every
 // workgroup gets about the same amount of work however unevenly Gaussians fall on tiles.
 // One block; tiles are scanned in order, so items are ordered by (tile, chunk).
-__global__ __launch_bounds__(1024) void k_work_items(int tiles, const int2* __restrict__ ranges, int4* __restrict__ items,
-                                                     int* __restrict__ num_items, int* __restrict__ tile_item0) {
+// counts != nullptr (counting-sort path): the tile ranges are the exclusive scan of the per-tile
+// pair counts and are written to `ranges` here; otherwise `ranges` is read.
+__global__ __launch_bounds__(1024) void k_work_items(int tiles, int2* __restrict__ ranges, const int* __restrict__ counts,
+                                                     int4* __restrict__ items, int* __restrict__ num_items,
+                                                     int* __restrict__ tile_item0) {
   typedef hipcub::BlockScan<int, 1024> Scan;
   __shared__ typename Scan::TempStorage tmp;
-  __shared__ int carry;
-  if (threadIdx.x == 0) carry = 0;
+  __shared__ int carry, pcarry;
+  if (threadIdx.x == 0) carry = pcarry = 0;
   __syncthreads();
   for (int base = 0; base < tiles; base += 1024) {
     const int t = base + (int)threadIdx.x;
     int2 r = make_int2(0, 0);
-    if (t < tiles) r = ranges[t];
+    if (counts) {
+      const int cnt = t < tiles ? counts[t] : 0;
+      int start, ptotal;
+      Scan(tmp).ExclusiveSum(cnt, start, ptotal);
+      __syncthreads();
+      if (cnt > 0) r = make_int2(pcarry + start, pcarry + start + cnt);
+      if (t < tiles) ranges[t] = r;
+      __syncthreads();
+      if (threadIdx.x == 0) pcarry += ptotal;
+    } else if (t < tiles) {
+      r = ranges[t];
+    }
     const int nch = (r.y - r.x + CH - 1) / CH;
     int excl, total;
     Scan(tmp).ExclusiveSum(nch, excl, total);
@@ -497,6 +561,159 @@ __device__ __forceinline__ int xcd_item(int b, int nwg) {
 #endif
   const int q = nwg >> 3, r = nwg & 7, xcd = b & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+// ---- Stable counting sort of the pairs by tile -------------------------------------------------
+// The emitted pairs are cut into columns of cw consecutive pairs, one workgroup of `waves` waves
+// per column, wave w owning the w-th part of its column.
+//   k_tile_count    counts each column's pairs per tile into M[column][tile];
+//   k_tile_colscan  scans M over the columns of each tile (S = start of (column, tile) within the
+//                   tile) and writes the tile's total T[tile];
+//   k_work_items    scans T into the tile ranges (and cuts the work items);
+//   k_tile_place    re-counts per wave, turns ranges + S into per-wave cursors and walks each wave's
+//                   pairs in order, 64 at a time.  Lanes holding the same tile in one step are ranked
+//                   by bit-plane ballots (one ballot per key bit: the lanes agreeing with this lane on
+//                   every bit), and the highest lane of each group advances the tile's cursor.
+// Everything is walked in pair order, so the Gaussian ids inside each tile come out ascending:
+// exactly the oracle's stable sort (oracle/gr_oracle.c gro_bin), and deterministic.
+constexpr int TS_SEG = 32;  // 64-pair steps per register-resident segment (2048 pairs per wave)
+
+__global__ __launch_bounds__(256) void k_tile_count(int64_t K, int cw, int cols, int tiles,
+                                                    const uint16_t* __restrict__ keys, int* __restrict__ M) {
+  extern __shared__ int hist[];
+  const int c = xcd_item(blockIdx.x, cols);
+  for (int t = threadIdx.x; t < tiles; t += 256) hist[t] = 0;
+  __syncthreads();
+  const int64_t k0 = (int64_t)c * cw, k1 = min(K, k0 + cw);
+  for (int64_t kb = k0 + threadIdx.x; kb < k1; kb += 256 * 8) {
+    int d[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = kb + j * 256 < k1 ? (int)keys[kb + j * 256] : -1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (d[j] >= 0) atomicAdd(&hist[d[j]], 1);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < tiles; t += 256) M[(size_t)c * tiles + t] = hist[t];
+}
+
+// Column scan of M: S[c][t] = sum of M[c'][t] over c' < c, T[t] = the tile's total.  A block takes 16
+// tiles x 64 column groups, so every wave reads 64-byte runs of 16 tiles and the whole chip is busy.
+constexpr int CS_T = 16, CS_G = 64;
+
+__global__ __launch_bounds__(1024) void k_tile_colscan(int cols, int tiles, const int* __restrict__ M,
+                                                       int* __restrict__ S, int* __restrict__ T) {
+  __shared__ int part[CS_G][CS_T + 1];
+  const int tl = (int)threadIdx.x % CS_T, g = (int)threadIdx.x / CS_T;
+  const int t = (int)blockIdx.x * CS_T + tl;
+  const int per = (cols + CS_G - 1) / CS_G;
+  const int c0 = min(cols, g * per), c1 = min(cols, c0 + per);
+  int sum = 0;
+  if (t < tiles) {
+#pragma unroll 8
+    for (int c = c0; c < c1; ++c) sum += M[(size_t)c * tiles + t];
+  }
+  part[g][tl] = sum;
+  __syncthreads();
+  if (g == 0) {
+    int run = 0;
+    for (int u = 0; u < CS_G; ++u) {
+      const int v = part[u][tl];
+      part[u][tl] = run;
+      run += v;
+    }
+    if (t < tiles) T[t] = run;
+  }
+  __syncthreads();
+  if (t < tiles) {
+    int run = part[g][tl];
+#pragma unroll 8
+    for (int c = c0; c < c1; ++c) {
+      const int v = M[(size_t)c * tiles + t];
+      S[(size_t)c * tiles + t] = run;
+      run += v;
+    }
+  }
+}
+
+__device__ __forceinline__ void ts_load(int64_t kb, int64_t k1, int64_t klast, int lane, const uint16_t* __restrict__ keys,
+                                        const int* __restrict__ ids_in, int (&d)[TS_SEG], int (&id)[TS_SEG]) {
+  // branch-free: out-of-range lanes load the last pair (K >= 1) and are marked d = -1
+#pragma unroll
+  for (int j = 0; j < TS_SEG; ++j) {
+    const int64_t k = kb + j * 64 + lane;
+    const int64_t kc = k < k1 ? k : klast;
+    const int key = (int)keys[kc];
+    id[j] = ids_in[kc];
+    d[j] = k < k1 ? key : -1;
+  }
+}
+
+// One register-resident segment of k_tile_place: 32 steps of 64 pairs, in pair order.
+__device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int (&d)[TS_SEG], const int (&id)[TS_SEG],
+                                         int* __restrict__ ids_out) {
+  const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int j = 0; j < TS_SEG; ++j) {
+    const bool ok = d[j] >= 0;
+    uint64_t m = __ballot(ok);
+    if (m == 0) break;  // wave-uniform: the rest of this wave's range is past its end
+    for (int b = 0; b < bits; ++b) {
+      const bool bit = (d[j] >> b) & 1;
+      const uint64_t v = __ballot(bit);
+      m &= bit ? v : ~v;
+    }
+    if (ok) {
+      const int pos = my[d[j]] + __popcll(m & below);
+      ids_out[pos] = id[j];
+      __builtin_amdgcn_wave_barrier();  // every lane has read the cursor before it moves
+      if ((m >> lane) == 1ull) my[d[j]] = pos + 1;  // highest lane of its group
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_tile_place(int64_t K, int cw, int cols, int tiles, int bits,
+                                                    const uint16_t* __restrict__ keys, const int* __restrict__ ids_in,
+                                                    const int* __restrict__ S, const int2* __restrict__ ranges,
+                                                    int* __restrict__ ids_out) {
+  extern __shared__ int cur[];  // [waves][tiles]
+  const int c = xcd_item(blockIdx.x, cols);
+  const int waves = (int)blockDim.x >> 6, w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+  int* my = cur + (size_t)w * tiles;
+  const int pw = cw / waves, nseg = pw / (64 * TS_SEG);
+  const int64_t k0 = (int64_t)c * cw + (int64_t)w * pw, k1 = min(K, k0 + pw);
+  int d[TS_SEG], id[TS_SEG];
+  ts_load(k0, k1, K - 1, lane, keys, ids_in, d, id);  // in flight while the counters are cleared
+  for (int t = lane; t < tiles; t += 64) my[t] = 0;
+  __builtin_amdgcn_wave_barrier();
+  for (int seg = 0; seg < nseg; ++seg) {  // this wave's count per tile
+    if (seg > 0) ts_load(k0 + (int64_t)seg * 64 * TS_SEG, k1, K - 1, lane, keys, ids_in, d, id);
+    // ids are >= 0, so the increment is 1; using id[j] here makes the wave wait for the id loads
+    // now, before any store: on gfx9 loads and stores share vmcnt, and a load still pending after a
+    // store forces a full vmcnt(0) (i.e. waiting for every earlier store) before each later store.
+#pragma unroll
+    for (int j = 0; j < TS_SEG; ++j) atomicAdd(&my[d[j] < 0 ? 0 : d[j]], (d[j] < 0 ? 0 : 1) + (id[j] >> 31));
+  }
+  __syncthreads();
+  // cursor of (tile, wave) = tile start + column start within the tile + lower waves' counts
+#pragma unroll 4
+  for (int t = threadIdx.x; t < tiles; t += blockDim.x) {
+    int run = ranges[t].x + S[(size_t)c * tiles + t];
+    for (int u = 0; u < waves; ++u) {
+      const int n = cur[(size_t)u * tiles + t];
+      cur[(size_t)u * tiles + t] = run;
+      run += n;
+    }
+  }
+  __syncthreads();
+  if (nseg == 1) {
+    ts_place(lane, bits, my, d, id, ids_out);  // keys and ids are still in registers
+  } else {
+    for (int seg = 0; seg < nseg; ++seg) {
+      ts_load(k0 + (int64_t)seg * 64 * TS_SEG, k1, K - 1, lane, keys, ids_in, d, id);
+      ts_place(lane, bits, my, d, id, ids_out);
+    }
+  }
 }
 
 // Forward: one workgroup (4 waves) per work item.  Batches of 256 Gaussians go through a double-
@@ -1225,8 +1442,7 @@ size_t gr_fwd_scratch_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
   const int tiles = tiles_x_of(v->width) * tiles_y_of(v->height);
   size_t off[3];
-  return scratch_fixed(tiles, plan->num_pairs, off) +
-         align_up(sort_tmp_bytes<uint32_t>(plan->num_pairs, bits_for((uint32_t)tiles)));
+  return scratch_fixed(tiles, plan->num_pairs, off) + align_up(tile_sort_tmp_bytes(plan->num_pairs, tiles));
 }
 
 // Backward workspace: pair partials (one 9-float slot per rectangle tile) + per-pixel upstream
@@ -1288,27 +1504,57 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
   const int tiles = vk.tiles_x * vk.tiles_y;
   Bins b = bins_view(bins, tiles, num_pairs);
   Scratch sc = scratch_view(scratch, tiles, num_pairs);
-  GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * tiles, s));
   prof_mark(PROF_BINNING, s);
   if (n > 0 && num_pairs > 0) {
     Geom g = geom_view((void*)geom, n);
-    hipLaunchKernelGGL((k_emit<uint32_t, unsigned long long>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
-                       (const int4*)g.rect, (const unsigned long long*)g.counts, (const unsigned long long*)g.offsets,
-                       (const float4*)g.recA, (const uint32_t*)nullptr, sc.keys_in, sc.ids_in);
-    GR_HIP_TRY(hipGetLastError());
-    const int bits = bits_for((uint32_t)tiles);
-    size_t tmp = sort_tmp_bytes<uint32_t>(num_pairs, bits);
-    GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp, tmp, sc.keys_in, b.keys, sc.ids_in, b.ids, (int)num_pairs, 0,
-                                                  bits, s));
-    hipLaunchKernelGGL(k_ranges<uint32_t>, dim3(blocks_for(num_pairs)), dim3(256), 0, s, num_pairs, b.keys, b.ranges);
-    GR_HIP_TRY(hipGetLastError());
+    const auto* cnt = (const unsigned long long*)g.counts;
+    const auto* offs = (const unsigned long long*)g.offsets;
+    if (short_keys(tiles)) {
+      hipLaunchKernelGGL((k_emit<uint16_t, unsigned long long>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
+                         (const int4*)g.rect, cnt, offs, (const float4*)g.recA, (const uint16_t*)nullptr,
+                         (uint16_t*)sc.keys_in, sc.ids_in);
+      GR_HIP_TRY(hipGetLastError());
+      const TSortPlan tp = tsort_plan(num_pairs, tiles);
+      int* M = (int*)sc.sort_tmp;
+      int* S = (int*)((char*)sc.sort_tmp + align_up(tp.cells * sizeof(int)));
+      int* Tt = (int*)((char*)S + align_up(tp.cells * sizeof(int)));
+      const size_t lds_count = (size_t)tiles * sizeof(int), lds_place = lds_count * tp.waves;
+      hipLaunchKernelGGL(k_tile_count, dim3(tp.cols), dim3(256), lds_count, s, num_pairs, tp.cw, tp.cols, tiles,
+                         (const uint16_t*)sc.keys_in, M);
+      GR_HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_tile_colscan, dim3((tiles + CS_T - 1) / CS_T), dim3(CS_T * CS_G), 0, s, tp.cols, tiles,
+                         (const int*)M, S, Tt);
+      GR_HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, tiles, b.ranges, (const int*)Tt, b.items,
+                         b.num_items, b.tile_item0);
+      GR_HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_tile_place, dim3(tp.cols), dim3(64 * tp.waves), lds_place, s, num_pairs, tp.cw, tp.cols,
+                         tiles, bits_for((uint32_t)tiles), (const uint16_t*)sc.keys_in, (const int*)sc.ids_in,
+                         (const int*)S, (const int2*)b.ranges, b.ids);
+    } else {
+      hipLaunchKernelGGL((k_emit<uint32_t, unsigned long long>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
+                         (const int4*)g.rect, cnt, offs, (const float4*)g.recA, (const uint32_t*)nullptr, sc.keys_in,
+                         sc.ids_in);
+      GR_HIP_TRY(hipGetLastError());
+      GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * tiles, s));
+      const int bits = bits_for((uint32_t)tiles);
+      size_t tmp = tile_sort_tmp_bytes(num_pairs, tiles);
+      GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp, tmp, sc.keys_in, b.keys, sc.ids_in, b.ids,
+                                                    (int)num_pairs, 0, bits, s));
+      hipLaunchKernelGGL(k_ranges<uint32_t>, dim3(blocks_for(num_pairs)), dim3(256), 0, s, num_pairs, b.keys, b.ranges);
+      GR_HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, tiles, b.ranges, (const int*)nullptr, b.items,
+                         b.num_items, b.tile_item0);
+    }
+  } else {
+    GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * tiles, s));
+    hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, tiles, b.ranges, (const int*)nullptr, b.items,
+                       b.num_items, b.tile_item0);
   }
-  Geom g = geom_view((void*)geom, n > 0 ? n : 1);
-  const size_t HW = (size_t)v->width * v->height;
-  hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, tiles, (const int2*)b.ranges, b.items, b.num_items,
-                     b.tile_item0);
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_BINNING, s);
+  Geom g = geom_view((void*)geom, n > 0 ? n : 1);
+  const size_t HW = (size_t)v->width * v->height;
   const int64_t cap = item_cap(tiles, num_pairs);
   if (num_pairs > 0) {
     prof_mark(PROF_RASTER_FWD, s);

@@ -108,15 +108,19 @@ def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=CUTOFF)
     bins = st.bins.cpu().numpy()
     K = st.num_pairs
     tiles = ((W + 15) // 16) * ((H + 15) // 16)
-    keys = bins[b_off[0]: b_off[0] + 4 * K].view(np.uint32)
     ids = bins[b_off[1]: b_off[1] + 4 * K].view(np.int32)
     ranges = bins[b_off[2]: b_off[2] + 8 * tiles].view(np.int32).reshape(tiles, 2)
+    # the counting sort keeps no sorted key array: the sorted keys are implied by the tile ranges
+    keys = np.repeat(np.arange(tiles, dtype=np.uint32), np.maximum(ranges[:, 1] - ranges[:, 0], 0))
+    assert keys.size == K
     return dict(recA=recA, rect=rect, counts=counts, offsets=offsets, keys=keys, ids=ids, ranges=ranges, K=K, areas=areas,
                 slots=int(st.plan.num_slots))
 
 
-@pytest.mark.parametrize("case", ["f1_n300_64x48", "f2_c1_view1", "c2_100k_512", "edge_big_sigma"])
+@pytest.mark.parametrize("case", ["f1_n300_64x48", "f2_c1_view1", "c2_100k_512", "edge_big_sigma", "hd_1920x1080",
+                                  "xl_2304x2304"])
 def test_bins_bit_exact(pkg, cuda, case):
+    """hd: 8160 tiles (counting sort, 2 waves per column); xl: 20736 tiles (radix-sort fallback)."""
     if case.startswith("f"):
         d = golden(case)
         scene = orc.Scene(d["means"], d["scales"], d["colors"], d["opacities"])
@@ -125,6 +129,10 @@ def test_bins_bit_exact(pkg, cuda, case):
         scene = orc.synthetic_scene(100_000, seed=3)
         view, proj = orc.orbit_cameras(8, 512, 512)[5]
         W = H = 512
+    elif case in ("hd_1920x1080", "xl_2304x2304"):
+        W, H = (1920, 1080) if case.startswith("hd") else (2304, 2304)
+        scene = orc.synthetic_scene(60_000, seed=6)
+        view, proj = orc.orbit_cameras(8, W, H)[3]
     else:
         scene = orc.synthetic_scene(2000, seed=4, scale=0.4)  # huge footprints, many clipped rects
         view, proj = orc.orbit_cameras(3, 200, 120)[1]
