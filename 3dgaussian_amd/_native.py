@@ -154,7 +154,8 @@ def version() -> str:
 
 
 def geom_layout(n: int):
-    out = (ctypes.c_size_t * 6)()
+    """[records (n x 64 B), rect, counts, offsets, end of the fixed part] (include/gr_hip.h)."""
+    out = (ctypes.c_size_t * 5)()
     lib().gr_geom_layout(int(n), out)
     return list(out)
 

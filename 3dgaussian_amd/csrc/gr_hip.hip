@@ -166,7 +166,7 @@ __device__ __forceinline__ int tile_rect(const ViewK& v, const Proj& p, float op
 
 // Tile culling inside the rectangle (oracle/gr_oracle.c tile_pass, bit-exact): keep tile (tx,ty) iff
 // the Gaussian's largest weight over the tile's pixel centres (clipped to the image) is
-// >= o * exp(-cutoff^2/2).  q = -0.5 log2(e) / sigma^2 as stored in recA.
+// >= o * exp(-cutoff^2/2).  q = -0.5 log2(e) / sigma^2 as stored in record word A.
 __device__ __forceinline__ bool tile_pass(const ViewK& v, float px, float py, float qx, float qy, int tx, int ty) {
   const float thr = (-0.5f * LOG2E) * (v.cutoff * v.cutoff);
   const int xe = min(tx * T + T - 1, v.W - 1), ye = min(ty * T + T - 1, v.H - 1);
@@ -181,19 +181,26 @@ __device__ __forceinline__ bool tile_pass(const ViewK& v, float px, float py, fl
 
 __device__ __forceinline__ float qcoef(float s) { return (-0.5f * LOG2E) / (s * s); }
 
-// Partial-sum slot of pair (Gaussian, tile (tx,ty)): the Gaussian's first slot (high word of its
-// packed offset) + the tile's index inside its rectangle (culled tiles leave unused slots).
-__device__ __forceinline__ int pair_slot(unsigned long long off, const int4 r, int tx, int ty) {
-  return (int)(off >> 32) + (ty - r.y) * (r.z - r.x + 1) + (tx - r.x);
+// Partial-sum slot of pair (Gaussian, tile (tx,ty)) from the record's word C: the Gaussian's first
+// slot + the tile's index inside its rectangle (culled tiles leave unused slots).
+__device__ __forceinline__ int pair_slot(const float4 c, int tx, int ty) {
+  const unsigned rxy = __float_as_uint(c.z);
+  return (int)__float_as_uint(c.y) + (ty - (int)(rxy >> 16)) * (int)__float_as_uint(c.w) + (tx - (int)(rxy & 0xffffu));
 }
 
 // ------------------------------------------------------------------------------------------------
 // Geometry buffer layout.
 // ------------------------------------------------------------------------------------------------
+// Per-Gaussian raster record, 64 bytes = one aligned 64-byte segment, so the random per-pair gathers of
+// the raster kernels touch one memory segment per pair (instead of one per field array):
+//   rec[4i+0] = A: px, py, qx, qy  (q = -0.5*log2(e)/sigma^2)
+//   rec[4i+1] = B: o, r, g, b (clamped)
+//   rec[4i+2] = C: z_abs, first slot (int bits, written by k_emit), rect.x | rect.y << 16, rect width
+//   rec[4i+3] = unused (zero)
+constexpr int REC4 = 4;  // float4 per record
+
 struct Geom {
-  float4* recA;  // px, py, qx, qy  (q = -0.5*log2(e)/sigma^2)
-  float4* recB;  // o, r, g, b (clamped)
-  float* recZ;   // z_abs
+  float4* rec;   // [n][4] raster records
   int4* rect;    // tile rectangle
   // packed (rect area << 32 | kept tiles): the exclusive scan gives, per Gaussian, the first pair
   // index (low word) and the first partial-sum slot (high word; one slot per rectangle tile)
@@ -203,15 +210,15 @@ struct Geom {
   size_t scan_tmp_bytes;
 };
 
-size_t geom_fixed(int n, size_t off[6]) {
+// off: [0] records, [1] rect, [2] counts, [3] offsets, [4] scan temp (= end of the fixed part)
+size_t geom_fixed(int n, size_t off[5]) {
   size_t o = 0;
   const size_t nn = (size_t)(n > 0 ? n : 1);
-  off[0] = o; o = align_up(o + nn * sizeof(float4));
-  off[1] = o; o = align_up(o + nn * sizeof(float4));
-  off[2] = o; o = align_up(o + nn * sizeof(float));
-  off[3] = o; o = align_up(o + nn * sizeof(int4));
-  off[4] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
-  off[5] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
+  off[0] = o; o = align_up(o + nn * REC4 * sizeof(float4));
+  off[1] = o; o = align_up(o + nn * sizeof(int4));
+  off[2] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
+  off[3] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
+  off[4] = o;
   return o;
 }
 
@@ -224,16 +231,14 @@ size_t scan_tmp_bytes_t(int n) {
 size_t scan_tmp_bytes(int n) { return scan_tmp_bytes_t<unsigned long long>(n); }
 
 Geom geom_view(void* base, int n) {
-  size_t off[6];
+  size_t off[5];
   const size_t fixed = geom_fixed(n, off);
   char* b = (char*)base;
   Geom g;
-  g.recA = (float4*)(b + off[0]);
-  g.recB = (float4*)(b + off[1]);
-  g.recZ = (float*)(b + off[2]);
-  g.rect = (int4*)(b + off[3]);
-  g.counts = (unsigned long long*)(b + off[4]);
-  g.offsets = (unsigned long long*)(b + off[5]);
+  g.rec = (float4*)(b + off[0]);
+  g.rect = (int4*)(b + off[1]);
+  g.counts = (unsigned long long*)(b + off[2]);
+  g.offsets = (unsigned long long*)(b + off[3]);
   g.scan_tmp = b + fixed;
   g.scan_tmp_bytes = 0;
   return g;
@@ -396,9 +401,12 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, int n, const float*
     for (int ty = r.y; ty <= r.w; ++ty)
       for (int tx = r.x; tx <= r.z; ++tx) cnt += tile_pass(v, p.px, p.py, qx, qy, tx, ty) ? 1 : 0;
   }
-  g.recA[i] = make_float4(p.px, p.py, qx, qy);
-  g.recB[i] = make_float4(op < 0.0f ? 0.0f : op, clamp01(c[0]), clamp01(c[1]), clamp01(c[2]));
-  g.recZ[i] = p.za;
+  float4* rec = g.rec + (size_t)REC4 * i;
+  rec[0] = make_float4(p.px, p.py, qx, qy);
+  rec[1] = make_float4(op < 0.0f ? 0.0f : op, clamp01(c[0]), clamp01(c[1]), clamp01(c[2]));
+  rec[2] = make_float4(p.za, 0.0f, __uint_as_float((unsigned)r.x | ((unsigned)r.y << 16)),
+                       __uint_as_float((unsigned)(r.z - r.x + 1)));
+  rec[3] = make_float4(0.f, 0.f, 0.f, 0.f);
   g.rect[i] = r;
   g.counts[i] = cnt > 0 ? (((unsigned long long)area << 32) | (unsigned)cnt) : 0ull;
 }
@@ -410,9 +418,10 @@ constexpr int EWIN = 4096;  // pairs staged in LDS per emit block
 template <typename KeyT, typename OffT>
 __global__ __launch_bounds__(256) void k_emit(ViewK v, int n, const int4* __restrict__ rect,
                                               const OffT* __restrict__ counts, const OffT* __restrict__ offsets,
-                                              const float4* __restrict__ recA, const KeyT* __restrict__ low_keys,
+                                              float4* __restrict__ rec, const KeyT* __restrict__ low_keys,
                                               KeyT* keys, int* ids) {
-  // recA != nullptr: differentiable path, tiles culled by tile_pass; nullptr: legacy full rectangle
+  // rec != nullptr: differentiable path, tiles culled by tile_pass, first slot stored in the record;
+  // nullptr: legacy full rectangle
   __shared__ KeyT sK[EWIN];
   __shared__ int sI[EWIN];
   const int g0 = blockIdx.x * 256;
@@ -424,10 +433,16 @@ __global__ __launch_bounds__(256) void k_emit(ViewK v, int n, const int4* __rest
     const int4 r = rect[i];
     int k = (int)(offsets[i] & 0xffffffffu);  // pair index (low word when packed)
     const KeyT low = low_keys ? low_keys[i] : (KeyT)0;
-    const float4 a = recA ? recA[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (sizeof(OffT) == 8) {
+      if (rec) {
+        a = rec[(size_t)REC4 * i];
+        rec[(size_t)REC4 * i + 2].y = __uint_as_float((unsigned)(offsets[i] >> 32));
+      }
+    }
     for (int ty = r.y; ty <= r.w; ++ty)
       for (int tx = r.x; tx <= r.z; ++tx) {
-        if (recA && !tile_pass(v, a.x, a.y, a.z, a.w, tx, ty)) continue;
+        if (rec && !tile_pass(v, a.x, a.y, a.z, a.w, tx, ty)) continue;
         const KeyT t = (KeyT)(ty * v.tiles_x + tx);
         KeyT key;
         if constexpr (sizeof(KeyT) == 8)
@@ -522,8 +537,7 @@ __global__ __launch_bounds__(1024) void k_work_items(int tiles, int2* __restrict
 
 // Gaussian records of one 256-wide batch, staged through registers (load early, write late).
 struct StageRec {
-  float4 a, b;
-  float z;
+  float4 a, b, c;  // record words A, B, C
   int g;
 };
 
@@ -534,18 +548,18 @@ __device__ __forceinline__ int stage_id(int k, int k1, const int* __restrict__ i
 
 // Records of Gaussian g (g < 0: padding).  Padding has o = 0 and px = +huge, so every weight it
 // produces is exactly 0 (exp2(-inf) = 0) without a per-element select.
-__device__ __forceinline__ StageRec stage_rec(int g, const float4* __restrict__ recA, const float4* __restrict__ recB,
-                                             const float* __restrict__ recZ) {
+__device__ __forceinline__ StageRec stage_rec(int g, const float4* __restrict__ rec) {
   StageRec r;
   r.g = g;
   if (g >= 0) {
-    r.a = recA[g];
-    r.b = recB[g];
-    r.z = recZ[g];
+    const float4* p = rec + (size_t)REC4 * g;
+    r.a = p[0];
+    r.b = p[1];
+    r.c = p[2];
   } else {
     r.a = make_float4(1e30f, 1e30f, -1.0f, -1.0f);
     r.b = make_float4(0.f, 0.f, 0.f, 0.f);
-    r.z = 0.f;
+    r.c = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   return r;
 }
@@ -721,8 +735,7 @@ __global__ __launch_bounds__(256) void k_tile_place(int64_t K, int cw, int cols,
 // (the MFMA K dimension).  Padding entries are exact zeros, so whole blocks are processed.
 __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, const int4* __restrict__ items,
                                                          const int* __restrict__ num_items, const int2* __restrict__ ranges,
-                                                         const int* __restrict__ ids, const float4* __restrict__ recA,
-                                                         const float4* __restrict__ recB, const float* __restrict__ recZ,
+                                                         const int* __restrict__ ids, const float4* __restrict__ rec,
                                                          float* __restrict__ fwd_part, float* __restrict__ out_rgb,
                                                          float* __restrict__ out_alpha, float* __restrict__ out_depth,
                                                          float4* __restrict__ saved4, float* __restrict__ savedD) {
@@ -739,7 +752,7 @@ __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, const int4* __
   const float xc = (float)(tx * T + li) + 0.5f;  // A row = x
   const float yc = (float)(ty * T + li) + 0.5f;  // B col = y
   f32x4 cW = {0.f, 0.f, 0.f, 0.f}, cR = cW, cG = cW, cB = cW, cD = cW;
-  StageRec st = stage_rec(stage_id(k0 + tid, k1, ids), recA, recB, recZ);
+  StageRec st = stage_rec(stage_id(k0 + tid, k1, ids), rec);
   int idn = stage_id(k0 + TP + tid, k1, ids);
   int buf = 0;
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
@@ -748,9 +761,9 @@ __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, const int4* __
     float* sZ = reinterpret_cast<float*>(sB + TP);
     sA[tid] = st.a;
     sB[tid] = st.b;
-    sZ[tid] = st.z;
+    sZ[tid] = st.c.x;
     __syncthreads();  // the other buffer's readers (previous batch) are also past this point
-    st = stage_rec(idn, recA, recB, recZ);
+    st = stage_rec(idn, rec);
     idn = stage_id(base + 2 * TP + tid, k1, ids);
     const int cnt = min(TP, k1 - base) - wave * 64;           // Gaussians of this batch for this wave
     const int nblk = cnt <= 0 ? 0 : min(4, (cnt + 15) >> 4);  // blocks of 4 steps (16 Gaussians)
@@ -919,9 +932,7 @@ __device__ __forceinline__ float pair32(float ab, float cd) {
 
 __global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
     ViewK v, const int4* __restrict__ items, const int* __restrict__ num_items, const int* __restrict__ ids,
-    const float4* __restrict__ recA, const float4* __restrict__ recB, const float* __restrict__ recZ,
-    const int4* __restrict__ rect, const unsigned long long* __restrict__ offsets, const float* __restrict__ U,
-    float* __restrict__ partials) {
+    const float4* __restrict__ rec, const float* __restrict__ U, float* __restrict__ partials) {
   __shared__ __attribute__((aligned(16))) float4 sA[2][TP];
   __shared__ __attribute__((aligned(16))) float4 sB[2][TP];
   __shared__ float sZ[2][TP];
@@ -943,18 +954,18 @@ __global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
       for (int s = 0; s < 4; ++s) A[k][s] = Ut[k * TP + li * T + 4 * s + xs];
   }
   const float x0 = (float)(tx * T) + 0.5f, y0 = (float)(ty * T) + 0.5f;
-  StageRec st = stage_rec(stage_id(k0 + tid, k1, ids), recA, recB, recZ);
-  int slot = st.g >= 0 ? pair_slot(offsets[st.g], rect[st.g], tx, ty) : -1;
+  StageRec st = stage_rec(stage_id(k0 + tid, k1, ids), rec);
+  int slot = st.g >= 0 ? pair_slot(st.c, tx, ty) : -1;
   int idn = stage_id(k0 + TP + tid, k1, ids);
   int buf = 0;
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
     sA[buf][tid] = st.a;
     sB[buf][tid] = st.b;
-    sZ[buf][tid] = st.z;
+    sZ[buf][tid] = st.c.x;
     sSlot[buf][tid] = slot;
     __syncthreads();  // the other buffer's readers (previous batch) are also past this point
-    st = stage_rec(idn, recA, recB, recZ);
-    slot = st.g >= 0 ? pair_slot(offsets[st.g], rect[st.g], tx, ty) : -1;
+    st = stage_rec(idn, rec);
+    slot = st.g >= 0 ? pair_slot(st.c, tx, ty) : -1;
     idn = stage_id(base + 2 * TP + tid, k1, ids);
     const int cnt = min(TP, k1 - base) - wave * 64;
     const int ngr = cnt <= 0 ? 0 : min(4, (cnt + 15) >> 4);
@@ -1039,7 +1050,7 @@ __device__ void chain_rule(const ViewK& v, int i, const double* S, unsigned cnt,
 template <int CD>
 __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const float* __restrict__ means,
                                                     const float* __restrict__ scales, const float* __restrict__ colors,
-                                                    const float* __restrict__ opac, const float4* __restrict__ recA,
+                                                    const float* __restrict__ opac, const float4* __restrict__ rec,
                                                     const int4* __restrict__ rect,
                                                     const unsigned long long* __restrict__ counts,
                                                     const unsigned long long* __restrict__ offsets,
@@ -1082,7 +1093,7 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
       const long long base = (long long)(offsets[i] >> 32);
       const float* src = staged ? sP + (base * NPART - fa) : partials + base * NPART;
       const int4 r = rect[i];
-      const float4 a = recA[i];
+      const float4 a = rec[(size_t)REC4 * i];
       const int w = r.z - r.x + 1, area = w * (r.w - r.y + 1);
       // tiles j = q4, q4+4, ... of the rectangle in scan order, stepped without division
       int tx = r.x + q4, ty = r.y;
@@ -1413,7 +1424,7 @@ gr_status gr_profile_end(double total_ms[4], int launches[4]) {
 }
 const char* gr_version(void) { return GR_VERSION_STR; }
 
-void gr_geom_layout(int n, size_t offsets_out[6]) { geom_fixed(n, offsets_out); }
+void gr_geom_layout(int n, size_t offsets_out[5]) { geom_fixed(n, offsets_out); }
 
 void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[3]) {
   (void)n;
@@ -1425,7 +1436,7 @@ void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets
 }
 
 size_t gr_geom_bytes(int n) {
-  size_t off[6];
+  size_t off[5];
   return geom_fixed(n, off) + align_up(scan_tmp_bytes(n > 0 ? n : 1));
 }
 
@@ -1511,7 +1522,7 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
     const auto* offs = (const unsigned long long*)g.offsets;
     if (short_keys(tiles)) {
       hipLaunchKernelGGL((k_emit<uint16_t, unsigned long long>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
-                         (const int4*)g.rect, cnt, offs, (const float4*)g.recA, (const uint16_t*)nullptr,
+                         (const int4*)g.rect, cnt, offs, g.rec, (const uint16_t*)nullptr,
                          (uint16_t*)sc.keys_in, sc.ids_in);
       GR_HIP_TRY(hipGetLastError());
       const TSortPlan tp = tsort_plan(num_pairs, tiles);
@@ -1533,7 +1544,7 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
                          (const int*)S, (const int2*)b.ranges, b.ids);
     } else {
       hipLaunchKernelGGL((k_emit<uint32_t, unsigned long long>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
-                         (const int4*)g.rect, cnt, offs, (const float4*)g.recA, (const uint32_t*)nullptr, sc.keys_in,
+                         (const int4*)g.rect, cnt, offs, g.rec, (const uint32_t*)nullptr, sc.keys_in,
                          sc.ids_in);
       GR_HIP_TRY(hipGetLastError());
       GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * tiles, s));
@@ -1559,7 +1570,7 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
   if (num_pairs > 0) {
     prof_mark(PROF_RASTER_FWD, s);
     hipLaunchKernelGGL(k_raster_fwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, (const int4*)b.items,
-                       (const int*)b.num_items, (const int2*)b.ranges, (const int*)b.ids, g.recA, g.recB, g.recZ,
+                       (const int*)b.num_items, (const int2*)b.ranges, (const int*)b.ids, (const float4*)g.rec,
                        sc.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_FWD, s);
@@ -1599,20 +1610,19 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
     const int64_t cap = item_cap(tiles, num_pairs);
     prof_mark(PROF_RASTER_BWD, s);
     hipLaunchKernelGGL(k_raster_bwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, (const int4*)b.items,
-                       (const int*)b.num_items, (const int*)b.ids, g.recA, g.recB, g.recZ, g.rect,
-                       (const unsigned long long*)g.offsets, (const float*)U, partials);
+                       (const int*)b.num_items, (const int*)b.ids, (const float4*)g.rec, (const float*)U, partials);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_BWD, s);
   }
   prof_mark(PROF_REDUCE, s);
   if (color_dim == 3)
     hipLaunchKernelGGL(k_reduce_bwd<3>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
-                       (const float4*)g.recA, (const int4*)g.rect, (const unsigned long long*)g.counts,
+                       (const float4*)g.rec, (const int4*)g.rect, (const unsigned long long*)g.counts,
                        (const unsigned long long*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
                        d_opacities);
   else
     hipLaunchKernelGGL(k_reduce_bwd<12>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
-                       (const float4*)g.recA, (const int4*)g.rect, (const unsigned long long*)g.counts,
+                       (const float4*)g.rec, (const int4*)g.rect, (const unsigned long long*)g.counts,
                        (const unsigned long long*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
                        d_opacities);
   GR_HIP_TRY(hipGetLastError());
@@ -1707,7 +1717,7 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
       uint64_t* kout = (uint64_t*)(e + q_kout);
       // low 32 bits = depth key; high bits = tile
       hipLaunchKernelGGL((k_emit<uint64_t, int>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n, (const int4*)lr.rect,
-                         (const int*)lr.counts, (const int*)lr.offsets, (const float4*)nullptr, (const uint64_t*)nullptr,
+                         (const int*)lr.counts, (const int*)lr.offsets, (float4*)nullptr, (const uint64_t*)nullptr,
                          kin, (int*)(e + q_iin));
       GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_patch_depth, dim3(blocks_for(K)), dim3(256), 0, s, (int64_t)K, kin, (const int*)(e + q_iin),
@@ -1720,7 +1730,7 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
       uint32_t* kin = (uint32_t*)(e + q_kin);
       uint32_t* kout = (uint32_t*)(e + q_kout);
       hipLaunchKernelGGL((k_emit<uint32_t, int>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n, (const int4*)lr.rect,
-                         (const int*)lr.counts, (const int*)lr.offsets, (const float4*)nullptr, (const uint32_t*)nullptr,
+                         (const int*)lr.counts, (const int*)lr.offsets, (float4*)nullptr, (const uint32_t*)nullptr,
                          kin, (int*)(e + q_iin));
       GR_HIP_TRY(hipGetLastError());
       GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e + q_tmp, t2, kin, kout, (int*)(e + q_iin), (int*)(e + q_iout), K, 0,

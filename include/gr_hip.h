@@ -134,12 +134,16 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
 /* ------------------------------------------------------------------------------------------ */
 
 /* Byte offsets of the sub-buffers inside geom / bins, for debugging and bit-exact tests.
- *   geom: [0] rec_a float4[n] (px,py,qx,qy)  [1] rec_b float4[n] (o,r,g,b)  [2] rec_z float[n]
- *         [3] rect int4[n] (tx0,ty0,tx1,ty1) [4] counts u64[n+1] [5] offsets u64[n+1]
+ *   geom: [0] records float4[n][4], 64 bytes per Gaussian:
+ *             A = (px, py, qx, qy), B = (o, r, g, b), C = (z, first slot as int bits,
+ *             tx0 | ty0 << 16 as uint bits, rectangle width as int bits), D = 0
+ *         [1] rect int4[n] (tx0,ty0,tx1,ty1) [2] counts u64[n+1] [3] offsets u64[n+1]
+ *         [4] end of the fixed part (scan temp follows)
  *         (counts/offsets packed: rectangle area / first slot in the high word, kept tiles / first
  *         pair in the low word)
- *   bins: [0] keys uint32[K] [1] gaussian ids int32[K] (tile-sorted) [2] ranges int2[tiles]  */
-void gr_geom_layout(int n, size_t offsets_out[6]);
+ *   bins: [0] keys (radix-sort fallback only, > 16384 tiles) [1] gaussian ids int32[K] (tile-sorted)
+ *         [2] ranges int2[tiles]  */
+void gr_geom_layout(int n, size_t offsets_out[5]);
 void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[3]);
 
 /* Live kernel timing with HIP events on the launch stream (bench.py).  Between begin and end,

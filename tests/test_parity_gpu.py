@@ -96,11 +96,13 @@ def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=CUTOFF)
     n = m.shape[0]
     g_off = nat.geom_layout(n)
     geom = st.geom.cpu().numpy()
-    recA = geom[g_off[0]: g_off[0] + 16 * n].view(np.float32).reshape(n, 4)
-    rect = geom[g_off[3]: g_off[3] + 16 * n].view(np.int32).reshape(n, 4)
+    rec = geom[g_off[0]: g_off[0] + 64 * n].view(np.float32).reshape(n, 16)  # 64-byte records A|B|C|D
+    recA = rec[:, 0:4]
+    recC = rec[:, 8:12].view(np.uint32)
+    rect = geom[g_off[1]: g_off[1] + 16 * n].view(np.int32).reshape(n, 4)
     # packed u64: low word = kept tiles / first pair, high word = rectangle area / first slot
-    counts64 = geom[g_off[4]: g_off[4] + 8 * n].view(np.uint64)
-    offsets64 = geom[g_off[5]: g_off[5] + 8 * (n + 1)].view(np.uint64)
+    counts64 = geom[g_off[2]: g_off[2] + 8 * n].view(np.uint64)
+    offsets64 = geom[g_off[3]: g_off[3] + 8 * (n + 1)].view(np.uint64)
     counts = (counts64 & 0xFFFFFFFF).astype(np.int32)
     offsets = (offsets64 & 0xFFFFFFFF).astype(np.int32)
     areas = (counts64 >> 32).astype(np.int64)
@@ -113,7 +115,7 @@ def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=CUTOFF)
     # the counting sort keeps no sorted key array: the sorted keys are implied by the tile ranges
     keys = np.repeat(np.arange(tiles, dtype=np.uint32), np.maximum(ranges[:, 1] - ranges[:, 0], 0))
     assert keys.size == K
-    return dict(recA=recA, rect=rect, counts=counts, offsets=offsets, keys=keys, ids=ids, ranges=ranges, K=K, areas=areas,
+    return dict(recA=recA, recC=recC, offsets64=offsets64, rect=rect, counts=counts, offsets=offsets, keys=keys, ids=ids, ranges=ranges, K=K, areas=areas,
                 slots=int(st.plan.num_slots))
 
 
@@ -151,6 +153,11 @@ def test_bins_bit_exact(pkg, cuda, case):
     area = (rect[:, 2] - rect[:, 0] + 1) * (rect[:, 3] - rect[:, 1] + 1)
     np.testing.assert_array_equal(g["areas"], np.where(kept, area, 0))
     assert g["slots"] == int(np.where(kept, area, 0).sum())
+    # record word C of kept Gaussians: first slot, packed rectangle origin, rectangle width
+    C = g["recC"][kept]
+    np.testing.assert_array_equal(C[:, 1], (g["offsets64"][:-1][kept] >> 32).astype(np.uint32))
+    np.testing.assert_array_equal(C[:, 2], (rect[kept, 0] | (rect[kept, 1] << 16)).astype(np.uint32))
+    np.testing.assert_array_equal(C[:, 3], (rect[kept, 2] - rect[kept, 0] + 1).astype(np.uint32))
     offsets, keys, vals, ranges = orc.bin_pairs(v, rec, rect, counts)
     np.testing.assert_array_equal(g["offsets"], offsets)
     assert g["K"] == len(vals)
