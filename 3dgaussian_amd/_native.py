@@ -76,6 +76,7 @@ _PP = ctypes.POINTER(GrPlan)
 _SIG = {
     "gr_geom_bytes": (ctypes.c_size_t, [ctypes.c_int]),
     "gr_fwd_prepare": (ctypes.c_int, [_VP, ctypes.c_int, _P, _P, _P, ctypes.c_int, _P, _P, ctypes.c_size_t, _PP, _P]),
+    "gr_fwd_prepare_async": (ctypes.c_int, [_VP, ctypes.c_int, _P, _P, _P, ctypes.c_int, _P, _P, ctypes.c_size_t, _P, _P]),
     "gr_bins_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
     "gr_saved_floats": (ctypes.c_size_t, [_VP]),
     "gr_fwd_scratch_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
@@ -154,8 +155,8 @@ def version() -> str:
 
 
 def geom_layout(n: int):
-    """[records (n x 64 B), rect, counts, offsets, end of the fixed part] (include/gr_hip.h)."""
-    out = (ctypes.c_size_t * 5)()
+    """[records (n x 64 B), rect, counts, offsets, device plan, end of the fixed part] (gr_hip.h)."""
+    out = (ctypes.c_size_t * 6)()
     lib().gr_geom_layout(int(n), out)
     return list(out)
 

@@ -206,19 +206,22 @@ struct Geom {
   // index (low word) and the first partial-sum slot (high word; one slot per rectangle tile)
   unsigned long long* counts;   // n+1
   unsigned long long* offsets;  // n+1
+  gr_plan* plan;                // device copy of the plan (gr_fwd_prepare_async copies it to the host)
   void* scan_tmp;
   size_t scan_tmp_bytes;
 };
 
-// off: [0] records, [1] rect, [2] counts, [3] offsets, [4] scan temp (= end of the fixed part)
-size_t geom_fixed(int n, size_t off[5]) {
+// off: [0] records, [1] rect, [2] counts, [3] offsets, [4] device copy of the plan,
+//      [5] scan temp (= end of the fixed part)
+size_t geom_fixed(int n, size_t off[6]) {
   size_t o = 0;
   const size_t nn = (size_t)(n > 0 ? n : 1);
   off[0] = o; o = align_up(o + nn * REC4 * sizeof(float4));
   off[1] = o; o = align_up(o + nn * sizeof(int4));
   off[2] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
   off[3] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
-  off[4] = o;
+  off[4] = o; o = align_up(o + sizeof(gr_plan));
+  off[5] = o;
   return o;
 }
 
@@ -231,10 +234,11 @@ size_t scan_tmp_bytes_t(int n) {
 size_t scan_tmp_bytes(int n) { return scan_tmp_bytes_t<unsigned long long>(n); }
 
 Geom geom_view(void* base, int n) {
-  size_t off[5];
+  size_t off[6];
   const size_t fixed = geom_fixed(n, off);
   char* b = (char*)base;
   Geom g;
+  g.plan = (gr_plan*)(b + off[4]);
   g.rec = (float4*)(b + off[0]);
   g.rect = (int4*)(b + off[1]);
   g.counts = (unsigned long long*)(b + off[2]);
@@ -1424,7 +1428,7 @@ gr_status gr_profile_end(double total_ms[4], int launches[4]) {
 }
 const char* gr_version(void) { return GR_VERSION_STR; }
 
-void gr_geom_layout(int n, size_t offsets_out[5]) { geom_fixed(n, offsets_out); }
+void gr_geom_layout(int n, size_t offsets_out[6]) { geom_fixed(n, offsets_out); }
 
 void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[3]) {
   (void)n;
@@ -1436,7 +1440,7 @@ void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets
 }
 
 size_t gr_geom_bytes(int n) {
-  size_t off[5];
+  size_t off[6];
   return geom_fixed(n, off) + align_up(scan_tmp_bytes(n > 0 ? n : 1));
 }
 
@@ -1465,17 +1469,29 @@ size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan) {
          align_up(tiles * 5 * TP * sizeof(float));
 }
 
-gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const float* scales, const float* colors,
-                         int color_dim, const float* opacities, void* geom, size_t geom_bytes, gr_plan* plan,
-                         void* stream) {
+// Decode the scanned total (high word: partial-sum slots, low word: pairs) into the plan; a count
+// that does not fit int32 is flagged as num_pairs = -1 (gr_fwd_render then reports the overflow).
+__global__ void k_plan(const unsigned long long* __restrict__ total, gr_plan* plan) {
+  const unsigned long long t = *total;
+  const long long pairs = (long long)(t & 0xffffffffull), slots = (long long)(t >> 32);
+  const bool ok = pairs < (1ll << 31) && slots < (1ll << 31);
+  plan->num_pairs = ok ? pairs : -1;
+  plan->num_slots = ok ? slots : -1;
+}
+
+gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, const float* scales, const float* colors,
+                               int color_dim, const float* opacities, void* geom, size_t geom_bytes, gr_plan* plan,
+                               void* stream) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
   if (n < 0) return set_error(GR_ERR_INVALID_ARGUMENT, "n must be >= 0");
   if (color_dim != 3 && color_dim != 12) return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3)");
   if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
-  plan->num_pairs = 0;
-  plan->num_slots = 0;
-  if (n == 0) return GR_OK;
+  if (n == 0) {
+    plan->num_pairs = 0;
+    plan->num_slots = 0;
+    return GR_OK;
+  }
   if (!means || !scales || !colors || !opacities || !geom) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
   if (geom_bytes < gr_geom_bytes(n)) return set_error(GR_ERR_WORKSPACE, "geom workspace too small");
   hipStream_t s = (hipStream_t)stream;
@@ -1488,13 +1504,23 @@ gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const floa
   GR_HIP_TRY(hipGetLastError());
   size_t tmp = scan_tmp_bytes(n);
   GR_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(g.scan_tmp, tmp, g.counts, g.offsets, n + 1, s));
-  unsigned long long total = 0;
-  GR_HIP_TRY(hipMemcpyAsync(&total, g.offsets + n, sizeof(total), hipMemcpyDeviceToHost, s));
-  GR_HIP_TRY(hipStreamSynchronize(s));
-  const unsigned long long pairs = total & 0xffffffffull, slots = total >> 32;
-  if (pairs >= (1ull << 31) || slots >= (1ull << 31)) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
-  plan->num_pairs = (int64_t)pairs;
-  plan->num_slots = (int64_t)slots;
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1), 0, s, (const unsigned long long*)(g.offsets + n), g.plan);
+  GR_HIP_TRY(hipGetLastError());
+  GR_HIP_TRY(hipMemcpyAsync(plan, g.plan, sizeof(gr_plan), hipMemcpyDeviceToHost, s));
+  return GR_OK;
+}
+
+gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const float* scales, const float* colors,
+                         int color_dim, const float* opacities, void* geom, size_t geom_bytes, gr_plan* plan,
+                         void* stream) {
+  if (plan) {
+    plan->num_pairs = 0;
+    plan->num_slots = 0;
+  }
+  gr_status st = gr_fwd_prepare_async(v, n, means, scales, colors, color_dim, opacities, geom, geom_bytes, plan, stream);
+  if (st != GR_OK || n == 0) return st;
+  GR_HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  if (plan->num_pairs < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
   return GR_OK;
 }
 
@@ -1504,6 +1530,7 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
   if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
+  if (plan->num_pairs < 0 || plan->num_slots < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
   if (!out_rgb || !saved) return set_error(GR_ERR_INVALID_ARGUMENT, "out_rgb and saved are required");
   if (n > 0 && (!geom || !bins)) return set_error(GR_ERR_INVALID_ARGUMENT, "null workspace");
   const int64_t num_pairs = plan->num_pairs;

@@ -104,9 +104,10 @@ def densify_and_prune(params: dict, max_gaussians: int, densify_ratio: float, pr
     return {k: torch.nn.Parameter(v.to(device)) for k, v in out.items()}
 
 
-def hip_render(means, scales, colors, opacities, cam, width, height, background):
+def hip_render(means, scales, colors, opacities, cam, width, height, background, prepared=None):
     return tr.render_gaussians_torch(means, scales, colors, opacities, cam, width=width, height=height,
-                                     background=background, max_gaussians=max(10000, int(means.shape[0])), return_aux=True)
+                                     background=background, max_gaussians=max(10000, int(means.shape[0])), return_aux=True,
+                                     prepared=prepared)
 
 
 class ViewShardedFitter:
@@ -132,10 +133,22 @@ class ViewShardedFitter:
     def reset_optimizer(self) -> None:
         self.opt = torch.optim.Adam(list(self.params.values()), lr=self.lr)
 
-    def view_loss(self, i: int, means, scales, colors, opacities) -> torch.Tensor:
+    def _background(self, device) -> torch.Tensor:
+        # one persistent tensor: the renderer reads its value on the host once, not per view
+        if getattr(self, "_bg", None) is None or self._bg.device != device:
+            self._bg = torch.zeros(3, device=device)
+        return self._bg
+
+    def _prepare(self, i: int, means, scales, colors, opacities):
+        cam = self.cams[i]
+        return tr.prepare_view(means, scales, colors, opacities, cam.view, cam.proj, self.width, self.height,
+                               self._background(means.device))
+
+    def view_loss(self, i: int, means, scales, colors, opacities, prepared=None) -> torch.Tensor:
         device = means.device
+        kw = {} if prepared is None else {"prepared": prepared}
         pred, alpha, depth = self.render_fn(means, scales, colors, opacities, self.cams[i], self.width, self.height,
-                                            torch.zeros(3, device=device))
+                                            self._background(device), **kw)
         loss = torch.mean(torch.abs(pred - self.targets[i]))
         if self.masks is not None and self.w_sil > 0.0:
             loss = loss + self.w_sil * torch.mean(torch.abs(alpha - self.masks[i]))
@@ -150,8 +163,16 @@ class ViewShardedFitter:
         means, scales, colors, opacities = activations(self.params)
         device = means.device
         total = torch.zeros((), device=device)
-        for i in self.my_views:
-            total = total + self.view_loss(i, means, scales, colors, opacities)
+        # HIP renderer: the next view's preparation is enqueued before this view renders, so the
+        # host reads each view's pair count while the device is still busy (no idle gap per view)
+        prefetch = self.render_fn is hip_render and means.device.type == "cuda" and means.shape[0] > 0
+        views = self.my_views
+        nxt = self._prepare(views[0], means, scales, colors, opacities) if prefetch and views else None
+        for j, i in enumerate(views):
+            cur = nxt
+            if prefetch and j + 1 < len(views):
+                nxt = self._prepare(views[j + 1], means, scales, colors, opacities)
+            total = total + self.view_loss(i, means, scales, colors, opacities, prepared=cur)
         loss = total / len(self.targets)
         if self.rank == 0:
             loss = loss + self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean()

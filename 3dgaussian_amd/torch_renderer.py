@@ -87,16 +87,23 @@ def look_at(eye: torch.Tensor, target: torch.Tensor, up: torch.Tensor) -> torch.
 _MAT_CACHE: dict = {}
 
 
-def _host_matrix(t: torch.Tensor) -> np.ndarray:
+def _host_copy(t: torch.Tensor, shape) -> np.ndarray:
+    """Host copy of a small (camera / background) tensor, cached per tensor and version: reading a
+    device tensor waits for the whole stream, so a view built from the same tensors twice must not
+    read them twice."""
     key = (id(t), t.data_ptr(), t._version, str(t.device))
     hit = _MAT_CACHE.get(key)
     if hit is not None and hit[0] is t:
         return hit[1]
-    m = t.detach().to(device="cpu", dtype=torch.float32).reshape(4, 4).numpy().copy()
+    m = t.detach().to(device="cpu", dtype=torch.float32).reshape(shape).numpy().copy()
     if len(_MAT_CACHE) > 4096:
         _MAT_CACHE.clear()
     _MAT_CACHE[key] = (t, m)
     return m
+
+
+def _host_matrix(t: torch.Tensor) -> np.ndarray:
+    return _host_copy(t, (4, 4))
 
 
 def make_view(view, proj, width: int, height: int, background=None, cutoff: float = DEFAULT_CUTOFF) -> _native.GrView:
@@ -112,7 +119,7 @@ def make_view(view, proj, width: int, height: int, background=None, cutoff: floa
     if background is None:
         bg = [0.0, 0.0, 0.0]
     elif isinstance(background, torch.Tensor):
-        bg = background.detach().to("cpu", torch.float32).reshape(3).tolist()
+        bg = _host_copy(background, (3,)).tolist()
     else:
         bg = np.asarray(background, np.float32).reshape(3).tolist()
     gv.background[:] = bg
@@ -140,19 +147,56 @@ class RenderState:
         return int(self.plan.num_pairs)
 
 
-def forward_native(means, scales, colors, opacities, gv: _native.GrView):
-    """Run gr_fwd_prepare + gr_fwd_render.  Returns (out, alpha, depth, RenderState)."""
+class Prepared:
+    """A view whose projection, culling and pair counting (gr_fwd_prepare_async) are enqueued.
+
+    The plan (pair / slot counts) arrives in pinned host memory; ``plan()`` waits for it.  Preparing
+    the next view before rendering the current one keeps the device busy while the host reads the
+    plan (ViewShardedFitter does this)."""
+
+    __slots__ = ("gv", "n", "geom", "plan_host", "event")
+
+    def __init__(self, gv, n, geom, plan_host, event):
+        self.gv, self.n, self.geom, self.plan_host, self.event = gv, n, geom, plan_host, event
+
+    def plan(self) -> _native.GrPlan:
+        self.event.synchronize()
+        pairs, slots = (int(x) for x in self.plan_host.tolist())
+        if pairs < 0 or slots < 0:
+            raise RuntimeError("gr_fwd_prepare: pair count overflows int32")
+        return _native.GrPlan(pairs, slots)
+
+
+def prepare_native(means, scales, colors, opacities, gv: _native.GrView) -> Prepared:
+    """Enqueue gr_fwd_prepare_async for one view on the current stream (no host wait)."""
+    L = _native.lib()
+    dev = means.device
+    n = int(means.shape[0])
+    cd = 3 if colors.dim() == 2 else 12
+    geom = torch.empty((int(L.gr_geom_bytes(n)),), dtype=torch.uint8, device=dev)
+    plan_host = torch.zeros(2, dtype=torch.int64, pin_memory=True)  # gr_plan {num_pairs, num_slots}
+    _native.check(L.gr_fwd_prepare_async(ctypes.byref(gv), n, _native.ptr(means), _native.ptr(scales),
+                                         _native.ptr(colors), cd, _native.ptr(opacities), _native.ptr(geom),
+                                         geom.numel(), ctypes.c_void_p(plan_host.data_ptr()), _stream(dev)),
+                  "gr_fwd_prepare_async")
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    return Prepared(gv, n, geom, plan_host, ev)
+
+
+def forward_native(means, scales, colors, opacities, gv: _native.GrView, prepared: Optional[Prepared] = None):
+    """Run gr_fwd_prepare(_async) + gr_fwd_render.  Returns (out, alpha, depth, RenderState)."""
     L = _native.lib()
     dev = means.device
     n = int(means.shape[0])
     H, W = gv.height, gv.width
-    cd = 3 if colors.dim() == 2 else 12
     s = _stream(dev)
-    geom = torch.empty((int(L.gr_geom_bytes(n)),), dtype=torch.uint8, device=dev)
-    plan = _native.GrPlan()
-    _native.check(L.gr_fwd_prepare(ctypes.byref(gv), n, _native.ptr(means), _native.ptr(scales), _native.ptr(colors), cd,
-                                   _native.ptr(opacities), _native.ptr(geom), geom.numel(), ctypes.byref(plan), s),
-                  "gr_fwd_prepare")
+    if prepared is None:
+        prepared = prepare_native(means, scales, colors, opacities, gv)
+    elif prepared.n != n or prepared.gv.width != W or prepared.gv.height != H:
+        raise ValueError("prepared view does not match this render (Gaussian count or image size)")
+    geom = prepared.geom
+    plan = prepared.plan()
     bins = torch.empty((int(L.gr_bins_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8, device=dev)
     out = torch.empty((H, W, 3), dtype=torch.float32, device=dev)
     alpha = torch.empty((H, W), dtype=torch.float32, device=dev)
@@ -198,8 +242,8 @@ def _grad_background(st: RenderState, background: torch.Tensor, g_out: torch.Ten
 
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, means, scales, colors, opacities, background, gv):
-        out, alpha, depth, st = forward_native(means, scales, colors, opacities, gv)
+    def forward(ctx, means, scales, colors, opacities, background, gv, prepared):
+        out, alpha, depth, st = forward_native(means, scales, colors, opacities, gv, prepared)
         ctx.st = st
         ctx.save_for_backward(means, scales, colors, opacities, background)
         return out, alpha, depth
@@ -215,23 +259,38 @@ class _RasterizeGaussians(torch.autograd.Function):
         g_depth = None if g_depth is None else g_depth.contiguous().float()
         dm, ds, dc, do = backward_native(means, scales, colors, opacities, st, g_out, g_alpha, g_depth)
         dbg = _grad_background(st, background, g_out) if ctx.needs_input_grad[4] else None
-        return dm, ds, dc, do, dbg, None
+        return dm, ds, dc, do, dbg, None, None
 
 
-def rasterize(means, scales, colors, opacities, view, proj, width, height, background=None, cutoff=DEFAULT_CUTOFF):
-    """Differentiable render of one view on the HIP device: returns (rgb (H,W,3), alpha (H,W), depth (H,W))."""
+def _device_inputs(means, scales, colors, opacities):
     dev = means.device
     if dev.type != "cuda":
         raise RuntimeError("the MI355X renderer needs tensors on a HIP device (got %s); there is no CPU path" % dev)
+    return (means.to(torch.float32).contiguous(), scales.to(device=dev, dtype=torch.float32).contiguous(),
+            colors.to(device=dev, dtype=torch.float32).contiguous(),
+            opacities.to(device=dev, dtype=torch.float32).contiguous())
+
+
+def prepare_view(means, scales, colors, opacities, view, proj, width, height, background=None,
+                 cutoff=DEFAULT_CUTOFF) -> Prepared:
+    """Enqueue the preparation of one view (see ``Prepared``); pass it to ``rasterize(prepared=...)``
+    with the same tensors.  The tensors' values must not change in between."""
+    gv = make_view(view, proj, width, height, background, cutoff)
+    return prepare_native(*_device_inputs(means, scales, colors, opacities), gv)
+
+
+def rasterize(means, scales, colors, opacities, view, proj, width, height, background=None, cutoff=DEFAULT_CUTOFF,
+              prepared: Optional[Prepared] = None):
+    """Differentiable render of one view on the HIP device: returns (rgb (H,W,3), alpha (H,W), depth (H,W)).
+
+    ``prepared`` (from ``prepare_view`` with the same inputs) skips the preparation step."""
+    dev = means.device
+    m, s, c, o = _device_inputs(means, scales, colors, opacities)
     if background is None:
         background = torch.zeros(3, dtype=torch.float32, device=dev)
     background = background.to(dtype=torch.float32, device=dev)
     gv = make_view(view, proj, width, height, background, cutoff)
-    m = means.to(torch.float32).contiguous()
-    s = scales.to(device=dev, dtype=torch.float32).contiguous()
-    c = colors.to(device=dev, dtype=torch.float32).contiguous()
-    o = opacities.to(device=dev, dtype=torch.float32).contiguous()
-    return _RasterizeGaussians.apply(m, s, c, o, background, gv)
+    return _RasterizeGaussians.apply(m, s, c, o, background, gv, prepared)
 
 
 def render_gaussians_torch(
@@ -247,11 +306,13 @@ def render_gaussians_torch(
     chunk_size: int = 256,
     return_aux: bool = False,
     cutoff: float = DEFAULT_CUTOFF,
+    prepared: Optional[Prepared] = None,
 ):
     """Differentiable Gaussian splat; signature, results and errors of torch_renderer.py:109-203.
 
     Returns ``out`` (H,W,3) or ``(out, alpha, depth)`` when ``return_aux``; ``n == 0`` returns a
-    single zero image even with ``return_aux`` (torch_renderer.py:135-136).
+    single zero image even with ``return_aux`` (torch_renderer.py:135-136).  ``cutoff`` and
+    ``prepared`` (see ``prepare_view``) are extensions; the reference has neither.
     """
     if background is None:
         background = torch.tensor([0.0, 0.0, 0.0], dtype=torch.float32, device=means.device)
@@ -268,11 +329,12 @@ def render_gaussians_torch(
         raise ValueError("colors must be (N,3) or SH coeffs (N,4,3)")
 
     out, alpha, depth = rasterize(means, scales, colors, opacities, camera.view, camera.proj, width, height,
-                                  background=background, cutoff=cutoff)
+                                  background=background, cutoff=cutoff, prepared=prepared)
     if not return_aux:
         return out
     return out, alpha, depth
 
 
 __all__ = ["Camera", "get_default_device", "perspective", "look_at", "render_gaussians_torch", "rasterize",
-           "make_view", "forward_native", "backward_native", "DEFAULT_CUTOFF"]
+           "make_view", "prepare_view", "prepare_native", "Prepared", "forward_native", "backward_native",
+           "DEFAULT_CUTOFF"]

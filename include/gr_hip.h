@@ -22,7 +22,9 @@
  *     are reentrant and stream-ordered (unlike renderer.cu:349's function-static buffers).
  *     Workspace sizes come from the *_bytes() queries.
  *   - gr_fwd_prepare is the one call that synchronises its stream: it returns the number of
- *     (Gaussian, tile) pairs, which sizes the binning workspace.
+ *     (Gaussian, tile) pairs, which sizes the binning workspace.  gr_fwd_prepare_async enqueues
+ *     the same work plus a copy of the plan into caller memory (pinned, for a truly asynchronous
+ *     copy) and returns at once, so the preparation of the next views overlaps the current one.
  *   - gr_render_u8 takes HOST pointers (as gr::render_gaussians does) and is synchronous.
  *   - Every function returns GR_OK or an error code; gr_last_error() gives a thread-local message.
  */
@@ -91,6 +93,15 @@ gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const floa
                          const float* colors, int color_dim, const float* opacities, void* geom,
                          size_t geom_bytes, gr_plan* plan, void* stream);
 
+/* Same work, stream-ordered: *plan is written by a device-to-host copy enqueued on `stream` and is
+ * valid once the stream (or an event recorded after this call) has completed.  A pair count that
+ * does not fit int32 reads back as num_pairs = -1, which gr_fwd_render reports as
+ * GR_ERR_OVERFLOW.  *plan should be pinned host memory (hipHostMalloc / torch pin_memory);
+ * pageable memory works but makes the copy synchronous. */
+gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, const float* scales,
+                               const float* colors, int color_dim, const float* opacities,
+                               void* geom, size_t geom_bytes, gr_plan* plan, void* stream);
+
 /* Tile-sorted (tile, Gaussian) pair lists, per-tile ranges and work items. */
 size_t gr_bins_bytes(const gr_view* v, int n, const gr_plan* plan);
 
@@ -138,12 +149,12 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
  *             A = (px, py, qx, qy), B = (o, r, g, b), C = (z, first slot as int bits,
  *             tx0 | ty0 << 16 as uint bits, rectangle width as int bits), D = 0
  *         [1] rect int4[n] (tx0,ty0,tx1,ty1) [2] counts u64[n+1] [3] offsets u64[n+1]
- *         [4] end of the fixed part (scan temp follows)
+ *         [4] device copy of the plan (gr_plan) [5] end of the fixed part (scan temp follows)
  *         (counts/offsets packed: rectangle area / first slot in the high word, kept tiles / first
  *         pair in the low word)
  *   bins: [0] keys (radix-sort fallback only, > 16384 tiles) [1] gaussian ids int32[K] (tile-sorted)
  *         [2] ranges int2[tiles]  */
-void gr_geom_layout(int n, size_t offsets_out[5]);
+void gr_geom_layout(int n, size_t offsets_out[6]);
 void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[3]);
 
 /* Live kernel timing with HIP events on the launch stream (bench.py).  Between begin and end,

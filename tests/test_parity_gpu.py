@@ -210,3 +210,22 @@ def test_legacy_u8_matches_reference_cpu(pkg, cuda, name):
     diff = np.abs(out.astype(np.int32) - d["rgba"].astype(np.int32))
     assert diff.max() <= 1, f"{name}: max diff {diff.max()}"
     assert (diff > 0).mean() < 0.01
+
+
+def test_prepared_view_matches_direct_render(pkg, cuda):
+    """gr_fwd_prepare_async (prepare_view, used by the fit loop to overlap views) gives bit-identical
+    outputs and gradients to the synchronous path."""
+    tr = pkg.torch_renderer
+    d = golden("f2_c1_view1")
+    W, H = int(d["width"]), int(d["height"])
+    res = []
+    for use_prepared in (False, True):
+        t = [torch.from_numpy(np.ascontiguousarray(d[k])).to(cuda).requires_grad_(True)
+             for k in ("means", "scales", "colors", "opacities")]
+        bg = torch.from_numpy(d["background"]).to(cuda)
+        prep = tr.prepare_view(*[x.detach() for x in t], d["view"], d["proj"], W, H, bg) if use_prepared else None
+        out, alpha, depth = tr.rasterize(*t, d["view"], d["proj"], W, H, background=bg, prepared=prep)
+        (out * torch.from_numpy(d["g_rgb"]).to(cuda)).sum().backward()
+        res.append([out.detach().cpu().numpy()] + [x.grad.cpu().numpy() for x in t])
+    for a, b in zip(*res):
+        np.testing.assert_array_equal(a, b)
