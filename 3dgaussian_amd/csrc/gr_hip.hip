@@ -913,13 +913,22 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
   for (int k = 0; k < 5; ++k) dst[k * TP + tid] = u[k];
 }
 
-// Backward: one workgroup (4 waves) per work item.  A = U_k^T (tile-constant, 20 registers per
-// lane), B = f(x) ex_g(x) for 16 Gaussians on the MFMA columns; wave w takes groups [4w, 4w+4) of
-// each staged batch of 256 Gaussians.  Partials per pair (9 floats) go to the pair's slot
-// (Gaussian's first slot + index of the tile inside its rectangle), so k_reduce_bwd reads each
-// Gaussian's partials contiguously and in a fixed order.
+// Backward: one workgroup (4 waves) per work item; wave w takes groups [4w, 4w+4) of 16 Gaussians of
+// each staged batch of 256.  Per group two sets of five K = 16 contractions (one per upstream
+// channel k, U = (dC_r, dC_g, dC_b, dW, dD)):
+//   T_k[y][g] = sum_x U_k[x][y] ex_g(x)     (over x; the VALU then weights rows y by ey, dy, dy^2)
+//   R_k[x][g] = sum_y U_k[x][y] ey_g(y)     (over y; rows x weighted by ex, dx, dx^2)
+// which give every moment the 9 pair partials need:
+//   S0..2 = sum_y ey T_{rgb}, S3 = sum_y ey T_D (times o), and with the colour/depth fold
+//   G = sum_k vv_k (.)_k, vv = (r, g, b, 1, z):  S4 = sum_y ey G_T, S6 = sum_y ey dy G_T,
+//   S8 = sum_y ey dy^2 G_T, S5 = sum_x ex dx G_R, S7 = sum_x ex dx^2 G_R.
+// 40 MFMA 16x16x4 per 16 pairs (the dx-weighted x contractions of a single-axis form need 60).
+// K step s of lane row xs covers pixel 4 xs + s on the contracted axis, so the ex (ey) a lane feeds
+// to the T (R) MFMA are exactly the weights its R (T) output rows need: 8 exponentials per lane.
+// Partials per pair (9 floats) go to the pair's slot (Gaussian's first slot + index of the tile
+// inside its rectangle), so k_reduce_bwd reads each Gaussian's partials contiguously and in order.
 #ifndef GR_BWD_WAVES
-#define GR_BWD_WAVES 4
+#define GR_BWD_WAVES 3
 #endif
 
 // Sum over the 4 lane rows (lanes l, l+16, l+32, l+48) of a pair of values with one
@@ -949,15 +958,22 @@ __global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int li = lane & 15, xs = lane >> 4;
-  float A[5][4];
+  // A operands (tile-constant): AT[k][s] = U_k(x = 4xs+s, y = li), AR[k][s] = U_k(x = li, y = 4xs+s)
+  float AT[5][4], AR[5][4];
   {
     const float* Ut = U + (size_t)tile * 5 * TP;
 #pragma unroll
-    for (int k = 0; k < 5; ++k)
+    for (int k = 0; k < 5; ++k) {
+      const float4 t4 = *reinterpret_cast<const float4*>(Ut + k * TP + li * T + 4 * xs);
+      AT[k][0] = t4.x;
+      AT[k][1] = t4.y;
+      AT[k][2] = t4.z;
+      AT[k][3] = t4.w;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) A[k][s] = Ut[k * TP + li * T + 4 * s + xs];
+      for (int s = 0; s < 4; ++s) AR[k][s] = Ut[k * TP + (4 * xs + s) * T + li];
+    }
   }
-  const float x0 = (float)(tx * T) + 0.5f, y0 = (float)(ty * T) + 0.5f;
+  const float x0 = (float)(tx * T + 4 * xs) + 0.5f, y0 = (float)(ty * T + 4 * xs) + 0.5f;
   StageRec st = stage_rec(stage_id(k0 + tid, k1, ids), rec);
   int slot = st.g >= 0 ? pair_slot(st.c, tx, ty) : -1;
   int idn = stage_id(k0 + TP + tid, k1, ids);
@@ -979,44 +995,45 @@ __global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
       const float4 b = sB[buf][j];
       const float z = sZ[buf][j];
       const int myslot = sSlot[buf][j];
-      const float vv[5] = {b.y, b.z, b.w, 1.0f, z};
-      f32x4 D1[5];
-#pragma unroll
-      for (int k = 0; k < 5; ++k) D1[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-      // dx / dx^2 contractions summed over the 5 channels, two accumulators each (no MFMA waits on
-      // the one before it: 16x16x4 f32 has a 32-cycle issue and a 40-cycle dependent latency)
-      f32x4 Ddx[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, Ddx2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      float ex[4], ey[4], dx[4], dy[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const float dx = (x0 + (float)(4 * s + xs)) - a.x;
-        const float ex = __builtin_amdgcn_exp2f(dx * a.z * dx);  // exactly 0 for padding
-        const float edx = ex * dx, edx2 = edx * dx;
+        dx[s] = (x0 + (float)s) - a.x;
+        dy[s] = (y0 + (float)s) - a.y;
+        ex[s] = __builtin_amdgcn_exp2f(dx[s] * a.z * dx[s]);  // exactly 0 for padding
+        ey[s] = __builtin_amdgcn_exp2f(dy[s] * a.w * dy[s]);
+      }
+      f32x4 DT[5], DR[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        DT[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        DR[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
-          D1[k] = mfma4(A[k][s], ex, D1[k]);
-          Ddx[k & 1] = mfma4(A[k][s], vv[k] * edx, Ddx[k & 1]);
-          Ddx2[k & 1] = mfma4(A[k][s], vv[k] * edx2, Ddx2[k & 1]);
+          DT[k] = mfma4(AT[k][s], ex[s], DT[k]);
+          DR[k] = mfma4(AR[k][s], ey[s], DR[k]);
         }
-      }
-      const f32x4 Dx = Ddx[0] + Ddx[1], Dx2 = Ddx2[0] + Ddx2[1];
-      // lane holds D[y = 4*xs + r][g = li]; sum its 4 rows, then across the 4 lane rows
+      // lane holds T[y = 4xs + r][g = li] and R[x = 4xs + r][g = li]
       float S[NPART] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float dy = (y0 + (float)(4 * xs + r)) - a.y;
-        const float ey = __builtin_amdgcn_exp2f(dy * a.w * dy);
-        S[0] = fmaf(ey, D1[0][r], S[0]);
-        S[1] = fmaf(ey, D1[1][r], S[1]);
-        S[2] = fmaf(ey, D1[2][r], S[2]);
-        S[3] = fmaf(ey, D1[4][r], S[3]);
-        const float G1 = fmaf(z, D1[4][r], fmaf(vv[2], D1[2][r], fmaf(vv[1], D1[1][r], fmaf(vv[0], D1[0][r], D1[3][r]))));
-        const float t = ey * G1;
+        S[0] = fmaf(ey[r], DT[0][r], S[0]);
+        S[1] = fmaf(ey[r], DT[1][r], S[1]);
+        S[2] = fmaf(ey[r], DT[2][r], S[2]);
+        S[3] = fmaf(ey[r], DT[4][r], S[3]);
+        const float GT = fmaf(z, DT[4][r], fmaf(b.w, DT[2][r], fmaf(b.z, DT[1][r], fmaf(b.y, DT[0][r], DT[3][r]))));
+        const float t = ey[r] * GT;
         S[4] += t;
-        const float tdy = t * dy;
+        const float tdy = t * dy[r];
         S[6] += tdy;
-        S[8] = fmaf(tdy, dy, S[8]);
-        S[5] = fmaf(ey, Dx[r], S[5]);
-        S[7] = fmaf(ey, Dx2[r], S[7]);
+        S[8] = fmaf(tdy, dy[r], S[8]);
+        const float GR = fmaf(z, DR[4][r], fmaf(b.w, DR[2][r], fmaf(b.z, DR[1][r], fmaf(b.y, DR[0][r], DR[3][r]))));
+        const float tdx = (ex[r] * GR) * dx[r];  // (0 * G) * dx: padding stays 0, never 0 * inf
+        S[5] += tdx;
+        S[7] = fmaf(tdx, dx[r], S[7]);
       }
       // row r of R03 holds the total of S_r, of R47 the total of S_{4+r}; rows 0 and 1 of R8 hold S8
       const float R03 = pair32(pair16(S[0], S[1]), pair16(S[2], S[3]));

@@ -46,7 +46,7 @@ fm = importlib.import_module("3dgaussian_amd.fit_multiview")
 
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 (f32-in MFMA) dense peak
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak (spec)
-FLOP_PER_PAIR_BWD = 60 / 16 * 2 * 16 * 16 * 4  # 60 MFMA 16x16x4 per 16 Gaussians per tile
+FLOP_PER_PAIR_BWD = 40 / 16 * 2 * 16 * 16 * 4  # 40 MFMA 16x16x4 per 16 Gaussians per tile (T + R contractions)
 FLOP_PER_PAIR_FWD = 5 / 4 * 2 * 16 * 16 * 4  # 5 MFMA 16x16x4 per 4 Gaussians per tile
 
 
