@@ -39,6 +39,7 @@ class GrView(ctypes.Structure):
         ("background", ctypes.c_float * 3),
         ("cam_pos", ctypes.c_float * 3),
         ("cutoff", ctypes.c_float),
+        ("core_cutoff", ctypes.c_float),
     ]
 
 
@@ -61,7 +62,7 @@ class GrRenderParams(ctypes.Structure):
 class GrPlan(ctypes.Structure):
     """gr_plan (include/gr_hip.h): sizes produced by gr_fwd_prepare."""
 
-    _fields_ = [("num_pairs", ctypes.c_int64), ("num_slots", ctypes.c_int64)]
+    _fields_ = [("num_pairs", ctypes.c_int64), ("num_slots", ctypes.c_int64), ("num_core_pairs", ctypes.c_int64)]
 
 
 class NativeLibraryError(ImportError):
@@ -154,15 +155,19 @@ def version() -> str:
     return lib().gr_version().decode()
 
 
+GEOM_PARTS = 8
+
+
 def geom_layout(n: int):
-    """[records (n x 64 B), rect, counts, offsets, device plan, end of the fixed part] (gr_hip.h)."""
-    out = (ctypes.c_size_t * 6)()
+    """[records ((n+1) x 64 B), rect, counts, offsets, device plan, tail counts, tail offsets, end of the
+    fixed part] (gr_hip.h gr_geom_layout)."""
+    out = (ctypes.c_size_t * GEOM_PARTS)()
     lib().gr_geom_layout(int(n), out)
     return list(out)
 
 
 def bins_layout(gv: GrView, n: int, num_pairs: int):
     out = (ctypes.c_size_t * 3)()
-    plan = GrPlan(int(num_pairs), 0)
+    plan = GrPlan(int(num_pairs), 0, 0)
     lib().gr_bins_layout(ctypes.byref(gv), int(n), ctypes.byref(plan), out)
     return list(out)

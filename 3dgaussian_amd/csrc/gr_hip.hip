@@ -67,6 +67,9 @@ inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 inline int tiles_x_of(int w) { return (w + T - 1) / T; }
 inline int tiles_y_of(int h) { return (h + T - 1) / T; }
+// Binning unit of the differentiable path: virtual tile 2t holds tile t's core pairs, 2t+1 its tail
+// pairs (two-zone footprint), so the pair lists, ranges and work items are per virtual tile.
+inline int vtiles_of(const gr_view* v) { return 2 * tiles_x_of(v->width) * tiles_y_of(v->height); }
 
 int bits_for(uint32_t maxval) {
   int b = 1;
@@ -81,6 +84,7 @@ struct ViewK {
   float bg[3];
   float cam[3];
   float cutoff;
+  float core;  // core radius of the two-zone footprint (= cutoff: one zone)
 };
 
 ViewK make_viewk(const gr_view* v) {
@@ -94,6 +98,7 @@ ViewK make_viewk(const gr_view* v) {
   std::memcpy(k.bg, v->background, sizeof(k.bg));
   std::memcpy(k.cam, v->cam_pos, sizeof(k.cam));
   k.cutoff = v->cutoff > 0.0f ? v->cutoff : 7.0f;
+  k.core = (v->core_cutoff > 0.0f && v->core_cutoff < k.cutoff) ? v->core_cutoff : k.cutoff;
   return k;
 }
 
@@ -164,19 +169,33 @@ __device__ __forceinline__ int tile_rect(const ViewK& v, const Proj& p, float op
   return (r.z - r.x + 1) * (r.w - r.y + 1);
 }
 
-// Tile culling inside the rectangle (oracle/gr_oracle.c tile_pass, bit-exact): keep tile (tx,ty) iff
-// the Gaussian's largest weight over the tile's pixel centres (clipped to the image) is
-// >= o * exp(-cutoff^2/2).  q = -0.5 log2(e) / sigma^2 as stored in record word A.
-__device__ __forceinline__ bool tile_pass(const ViewK& v, float px, float py, float qx, float qy, int tx, int ty) {
-  const float thr = (-0.5f * LOG2E) * (v.cutoff * v.cutoff);
+// Largest weight of a Gaussian over tile (tx,ty)'s pixel centres (clipped to the image), as the exp2
+// exponent e = log2(w/o); q = -0.5 log2(e) / sigma^2 as stored in record word A
+// (oracle/gr_oracle.c tile_emax, bit-exact).
+__device__ __forceinline__ float tile_emax(const ViewK& v, float px, float py, float qx, float qy, int tx, int ty) {
   const int xe = min(tx * T + T - 1, v.W - 1), ye = min(ty * T + T - 1, v.H - 1);
   const float lox = (float)(tx * T) + 0.5f, hix = (float)xe + 0.5f;
   const float loy = (float)(ty * T) + 0.5f, hiy = (float)ye + 0.5f;
   const float cx = px < lox ? lox : (px > hix ? hix : px);
   const float cy = py < loy ? loy : (py > hiy ? hiy : py);
   const float dx = cx - px, dy = cy - py;
-  const float e = (dx * dx) * qx + (dy * dy) * qy;
-  return e >= thr;
+  return (dx * dx) * qx + (dy * dy) * qy;
+}
+
+__device__ __forceinline__ float radius_thr(float R) { return (-0.5f * LOG2E) * (R * R); }
+
+// Tile culling inside the rectangle: keep tile (tx,ty) iff the Gaussian's largest weight over it is
+// >= o * exp(-cutoff^2/2).
+__device__ __forceinline__ bool tile_pass(const ViewK& v, float px, float py, float qx, float qy, int tx, int ty) {
+  return tile_emax(v, px, py, qx, qy, tx, ty) >= radius_thr(v.cutoff);
+}
+
+// Two-zone footprint (oracle/gr_oracle.c tile_class): 0 culled, 1 tail (largest weight below
+// o * exp(-core^2/2): W and D forward, depth-coupled terms backward), 2 core (every channel).
+__device__ __forceinline__ int tile_class(const ViewK& v, float px, float py, float qx, float qy, int tx, int ty) {
+  const float e = tile_emax(v, px, py, qx, qy, tx, ty);
+  if (!(e >= radius_thr(v.cutoff))) return 0;
+  return e >= radius_thr(v.core) ? 2 : 1;
 }
 
 __device__ __forceinline__ float qcoef(float s) { return (-0.5f * LOG2E) / (s * s); }
@@ -202,26 +221,32 @@ constexpr int REC4 = 4;  // float4 per record
 struct Geom {
   float4* rec;   // [n][4] raster records
   int4* rect;    // tile rectangle
-  // packed (rect area << 32 | kept tiles): the exclusive scan gives, per Gaussian, the first pair
-  // index (low word) and the first partial-sum slot (high word; one slot per rectangle tile)
+  // packed (rect area << 32 | core tiles): the exclusive scan gives, per Gaussian, the first core
+  // pair (low word) and the first partial-sum slot (high word; one slot per rectangle tile);
+  // tail tiles are counted and scanned separately (tcounts / toffsets): core pairs fill [0, Kc),
+  // tail pairs [Kc, K) of the pair arrays
   unsigned long long* counts;   // n+1
   unsigned long long* offsets;  // n+1
   gr_plan* plan;                // device copy of the plan (gr_fwd_prepare_async copies it to the host)
+  unsigned* tcounts;            // n+1
+  unsigned* toffsets;           // n+1
   void* scan_tmp;
   size_t scan_tmp_bytes;
 };
 
-// off: [0] records, [1] rect, [2] counts, [3] offsets, [4] device copy of the plan,
-//      [5] scan temp (= end of the fixed part)
-size_t geom_fixed(int n, size_t off[6]) {
+// off: [0] records, [1] rect, [2] counts, [3] offsets, [4] device copy of the plan, [5] tail counts,
+//      [6] tail offsets, [7] scan temp (= end of the fixed part)
+size_t geom_fixed(int n, size_t off[GR_GEOM_PARTS]) {
   size_t o = 0;
   const size_t nn = (size_t)(n > 0 ? n : 1);
-  off[0] = o; o = align_up(o + nn * REC4 * sizeof(float4));
+  off[0] = o; o = align_up(o + (nn + 1) * REC4 * sizeof(float4));  // + the pad record rec[n]
   off[1] = o; o = align_up(o + nn * sizeof(int4));
   off[2] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
   off[3] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
   off[4] = o; o = align_up(o + sizeof(gr_plan));
-  off[5] = o;
+  off[5] = o; o = align_up(o + (nn + 1) * sizeof(unsigned));
+  off[6] = o; o = align_up(o + (nn + 1) * sizeof(unsigned));
+  off[7] = o;
   return o;
 }
 
@@ -231,10 +256,13 @@ size_t scan_tmp_bytes_t(int n) {
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (CountT*)nullptr, (CountT*)nullptr, n + 1, (hipStream_t)0);
   return tmp;
 }
-size_t scan_tmp_bytes(int n) { return scan_tmp_bytes_t<unsigned long long>(n); }
+size_t scan_tmp_bytes(int n) {
+  const size_t a = scan_tmp_bytes_t<unsigned long long>(n), b = scan_tmp_bytes_t<unsigned>(n);
+  return a > b ? a : b;
+}
 
 Geom geom_view(void* base, int n) {
-  size_t off[6];
+  size_t off[GR_GEOM_PARTS];
   const size_t fixed = geom_fixed(n, off);
   char* b = (char*)base;
   Geom g;
@@ -243,6 +271,8 @@ Geom geom_view(void* base, int n) {
   g.rect = (int4*)(b + off[1]);
   g.counts = (unsigned long long*)(b + off[2]);
   g.offsets = (unsigned long long*)(b + off[3]);
+  g.tcounts = (unsigned*)(b + off[5]);
+  g.toffsets = (unsigned*)(b + off[6]);
   g.scan_tmp = b + fixed;
   g.scan_tmp_bytes = 0;
   return g;
@@ -274,7 +304,9 @@ struct Scratch {
 
 inline int64_t item_cap(int tiles, int64_t K) { return (K + CH - 1) / CH + tiles; }
 
-size_t bins_fixed(int tiles, int64_t K, size_t off[6]) {
+// `vtiles` = 2 x tiles (core and tail lists of each tile) on the differentiable path.
+size_t bins_fixed(int vtiles, int64_t K, size_t off[6]) {
+  const int tiles = vtiles;
   const size_t kk = (size_t)(K > 0 ? K : 1);
   const size_t cap = (size_t)item_cap(tiles, K);
   size_t o = 0;
@@ -287,7 +319,8 @@ size_t bins_fixed(int tiles, int64_t K, size_t off[6]) {
   return o;
 }
 
-size_t scratch_fixed(int tiles, int64_t K, size_t off[3]) {
+size_t scratch_fixed(int vtiles, int64_t K, size_t off[3]) {
+  const int tiles = vtiles;
   const size_t kk = (size_t)(K > 0 ? K : 1);
   const size_t cap = (size_t)item_cap(tiles, K);
   size_t o = 0;
@@ -334,10 +367,17 @@ inline TSortPlan tsort_plan(int64_t K, int tiles) {
 
 // Scratch behind the fixed part: counting sort = count matrix M, its row scan S, tile totals T;
 // radix sort = its temp storage.
+// `tiles` = virtual tiles (2 x screen tiles).  Counting sort: one count matrix M (reused by the two
+// regions), per region its row scan S and tile totals T.  Every matrix is bounded by the cells of the
+// whole array at the smallest column width (a region's plan never has more).
+size_t tsort_cells_bound(int64_t K, int tiles) {
+  const int64_t cw = 2048ll * GR_TSORT_NSEG * tsort_waves(tiles), kk = K > 0 ? K : 1;
+  return (size_t)tiles * (size_t)((kk + cw - 1) / cw);
+}
 size_t tile_sort_tmp_bytes(int64_t K, int tiles) {
   if (short_keys(tiles)) {
-    const TSortPlan p = tsort_plan(K, tiles);
-    return 2 * align_up(p.cells * sizeof(int)) + align_up((size_t)tiles * sizeof(int));
+    const int st = tiles / 2;
+    return 3 * align_up(tsort_cells_bound(K, st) * sizeof(int)) + 2 * align_up((size_t)st * sizeof(int));
   }
   size_t tmp = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const int*)nullptr,
@@ -388,7 +428,13 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, int n, const float*
                                                     const float* __restrict__ scales, const float* __restrict__ colors,
                                                     const float* __restrict__ opac, Geom g) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == n) g.counts[n] = 0;
+  if (i == n) {
+    g.counts[n] = 0;
+    g.tcounts[n] = 0;
+    float4* pad = g.rec + (size_t)REC4 * n;  // padding record of the raster batches (rec_of)
+    pad[0] = make_float4(1e30f, 1e30f, -1.0f, -1.0f);
+    pad[1] = pad[2] = pad[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   if (i >= n) return;
   const float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
   Proj p;
@@ -399,11 +445,15 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, int n, const float*
   int4 r;
   const float qx = qcoef(p.sx);
   const float qy = qcoef(p.sy);
-  int cnt = 0;
+  int core = 0, tail = 0;
   const int area = tile_rect(v, p, op, r);
   if (area > 0) {
     for (int ty = r.y; ty <= r.w; ++ty)
-      for (int tx = r.x; tx <= r.z; ++tx) cnt += tile_pass(v, p.px, p.py, qx, qy, tx, ty) ? 1 : 0;
+      for (int tx = r.x; tx <= r.z; ++tx) {
+        const int cls = tile_class(v, p.px, p.py, qx, qy, tx, ty);
+        core += cls == 2;
+        tail += cls == 1;
+      }
   }
   float4* rec = g.rec + (size_t)REC4 * i;
   rec[0] = make_float4(p.px, p.py, qx, qy);
@@ -412,20 +462,19 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, int n, const float*
                        __uint_as_float((unsigned)(r.z - r.x + 1)));
   rec[3] = make_float4(0.f, 0.f, 0.f, 0.f);
   g.rect[i] = r;
-  g.counts[i] = cnt > 0 ? (((unsigned long long)area << 32) | (unsigned)cnt) : 0ull;
+  g.counts[i] = core + tail > 0 ? (((unsigned long long)area << 32) | (unsigned)core) : 0ull;
+  g.tcounts[i] = (unsigned)tail;
 }
 
 constexpr int EWIN = 4096;  // pairs staged in LDS per emit block
 
 // Pairs of 256 consecutive Gaussians form one contiguous range; they are built in LDS and written
 // out with coalesced stores (direct scattered stores only when a block overflows the window).
+// Legacy (uint8) path: every tile of the rectangle, one contiguous pair range per Gaussian.
 template <typename KeyT, typename OffT>
 __global__ __launch_bounds__(256) void k_emit(ViewK v, int n, const int4* __restrict__ rect,
                                               const OffT* __restrict__ counts, const OffT* __restrict__ offsets,
-                                              float4* __restrict__ rec, const KeyT* __restrict__ low_keys,
-                                              KeyT* keys, int* ids) {
-  // rec != nullptr: differentiable path, tiles culled by tile_pass, first slot stored in the record;
-  // nullptr: legacy full rectangle
+                                              const KeyT* __restrict__ low_keys, KeyT* keys, int* ids) {
   __shared__ KeyT sK[EWIN];
   __shared__ int sI[EWIN];
   const int g0 = blockIdx.x * 256;
@@ -437,16 +486,8 @@ __global__ __launch_bounds__(256) void k_emit(ViewK v, int n, const int4* __rest
     const int4 r = rect[i];
     int k = (int)(offsets[i] & 0xffffffffu);  // pair index (low word when packed)
     const KeyT low = low_keys ? low_keys[i] : (KeyT)0;
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (sizeof(OffT) == 8) {
-      if (rec) {
-        a = rec[(size_t)REC4 * i];
-        rec[(size_t)REC4 * i + 2].y = __uint_as_float((unsigned)(offsets[i] >> 32));
-      }
-    }
     for (int ty = r.y; ty <= r.w; ++ty)
       for (int tx = r.x; tx <= r.z; ++tx) {
-        if (rec && !tile_pass(v, a.x, a.y, a.z, a.w, tx, ty)) continue;
         const KeyT t = (KeyT)(ty * v.tiles_x + tx);
         KeyT key;
         if constexpr (sizeof(KeyT) == 8)
@@ -468,6 +509,59 @@ __global__ __launch_bounds__(256) void k_emit(ViewK v, int n, const int4* __rest
   for (int e = (int)threadIdx.x; e < k1 - k0; e += 256) {
     keys[k0 + e] = sK[e];
     ids[k0 + e] = sI[e];
+  }
+}
+
+// Differentiable path: pairs of the kept tiles (tile_class), core pairs at [0, Kc) and tail pairs at
+// [Kc, K), each in Gaussian order; the Gaussian's first partial-sum slot goes into its record (word
+// C.y).  Keys: the tile (VKEY = false: each region is counting-sorted on its own) or the virtual
+// tile 2*tile + tail (VKEY = true: one radix sort of the whole array).  The pairs of 256 consecutive
+// Gaussians are built in LDS and written out with coalesced stores.
+template <typename KeyT, bool VKEY>
+__global__ __launch_bounds__(256) void k_emit_zones(ViewK v, int n, const int4* __restrict__ rect,
+                                                    const unsigned long long* __restrict__ counts,
+                                                    const unsigned long long* __restrict__ offsets,
+                                                    const unsigned* __restrict__ toffsets, float4* __restrict__ rec,
+                                                    KeyT* keys, int* ids) {
+  __shared__ KeyT sK[EWIN];
+  __shared__ int sI[EWIN];
+  const int g0 = blockIdx.x * 256;
+  const int i = g0 + (int)threadIdx.x;
+  const int gend = min(n, g0 + 256);
+  const int Kc = (int)(offsets[n] & 0xffffffffu);
+  const int c0 = (int)(offsets[g0] & 0xffffffffu), c1 = (int)(offsets[gend] & 0xffffffffu);
+  const int t0 = (int)toffsets[g0], t1 = (int)toffsets[gend];
+  const int nc = c1 - c0;
+  const bool staged = nc + (t1 - t0) <= EWIN;
+  if (i < n && counts[i] != 0) {
+    const int4 r = rect[i];
+    const float4 a = rec[(size_t)REC4 * i];
+    rec[(size_t)REC4 * i + 2].y = __uint_as_float((unsigned)(offsets[i] >> 32));
+    int kc = (int)(offsets[i] & 0xffffffffu), kt = (int)toffsets[i];
+    for (int ty = r.y; ty <= r.w; ++ty)
+      for (int tx = r.x; tx <= r.z; ++tx) {
+        const int cls = tile_class(v, a.x, a.y, a.z, a.w, tx, ty);
+        if (cls == 0) continue;
+        const int t = ty * v.tiles_x + tx;
+        const KeyT key = (KeyT)(VKEY ? 2 * t + (cls == 1) : t);
+        const int e = cls == 2 ? kc++ - c0 : nc + (kt++ - t0);  // index in the block's window
+        if (staged) {
+          sK[e] = key;
+          sI[e] = i;
+        } else {
+          const int k = e < nc ? c0 + e : Kc + t0 + (e - nc);
+          keys[k] = key;
+          ids[k] = i;
+        }
+      }
+  }
+  if (!staged) return;  // uniform per block
+  __syncthreads();
+  const int ne = nc + (t1 - t0);
+  for (int e = (int)threadIdx.x; e < ne; e += 256) {
+    const int k = e < nc ? c0 + e : Kc + t0 + (e - nc);
+    keys[k] = sK[e];
+    ids[k] = sI[e];
   }
 }
 
@@ -496,39 +590,26 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// Work items: each non-empty tile's pair list is cut into chunks of CH Gaussians, so every
+// Work items: each non-empty (virtual) tile's pair list is cut into chunks of CH Gaussians, so every
 // workgroup gets about the same amount of work however unevenly Gaussians fall on tiles.
-// One block; tiles are scanned in order, so items are ordered by (tile, chunk).
-// counts != nullptr (counting-sort path): the tile ranges are the exclusive scan of the per-tile
-// pair counts and are written to `ranges` here; otherwise `ranges` is read.
-__global__ __launch_bounds__(1024) void k_work_items(int tiles, int2* __restrict__ ranges, const int* __restrict__ counts,
-                                                     int4* __restrict__ items, int* __restrict__ num_items,
-                                                     int* __restrict__ tile_item0) {
+// One block; virtual tiles are scanned in order, so items are ordered by (virtual tile, chunk) and
+// the core and tail items of a tile are adjacent.  k_work_items reads existing per-virtual-tile
+// ranges (radix-sort path, empty views).
+__global__ __launch_bounds__(1024) void k_work_items(int vtiles, const int2* __restrict__ ranges, int4* __restrict__ items,
+                                                     int* __restrict__ num_items, int* __restrict__ tile_item0) {
   typedef hipcub::BlockScan<int, 1024> Scan;
   __shared__ typename Scan::TempStorage tmp;
-  __shared__ int carry, pcarry;
-  if (threadIdx.x == 0) carry = pcarry = 0;
+  __shared__ int carry;
+  if (threadIdx.x == 0) carry = 0;
   __syncthreads();
-  for (int base = 0; base < tiles; base += 1024) {
+  for (int base = 0; base < vtiles; base += 1024) {
     const int t = base + (int)threadIdx.x;
-    int2 r = make_int2(0, 0);
-    if (counts) {
-      const int cnt = t < tiles ? counts[t] : 0;
-      int start, ptotal;
-      Scan(tmp).ExclusiveSum(cnt, start, ptotal);
-      __syncthreads();
-      if (cnt > 0) r = make_int2(pcarry + start, pcarry + start + cnt);
-      if (t < tiles) ranges[t] = r;
-      __syncthreads();
-      if (threadIdx.x == 0) pcarry += ptotal;
-    } else if (t < tiles) {
-      r = ranges[t];
-    }
+    const int2 r = t < vtiles ? ranges[t] : make_int2(0, 0);
     const int nch = (r.y - r.x + CH - 1) / CH;
     int excl, total;
     Scan(tmp).ExclusiveSum(nch, excl, total);
     const int first = carry + excl;
-    if (t < tiles) {
+    if (t < vtiles) {
       tile_item0[t] = first;
       for (int c = 0; c < nch; ++c) items[first + c] = make_int4(t, r.x + c * CH, min(r.y, r.x + (c + 1) * CH), c);
     }
@@ -539,33 +620,89 @@ __global__ __launch_bounds__(1024) void k_work_items(int tiles, int2* __restrict
   if (threadIdx.x == 0) *num_items = carry;
 }
 
-// Gaussian records of one 256-wide batch, staged through registers (load early, write late).
-struct StageRec {
-  float4 a, b, c;  // record words A, B, C
-  int g;
-};
-
-// Staging pipeline for the 256-wide Gaussian batches of a work item: the Gaussian id of batch b+2
-// and the records of batch b+1 are in flight while batch b is computed, so neither the id load nor
-// the dependent record gathers sit on the critical path.
-__device__ __forceinline__ int stage_id(int k, int k1, const int* __restrict__ ids) { return k < k1 ? ids[k] : -1; }
-
-// Records of Gaussian g (g < 0: padding).  Padding has o = 0 and px = +huge, so every weight it
-// produces is exactly 0 (exp2(-inf) = 0) without a per-element select.
-__device__ __forceinline__ StageRec stage_rec(int g, const float4* __restrict__ rec) {
-  StageRec r;
-  r.g = g;
-  if (g >= 0) {
-    const float4* p = rec + (size_t)REC4 * g;
-    r.a = p[0];
-    r.b = p[1];
-    r.c = p[2];
-  } else {
-    r.a = make_float4(1e30f, 1e30f, -1.0f, -1.0f);
-    r.b = make_float4(0.f, 0.f, 0.f, 0.f);
-    r.c = make_float4(0.f, 0.f, 0.f, 0.f);
+// Counting-sort path: per-tile pair totals of the core region (Tc) and of the tail region (Tt,
+// starting at Kc) are scanned into the virtual-tile ranges (2t: core, 2t+1: tail), then cut.
+__global__ __launch_bounds__(1024) void k_work_items_zones(int tiles, int Kc, const int* __restrict__ Tc,
+                                                           const int* __restrict__ Tt, int2* __restrict__ ranges,
+                                                           int4* __restrict__ items, int* __restrict__ num_items,
+                                                           int* __restrict__ tile_item0) {
+  typedef hipcub::BlockScan<int, 1024> Scan;
+  __shared__ typename Scan::TempStorage tmp;
+  __shared__ int carry, ccarry, tcarry;
+  if (threadIdx.x == 0) carry = ccarry = tcarry = 0;
+  __syncthreads();
+  for (int base = 0; base < tiles; base += 1024) {
+    const int t = base + (int)threadIdx.x;
+    const int nc = t < tiles ? Tc[t] : 0, nt = t < tiles ? Tt[t] : 0;
+    int sc, totc, st, tott;
+    Scan(tmp).ExclusiveSum(nc, sc, totc);
+    __syncthreads();
+    Scan(tmp).ExclusiveSum(nt, st, tott);
+    __syncthreads();
+    const int2 rc = nc > 0 ? make_int2(ccarry + sc, ccarry + sc + nc) : make_int2(0, 0);
+    const int2 rt = nt > 0 ? make_int2(Kc + tcarry + st, Kc + tcarry + st + nt) : make_int2(0, 0);
+    const int chc = (nc + CH - 1) / CH, cht = (nt + CH - 1) / CH;
+    int excl, total;
+    Scan(tmp).ExclusiveSum(chc + cht, excl, total);
+    const int first = carry + excl;
+    if (t < tiles) {
+      ranges[2 * t] = rc;
+      ranges[2 * t + 1] = rt;
+      tile_item0[2 * t] = first;
+      tile_item0[2 * t + 1] = first + chc;
+      for (int c = 0; c < chc; ++c) items[first + c] = make_int4(2 * t, rc.x + c * CH, min(rc.y, rc.x + (c + 1) * CH), c);
+      for (int c = 0; c < cht; ++c)
+        items[first + chc + c] = make_int4(2 * t + 1, rt.x + c * CH, min(rt.y, rt.x + (c + 1) * CH), c);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      carry += total;
+      ccarry += totc;
+      tcarry += tott;
+    }
+    __syncthreads();
   }
-  return r;
+  if (threadIdx.x == 0) *num_items = carry;
+}
+
+// Staging pipeline for the 256-wide Gaussian batches of a work item: the records of batch b+1 are
+// copied global -> LDS by LDS-DMA (global_load_lds, no VGPR destination) while batch b is computed,
+// and the Gaussian ids of batch b+2 are in flight in a register, so neither the id load nor the
+// dependent record gathers sit on the critical path.  The __syncthreads() at the top of each batch
+// waits for this wave's DMA (vmcnt(0)) and, as a barrier, for every other wave's.
+// Unconditional load (index clamped into the item, k1 > k0): a predicated load would make the
+// compiler wait for all outstanding memory operations, the in-flight DMA included, at the join.
+__device__ __forceinline__ int stage_id(int k, int k1, const int* __restrict__ ids) {
+  const int g = ids[min(k, k1 - 1)];
+  return k < k1 ? g : -1;
+}
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// One LDS-DMA per lane: 16 (4) bytes from gsrc to wave_base + lane * 16 (4).  Issued from inline asm
+// so the compiler does not track it: hipcc would otherwise wait for the DMA (vmcnt(0)) before the
+// first LDS read of the batch being computed, serialising the copy with the compute.  Completion is
+// awaited explicitly by stage_wait() before the barrier that publishes the buffer.
+__device__ __forceinline__ uint32_t lds_addr(void* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)p);
+}
+__device__ __forceinline__ void glds16(const void* gsrc, void* wave_base) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_addr(wave_base)) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* gsrc, void* wave_base) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_addr(wave_base)) : "memory");
+}
+// This wave's LDS-DMAs (and every other vector memory op) have completed; follow with a barrier.
+__device__ __forceinline__ void stage_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Record of Gaussian g; g < 0 (padding) reads the pad record rec[n] written by k_preprocess: o = 0
+// and px = +huge, so every weight it produces is exactly 0 (exp2(-inf) = 0) without a select.
+__device__ __forceinline__ const float4* rec_of(int g, int n, const float4* __restrict__ rec) {
+  return rec + (size_t)REC4 * (g >= 0 ? g : n);
 }
 
 // XCD-aware work-item order: the dispatcher deals workgroups round-robin over the 8 XCDs
@@ -690,10 +827,11 @@ __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int 
   }
 }
 
+// ranges: per virtual tile; this region's pairs go to tile t's list 2t + zone.
 __global__ __launch_bounds__(256) void k_tile_place(int64_t K, int cw, int cols, int tiles, int bits,
                                                     const uint16_t* __restrict__ keys, const int* __restrict__ ids_in,
                                                     const int* __restrict__ S, const int2* __restrict__ ranges,
-                                                    int* __restrict__ ids_out) {
+                                                    int zone, int* __restrict__ ids_out) {
   extern __shared__ int cur[];  // [waves][tiles]
   const int c = xcd_item(blockIdx.x, cols);
   const int waves = (int)blockDim.x >> 6, w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
@@ -716,7 +854,7 @@ __global__ __launch_bounds__(256) void k_tile_place(int64_t K, int cw, int cols,
   // cursor of (tile, wave) = tile start + column start within the tile + lower waves' counts
 #pragma unroll 4
   for (int t = threadIdx.x; t < tiles; t += blockDim.x) {
-    int run = ranges[t].x + S[(size_t)c * tiles + t];
+    int run = ranges[2 * t + zone].x + S[(size_t)c * tiles + t];
     for (int u = 0; u < waves; ++u) {
       const int n = cur[(size_t)u * tiles + t];
       cur[(size_t)u * tiles + t] = run;
@@ -737,7 +875,91 @@ __global__ __launch_bounds__(256) void k_tile_place(int64_t K, int cw, int cols,
 // Forward: one workgroup (4 waves) per work item.  Batches of 256 Gaussians go through a double-
 // buffered LDS stage; wave w takes Gaussians [64w, 64w+64) of each batch in blocks of 4 steps of 4
 // (the MFMA K dimension).  Padding entries are exact zeros, so whole blocks are processed.
-__global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, const int4* __restrict__ items,
+// TAIL items (tail pairs of the two-zone footprint) accumulate W and D only: 2 MFMA per step.
+template <bool TAIL>
+__device__ __forceinline__ void fwd_accumulate(float* smem, int n, int k0, int k1, int tid, int wave, float xc, float yc,
+                                               int gs, const int* __restrict__ ids, const float4* __restrict__ rec,
+                                               f32x4& cW, f32x4& cR, f32x4& cG, f32x4& cB, f32x4& cD) {
+  // buffer b: float4 A[TP], float4 B[TP], float Z[TP] (lane-linear per wave, as LDS-DMA writes them)
+  constexpr int BUF = 2 * TP + TP / 4;  // float4 units per buffer
+  auto stage = [&](int g, int b) {
+    const float4* p = rec_of(g, n, rec);
+    float4* sA = reinterpret_cast<float4*>(smem) + b * BUF;
+    glds16(p, sA + 64 * wave);
+    glds16(p + 1, sA + TP + 64 * wave);
+    glds4(p + 2, reinterpret_cast<float*>(sA + 2 * TP) + 64 * wave);  // z = word C .x
+  };
+  stage(stage_id(k0 + tid, k1, ids), 0);
+  int idn = stage_id(k0 + TP + tid, k1, ids);
+  int buf = 0;
+  for (int base = k0; base < k1; base += TP, buf ^= 1) {
+    stage_wait();
+    __syncthreads();  // batch `buf` has landed; the other buffer's readers (previous batch) are done
+    if (base + TP < k1) stage(idn, buf ^ 1);
+    idn = stage_id(base + 2 * TP + tid, k1, ids);
+    const float4* sA = reinterpret_cast<const float4*>(smem) + buf * BUF;
+    const float4* sB = sA + TP;
+    const float* sZ = reinterpret_cast<const float*>(sB + TP);
+    const int cnt = min(TP, k1 - base) - wave * 64;           // Gaussians of this batch for this wave
+    const int nblk = cnt <= 0 ? 0 : min(4, (cnt + 15) >> 4);  // blocks of 4 steps (16 Gaussians)
+    for (int blk = 0; blk < nblk; ++blk) {
+      float A0[4], A1[4], A2[4], A3[4], A4[4], Bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = wave * 64 + blk * 16 + 4 * u + gs;
+        const float4 a = sA[j];
+        const float z = sZ[j];
+        const float dx = xc - a.x, dy = yc - a.y;
+        const float ex = __builtin_amdgcn_exp2f(dx * a.z * dx);
+        Bv[u] = __builtin_amdgcn_exp2f(dy * a.w * dy);
+        if constexpr (TAIL) {
+          const float oe = sB[j].x * ex;
+          A0[u] = oe;
+          A4[u] = oe * z;
+        } else {
+          const float4 b = sB[j];
+          const float oe = b.x * ex;
+          A0[u] = oe;
+          A1[u] = oe * b.y;
+          A2[u] = oe * b.z;
+          A3[u] = oe * b.w;
+          A4[u] = oe * z;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        cW = mfma4(A0[u], Bv[u], cW);
+        if constexpr (!TAIL) {
+          cR = mfma4(A1[u], Bv[u], cR);
+          cG = mfma4(A2[u], Bv[u], cG);
+          cB = mfma4(A3[u], Bv[u], cB);
+        }
+        cD = mfma4(A4[u], Bv[u], cD);
+      }
+    }
+  }
+}
+
+// Items of a tile (virtual tiles 2t: core, 2t+1: tail; contiguous in the item list).
+__device__ __forceinline__ int tile_chunks(int2 r) { return (r.y - r.x + CH - 1) / CH; }
+
+__device__ __forceinline__ void write_pixel(const ViewK& v, int p, const float* acc, float* __restrict__ out_rgb,
+                                            float* __restrict__ out_alpha, float* __restrict__ out_depth,
+                                            float4* __restrict__ saved4, float* __restrict__ savedD) {
+  const float aW = acc[0], den = 1.0f + aW;
+  out_rgb[3 * p + 0] = clamp01((v.bg[0] + acc[1]) / den);
+  out_rgb[3 * p + 1] = clamp01((v.bg[1] + acc[2]) / den);
+  out_rgb[3 * p + 2] = clamp01((v.bg[2] + acc[3]) / den);
+  if (out_alpha) out_alpha[p] = clamp01(aW / den);
+  if (out_depth) {
+    const float d = acc[4] / (aW + 1e-6f);
+    out_depth[p] = d < 0.0f ? 0.0f : d;
+  }
+  saved4[p] = make_float4(aW, acc[1], acc[2], acc[3]);
+  savedD[p] = acc[4];
+}
+
+__global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, int n, const int4* __restrict__ items,
                                                          const int* __restrict__ num_items, const int2* __restrict__ ranges,
                                                          const int* __restrict__ ids, const float4* __restrict__ rec,
                                                          float* __restrict__ fwd_part, float* __restrict__ out_rgb,
@@ -749,56 +971,17 @@ __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, const int4* __
   if ((int)blockIdx.x >= nitems) return;
   const int item = xcd_item(blockIdx.x, nitems);
   const int4 it = items[item];
-  const int tile = it.x, k0 = it.y, k1 = it.z;
+  const int tile = it.x >> 1, k0 = it.y, k1 = it.z;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int li = lane & 15, gs = lane >> 4;
   const float xc = (float)(tx * T + li) + 0.5f;  // A row = x
   const float yc = (float)(ty * T + li) + 0.5f;  // B col = y
   f32x4 cW = {0.f, 0.f, 0.f, 0.f}, cR = cW, cG = cW, cB = cW, cD = cW;
-  StageRec st = stage_rec(stage_id(k0 + tid, k1, ids), rec);
-  int idn = stage_id(k0 + TP + tid, k1, ids);
-  int buf = 0;
-  for (int base = k0; base < k1; base += TP, buf ^= 1) {
-    float4* sA = reinterpret_cast<float4*>(smem) + buf * (2 * TP + TP / 4);
-    float4* sB = sA + TP;
-    float* sZ = reinterpret_cast<float*>(sB + TP);
-    sA[tid] = st.a;
-    sB[tid] = st.b;
-    sZ[tid] = st.c.x;
-    __syncthreads();  // the other buffer's readers (previous batch) are also past this point
-    st = stage_rec(idn, rec);
-    idn = stage_id(base + 2 * TP + tid, k1, ids);
-    const int cnt = min(TP, k1 - base) - wave * 64;           // Gaussians of this batch for this wave
-    const int nblk = cnt <= 0 ? 0 : min(4, (cnt + 15) >> 4);  // blocks of 4 steps (16 Gaussians)
-    for (int blk = 0; blk < nblk; ++blk) {
-      float A0[4], A1[4], A2[4], A3[4], A4[4], Bv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = wave * 64 + blk * 16 + 4 * u + gs;
-        const float4 a = sA[j];
-        const float4 b = sB[j];
-        const float z = sZ[j];
-        const float dx = xc - a.x, dy = yc - a.y;
-        const float ex = __builtin_amdgcn_exp2f(dx * a.z * dx);
-        Bv[u] = __builtin_amdgcn_exp2f(dy * a.w * dy);
-        const float oe = b.x * ex;
-        A0[u] = oe;
-        A1[u] = oe * b.y;
-        A2[u] = oe * b.z;
-        A3[u] = oe * b.w;
-        A4[u] = oe * z;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        cW = mfma4(A0[u], Bv[u], cW);
-        cR = mfma4(A1[u], Bv[u], cR);
-        cG = mfma4(A2[u], Bv[u], cG);
-        cB = mfma4(A3[u], Bv[u], cB);
-        cD = mfma4(A4[u], Bv[u], cD);
-      }
-    }
-  }
+  if (it.x & 1)
+    fwd_accumulate<true>(smem, n, k0, k1, tid, wave, xc, yc, gs, ids, rec, cW, cR, cG, cB, cD);
+  else
+    fwd_accumulate<false>(smem, n, k0, k1, tid, wave, xc, yc, gs, ids, rec, cW, cR, cG, cB, cD);
   __syncthreads();
   {  // lane holds C[x = 4*gs + r][y = li]: pixel index y*16 + x, 4 consecutive x
     float* rw = smem + wave * 5 * TP + li * T + 4 * gs;
@@ -814,8 +997,8 @@ __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, const int4* __
   for (int c = 0; c < 5; ++c)
     acc[c] = ((smem[0 * 5 * TP + c * TP + tid] + smem[1 * 5 * TP + c * TP + tid]) + smem[2 * 5 * TP + c * TP + tid]) +
              smem[3 * 5 * TP + c * TP + tid];
-  const int2 rg = ranges[tile];
-  if (rg.y - rg.x > CH) {  // tile split over several items: combine in k_fwd_finalize
+  if (tile_chunks(ranges[2 * tile]) + tile_chunks(ranges[2 * tile + 1]) > 1) {
+    // tile split over several items: combine in k_fwd_finalize
     float* dst = fwd_part + (size_t)item * 5 * TP;
 #pragma unroll
     for (int c = 0; c < 5; ++c) dst[c * TP + tid] = acc[c];
@@ -823,52 +1006,31 @@ __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, const int4* __
   }
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
   if (x >= v.W || y >= v.H) return;
-  const int p = y * v.W + x;
-  const float aW = acc[0], den = 1.0f + aW;
-  out_rgb[3 * p + 0] = clamp01((v.bg[0] + acc[1]) / den);
-  out_rgb[3 * p + 1] = clamp01((v.bg[1] + acc[2]) / den);
-  out_rgb[3 * p + 2] = clamp01((v.bg[2] + acc[3]) / den);
-  if (out_alpha) out_alpha[p] = clamp01(aW / den);
-  if (out_depth) {
-    const float d = acc[4] / (aW + 1e-6f);
-    out_depth[p] = d < 0.0f ? 0.0f : d;
-  }
-  saved4[p] = make_float4(aW, acc[1], acc[2], acc[3]);
-  savedD[p] = acc[4];
+  write_pixel(v, y * v.W + x, acc, out_rgb, out_alpha, out_depth, saved4, savedD);
 }
 
 // Tiles with no Gaussians (background) or split over several work items: sum the items' partial
-// accumulators in chunk order (deterministic) and write the outputs.
+// accumulators in item order (core chunks, then tail chunks: deterministic) and write the outputs.
 __global__ __launch_bounds__(256) void k_fwd_finalize(ViewK v, const int2* __restrict__ ranges,
                                                       const int* __restrict__ tile_item0, const float* __restrict__ fwd_part,
                                                       float* __restrict__ out_rgb, float* __restrict__ out_alpha,
                                                       float* __restrict__ out_depth, float4* __restrict__ saved4,
                                                       float* __restrict__ savedD) {
   const int tile = blockIdx.x, tid = threadIdx.x;
-  const int2 rg = ranges[tile];
-  const int nch = (rg.y - rg.x + CH - 1) / CH;
+  const int nch = tile_chunks(ranges[2 * tile]) + tile_chunks(ranges[2 * tile + 1]);
   if (nch == 1) return;  // written by k_raster_fwd_mfma
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  const float* src = fwd_part + (size_t)(nch > 0 ? tile_item0[tile] : 0) * 5 * TP;
+  const float* src = fwd_part + (size_t)(nch > 0 ? tile_item0[2 * tile] : 0) * 5 * TP;
   for (int c = 0; c < nch; ++c)
 #pragma unroll
     for (int q = 0; q < 5; ++q) acc[q] += src[(size_t)c * 5 * TP + q * TP + tid];
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
   if (x >= v.W || y >= v.H) return;
-  const int p = y * v.W + x;
-  const float aW = acc[0], den = 1.0f + aW;
-  out_rgb[3 * p + 0] = clamp01((v.bg[0] + acc[1]) / den);
-  out_rgb[3 * p + 1] = clamp01((v.bg[1] + acc[2]) / den);
-  out_rgb[3 * p + 2] = clamp01((v.bg[2] + acc[3]) / den);
-  if (out_alpha) out_alpha[p] = clamp01(aW / den);
-  if (out_depth) {
-    const float d = acc[4] / (aW + 1e-6f);
-    out_depth[p] = d < 0.0f ? 0.0f : d;
-  }
-  saved4[p] = make_float4(aW, acc[1], acc[2], acc[3]);
-  savedD[p] = acc[4];
+  write_pixel(v, y * v.W + x, acc, out_rgb, out_alpha, out_depth, saved4, savedD);
 }
+
+constexpr int UL = 5 * 2 * TP;  // floats of backward operands per tile (k_pixel_grads)
 
 // Per-pixel upstream vector U = (dC_r, dC_g, dC_b, dW, dD) of the OIT finalize
 // (torch_renderer.py:192-203), laid out [tile][channel][256] for the backward work items.
@@ -908,9 +1070,16 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
     }
     u[3] = gW;
   }
-  float* dst = U + (size_t)tile * 5 * TP;
+  // operand layout of k_raster_bwd_mfma (UL floats per tile): per channel k, AT[l][s] = U_k(x = 4xs+s,
+  // y = li) and then AR[l][s] = U_k(x = li, y = 4xs+s), l = li + 16 xs: lane l reads one float4 each
+  float* dst = U + (size_t)tile * UL;
+  const int px = tid & (T - 1), py = tid >> 4;
+  const int at = (py + 16 * (px >> 2)) * 4 + (px & 3), ar = TP + (px + 16 * (py >> 2)) * 4 + (py & 3);
 #pragma unroll
-  for (int k = 0; k < 5; ++k) dst[k * TP + tid] = u[k];
+  for (int k = 0; k < 5; ++k) {
+    dst[k * 2 * TP + at] = u[k];
+    dst[k * 2 * TP + ar] = u[k];
+  }
 }
 
 // Backward: one workgroup (4 waves) per work item; wave w takes groups [4w, 4w+4) of 16 Gaussians of
@@ -928,7 +1097,7 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
 // Partials per pair (9 floats) go to the pair's slot (Gaussian's first slot + index of the tile
 // inside its rectangle), so k_reduce_bwd reads each Gaussian's partials contiguously and in order.
 #ifndef GR_BWD_WAVES
-#define GR_BWD_WAVES 3
+#define GR_BWD_WAVES 4
 #endif
 
 // Sum over the 4 lane rows (lanes l, l+16, l+32, l+48) of a pair of values with one
@@ -943,58 +1112,47 @@ __device__ __forceinline__ float pair32(float ab, float cd) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-__global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
-    ViewK v, const int4* __restrict__ items, const int* __restrict__ num_items, const int* __restrict__ ids,
-    const float4* __restrict__ rec, const float* __restrict__ U, float* __restrict__ partials) {
-  __shared__ __attribute__((aligned(16))) float4 sA[2][TP];
-  __shared__ __attribute__((aligned(16))) float4 sB[2][TP];
-  __shared__ float sZ[2][TP];
-  __shared__ int sSlot[2][TP];
-  const int nitems = *num_items;
-  if ((int)blockIdx.x >= nitems) return;
-  const int item = xcd_item(blockIdx.x, nitems);
-  const int4 it = items[item];
-  const int tile = it.x, k0 = it.y, k1 = it.z;
-  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int li = lane & 15, xs = lane >> 4;
-  // A operands (tile-constant): AT[k][s] = U_k(x = 4xs+s, y = li), AR[k][s] = U_k(x = li, y = 4xs+s)
-  float AT[5][4], AR[5][4];
+// One staged batch loop of a backward work item.  TAIL items (tail pairs of the two-zone
+// footprint) carry only the depth-coupled terms: channels dW and dD (16 MFMA per 16 pairs), colour
+// sums 0, gw = dW + z dD.
+template <bool TAIL>
+__device__ __forceinline__ void bwd_item(int n, int tile, int k0, int k1, int tid, int wave, int li, int xs, int tx, int ty,
+                                         const float* __restrict__ U, const int* __restrict__ ids,
+                                         const float4* __restrict__ rec, float* __restrict__ partials,
+                                         float4 (*sA)[TP], float4 (*sB)[TP], float4 (*sC)[TP], float4* sU) {
+  constexpr int KLO = TAIL ? 3 : 0;  // first upstream channel contracted
+  const int lane = tid & 63;
+  // A operands (tile-constant) staged in LDS in lane order: sU[k][0][l] = AT_k, sU[k][1][l] = AR_k,
+  // AT_k[s] = U_k(x = 4xs+s, y = li), AR_k[s] = U_k(x = li, y = 4xs+s)
   {
-    const float* Ut = U + (size_t)tile * 5 * TP;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const float4 t4 = *reinterpret_cast<const float4*>(Ut + k * TP + li * T + 4 * xs);
-      AT[k][0] = t4.x;
-      AT[k][1] = t4.y;
-      AT[k][2] = t4.z;
-      AT[k][3] = t4.w;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) AR[k][s] = Ut[k * TP + (4 * xs + s) * T + li];
-    }
+    const float4* Ug = reinterpret_cast<const float4*>(U + (size_t)tile * UL);
+    for (int c = wave; c < UL / 256; c += 4) glds16(Ug + 64 * c + lane, sU + 64 * c);
   }
   const float x0 = (float)(tx * T + 4 * xs) + 0.5f, y0 = (float)(ty * T + 4 * xs) + 0.5f;
-  StageRec st = stage_rec(stage_id(k0 + tid, k1, ids), rec);
-  int slot = st.g >= 0 ? pair_slot(st.c, tx, ty) : -1;
+  auto stage = [&](int g, int b) {
+    const float4* p = rec_of(g, n, rec);
+    glds16(p, &sA[b][64 * wave]);
+    glds16(p + 1, &sB[b][64 * wave]);
+    glds16(p + 2, &sC[b][64 * wave]);
+  };
+  stage(stage_id(k0 + tid, k1, ids), 0);
   int idn = stage_id(k0 + TP + tid, k1, ids);
   int buf = 0;
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
-    sA[buf][tid] = st.a;
-    sB[buf][tid] = st.b;
-    sZ[buf][tid] = st.c.x;
-    sSlot[buf][tid] = slot;
-    __syncthreads();  // the other buffer's readers (previous batch) are also past this point
-    st = stage_rec(idn, rec);
-    slot = st.g >= 0 ? pair_slot(st.c, tx, ty) : -1;
+    stage_wait();
+    __syncthreads();  // batch `buf` has landed; the other buffer's readers (previous batch) are done
+    if (base + TP < k1) stage(idn, buf ^ 1);
     idn = stage_id(base + 2 * TP + tid, k1, ids);
-    const int cnt = min(TP, k1 - base) - wave * 64;
+    const int nb = min(TP, k1 - base);  // Gaussians of this batch
+    const int cnt = nb - wave * 64;
     const int ngr = cnt <= 0 ? 0 : min(4, (cnt + 15) >> 4);
     for (int gi = 0; gi < ngr; ++gi) {
       const int j = wave * 64 + gi * 16 + li;
       const float4 a = sA[buf][j];
       const float4 b = sB[buf][j];
-      const float z = sZ[buf][j];
-      const int myslot = sSlot[buf][j];
+      const float4 c = sC[buf][j];
+      const float z = c.x;
+      const int myslot = j < nb ? pair_slot(c, tx, ty) : -1;
       float ex[4], ey[4], dx[4], dy[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -1005,32 +1163,41 @@ __global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
       }
       f32x4 DT[5], DR[5];
 #pragma unroll
-      for (int k = 0; k < 5; ++k) {
+      for (int k = KLO; k < 5; ++k) {
         DT[k] = f32x4{0.f, 0.f, 0.f, 0.f};
         DR[k] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          DT[k] = mfma4(AT[k][s], ex[s], DT[k]);
-          DR[k] = mfma4(AR[k][s], ey[s], DR[k]);
-        }
+      for (int k = KLO; k < 5; ++k) {
+        const float4 at = sU[(2 * k) * 64 + lane], ar = sU[(2 * k + 1) * 64 + lane];
+        DT[k] = mfma4(at.x, ex[0], DT[k]);
+        DR[k] = mfma4(ar.x, ey[0], DR[k]);
+        DT[k] = mfma4(at.y, ex[1], DT[k]);
+        DR[k] = mfma4(ar.y, ey[1], DR[k]);
+        DT[k] = mfma4(at.z, ex[2], DT[k]);
+        DR[k] = mfma4(ar.z, ey[2], DR[k]);
+        DT[k] = mfma4(at.w, ex[3], DT[k]);
+        DR[k] = mfma4(ar.w, ey[3], DR[k]);
+      }
       // lane holds T[y = 4xs + r][g = li] and R[x = 4xs + r][g = li]
       float S[NPART] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        S[0] = fmaf(ey[r], DT[0][r], S[0]);
-        S[1] = fmaf(ey[r], DT[1][r], S[1]);
-        S[2] = fmaf(ey[r], DT[2][r], S[2]);
+        if constexpr (!TAIL) {
+          S[0] = fmaf(ey[r], DT[0][r], S[0]);
+          S[1] = fmaf(ey[r], DT[1][r], S[1]);
+          S[2] = fmaf(ey[r], DT[2][r], S[2]);
+        }
         S[3] = fmaf(ey[r], DT[4][r], S[3]);
-        const float GT = fmaf(z, DT[4][r], fmaf(b.w, DT[2][r], fmaf(b.z, DT[1][r], fmaf(b.y, DT[0][r], DT[3][r]))));
+        const float GT = TAIL ? fmaf(z, DT[4][r], DT[3][r])
+                              : fmaf(z, DT[4][r], fmaf(b.w, DT[2][r], fmaf(b.z, DT[1][r], fmaf(b.y, DT[0][r], DT[3][r]))));
         const float t = ey[r] * GT;
         S[4] += t;
         const float tdy = t * dy[r];
         S[6] += tdy;
         S[8] = fmaf(tdy, dy[r], S[8]);
-        const float GR = fmaf(z, DR[4][r], fmaf(b.w, DR[2][r], fmaf(b.z, DR[1][r], fmaf(b.y, DR[0][r], DR[3][r]))));
+        const float GR = TAIL ? fmaf(z, DR[4][r], DR[3][r])
+                              : fmaf(z, DR[4][r], fmaf(b.w, DR[2][r], fmaf(b.z, DR[1][r], fmaf(b.y, DR[0][r], DR[3][r]))));
         const float tdx = (ex[r] * GR) * dx[r];  // (0 * G) * dx: padding stays 0, never 0 * inf
         S[5] += tdx;
         S[7] = fmaf(tdx, dx[r], S[7]);
@@ -1047,6 +1214,31 @@ __global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
       }
     }
   }
+}
+
+// depth = 0 (no upstream depth gradient): tail items have nothing to add and return at once; their
+// slots are never read (k_reduce_bwd skips tail tiles in that mode).
+__global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
+    ViewK v, int n, const int4* __restrict__ items, const int* __restrict__ num_items, const int* __restrict__ ids,
+    const float4* __restrict__ rec, const float* __restrict__ U, float* __restrict__ partials, int depth) {
+  __shared__ __attribute__((aligned(16))) float4 sA[2][TP];
+  __shared__ __attribute__((aligned(16))) float4 sB[2][TP];
+  __shared__ __attribute__((aligned(16))) float4 sC[2][TP];
+  __shared__ __attribute__((aligned(16))) float4 sU[UL / 4];
+  const int nitems = *num_items;
+  if ((int)blockIdx.x >= nitems) return;
+  const int item = xcd_item(blockIdx.x, nitems);
+  const int4 it = items[item];
+  const bool tail = it.x & 1;
+  if (tail && !depth) return;
+  const int tile = it.x >> 1, k0 = it.y, k1 = it.z;
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int li = lane & 15, xs = lane >> 4;
+  if (tail)
+    bwd_item<true>(n, tile, k0, k1, tid, wave, li, xs, tx, ty, U, ids, rec, partials, sA, sB, sC, sU);
+  else
+    bwd_item<false>(n, tile, k0, k1, tid, wave, li, xs, tx, ty, U, ids, rec, partials, sA, sB, sC, sU);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1077,7 +1269,7 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
                                                     const unsigned long long* __restrict__ offsets,
                                                     const float* __restrict__ partials, float* __restrict__ d_means,
                                                     float* __restrict__ d_scales, float* __restrict__ d_colors,
-                                                    float* __restrict__ d_opac) {
+                                                    float* __restrict__ d_opac, int depth) {
   __shared__ __attribute__((aligned(16))) float sP[RWIN * NPART + 4];
   const int g0 = blockIdx.x * RG;
   const int tid = threadIdx.x, q4 = tid & 3;
@@ -1109,7 +1301,7 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
   for (int q = 0; q < NPART; ++q) S[q] = 0.0;
   unsigned cnt = 0;
   if (i < n) {
-    cnt = (unsigned)(counts[i] & 0xffffffffu);
+    cnt = counts[i] != 0 ? 1u : 0u;  // any kept tile (core or tail)
     if (cnt > 0) {
       const long long base = (long long)(offsets[i] >> 32);
       const float* src = staged ? sP + (base * NPART - fa) : partials + base * NPART;
@@ -1123,7 +1315,8 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
         ++ty;
       }
       for (int j = q4; j < area; j += 4) {
-        if (tile_pass(v, a.x, a.y, a.z, a.w, tx, ty)) {
+        const int cls = tile_class(v, a.x, a.y, a.z, a.w, tx, ty);
+        if (cls == 2 || (cls == 1 && depth)) {  // tail slots are written only with depth gradients
 #pragma unroll
           for (int q = 0; q < NPART; ++q) S[q] += (double)src[j * NPART + q];
         }
@@ -1445,19 +1638,19 @@ gr_status gr_profile_end(double total_ms[4], int launches[4]) {
 }
 const char* gr_version(void) { return GR_VERSION_STR; }
 
-void gr_geom_layout(int n, size_t offsets_out[6]) { geom_fixed(n, offsets_out); }
+void gr_geom_layout(int n, size_t offsets_out[GR_GEOM_PARTS]) { geom_fixed(n, offsets_out); }
 
 void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[3]) {
   (void)n;
   size_t off[6];
-  bins_fixed(tiles_x_of(v->width) * tiles_y_of(v->height), plan ? plan->num_pairs : 0, off);
+  bins_fixed(vtiles_of(v), plan ? plan->num_pairs : 0, off);
   offsets_out[0] = off[0];
   offsets_out[1] = off[1];
   offsets_out[2] = off[2];
 }
 
 size_t gr_geom_bytes(int n) {
-  size_t off[6];
+  size_t off[GR_GEOM_PARTS];
   return geom_fixed(n, off) + align_up(scan_tmp_bytes(n > 0 ? n : 1));
 }
 
@@ -1465,16 +1658,15 @@ size_t gr_saved_floats(const gr_view* v) { return (size_t)5 * v->width * v->heig
 
 size_t gr_bins_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
-  const int tiles = tiles_x_of(v->width) * tiles_y_of(v->height);
   size_t off[6];
-  return bins_fixed(tiles, plan->num_pairs, off);
+  return bins_fixed(vtiles_of(v), plan->num_pairs, off);
 }
 
 size_t gr_fwd_scratch_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
-  const int tiles = tiles_x_of(v->width) * tiles_y_of(v->height);
+  const int vtiles = vtiles_of(v);
   size_t off[3];
-  return scratch_fixed(tiles, plan->num_pairs, off) + align_up(tile_sort_tmp_bytes(plan->num_pairs, tiles));
+  return scratch_fixed(vtiles, plan->num_pairs, off) + align_up(tile_sort_tmp_bytes(plan->num_pairs, vtiles));
 }
 
 // Backward workspace: pair partials (one 9-float slot per rectangle tile) + per-pixel upstream
@@ -1483,17 +1675,19 @@ size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
   const size_t tiles = (size_t)tiles_x_of(v->width) * tiles_y_of(v->height);
   return align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)) +
-         align_up(tiles * 5 * TP * sizeof(float));
+         align_up(tiles * UL * sizeof(float));
 }
 
 // Decode the scanned total (high word: partial-sum slots, low word: pairs) into the plan; a count
 // that does not fit int32 is flagged as num_pairs = -1 (gr_fwd_render then reports the overflow).
-__global__ void k_plan(const unsigned long long* __restrict__ total, gr_plan* plan) {
+__global__ void k_plan(const unsigned long long* __restrict__ total, const unsigned* __restrict__ ttotal, gr_plan* plan) {
   const unsigned long long t = *total;
-  const long long pairs = (long long)(t & 0xffffffffull), slots = (long long)(t >> 32);
+  const long long core = (long long)(t & 0xffffffffull), slots = (long long)(t >> 32);
+  const long long pairs = core + (long long)*ttotal;
   const bool ok = pairs < (1ll << 31) && slots < (1ll << 31);
   plan->num_pairs = ok ? pairs : -1;
   plan->num_slots = ok ? slots : -1;
+  plan->num_core_pairs = ok ? core : -1;
 }
 
 gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, const float* scales, const float* colors,
@@ -1507,6 +1701,7 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
   if (n == 0) {
     plan->num_pairs = 0;
     plan->num_slots = 0;
+    plan->num_core_pairs = 0;
     return GR_OK;
   }
   if (!means || !scales || !colors || !opacities || !geom) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
@@ -1521,7 +1716,10 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
   GR_HIP_TRY(hipGetLastError());
   size_t tmp = scan_tmp_bytes(n);
   GR_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(g.scan_tmp, tmp, g.counts, g.offsets, n + 1, s));
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1), 0, s, (const unsigned long long*)(g.offsets + n), g.plan);
+  tmp = scan_tmp_bytes(n);
+  GR_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(g.scan_tmp, tmp, g.tcounts, g.toffsets, n + 1, s));
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1), 0, s, (const unsigned long long*)(g.offsets + n),
+                     (const unsigned*)(g.toffsets + n), g.plan);
   GR_HIP_TRY(hipGetLastError());
   GR_HIP_TRY(hipMemcpyAsync(plan, g.plan, sizeof(gr_plan), hipMemcpyDeviceToHost, s));
   return GR_OK;
@@ -1533,6 +1731,7 @@ gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const floa
   if (plan) {
     plan->num_pairs = 0;
     plan->num_slots = 0;
+    plan->num_core_pairs = 0;
   }
   gr_status st = gr_fwd_prepare_async(v, n, means, scales, colors, color_dim, opacities, geom, geom_bytes, plan, stream);
   if (st != GR_OK || n == 0) return st;
@@ -1556,64 +1755,87 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
     return set_error(GR_ERR_WORKSPACE, "forward scratch workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const ViewK vk = make_viewk(v);
-  const int tiles = vk.tiles_x * vk.tiles_y;
-  Bins b = bins_view(bins, tiles, num_pairs);
-  Scratch sc = scratch_view(scratch, tiles, num_pairs);
+  const int tiles = vk.tiles_x * vk.tiles_y, vtiles = 2 * tiles;
+  Bins b = bins_view(bins, vtiles, num_pairs);
+  Scratch sc = scratch_view(scratch, vtiles, num_pairs);
   prof_mark(PROF_BINNING, s);
   if (n > 0 && num_pairs > 0) {
     Geom g = geom_view((void*)geom, n);
     const auto* cnt = (const unsigned long long*)g.counts;
     const auto* offs = (const unsigned long long*)g.offsets;
-    if (short_keys(tiles)) {
-      hipLaunchKernelGGL((k_emit<uint16_t, unsigned long long>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
-                         (const int4*)g.rect, cnt, offs, g.rec, (const uint16_t*)nullptr,
-                         (uint16_t*)sc.keys_in, sc.ids_in);
-      GR_HIP_TRY(hipGetLastError());
-      const TSortPlan tp = tsort_plan(num_pairs, tiles);
-      int* M = (int*)sc.sort_tmp;
-      int* S = (int*)((char*)sc.sort_tmp + align_up(tp.cells * sizeof(int)));
-      int* Tt = (int*)((char*)S + align_up(tp.cells * sizeof(int)));
-      const size_t lds_count = (size_t)tiles * sizeof(int), lds_place = lds_count * tp.waves;
-      hipLaunchKernelGGL(k_tile_count, dim3(tp.cols), dim3(256), lds_count, s, num_pairs, tp.cw, tp.cols, tiles,
-                         (const uint16_t*)sc.keys_in, M);
-      GR_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_tile_colscan, dim3((tiles + CS_T - 1) / CS_T), dim3(CS_T * CS_G), 0, s, tp.cols, tiles,
-                         (const int*)M, S, Tt);
-      GR_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, tiles, b.ranges, (const int*)Tt, b.items,
-                         b.num_items, b.tile_item0);
-      GR_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_tile_place, dim3(tp.cols), dim3(64 * tp.waves), lds_place, s, num_pairs, tp.cw, tp.cols,
-                         tiles, bits_for((uint32_t)tiles), (const uint16_t*)sc.keys_in, (const int*)sc.ids_in,
-                         (const int*)S, (const int2*)b.ranges, b.ids);
-    } else {
-      hipLaunchKernelGGL((k_emit<uint32_t, unsigned long long>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
-                         (const int4*)g.rect, cnt, offs, g.rec, (const uint32_t*)nullptr, sc.keys_in,
+    if (short_keys(vtiles)) {
+      // counting sort of each region (core pairs [0, Kc), tail pairs [Kc, K)) on 16-bit tile keys
+      const int64_t Kc = plan->num_core_pairs, Kr[2] = {Kc, num_pairs - Kc};
+      hipLaunchKernelGGL((k_emit_zones<uint16_t, false>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
+                         (const int4*)g.rect, cnt, offs, (const unsigned*)g.toffsets, g.rec, (uint16_t*)sc.keys_in,
                          sc.ids_in);
       GR_HIP_TRY(hipGetLastError());
-      GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * tiles, s));
-      const int bits = bits_for((uint32_t)tiles);
-      size_t tmp = tile_sort_tmp_bytes(num_pairs, tiles);
+      TSortPlan tp[2];
+      int* Sz[2];
+      int* Tz[2];
+      char* q = (char*)sc.sort_tmp;
+      int* M = (int*)q;
+      const size_t cells = tsort_cells_bound(num_pairs, tiles);
+      q += align_up(cells * sizeof(int));
+      for (int z = 0; z < 2; ++z) {
+        tp[z] = tsort_plan(Kr[z], tiles);
+        Sz[z] = (int*)q;
+        q += align_up(cells * sizeof(int));
+        Tz[z] = (int*)q;
+        q += align_up((size_t)tiles * sizeof(int));
+      }
+      const uint16_t* kz[2] = {(const uint16_t*)sc.keys_in, (const uint16_t*)sc.keys_in + Kc};
+      const int* iz[2] = {sc.ids_in, sc.ids_in + Kc};
+      for (int z = 0; z < 2; ++z) {
+        if (Kr[z] > 0) {
+          hipLaunchKernelGGL(k_tile_count, dim3(tp[z].cols), dim3(256), (size_t)tiles * sizeof(int), s, Kr[z], tp[z].cw,
+                             tp[z].cols, tiles, kz[z], M);
+          GR_HIP_TRY(hipGetLastError());
+          hipLaunchKernelGGL(k_tile_colscan, dim3((tiles + CS_T - 1) / CS_T), dim3(CS_T * CS_G), 0, s, tp[z].cols, tiles,
+                             (const int*)M, Sz[z], Tz[z]);
+        } else {
+          GR_HIP_TRY(hipMemsetAsync(Tz[z], 0, (size_t)tiles * sizeof(int), s));
+        }
+        GR_HIP_TRY(hipGetLastError());
+      }
+      hipLaunchKernelGGL(k_work_items_zones, dim3(1), dim3(1024), 0, s, tiles, (int)Kc, (const int*)Tz[0],
+                         (const int*)Tz[1], b.ranges, b.items, b.num_items, b.tile_item0);
+      GR_HIP_TRY(hipGetLastError());
+      for (int z = 0; z < 2; ++z) {
+        if (Kr[z] == 0) continue;
+        hipLaunchKernelGGL(k_tile_place, dim3(tp[z].cols), dim3(64 * tp[z].waves), (size_t)tiles * sizeof(int) * tp[z].waves,
+                           s, Kr[z], tp[z].cw, tp[z].cols, tiles, bits_for((uint32_t)tiles), kz[z], iz[z],
+                           (const int*)Sz[z], (const int2*)b.ranges, z, b.ids);
+        GR_HIP_TRY(hipGetLastError());
+      }
+    } else {
+      // radix sort of the whole pair array on virtual-tile keys (> TSORT_MAX_TILES tiles)
+      hipLaunchKernelGGL((k_emit_zones<uint32_t, true>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
+                         (const int4*)g.rect, cnt, offs, (const unsigned*)g.toffsets, g.rec, sc.keys_in, sc.ids_in);
+      GR_HIP_TRY(hipGetLastError());
+      GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * vtiles, s));
+      const int bits = bits_for((uint32_t)vtiles);
+      size_t tmp = tile_sort_tmp_bytes(num_pairs, vtiles);
       GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp, tmp, sc.keys_in, b.keys, sc.ids_in, b.ids,
                                                     (int)num_pairs, 0, bits, s));
       hipLaunchKernelGGL(k_ranges<uint32_t>, dim3(blocks_for(num_pairs)), dim3(256), 0, s, num_pairs, b.keys, b.ranges);
       GR_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, tiles, b.ranges, (const int*)nullptr, b.items,
-                         b.num_items, b.tile_item0);
+      hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
+                         b.tile_item0);
     }
   } else {
-    GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * tiles, s));
-    hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, tiles, b.ranges, (const int*)nullptr, b.items,
-                       b.num_items, b.tile_item0);
+    GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * vtiles, s));
+    hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
+                       b.tile_item0);
   }
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_BINNING, s);
   Geom g = geom_view((void*)geom, n > 0 ? n : 1);
   const size_t HW = (size_t)v->width * v->height;
-  const int64_t cap = item_cap(tiles, num_pairs);
+  const int64_t cap = item_cap(vtiles, num_pairs);
   if (num_pairs > 0) {
     prof_mark(PROF_RASTER_FWD, s);
-    hipLaunchKernelGGL(k_raster_fwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, (const int4*)b.items,
+    hipLaunchKernelGGL(k_raster_fwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
                        (const int*)b.num_items, (const int2*)b.ranges, (const int*)b.ids, (const float4*)g.rec,
                        sc.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
     GR_HIP_TRY(hipGetLastError());
@@ -1643,7 +1865,7 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
   const ViewK vk = make_viewk(v);
   const int tiles = vk.tiles_x * vk.tiles_y;
   Geom g = geom_view((void*)geom, n);
-  Bins b = bins_view((void*)bins, tiles, num_pairs);
+  Bins b = bins_view((void*)bins, 2 * tiles, num_pairs);
   const size_t HW = (size_t)v->width * v->height;
   float* partials = (float*)ws;
   if (num_pairs > 0) {
@@ -1651,10 +1873,11 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
     hipLaunchKernelGGL(k_pixel_grads, dim3(tiles), dim3(256), 0, s, vk, (const float4*)saved, saved + 4 * HW, g_rgb,
                        g_alpha, g_depth, U);
     GR_HIP_TRY(hipGetLastError());
-    const int64_t cap = item_cap(tiles, num_pairs);
+    const int64_t cap = item_cap(2 * tiles, num_pairs);
     prof_mark(PROF_RASTER_BWD, s);
-    hipLaunchKernelGGL(k_raster_bwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, (const int4*)b.items,
-                       (const int*)b.num_items, (const int*)b.ids, (const float4*)g.rec, (const float*)U, partials);
+    hipLaunchKernelGGL(k_raster_bwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
+                       (const int*)b.num_items, (const int*)b.ids, (const float4*)g.rec, (const float*)U, partials,
+                       g_depth != nullptr ? 1 : 0);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_BWD, s);
   }
@@ -1663,12 +1886,12 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
     hipLaunchKernelGGL(k_reduce_bwd<3>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
                        (const float4*)g.rec, (const int4*)g.rect, (const unsigned long long*)g.counts,
                        (const unsigned long long*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
-                       d_opacities);
+                       d_opacities, g_depth != nullptr ? 1 : 0);
   else
     hipLaunchKernelGGL(k_reduce_bwd<12>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
                        (const float4*)g.rec, (const int4*)g.rect, (const unsigned long long*)g.counts,
                        (const unsigned long long*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
-                       d_opacities);
+                       d_opacities, g_depth != nullptr ? 1 : 0);
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_REDUCE, s);
   return GR_OK;
@@ -1761,7 +1984,7 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
       uint64_t* kout = (uint64_t*)(e + q_kout);
       // low 32 bits = depth key; high bits = tile
       hipLaunchKernelGGL((k_emit<uint64_t, int>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n, (const int4*)lr.rect,
-                         (const int*)lr.counts, (const int*)lr.offsets, (float4*)nullptr, (const uint64_t*)nullptr,
+                         (const int*)lr.counts, (const int*)lr.offsets, (const uint64_t*)nullptr,
                          kin, (int*)(e + q_iin));
       GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_patch_depth, dim3(blocks_for(K)), dim3(256), 0, s, (int64_t)K, kin, (const int*)(e + q_iin),
@@ -1774,7 +1997,7 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
       uint32_t* kin = (uint32_t*)(e + q_kin);
       uint32_t* kout = (uint32_t*)(e + q_kout);
       hipLaunchKernelGGL((k_emit<uint32_t, int>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n, (const int4*)lr.rect,
-                         (const int*)lr.counts, (const int*)lr.offsets, (float4*)nullptr, (const uint32_t*)nullptr,
+                         (const int*)lr.counts, (const int*)lr.offsets, (const uint32_t*)nullptr,
                          kin, (int*)(e + q_iin));
       GR_HIP_TRY(hipGetLastError());
       GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e + q_tmp, t2, kin, kout, (int*)(e + q_iin), (int*)(e + q_iout), K, 0,

@@ -8,8 +8,10 @@ libgr_hip.so through a ``torch.autograd.Function`` — not by torch ops.  Differ
 (DESIGN.md §Semantics):
 
 * a Gaussian is evaluated on the 16x16 tiles where its largest weight is >= o*exp(-cutoff^2/2)
-  (default cutoff 7: outputs and gradients agree with the dense reference to <=1e-5 relative L2 on
-  its own fixtures, including depth gradients on near-empty pixels);
+  (default cutoff 7); tiles where it stays below o*exp(-core_cutoff^2/2) (default 5.5) are "tail"
+  tiles that carry only the weight and depth sums forward and the depth-coupled gradient terms
+  backward (only when an upstream depth gradient is given): outputs and gradients agree with the
+  dense reference to <=5e-6 relative L2 on its own fixtures, with and without depth gradients;
 * ``chunk_size`` is accepted and ignored (no chunk loop);
 * gradients flow to means, scales, colours/SH, opacities and background; not to the camera matrices;
 * tensors must live on a HIP device: CPU tensors raise ``RuntimeError`` (there is no CPU fallback).
@@ -29,6 +31,7 @@ except ImportError:  # pragma: no cover
     import _native  # type: ignore
 
 DEFAULT_CUTOFF = 7.0
+DEFAULT_CORE_CUTOFF = 5.5
 
 
 @dataclass
@@ -106,7 +109,8 @@ def _host_matrix(t: torch.Tensor) -> np.ndarray:
     return _host_copy(t, (4, 4))
 
 
-def make_view(view, proj, width: int, height: int, background=None, cutoff: float = DEFAULT_CUTOFF) -> _native.GrView:
+def make_view(view, proj, width: int, height: int, background=None, cutoff: float = DEFAULT_CUTOFF,
+              core_cutoff: float = DEFAULT_CORE_CUTOFF) -> _native.GrView:
     """Build a gr_view from host (numpy / tensor) matrices."""
     V = view if isinstance(view, np.ndarray) else _host_matrix(view)
     P = proj if isinstance(proj, np.ndarray) else _host_matrix(proj)
@@ -127,6 +131,7 @@ def make_view(view, proj, width: int, height: int, background=None, cutoff: floa
     cam = np.linalg.inv(V.astype(np.float64))[:3, 3]
     gv.cam_pos[:] = cam.astype(np.float32).tolist()
     gv.cutoff = float(cutoff)
+    gv.core_cutoff = float(core_cutoff)
     return gv
 
 
@@ -161,10 +166,10 @@ class Prepared:
 
     def plan(self) -> _native.GrPlan:
         self.event.synchronize()
-        pairs, slots = (int(x) for x in self.plan_host.tolist())
+        pairs, slots, core = (int(x) for x in self.plan_host.tolist())
         if pairs < 0 or slots < 0:
             raise RuntimeError("gr_fwd_prepare: pair count overflows int32")
-        return _native.GrPlan(pairs, slots)
+        return _native.GrPlan(pairs, slots, core)
 
 
 def prepare_native(means, scales, colors, opacities, gv: _native.GrView) -> Prepared:
@@ -174,7 +179,7 @@ def prepare_native(means, scales, colors, opacities, gv: _native.GrView) -> Prep
     n = int(means.shape[0])
     cd = 3 if colors.dim() == 2 else 12
     geom = torch.empty((int(L.gr_geom_bytes(n)),), dtype=torch.uint8, device=dev)
-    plan_host = torch.zeros(2, dtype=torch.int64, pin_memory=True)  # gr_plan {num_pairs, num_slots}
+    plan_host = torch.zeros(3, dtype=torch.int64, pin_memory=True)  # gr_plan {num_pairs, num_slots, num_core_pairs}
     _native.check(L.gr_fwd_prepare_async(ctypes.byref(gv), n, _native.ptr(means), _native.ptr(scales),
                                          _native.ptr(colors), cd, _native.ptr(opacities), _native.ptr(geom),
                                          geom.numel(), ctypes.c_void_p(plan_host.data_ptr()), _stream(dev)),
@@ -244,6 +249,9 @@ class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means, scales, colors, opacities, background, gv, prepared):
         out, alpha, depth, st = forward_native(means, scales, colors, opacities, gv, prepared)
+        # an output the loss does not use gets a None gradient instead of zeros, so an unused depth
+        # output lets the backward skip the tail pairs (gr_bwd with g_depth = NULL)
+        ctx.set_materialize_grads(False)
         ctx.st = st
         ctx.save_for_backward(means, scales, colors, opacities, background)
         return out, alpha, depth
@@ -272,15 +280,15 @@ def _device_inputs(means, scales, colors, opacities):
 
 
 def prepare_view(means, scales, colors, opacities, view, proj, width, height, background=None,
-                 cutoff=DEFAULT_CUTOFF) -> Prepared:
+                 cutoff=DEFAULT_CUTOFF, core_cutoff=DEFAULT_CORE_CUTOFF) -> Prepared:
     """Enqueue the preparation of one view (see ``Prepared``); pass it to ``rasterize(prepared=...)``
     with the same tensors.  The tensors' values must not change in between."""
-    gv = make_view(view, proj, width, height, background, cutoff)
+    gv = make_view(view, proj, width, height, background, cutoff, core_cutoff)
     return prepare_native(*_device_inputs(means, scales, colors, opacities), gv)
 
 
 def rasterize(means, scales, colors, opacities, view, proj, width, height, background=None, cutoff=DEFAULT_CUTOFF,
-              prepared: Optional[Prepared] = None):
+              prepared: Optional[Prepared] = None, core_cutoff=DEFAULT_CORE_CUTOFF):
     """Differentiable render of one view on the HIP device: returns (rgb (H,W,3), alpha (H,W), depth (H,W)).
 
     ``prepared`` (from ``prepare_view`` with the same inputs) skips the preparation step."""
@@ -289,7 +297,7 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
     if background is None:
         background = torch.zeros(3, dtype=torch.float32, device=dev)
     background = background.to(dtype=torch.float32, device=dev)
-    gv = make_view(view, proj, width, height, background, cutoff)
+    gv = make_view(view, proj, width, height, background, cutoff, core_cutoff)
     return _RasterizeGaussians.apply(m, s, c, o, background, gv, prepared)
 
 
@@ -307,12 +315,13 @@ def render_gaussians_torch(
     return_aux: bool = False,
     cutoff: float = DEFAULT_CUTOFF,
     prepared: Optional[Prepared] = None,
+    core_cutoff: float = DEFAULT_CORE_CUTOFF,
 ):
     """Differentiable Gaussian splat; signature, results and errors of torch_renderer.py:109-203.
 
     Returns ``out`` (H,W,3) or ``(out, alpha, depth)`` when ``return_aux``; ``n == 0`` returns a
-    single zero image even with ``return_aux`` (torch_renderer.py:135-136).  ``cutoff`` and
-    ``prepared`` (see ``prepare_view``) are extensions; the reference has neither.
+    single zero image even with ``return_aux`` (torch_renderer.py:135-136).  ``cutoff``,
+    ``core_cutoff`` and ``prepared`` (see ``prepare_view``) are extensions; the reference has none.
     """
     if background is None:
         background = torch.tensor([0.0, 0.0, 0.0], dtype=torch.float32, device=means.device)
@@ -329,7 +338,7 @@ def render_gaussians_torch(
         raise ValueError("colors must be (N,3) or SH coeffs (N,4,3)")
 
     out, alpha, depth = rasterize(means, scales, colors, opacities, camera.view, camera.proj, width, height,
-                                  background=background, cutoff=cutoff, prepared=prepared)
+                                  background=background, cutoff=cutoff, prepared=prepared, core_cutoff=core_cutoff)
     if not return_aux:
         return out
     return out, alpha, depth
@@ -337,4 +346,4 @@ def render_gaussians_torch(
 
 __all__ = ["Camera", "get_default_device", "perspective", "look_at", "render_gaussians_torch", "rasterize",
            "make_view", "prepare_view", "prepare_native", "Prepared", "forward_native", "backward_native",
-           "DEFAULT_CUTOFF"]
+           "DEFAULT_CUTOFF", "DEFAULT_CORE_CUTOFF"]

@@ -80,7 +80,7 @@ def cpu_baseline(n: int, res: int, views: int) -> dict:
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     scene = orc.synthetic_scene(n, seed=0)
     view, proj = orc.orbit_cameras(views, res, res)[0]
-    v = orc.make_view(view, proj, res, res, cutoff=tr.DEFAULT_CUTOFF)
+    v = orc.make_view(view, proj, res, res, cutoff=tr.DEFAULT_CUTOFF, core_cutoff=tr.DEFAULT_CORE_CUTOFF)
     g = np.random.default_rng(0).standard_normal((res, res, 3)).astype(np.float32)
     t0 = time.perf_counter()
     orc.forward(v, scene, binned=True)
@@ -165,6 +165,7 @@ def main():
             "data": "synthetic (seeded Gaussians per SURVEY.md 8(d), random targets)",
             "config": {"workload": f"C4: {n} Gaussians, {V} orbit views {R}x{R}, fwd+bwd+grad all-reduce+Adam per step",
                        "gaussians": n, "views": V, "width": R, "height": R, "cutoff_sigma": tr.DEFAULT_CUTOFF,
+                       "core_cutoff_sigma": tr.DEFAULT_CORE_CUTOFF,
                        "scale": round(0.1061 * (1200.0 / n) ** (1.0 / 3.0), 5), "seed": 0,
                        "parallelism": f"view-sharded dp{world}", "pairs_per_view": int(avg_pairs)},
             "roofline": {"bound": "mfma", "kernel": "k_raster_bwd_mfma", "achieved": round(achieved, 2),

@@ -71,6 +71,10 @@ typedef struct gr_view {
   float background[3]; /* background colour (torch_renderer.py:128-130)                    */
   float cam_pos[3];    /* inv(view)[:3,3] (torch_renderer.py:81-83); used by SH colours    */
   float cutoff;        /* footprint: tiles where max weight >= o*exp(-cutoff^2/2) (def. 7) */
+  float core_cutoff;   /* two-zone footprint: kept tiles whose max weight is  */
+                       /* below o*exp(-core_cutoff^2/2) are "tail" tiles that carry only W and */
+                       /* D forward and the depth-coupled terms backward; <= 0 or >= cutoff  */
+                       /* means one zone (def. 5.5)                                            */
 } gr_view;
 
 /* ------------------------------------------------------------------------------------------ */
@@ -81,8 +85,9 @@ typedef struct gr_view {
 
 /* Sizes produced by gr_fwd_prepare for one view. */
 typedef struct gr_plan {
-  int64_t num_pairs; /* kept (Gaussian, tile) pairs: the splat work                        */
-  int64_t num_slots; /* backward partial-sum slots: one per tile of each Gaussian's rectangle */
+  int64_t num_pairs;      /* kept (Gaussian, tile) pairs: the splat work                     */
+  int64_t num_slots;      /* backward partial-sum slots: one per tile of each Gaussian's rectangle */
+  int64_t num_core_pairs; /* of num_pairs, the core pairs (two-zone footprint, gr_view)       */
 } gr_plan;
 
 /* Per-Gaussian projection records, tile rectangles, pair counts and offsets. */
@@ -145,16 +150,18 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
 /* ------------------------------------------------------------------------------------------ */
 
 /* Byte offsets of the sub-buffers inside geom / bins, for debugging and bit-exact tests.
- *   geom: [0] records float4[n][4], 64 bytes per Gaussian:
+ *   geom: [0] records float4[n+1][4], 64 bytes per Gaussian (record n: padding, o = 0):
  *             A = (px, py, qx, qy), B = (o, r, g, b), C = (z, first slot as int bits,
  *             tx0 | ty0 << 16 as uint bits, rectangle width as int bits), D = 0
  *         [1] rect int4[n] (tx0,ty0,tx1,ty1) [2] counts u64[n+1] [3] offsets u64[n+1]
- *         [4] device copy of the plan (gr_plan) [5] end of the fixed part (scan temp follows)
- *         (counts/offsets packed: rectangle area / first slot in the high word, kept tiles / first
- *         pair in the low word)
- *   bins: [0] keys (radix-sort fallback only, > 16384 tiles) [1] gaussian ids int32[K] (tile-sorted)
- *         [2] ranges int2[tiles]  */
-void gr_geom_layout(int n, size_t offsets_out[6]);
+ *         [4] device copy of the plan (gr_plan) [5] tail counts u32[n+1] [6] tail offsets u32[n+1]
+ *         [7] end of the fixed part (scan temp follows)
+ *         (counts/offsets packed: rectangle area / first slot in the high word, core tiles / first
+ *         core pair in the low word; tail pairs follow the num_core_pairs core pairs)
+ *   bins: [0] keys (radix-sort fallback only, > 8192 tiles) [1] gaussian ids int32[K]
+ *         [2] ranges int2[2 * tiles]: per virtual tile (2t: core list of tile t, 2t+1: its tail list) */
+#define GR_GEOM_PARTS 8
+void gr_geom_layout(int n, size_t offsets_out[GR_GEOM_PARTS]);
 void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[3]);
 
 /* Live kernel timing with HIP events on the launch stream (bench.py).  Between begin and end,

@@ -36,6 +36,7 @@ class GrView(ctypes.Structure):
         ("background", ctypes.c_float * 3),
         ("cam_pos", ctypes.c_float * 3),
         ("cutoff", ctypes.c_float),
+        ("core_cutoff", ctypes.c_float),
     ]
 
 
@@ -102,7 +103,8 @@ def camera_position(view: np.ndarray) -> np.ndarray:
     return np.linalg.inv(np.asarray(view, dtype=np.float64))[:3, 3].astype(np.float32)
 
 
-def make_view(view, proj, width, height, background=None, cutoff=5.0) -> GrView:
+def make_view(view, proj, width, height, background=None, cutoff=7.0, core_cutoff=0.0) -> GrView:
+    """core_cutoff <= 0 (default) = one zone; the product's default is DEFAULT_CORE_CUTOFF (5.5)."""
     v = GrView()
     v.width, v.height = int(width), int(height)
     v.view[:] = [float(x) for x in np.asarray(view, dtype=np.float32).reshape(16)]
@@ -111,6 +113,7 @@ def make_view(view, proj, width, height, background=None, cutoff=5.0) -> GrView:
     v.background[:] = [float(x) for x in bg]
     v.cam_pos[:] = [float(x) for x in camera_position(view)]
     v.cutoff = float(cutoff)
+    v.core_cutoff = float(core_cutoff)
     return v
 
 
@@ -133,7 +136,8 @@ def preprocess(v: GrView, scene: Scene):
 
 
 def bin_pairs(v: GrView, rec: np.ndarray, rect: np.ndarray, counts: np.ndarray):
-    """Stable (tile, Gaussian) pair lists; rec/rect/counts from preprocess()."""
+    """Stable (virtual tile, Gaussian) pair lists, virtual tile = 2*tile + (1 for a tail pair);
+    rec/rect/counts from preprocess().  ranges: (2*tiles, 2)."""
     n = counts.shape[0]
     rec = np.ascontiguousarray(rec, np.float32)
     tiles = math.ceil(v.width / TILE) * math.ceil(v.height / TILE)
@@ -143,7 +147,7 @@ def bin_pairs(v: GrView, rec: np.ndarray, rect: np.ndarray, counts: np.ndarray):
     K = lib().gro_bin(ctypes.byref(v), n, _p(rec), _p(rect), _p(counts), _p(offsets), None, None, None)
     keys = np.zeros((max(K, 1),), np.uint32)
     vals = np.zeros((max(K, 1),), np.int32)
-    ranges = np.zeros((tiles, 2), np.int32)
+    ranges = np.zeros((2 * tiles, 2), np.int32)
     lib().gro_bin(ctypes.byref(v), n, _p(rec), _p(rect), _p(counts), _p(offsets), _p(keys), _p(vals), _p(ranges))
     return offsets, keys[:K], vals[:K], ranges
 

@@ -21,10 +21,11 @@ from oracle import oracle as orc
 pytestmark = pytest.mark.gpu
 
 GRAD_KEYS = ("d_means", "d_scales", "d_colors", "d_opacities")
-CUTOFF = 7.0  # product default (3dgaussian_amd/torch_renderer.py DEFAULT_CUTOFF)
+CUTOFF = 7.0  # product defaults (3dgaussian_amd/torch_renderer.py DEFAULT_CUTOFF, DEFAULT_CORE_CUTOFF)
+CORE = 5.5
 
 
-def _run_hip(pkg, d, device, cutoff=None):
+def _run_hip(pkg, d, device, cutoff=None, with_depth=True):
     tr = pkg.torch_renderer
     W, H = int(d["width"]), int(d["height"])
     t = {k: torch.from_numpy(np.ascontiguousarray(d[k])).to(device).requires_grad_(True)
@@ -37,20 +38,22 @@ def _run_hip(pkg, d, device, cutoff=None):
     if d["means"].shape[0] == 0:
         return {"out_rgb": res.cpu().numpy()}
     out, alpha, depth = res
-    loss = ((out * torch.from_numpy(d["g_rgb"]).to(device)).sum() + (alpha * torch.from_numpy(d["g_alpha"]).to(device)).sum()
-            + (depth * torch.from_numpy(d["g_depth"]).to(device)).sum())
+    loss = ((out * torch.from_numpy(d["g_rgb"]).to(device)).sum() + (alpha * torch.from_numpy(d["g_alpha"]).to(device)).sum())
+    if with_depth:  # else: no upstream depth gradient (gr_bwd gets g_depth = NULL, tail pairs skipped)
+        loss = loss + (res[2] * torch.from_numpy(d["g_depth"]).to(device)).sum()
     loss.backward()
-    r = {"out_rgb": out.detach().cpu().numpy(), "out_alpha": alpha.detach().cpu().numpy(), "out_depth": depth.detach().cpu().numpy()}
+    r = {"out_rgb": out.detach().cpu().numpy(), "out_alpha": alpha.detach().cpu().numpy(), "out_depth": res[2].detach().cpu().numpy()}
     for k, name in zip(GRAD_KEYS, ("means", "scales", "colors", "opacities")):
         r[k] = t[name].grad.cpu().numpy()
     return r
 
 
-def _oracle(d, binned):
-    v = orc.make_view(d["view"], d["proj"], int(d["width"]), int(d["height"]), d["background"], cutoff=CUTOFF)
+def _oracle(d, binned, with_depth=True):
+    v = orc.make_view(d["view"], d["proj"], int(d["width"]), int(d["height"]), d["background"], cutoff=CUTOFF,
+                      core_cutoff=CORE)
     sc = orc.Scene(d["means"], d["scales"], d["colors"], d["opacities"])
     out, alpha, depth = orc.forward(v, sc, binned=binned)
-    dm, ds, dc, do = orc.backward(v, sc, d["g_rgb"], d["g_alpha"], d["g_depth"], binned=binned)
+    dm, ds, dc, do = orc.backward(v, sc, d["g_rgb"], d["g_alpha"], d["g_depth"] if with_depth else None, binned=binned)
     return {"out_rgb": out, "out_alpha": alpha, "out_depth": depth, "d_means": dm, "d_scales": ds, "d_colors": dc, "d_opacities": do}
 
 
@@ -86,11 +89,25 @@ def test_fwd_bwd_matches_binned_oracle(pkg, cuda, name):
         assert orc.rel_l2(hip[k], ora[k]) <= 1e-4, k
 
 
+@pytest.mark.parametrize("name", ["f1_n300_64x48", "f1_n64_32x32_sh", "f2_c1_view0", "f2_c1_view2"])
+def test_no_depth_gradient(pkg, cuda, name):
+    """Loss without the depth output (the fit loop's L1 + silhouette): the backward gets no depth
+    gradient and skips the tail pairs of the two-zone footprint.  Against the binned oracle with the
+    same semantics, and against the exact dense answer."""
+    d = golden(name)
+    hip = _run_hip(pkg, d, cuda, with_depth=False)
+    ora = _oracle(d, binned=True, with_depth=False)
+    exact = _oracle(d, binned=False, with_depth=False)
+    for k in GRAD_KEYS:
+        assert orc.rel_l2(hip[k], ora[k]) <= 1e-4, k
+        assert orc.rel_l2(hip[k], exact[k]) <= 1e-4, k
+
+
 def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=CUTOFF):
     tr = pkg.torch_renderer
     nat = pkg._native
     m, s, c, o = (torch.from_numpy(a).to(device) for a in scene.arrays())
-    gv = tr.make_view(view, proj, W, H, None, cutoff)
+    gv = tr.make_view(view, proj, W, H, None, cutoff, CORE)
     out, alpha, depth, st = tr.forward_native(m, s, c, o, gv)
     torch.cuda.synchronize()
     n = m.shape[0]
@@ -103,7 +120,9 @@ def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=CUTOFF)
     # packed u64: low word = kept tiles / first pair, high word = rectangle area / first slot
     counts64 = geom[g_off[2]: g_off[2] + 8 * n].view(np.uint64)
     offsets64 = geom[g_off[3]: g_off[3] + 8 * (n + 1)].view(np.uint64)
-    counts = (counts64 & 0xFFFFFFFF).astype(np.int32)
+    core = (counts64 & 0xFFFFFFFF).astype(np.int32)  # core tiles; tail tiles counted apart
+    tail = geom[g_off[5]: g_off[5] + 4 * n].view(np.uint32).astype(np.int32)
+    counts = core + tail
     offsets = (offsets64 & 0xFFFFFFFF).astype(np.int32)
     areas = (counts64 >> 32).astype(np.int64)
     b_off = nat.bins_layout(gv, n, st.num_pairs)
@@ -111,11 +130,9 @@ def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=CUTOFF)
     K = st.num_pairs
     tiles = ((W + 15) // 16) * ((H + 15) // 16)
     ids = bins[b_off[1]: b_off[1] + 4 * K].view(np.int32)
-    ranges = bins[b_off[2]: b_off[2] + 8 * tiles].view(np.int32).reshape(tiles, 2)
-    # the counting sort keeps no sorted key array: the sorted keys are implied by the tile ranges
-    keys = np.repeat(np.arange(tiles, dtype=np.uint32), np.maximum(ranges[:, 1] - ranges[:, 0], 0))
-    assert keys.size == K
-    return dict(recA=recA, recC=recC, offsets64=offsets64, rect=rect, counts=counts, offsets=offsets, keys=keys, ids=ids, ranges=ranges, K=K, areas=areas,
+    ranges = bins[b_off[2]: b_off[2] + 16 * tiles].view(np.int32).reshape(2 * tiles, 2)  # per virtual tile
+    return dict(recA=recA, recC=recC, offsets64=offsets64, rect=rect, counts=counts, core=core, tail=tail,
+                offsets=offsets, ids=ids, ranges=ranges, K=K, Kc=int(st.plan.num_core_pairs), areas=areas,
                 slots=int(st.plan.num_slots))
 
 
@@ -140,7 +157,7 @@ def test_bins_bit_exact(pkg, cuda, case):
         view, proj = orc.orbit_cameras(3, 200, 120)[1]
         W, H = 200, 120
     g = _native_bins(pkg, scene, view, proj, W, H, cuda)
-    v = orc.make_view(view, proj, W, H, None, cutoff=CUTOFF)
+    v = orc.make_view(view, proj, W, H, None, cutoff=CUTOFF, core_cutoff=CORE)
     rec, rect, counts = orc.preprocess(v, scene)
     # projected centres are float32-identical (same operation sequence, no FMA contraction)
     np.testing.assert_array_equal(g["recA"][:, 0].view(np.int32), rec[:, 0].view(np.int32))
@@ -158,14 +175,22 @@ def test_bins_bit_exact(pkg, cuda, case):
     np.testing.assert_array_equal(C[:, 1], (g["offsets64"][:-1][kept] >> 32).astype(np.uint32))
     np.testing.assert_array_equal(C[:, 2], (rect[kept, 0] | (rect[kept, 1] << 16)).astype(np.uint32))
     np.testing.assert_array_equal(C[:, 3], (rect[kept, 2] - rect[kept, 0] + 1).astype(np.uint32))
-    offsets, keys, vals, ranges = orc.bin_pairs(v, rec, rect, counts)
-    np.testing.assert_array_equal(g["offsets"], offsets)
+    _, keys, vals, ranges = orc.bin_pairs(v, rec, rect, counts)
     assert g["K"] == len(vals)
-    np.testing.assert_array_equal(g["keys"], keys)
-    np.testing.assert_array_equal(g["ids"], vals)
-    nonempty = ranges[:, 1] > ranges[:, 0]
-    np.testing.assert_array_equal(g["ranges"][nonempty], ranges[nonempty])
-    assert np.all(g["ranges"][~nonempty, 1] == g["ranges"][~nonempty, 0])
+    # core pairs first (Gaussian order, per-Gaussian offsets = scan of the core counts), tail after
+    tail_pair = (keys & 1).astype(bool)
+    assert g["Kc"] == int((~tail_pair).sum())
+    np.testing.assert_array_equal(g["core"], np.bincount(vals[~tail_pair], minlength=len(counts)))
+    np.testing.assert_array_equal(g["offsets"], np.concatenate([[0], np.cumsum(g["core"])]).astype(np.int32))
+    # every virtual tile's Gaussian list is bit-exact (ascending Gaussian index): the HIP lists sit
+    # in the core / tail regions of the pair array, the oracle's in virtual-tile order
+    lens = ranges[:, 1] - ranges[:, 0]
+    glens = np.maximum(g["ranges"][:, 1] - g["ranges"][:, 0], 0)
+    np.testing.assert_array_equal(glens, lens)
+    for t in np.nonzero(lens)[0]:
+        np.testing.assert_array_equal(g["ids"][g["ranges"][t, 0]:g["ranges"][t, 1]], vals[ranges[t, 0]:ranges[t, 1]])
+        if len(lens) <= 16384:  # counting-sort path: tail lists in the tail region (radix: by virtual tile)
+            assert (g["ranges"][t, 0] >= g["Kc"]) == bool(t & 1)
 
 
 def test_deterministic(pkg, cuda):

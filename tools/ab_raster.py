@@ -13,15 +13,24 @@ scene = orc.synthetic_scene(N, seed=0)
 views = orc.orbit_cameras(50, R, R)
 t = [torch.from_numpy(a).to(dev).requires_grad_(True) for a in scene.arrays()]
 g = torch.randn(R, R, 3, device=dev)
+gd = torch.randn(R, R, device=dev) if os.environ.get("AB_DEPTH") == "1" else None
+CORE = float(os.environ.get("AB_CORE", tr.DEFAULT_CORE_CUTOFF))  # 0: one zone
+
+
+def loss_of(out, d):
+    l = (out * g).sum()
+    return l + (d * gd).sum() if gd is not None else l
+
+
 for i in range(2):
-    out, a, d = tr.rasterize(*t, *views[i], R, R)
-    (out * g).sum().backward()
+    out, a, d = tr.rasterize(*t, *views[i], R, R, core_cutoff=CORE)
+    loss_of(out, d).backward()
 torch.cuda.synchronize()
 pkg._native.profile_begin()
 for i in range(reps):
-    out, a, d = tr.rasterize(*t, *views[i % 10], R, R)
-    (out * g).sum().backward()
+    out, a, d = tr.rasterize(*t, *views[i % 10], R, R, core_cutoff=CORE)
+    loss_of(out, d).backward()
 torch.cuda.synchronize()
 p = pkg._native.profile_end()
 lib = os.path.basename(os.environ.get("GR_HIP_LIB", "libgr_hip.so"))
-print(f"{lib:24s} " + "  ".join(f"{k} {1e3*v[0]/max(v[1],1):7.1f}us" for k, v in p.items()))
+print(f"{lib:20s} depth={int(gd is not None)} core={CORE} " + "  ".join(f"{k} {1e3*v[0]/max(v[1],1):7.1f}us" for k, v in p.items()))
