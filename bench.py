@@ -46,8 +46,12 @@ fm = importlib.import_module("3dgaussian_amd.fit_multiview")
 
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 (f32-in MFMA) dense peak
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak (spec)
-FLOP_PER_PAIR_BWD = 40 / 16 * 2 * 16 * 16 * 4  # 40 MFMA 16x16x4 per 16 Gaussians per tile (T + R contractions)
-FLOP_PER_PAIR_FWD = 5 / 4 * 2 * 16 * 16 * 4  # 5 MFMA 16x16x4 per 4 Gaussians per tile
+MFMA_FLOP = 2 * 16 * 16 * 4  # one v_mfma_f32_16x16x4_f32
+# algorithmic FLOP per (Gaussian, tile) pair: core pairs carry every channel, tail pairs
+# (two-zone footprint) W and D only; the bench's loss has no depth term, so the backward skips tails
+FLOP_PER_CORE_PAIR_FWD = 5 / 4 * MFMA_FLOP  # 5 MFMA per 4 Gaussians
+FLOP_PER_TAIL_PAIR_FWD = 2 / 4 * MFMA_FLOP  # 2 MFMA per 4 Gaussians
+FLOP_PER_CORE_PAIR_BWD = 40 / 16 * MFMA_FLOP  # 40 MFMA per 16 Gaussians (T + R contractions)
 
 
 def parse():
@@ -130,19 +134,21 @@ def main():
     elapsed = float(elapsed.item())
 
     # pairs per view for the algorithmic FLOP count (same binning as the kernels)
-    pairs = []
+    pairs, core = [], []
     with torch.no_grad():
         means, scales, colors, opac = fm.activations(params)
         for i in fitter.my_views:
             gv = tr.make_view(cams[i].view, cams[i].proj, R, R, None, tr.DEFAULT_CUTOFF)
             _, _, _, st = tr.forward_native(means.contiguous(), scales.contiguous(), colors.contiguous(), opac.contiguous(), gv)
             pairs.append(st.num_pairs)
+            core.append(int(st.plan.num_core_pairs))
     if rank == 0:
         bwd_ms, bwd_n = prof["raster_bwd"]
         fwd_ms, fwd_n = prof["raster_fwd"]
-        avg_pairs = float(np.mean(pairs))
+        avg_pairs, avg_core = float(np.mean(pairs)), float(np.mean(core))
         bwd_avg_s = bwd_ms / max(bwd_n, 1) / 1e3
-        achieved = FLOP_PER_PAIR_BWD * avg_pairs / bwd_avg_s / 1e12
+        achieved = FLOP_PER_CORE_PAIR_BWD * avg_core / bwd_avg_s / 1e12
+        fwd_flop = FLOP_PER_CORE_PAIR_FWD * avg_core + FLOP_PER_TAIL_PAIR_FWD * (avg_pairs - avg_core)
         traffic = None
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
@@ -167,12 +173,13 @@ def main():
                        "gaussians": n, "views": V, "width": R, "height": R, "cutoff_sigma": tr.DEFAULT_CUTOFF,
                        "core_cutoff_sigma": tr.DEFAULT_CORE_CUTOFF,
                        "scale": round(0.1061 * (1200.0 / n) ** (1.0 / 3.0), 5), "seed": 0,
-                       "parallelism": f"view-sharded dp{world}", "pairs_per_view": int(avg_pairs)},
+                       "parallelism": f"view-sharded dp{world}", "pairs_per_view": int(avg_pairs),
+                       "core_pairs_per_view": int(avg_core)},
             "roofline": {"bound": "mfma", "kernel": "k_raster_bwd_mfma", "achieved": round(achieved, 2),
                          "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
                          "traffic": traffic, "avg_launch_us": round(bwd_avg_s * 1e6, 1), "launches": bwd_n,
                          "fwd_kernel_avg_us": round(fwd_ms / max(fwd_n, 1) * 1e3, 1),
-                         "fwd_achieved_tflops": round(FLOP_PER_PAIR_FWD * avg_pairs / (fwd_ms / max(fwd_n, 1) / 1e3) / 1e12, 2)},
+                         "fwd_achieved_tflops": round(fwd_flop / (fwd_ms / max(fwd_n, 1) / 1e3) / 1e12, 2)},
             "loss": float(loss),
         }
         if not args.no_cpu_baseline and world == 1:
