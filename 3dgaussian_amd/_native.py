@@ -90,6 +90,10 @@ _SIG = {
     "gr_bins_layout": (None, [_VP, ctypes.c_int, _PP, ctypes.POINTER(ctypes.c_size_t)]),
     "gr_profile_begin": (None, []),
     "gr_profile_end": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
+    "gr_l1_loss_ws_bytes": (ctypes.c_size_t, []),
+    "gr_l1_loss_fwd": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, _P, ctypes.c_int64, ctypes.c_float, _P, _P,
+                                      ctypes.c_size_t, _P]),
+    "gr_l1_loss_bwd": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, _P, ctypes.c_int64, ctypes.c_float, _P, _P, _P, _P]),
     "gr_last_error": (ctypes.c_char_p, []),
     "gr_version": (ctypes.c_char_p, []),
 }
@@ -155,12 +159,12 @@ def version() -> str:
     return lib().gr_version().decode()
 
 
-GEOM_PARTS = 8
+GEOM_PARTS = 6
 
 
 def geom_layout(n: int):
-    """[records ((n+1) x 64 B), rect, counts, offsets, device plan, tail counts, tail offsets, end of the
-    fixed part] (gr_hip.h gr_geom_layout)."""
+    """[records ((n+1) x 64 B), rect, counts (core | tail << 32, u64), their exclusive scan, device plan,
+    end of the fixed part] (gr_hip.h gr_geom_layout)."""
     out = (ctypes.c_size_t * GEOM_PARTS)()
     lib().gr_geom_layout(int(n), out)
     return list(out)

@@ -200,12 +200,6 @@ __device__ __forceinline__ int tile_class(const ViewK& v, float px, float py, fl
 
 __device__ __forceinline__ float qcoef(float s) { return (-0.5f * LOG2E) / (s * s); }
 
-// Partial-sum slot of pair (Gaussian, tile (tx,ty)) from the record's word C: the Gaussian's first
-// slot + the tile's index inside its rectangle (culled tiles leave unused slots).
-__device__ __forceinline__ int pair_slot(const float4 c, int tx, int ty) {
-  const unsigned rxy = __float_as_uint(c.z);
-  return (int)__float_as_uint(c.y) + (ty - (int)(rxy >> 16)) * (int)__float_as_uint(c.w) + (tx - (int)(rxy & 0xffffu));
-}
 
 // ------------------------------------------------------------------------------------------------
 // Geometry buffer layout.
@@ -214,28 +208,35 @@ __device__ __forceinline__ int pair_slot(const float4 c, int tx, int ty) {
 // the raster kernels touch one memory segment per pair (instead of one per field array):
 //   rec[4i+0] = A: px, py, qx, qy  (q = -0.5*log2(e)/sigma^2)
 //   rec[4i+1] = B: o, r, g, b (clamped)
-//   rec[4i+2] = C: z_abs, first slot (int bits, written by k_emit), rect.x | rect.y << 16, rect width
+//   rec[4i+2] = C: z_abs, 0, 0, 0
 //   rec[4i+3] = unused (zero)
 constexpr int REC4 = 4;  // float4 per record
 
+// Per-Gaussian pair counts of the two zones, packed core | tail << 32 into one u64; its exclusive
+// scan gives each Gaussian's first core pair (low word, in [0, Kc)) and first tail pair (high word,
+// relative to Kc: tail pairs fill [Kc, K)).  A pair's index in this emission order is also its
+// backward partial-sum slot, so each Gaussian's partials are contiguous (k_reduce_bwd).  The packed
+// words cannot carry into each other as long as K < 2^31, which k_plan checks against an exact
+// 64-bit total (Geom::total) before trusting them.
+struct Cnt2 {
+  unsigned long long v;
+  __host__ __device__ unsigned c() const { return (unsigned)(v & 0xffffffffull); }
+  __host__ __device__ unsigned t() const { return (unsigned)(v >> 32); }
+};
+
 struct Geom {
-  float4* rec;   // [n][4] raster records
+  float4* rec;   // [n+1][4] raster records (record n: padding)
   int4* rect;    // tile rectangle
-  // packed (rect area << 32 | core tiles): the exclusive scan gives, per Gaussian, the first core
-  // pair (low word) and the first partial-sum slot (high word; one slot per rectangle tile);
-  // tail tiles are counted and scanned separately (tcounts / toffsets): core pairs fill [0, Kc),
-  // tail pairs [Kc, K) of the pair arrays
-  unsigned long long* counts;   // n+1
-  unsigned long long* offsets;  // n+1
+  unsigned long long* counts;   // n+1, packed Cnt2
+  unsigned long long* offsets;  // n+1, packed Cnt2
   gr_plan* plan;                // device copy of the plan (gr_fwd_prepare_async copies it to the host)
-  unsigned* tcounts;            // n+1
-  unsigned* toffsets;           // n+1
+  unsigned long long* total;    // [blocks of k_preprocess] exact per-block totals of kept pairs (overflow check)
   void* scan_tmp;
   size_t scan_tmp_bytes;
 };
 
-// off: [0] records, [1] rect, [2] counts, [3] offsets, [4] device copy of the plan, [5] tail counts,
-//      [6] tail offsets, [7] scan temp (= end of the fixed part)
+// off: [0] records, [1] rect, [2] counts, [3] offsets, [4] device copy of the plan + exact per-block
+//      totals, [5] scan temp (= end of the fixed part)
 size_t geom_fixed(int n, size_t off[GR_GEOM_PARTS]) {
   size_t o = 0;
   const size_t nn = (size_t)(n > 0 ? n : 1);
@@ -243,10 +244,8 @@ size_t geom_fixed(int n, size_t off[GR_GEOM_PARTS]) {
   off[1] = o; o = align_up(o + nn * sizeof(int4));
   off[2] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
   off[3] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
-  off[4] = o; o = align_up(o + sizeof(gr_plan));
-  off[5] = o; o = align_up(o + (nn + 1) * sizeof(unsigned));
-  off[6] = o; o = align_up(o + (nn + 1) * sizeof(unsigned));
-  off[7] = o;
+  off[4] = o; o = align_up(o + sizeof(gr_plan) + (nn / 256 + 2) * sizeof(unsigned long long));
+  off[5] = o;
   return o;
 }
 
@@ -256,10 +255,7 @@ size_t scan_tmp_bytes_t(int n) {
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (CountT*)nullptr, (CountT*)nullptr, n + 1, (hipStream_t)0);
   return tmp;
 }
-size_t scan_tmp_bytes(int n) {
-  const size_t a = scan_tmp_bytes_t<unsigned long long>(n), b = scan_tmp_bytes_t<unsigned>(n);
-  return a > b ? a : b;
-}
+size_t scan_tmp_bytes(int n) { return scan_tmp_bytes_t<unsigned long long>(n); }
 
 Geom geom_view(void* base, int n) {
   size_t off[GR_GEOM_PARTS];
@@ -271,8 +267,7 @@ Geom geom_view(void* base, int n) {
   g.rect = (int4*)(b + off[1]);
   g.counts = (unsigned long long*)(b + off[2]);
   g.offsets = (unsigned long long*)(b + off[3]);
-  g.tcounts = (unsigned*)(b + off[5]);
-  g.toffsets = (unsigned*)(b + off[6]);
+  g.total = (unsigned long long*)(b + off[4] + sizeof(gr_plan));
   g.scan_tmp = b + fixed;
   g.scan_tmp_bytes = 0;
   return g;
@@ -284,11 +279,17 @@ Geom geom_view(void* base, int n) {
 constexpr int CH = 1024;  // Gaussians per raster work item (one chunk of one tile's list)
 constexpr int NPART = 9;  // backward partial sums per (Gaussian, tile) pair
 
+// Virtual tiles up to which the pairs are grouped by the stable counting sort (16-bit keys; see
+// "Pair order by tile" below); past it, a radix sort.
+constexpr int TSORT_MAX_TILES = 16384;
+
+inline bool short_keys(int tiles) { return tiles <= TSORT_MAX_TILES; }
+
 // Persistent binning state (kept from forward to backward).
 struct Bins {
   uint32_t* keys;      // [K] sorted tile keys (radix-sort path only; the counting sort needs none)
-  int* ids;            // [K] sorted gaussian ids
-  int2* ranges;        // [tiles] pair range of each tile
+  int2* pairs;         // [K] sorted pairs: (gaussian id, emission index = partial-sum slot)
+  int2* ranges;        // [vtiles] pair range of each virtual tile
   int4* items;         // [cap] work items (tile, k0, k1, chunk)
   int* num_items;      // [1]
   int* tile_item0;     // [tiles] first work item of each tile
@@ -299,6 +300,7 @@ struct Scratch {
   uint32_t* keys_in;   // [K] tile key of each emitted pair (uint16_t when short_keys(tiles))
   int* ids_in;         // [K]
   float* fwd_part;     // [cap][5][256] partial accumulators of tiles split over several items
+  int2* pairs_in;      // [K] (radix path) unsorted (id, emission index) pairs
   void* sort_tmp;
 };
 
@@ -310,8 +312,8 @@ size_t bins_fixed(int vtiles, int64_t K, size_t off[6]) {
   const size_t kk = (size_t)(K > 0 ? K : 1);
   const size_t cap = (size_t)item_cap(tiles, K);
   size_t o = 0;
-  off[0] = o; o = align_up(o + kk * sizeof(uint32_t));
-  off[1] = o; o = align_up(o + kk * sizeof(int));
+  off[0] = o; o = align_up(o + (short_keys(tiles) ? 1 : kk) * sizeof(uint32_t));
+  off[1] = o; o = align_up(o + kk * sizeof(int2));
   off[2] = o; o = align_up(o + (size_t)tiles * sizeof(int2));
   off[3] = o; o = align_up(o + cap * sizeof(int4));
   off[4] = o; o = align_up(o + sizeof(int));
@@ -319,7 +321,8 @@ size_t bins_fixed(int vtiles, int64_t K, size_t off[6]) {
   return o;
 }
 
-size_t scratch_fixed(int vtiles, int64_t K, size_t off[3]) {
+// off: [0] emitted keys, [1] emitted ids, [2] split-tile partials, [3] (radix path) unsorted pairs
+size_t scratch_fixed(int vtiles, int64_t K, size_t off[4]) {
   const int tiles = vtiles;
   const size_t kk = (size_t)(K > 0 ? K : 1);
   const size_t cap = (size_t)item_cap(tiles, K);
@@ -327,6 +330,7 @@ size_t scratch_fixed(int vtiles, int64_t K, size_t off[3]) {
   off[0] = o; o = align_up(o + kk * sizeof(uint32_t));
   off[1] = o; o = align_up(o + kk * sizeof(int));
   off[2] = o; o = align_up(o + cap * 5 * TP * sizeof(float));
+  off[3] = o; o = align_up(o + (short_keys(tiles) ? 1 : kk) * sizeof(int2));
   return o;
 }
 
@@ -336,9 +340,6 @@ size_t scratch_fixed(int vtiles, int64_t K, size_t off[3]) {
 // k_tile_place below): the keys are read twice and the ids once, instead of a radix sort's
 // histogram + two scatter passes over keys and values.  Larger images use the hipcub radix sort on
 // 32-bit keys.
-constexpr int TSORT_MAX_TILES = 16384;
-
-inline bool short_keys(int tiles) { return tiles <= TSORT_MAX_TILES; }
 
 // Waves per column block: the per-wave tile counters (tiles ints per wave) stay within 64 KB LDS.
 inline int tsort_waves(int tiles) { return tiles <= 4096 ? 4 : tiles <= 8192 ? 2 : 1; }
@@ -380,8 +381,8 @@ size_t tile_sort_tmp_bytes(int64_t K, int tiles) {
     return 3 * align_up(tsort_cells_bound(K, st) * sizeof(int)) + 2 * align_up((size_t)st * sizeof(int));
   }
   size_t tmp = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const int*)nullptr,
-                                           (int*)nullptr, (int)(K > 0 ? K : 1), 0, bits_for((uint32_t)tiles),
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const int2*)nullptr,
+                                           (int2*)nullptr, (int)(K > 0 ? K : 1), 0, bits_for((uint32_t)tiles),
                                            (hipStream_t)0);
   return tmp;
 }
@@ -400,7 +401,7 @@ Bins bins_view(void* base, int tiles, int64_t K) {
   char* b = (char*)base;
   Bins r;
   r.keys = (uint32_t*)(b + off[0]);
-  r.ids = (int*)(b + off[1]);
+  r.pairs = (int2*)(b + off[1]);
   r.ranges = (int2*)(b + off[2]);
   r.items = (int4*)(b + off[3]);
   r.num_items = (int*)(b + off[4]);
@@ -409,13 +410,14 @@ Bins bins_view(void* base, int tiles, int64_t K) {
 }
 
 Scratch scratch_view(void* base, int tiles, int64_t K) {
-  size_t off[3];
+  size_t off[4];
   const size_t fixed = scratch_fixed(tiles, K, off);
   char* b = (char*)base;
   Scratch r;
   r.keys_in = (uint32_t*)(b + off[0]);
   r.ids_in = (int*)(b + off[1]);
   r.fwd_part = (float*)(b + off[2]);
+  r.pairs_in = (int2*)(b + off[3]);
   r.sort_tmp = b + fixed;
   return r;
 }
@@ -424,18 +426,38 @@ Scratch scratch_view(void* base, int tiles, int64_t K) {
 // Kernels: binning.
 // ------------------------------------------------------------------------------------------------
 template <int CD>
+__device__ __forceinline__ unsigned long long preprocess_one(const ViewK& v, int i, const float* __restrict__ means,
+                                                             const float* __restrict__ scales,
+                                                             const float* __restrict__ colors,
+                                                             const float* __restrict__ opac, Geom& g);
+
+template <int CD>
 __global__ __launch_bounds__(256) void k_preprocess(ViewK v, int n, const float* __restrict__ means,
                                                     const float* __restrict__ scales, const float* __restrict__ colors,
                                                     const float* __restrict__ opac, Geom g) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == n) {
-    g.counts[n] = 0;
-    g.tcounts[n] = 0;
+    g.counts[n] = 0ull;
     float4* pad = g.rec + (size_t)REC4 * n;  // padding record of the raster batches (rec_of)
     pad[0] = make_float4(1e30f, 1e30f, -1.0f, -1.0f);
     pad[1] = pad[2] = pad[3] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  if (i >= n) return;
+  unsigned long long kept = 0;
+  if (i < n) kept = preprocess_one<CD>(v, i, means, scales, colors, opac, g);
+  // exact 64-bit block total of kept pairs for the overflow check (k_plan sums the blocks)
+  __shared__ unsigned long long wsum[4];
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) kept += __shfl_xor(kept, m);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = kept;
+  __syncthreads();
+  if (threadIdx.x == 0) g.total[blockIdx.x] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+}
+
+template <int CD>
+__device__ __forceinline__ unsigned long long preprocess_one(const ViewK& v, int i, const float* __restrict__ means,
+                                                             const float* __restrict__ scales,
+                                                             const float* __restrict__ colors,
+                                                             const float* __restrict__ opac, Geom& g) {
   const float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
   Proj p;
   project(v, mx, my, mz, scales[3 * i], scales[3 * i + 1], p);
@@ -458,12 +480,11 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, int n, const float*
   float4* rec = g.rec + (size_t)REC4 * i;
   rec[0] = make_float4(p.px, p.py, qx, qy);
   rec[1] = make_float4(op < 0.0f ? 0.0f : op, clamp01(c[0]), clamp01(c[1]), clamp01(c[2]));
-  rec[2] = make_float4(p.za, 0.0f, __uint_as_float((unsigned)r.x | ((unsigned)r.y << 16)),
-                       __uint_as_float((unsigned)(r.z - r.x + 1)));
+  rec[2] = make_float4(p.za, 0.0f, 0.0f, 0.0f);
   rec[3] = make_float4(0.f, 0.f, 0.f, 0.f);
   g.rect[i] = r;
-  g.counts[i] = core + tail > 0 ? (((unsigned long long)area << 32) | (unsigned)core) : 0ull;
-  g.tcounts[i] = (unsigned)tail;
+  g.counts[i] = (unsigned long long)core | ((unsigned long long)tail << 32);
+  return (unsigned long long)(core + tail);
 }
 
 constexpr int EWIN = 4096;  // pairs staged in LDS per emit block
@@ -513,31 +534,27 @@ __global__ __launch_bounds__(256) void k_emit(ViewK v, int n, const int4* __rest
 }
 
 // Differentiable path: pairs of the kept tiles (tile_class), core pairs at [0, Kc) and tail pairs at
-// [Kc, K), each in Gaussian order; the Gaussian's first partial-sum slot goes into its record (word
-// C.y).  Keys: the tile (VKEY = false: each region is counting-sorted on its own) or the virtual
+// [Kc, K), each in Gaussian order (the index here is the pair's partial-sum slot).  Keys: the tile (VKEY = false: each region is counting-sorted on its own) or the virtual
 // tile 2*tile + tail (VKEY = true: one radix sort of the whole array).  The pairs of 256 consecutive
 // Gaussians are built in LDS and written out with coalesced stores.
 template <typename KeyT, bool VKEY>
 __global__ __launch_bounds__(256) void k_emit_zones(ViewK v, int n, const int4* __restrict__ rect,
-                                                    const unsigned long long* __restrict__ counts,
-                                                    const unsigned long long* __restrict__ offsets,
-                                                    const unsigned* __restrict__ toffsets, float4* __restrict__ rec,
-                                                    KeyT* keys, int* ids) {
+                                                    const Cnt2* __restrict__ counts, const Cnt2* __restrict__ offsets,
+                                                    const float4* __restrict__ rec, KeyT* keys, int* ids) {
   __shared__ KeyT sK[EWIN];
   __shared__ int sI[EWIN];
   const int g0 = blockIdx.x * 256;
   const int i = g0 + (int)threadIdx.x;
   const int gend = min(n, g0 + 256);
-  const int Kc = (int)(offsets[n] & 0xffffffffu);
-  const int c0 = (int)(offsets[g0] & 0xffffffffu), c1 = (int)(offsets[gend] & 0xffffffffu);
-  const int t0 = (int)toffsets[g0], t1 = (int)toffsets[gend];
+  const int Kc = (int)offsets[n].c();
+  const int c0 = (int)offsets[g0].c(), c1 = (int)offsets[gend].c();
+  const int t0 = (int)offsets[g0].t(), t1 = (int)offsets[gend].t();
   const int nc = c1 - c0;
   const bool staged = nc + (t1 - t0) <= EWIN;
-  if (i < n && counts[i] != 0) {
+  if (i < n && counts[i].v != 0) {
     const int4 r = rect[i];
     const float4 a = rec[(size_t)REC4 * i];
-    rec[(size_t)REC4 * i + 2].y = __uint_as_float((unsigned)(offsets[i] >> 32));
-    int kc = (int)(offsets[i] & 0xffffffffu), kt = (int)toffsets[i];
+    int kc = (int)offsets[i].c(), kt = (int)offsets[i].t();
     for (int ty = r.y; ty <= r.w; ++ty)
       for (int tx = r.x; tx <= r.z; ++tx) {
         const int cls = tile_class(v, a.x, a.y, a.z, a.w, tx, ty);
@@ -563,6 +580,12 @@ __global__ __launch_bounds__(256) void k_emit_zones(ViewK v, int n, const int4* 
     keys[k] = sK[e];
     ids[k] = sI[e];
   }
+}
+
+// Radix-sort path: the sort's values, (gaussian id, emission index).
+__global__ __launch_bounds__(256) void k_pair_values(int64_t K, const int* __restrict__ ids, int2* __restrict__ pairs) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < K) pairs[k] = make_int2(ids[k], (int)k);
 }
 
 template <typename KeyT>
@@ -672,9 +695,9 @@ __global__ __launch_bounds__(1024) void k_work_items_zones(int tiles, int Kc, co
 // waits for this wave's DMA (vmcnt(0)) and, as a barrier, for every other wave's.
 // Unconditional load (index clamped into the item, k1 > k0): a predicated load would make the
 // compiler wait for all outstanding memory operations, the in-flight DMA included, at the join.
-__device__ __forceinline__ int stage_id(int k, int k1, const int* __restrict__ ids) {
-  const int g = ids[min(k, k1 - 1)];
-  return k < k1 ? g : -1;
+__device__ __forceinline__ int2 stage_id(int k, int k1, const int2* __restrict__ pairs) {
+  const int2 p = pairs[min(k, k1 - 1)];
+  return k < k1 ? p : make_int2(-1, -1);
 }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -805,8 +828,9 @@ __device__ __forceinline__ void ts_load(int64_t kb, int64_t k1, int64_t klast, i
 }
 
 // One register-resident segment of k_tile_place: 32 steps of 64 pairs, in pair order.
+// kseg: emission index of the segment's first pair (the slot written next to the Gaussian id).
 __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int (&d)[TS_SEG], const int (&id)[TS_SEG],
-                                         int* __restrict__ ids_out) {
+                                         int kseg, int2* __restrict__ pairs_out) {
   const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
   for (int j = 0; j < TS_SEG; ++j) {
@@ -820,7 +844,7 @@ __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int 
     }
     if (ok) {
       const int pos = my[d[j]] + __popcll(m & below);
-      ids_out[pos] = id[j];
+      pairs_out[pos] = make_int2(id[j], kseg + j * 64 + lane);
       __builtin_amdgcn_wave_barrier();  // every lane has read the cursor before it moves
       if ((m >> lane) == 1ull) my[d[j]] = pos + 1;  // highest lane of its group
     }
@@ -831,7 +855,7 @@ __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int 
 __global__ __launch_bounds__(256) void k_tile_place(int64_t K, int cw, int cols, int tiles, int bits,
                                                     const uint16_t* __restrict__ keys, const int* __restrict__ ids_in,
                                                     const int* __restrict__ S, const int2* __restrict__ ranges,
-                                                    int zone, int* __restrict__ ids_out) {
+                                                    int zone, int zbase, int2* __restrict__ pairs_out) {
   extern __shared__ int cur[];  // [waves][tiles]
   const int c = xcd_item(blockIdx.x, cols);
   const int waves = (int)blockDim.x >> 6, w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
@@ -863,11 +887,11 @@ __global__ __launch_bounds__(256) void k_tile_place(int64_t K, int cw, int cols,
   }
   __syncthreads();
   if (nseg == 1) {
-    ts_place(lane, bits, my, d, id, ids_out);  // keys and ids are still in registers
+    ts_place(lane, bits, my, d, id, zbase + (int)k0, pairs_out);  // keys and ids are still in registers
   } else {
     for (int seg = 0; seg < nseg; ++seg) {
       ts_load(k0 + (int64_t)seg * 64 * TS_SEG, k1, K - 1, lane, keys, ids_in, d, id);
-      ts_place(lane, bits, my, d, id, ids_out);
+      ts_place(lane, bits, my, d, id, zbase + (int)(k0 + (int64_t)seg * 64 * TS_SEG), pairs_out);
     }
   }
 }
@@ -878,7 +902,7 @@ __global__ __launch_bounds__(256) void k_tile_place(int64_t K, int cw, int cols,
 // TAIL items (tail pairs of the two-zone footprint) accumulate W and D only: 2 MFMA per step.
 template <bool TAIL>
 __device__ __forceinline__ void fwd_accumulate(float* smem, int n, int k0, int k1, int tid, int wave, float xc, float yc,
-                                               int gs, const int* __restrict__ ids, const float4* __restrict__ rec,
+                                               int gs, const int2* __restrict__ pairs, const float4* __restrict__ rec,
                                                f32x4& cW, f32x4& cR, f32x4& cG, f32x4& cB, f32x4& cD) {
   // buffer b: float4 A[TP], float4 B[TP], float Z[TP] (lane-linear per wave, as LDS-DMA writes them)
   constexpr int BUF = 2 * TP + TP / 4;  // float4 units per buffer
@@ -889,14 +913,14 @@ __device__ __forceinline__ void fwd_accumulate(float* smem, int n, int k0, int k
     glds16(p + 1, sA + TP + 64 * wave);
     glds4(p + 2, reinterpret_cast<float*>(sA + 2 * TP) + 64 * wave);  // z = word C .x
   };
-  stage(stage_id(k0 + tid, k1, ids), 0);
-  int idn = stage_id(k0 + TP + tid, k1, ids);
+  stage(stage_id(k0 + tid, k1, pairs).x, 0);
+  int2 idn = stage_id(k0 + TP + tid, k1, pairs);
   int buf = 0;
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
     stage_wait();
     __syncthreads();  // batch `buf` has landed; the other buffer's readers (previous batch) are done
-    if (base + TP < k1) stage(idn, buf ^ 1);
-    idn = stage_id(base + 2 * TP + tid, k1, ids);
+    if (base + TP < k1) stage(idn.x, buf ^ 1);
+    idn = stage_id(base + 2 * TP + tid, k1, pairs);
     const float4* sA = reinterpret_cast<const float4*>(smem) + buf * BUF;
     const float4* sB = sA + TP;
     const float* sZ = reinterpret_cast<const float*>(sB + TP);
@@ -961,7 +985,7 @@ __device__ __forceinline__ void write_pixel(const ViewK& v, int p, const float* 
 
 __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, int n, const int4* __restrict__ items,
                                                          const int* __restrict__ num_items, const int2* __restrict__ ranges,
-                                                         const int* __restrict__ ids, const float4* __restrict__ rec,
+                                                         const int2* __restrict__ pairs, const float4* __restrict__ rec,
                                                          float* __restrict__ fwd_part, float* __restrict__ out_rgb,
                                                          float* __restrict__ out_alpha, float* __restrict__ out_depth,
                                                          float4* __restrict__ saved4, float* __restrict__ savedD) {
@@ -979,9 +1003,9 @@ __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, int n, const i
   const float yc = (float)(ty * T + li) + 0.5f;  // B col = y
   f32x4 cW = {0.f, 0.f, 0.f, 0.f}, cR = cW, cG = cW, cB = cW, cD = cW;
   if (it.x & 1)
-    fwd_accumulate<true>(smem, n, k0, k1, tid, wave, xc, yc, gs, ids, rec, cW, cR, cG, cB, cD);
+    fwd_accumulate<true>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
   else
-    fwd_accumulate<false>(smem, n, k0, k1, tid, wave, xc, yc, gs, ids, rec, cW, cR, cG, cB, cD);
+    fwd_accumulate<false>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
   __syncthreads();
   {  // lane holds C[x = 4*gs + r][y = li]: pixel index y*16 + x, 4 consecutive x
     float* rw = smem + wave * 5 * TP + li * T + 4 * gs;
@@ -1117,9 +1141,10 @@ __device__ __forceinline__ float pair32(float ab, float cd) {
 // sums 0, gw = dW + z dD.
 template <bool TAIL>
 __device__ __forceinline__ void bwd_item(int n, int tile, int k0, int k1, int tid, int wave, int li, int xs, int tx, int ty,
-                                         const float* __restrict__ U, const int* __restrict__ ids,
+                                         const float* __restrict__ U, const int2* __restrict__ pairs,
                                          const float4* __restrict__ rec, float* __restrict__ partials,
-                                         float4 (*sA)[TP], float4 (*sB)[TP], float4 (*sC)[TP], float4* sU) {
+                                         float4 (*sA)[TP], float4 (*sB)[TP], float (*sZ)[TP], int (*sSlot)[TP],
+                                         float4* sU) {
   constexpr int KLO = TAIL ? 3 : 0;  // first upstream channel contracted
   const int lane = tid & 63;
   // A operands (tile-constant) staged in LDS in lane order: sU[k][0][l] = AT_k, sU[k][1][l] = AR_k,
@@ -1129,20 +1154,22 @@ __device__ __forceinline__ void bwd_item(int n, int tile, int k0, int k1, int ti
     for (int c = wave; c < UL / 256; c += 4) glds16(Ug + 64 * c + lane, sU + 64 * c);
   }
   const float x0 = (float)(tx * T + 4 * xs) + 0.5f, y0 = (float)(ty * T + 4 * xs) + 0.5f;
-  auto stage = [&](int g, int b) {
-    const float4* p = rec_of(g, n, rec);
+  // records by LDS-DMA; the pair's partial-sum slot (its emission index) by a plain LDS store
+  auto stage = [&](int2 pr, int b) {
+    const float4* p = rec_of(pr.x, n, rec);
     glds16(p, &sA[b][64 * wave]);
     glds16(p + 1, &sB[b][64 * wave]);
-    glds16(p + 2, &sC[b][64 * wave]);
+    glds4(p + 2, &sZ[b][64 * wave]);
+    sSlot[b][tid] = pr.y;
   };
-  stage(stage_id(k0 + tid, k1, ids), 0);
-  int idn = stage_id(k0 + TP + tid, k1, ids);
+  stage(stage_id(k0 + tid, k1, pairs), 0);
+  int2 idn = stage_id(k0 + TP + tid, k1, pairs);
   int buf = 0;
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
     stage_wait();
     __syncthreads();  // batch `buf` has landed; the other buffer's readers (previous batch) are done
     if (base + TP < k1) stage(idn, buf ^ 1);
-    idn = stage_id(base + 2 * TP + tid, k1, ids);
+    idn = stage_id(base + 2 * TP + tid, k1, pairs);
     const int nb = min(TP, k1 - base);  // Gaussians of this batch
     const int cnt = nb - wave * 64;
     const int ngr = cnt <= 0 ? 0 : min(4, (cnt + 15) >> 4);
@@ -1150,9 +1177,8 @@ __device__ __forceinline__ void bwd_item(int n, int tile, int k0, int k1, int ti
       const int j = wave * 64 + gi * 16 + li;
       const float4 a = sA[buf][j];
       const float4 b = sB[buf][j];
-      const float4 c = sC[buf][j];
-      const float z = c.x;
-      const int myslot = j < nb ? pair_slot(c, tx, ty) : -1;
+      const float z = sZ[buf][j];
+      const int myslot = sSlot[buf][j];  // -1 for padding
       float ex[4], ey[4], dx[4], dy[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -1219,11 +1245,12 @@ __device__ __forceinline__ void bwd_item(int n, int tile, int k0, int k1, int ti
 // depth = 0 (no upstream depth gradient): tail items have nothing to add and return at once; their
 // slots are never read (k_reduce_bwd skips tail tiles in that mode).
 __global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
-    ViewK v, int n, const int4* __restrict__ items, const int* __restrict__ num_items, const int* __restrict__ ids,
+    ViewK v, int n, const int4* __restrict__ items, const int* __restrict__ num_items, const int2* __restrict__ pairs,
     const float4* __restrict__ rec, const float* __restrict__ U, float* __restrict__ partials, int depth) {
   __shared__ __attribute__((aligned(16))) float4 sA[2][TP];
   __shared__ __attribute__((aligned(16))) float4 sB[2][TP];
-  __shared__ __attribute__((aligned(16))) float4 sC[2][TP];
+  __shared__ float sZ[2][TP];
+  __shared__ int sSlot[2][TP];
   __shared__ __attribute__((aligned(16))) float4 sU[UL / 4];
   const int nitems = *num_items;
   if ((int)blockIdx.x >= nitems) return;
@@ -1236,9 +1263,9 @@ __global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int li = lane & 15, xs = lane >> 4;
   if (tail)
-    bwd_item<true>(n, tile, k0, k1, tid, wave, li, xs, tx, ty, U, ids, rec, partials, sA, sB, sC, sU);
+    bwd_item<true>(n, tile, k0, k1, tid, wave, li, xs, tx, ty, U, pairs, rec, partials, sA, sB, sZ, sSlot, sU);
   else
-    bwd_item<false>(n, tile, k0, k1, tid, wave, li, xs, tx, ty, U, ids, rec, partials, sA, sB, sC, sU);
+    bwd_item<false>(n, tile, k0, k1, tid, wave, li, xs, tx, ty, U, pairs, rec, partials, sA, sB, sZ, sSlot, sU);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1248,7 +1275,7 @@ __global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
 #define GR_RG 32
 #endif
 constexpr int RG = GR_RG;        // Gaussians per reduce block (4 lanes each)
-constexpr int RWIN = 18 * GR_RG;  // partial-sum slots staged in LDS per block (18 per Gaussian)
+constexpr int RWIN = 18 * GR_RG;  // partial-sum slots staged in LDS per block (18 per Gaussian, both zones)
 
 template <int CD>
 __device__ void chain_rule(const ViewK& v, int i, const double* S, unsigned cnt, const float* __restrict__ means,
@@ -1256,44 +1283,55 @@ __device__ void chain_rule(const ViewK& v, int i, const double* S, unsigned cnt,
                            const float* __restrict__ opac, float* __restrict__ d_means, float* __restrict__ d_scales,
                            float* __restrict__ d_colors, float* __restrict__ d_opac);
 
-// Block of RG Gaussians: their partial slots are one contiguous range (slots are ordered by
-// Gaussian), staged into LDS with coalesced loads; lane q of each Gaussian's 4 sums the kept tiles
-// j = q (mod 4) of its rectangle in scan order, the 4 sums are combined in a fixed order
-// (deterministic, no atomics), and lane 0 applies the chain rule.
+// Copy partial-sum slots [s0, s1) into LDS at dst (coalesced float4 loads, 4 in flight per lane);
+// returns the first float staged (s0 * NPART rounded down to a float4).
+__device__ __forceinline__ long long stage_slots(long long s0, long long s1, const float* __restrict__ partials, float* dst,
+                                                 int tid) {
+  const long long fa = (s0 * NPART) & ~3ll, fe = s1 * NPART;
+  const int nv = (int)((fe - fa + 3) >> 2);
+  const float4* src = reinterpret_cast<const float4*>(partials + fa);
+  float4* d4 = reinterpret_cast<float4*>(dst);
+  constexpr int NT = 4 * RG;
+  int e = tid;
+  for (; e + 3 * NT < nv; e += 4 * NT) {
+    const float4 x0 = src[e], x1 = src[e + NT], x2 = src[e + 2 * NT], x3 = src[e + 3 * NT];
+    d4[e] = x0;
+    d4[e + NT] = x1;
+    d4[e + 2 * NT] = x2;
+    d4[e + 3 * NT] = x3;
+  }
+  for (; e < nv; e += NT) d4[e] = src[e];
+  return fa;
+}
+
+// Block of RG Gaussians, 4 lanes each.  A Gaussian's partial-sum slots are its pairs' emission
+// indices: its core pairs [c_i, c_i + core_i) and (only with an upstream depth gradient; otherwise
+// the backward skipped them) its tail pairs Kc + [t_i, t_i + tail_i), each contiguous and, over the
+// block, one contiguous range per zone, staged into LDS.  Lane q sums slots q, q+4, ... (core, then
+// tail), the 4 sums are combined in a fixed order (deterministic, no atomics), and lane 0 applies
+// the chain rule.
 template <int CD>
 __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const float* __restrict__ means,
                                                     const float* __restrict__ scales, const float* __restrict__ colors,
-                                                    const float* __restrict__ opac, const float4* __restrict__ rec,
-                                                    const int4* __restrict__ rect,
-                                                    const unsigned long long* __restrict__ counts,
-                                                    const unsigned long long* __restrict__ offsets,
-                                                    const float* __restrict__ partials, float* __restrict__ d_means,
-                                                    float* __restrict__ d_scales, float* __restrict__ d_colors,
-                                                    float* __restrict__ d_opac, int depth) {
-  __shared__ __attribute__((aligned(16))) float sP[RWIN * NPART + 4];
+                                                    const float* __restrict__ opac, const Cnt2* __restrict__ counts,
+                                                    const Cnt2* __restrict__ offsets, const float* __restrict__ partials,
+                                                    float* __restrict__ d_means, float* __restrict__ d_scales,
+                                                    float* __restrict__ d_colors, float* __restrict__ d_opac, int depth) {
+  __shared__ __attribute__((aligned(16))) float sP[RWIN * NPART + 16];
   const int g0 = blockIdx.x * RG;
   const int tid = threadIdx.x, q4 = tid & 3;
   const int i = g0 + (tid >> 2);
   const int gend = min(n, g0 + RG);
-  const long long s0 = (long long)(offsets[g0] >> 32), s1 = (long long)(offsets[gend] >> 32);
-  const bool staged = (s1 - s0) <= RWIN;
-  // staged: LDS holds floats [fa, fe) of the partial array, fa rounded down to 16 B (float4 loads)
-  const long long fa = (s0 * NPART) & ~3ll;
+  const long long Kc = (long long)offsets[n].c();
+  const long long c0 = (long long)offsets[g0].c(), c1 = (long long)offsets[gend].c();
+  const long long t0 = depth ? Kc + (long long)offsets[g0].t() : 0, t1 = depth ? Kc + (long long)offsets[gend].t() : 0;
+  const bool staged = (c1 - c0) + (t1 - t0) <= RWIN;  // block-uniform
+  long long fc = 0, ft = 0;
+  // tail window after the core one: the core copy spans at most (c1 - c0) * NPART + 6 floats
+  float* sT = sP + (((c1 - c0) * NPART + 9) & ~3ll);
   if (staged) {
-    const long long fe = s1 * NPART;
-    const int nv = (int)((fe - fa + 3) >> 2);
-    const float4* src = reinterpret_cast<const float4*>(partials + fa);
-    float4* dst = reinterpret_cast<float4*>(sP);
-    int e = tid;
-    constexpr int NT = 4 * RG;
-    for (; e + 3 * NT < nv; e += 4 * NT) {  // 4 loads in flight per lane
-      const float4 x0 = src[e], x1 = src[e + NT], x2 = src[e + 2 * NT], x3 = src[e + 3 * NT];
-      dst[e] = x0;
-      dst[e + NT] = x1;
-      dst[e + 2 * NT] = x2;
-      dst[e + 3 * NT] = x3;
-    }
-    for (; e < nv; e += NT) dst[e] = src[e];
+    fc = stage_slots(c0, c1, partials, sP, tid);
+    if (t1 > t0) ft = stage_slots(t0, t1, partials, sT, tid);
   }
   __syncthreads();
   double S[NPART];
@@ -1301,31 +1339,18 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
   for (int q = 0; q < NPART; ++q) S[q] = 0.0;
   unsigned cnt = 0;
   if (i < n) {
-    cnt = counts[i] != 0 ? 1u : 0u;  // any kept tile (core or tail)
-    if (cnt > 0) {
-      const long long base = (long long)(offsets[i] >> 32);
-      const float* src = staged ? sP + (base * NPART - fa) : partials + base * NPART;
-      const int4 r = rect[i];
-      const float4 a = rec[(size_t)REC4 * i];
-      const int w = r.z - r.x + 1, area = w * (r.w - r.y + 1);
-      // tiles j = q4, q4+4, ... of the rectangle in scan order, stepped without division
-      int tx = r.x + q4, ty = r.y;
-      while (tx > r.z) {
-        tx -= w;
-        ++ty;
-      }
-      for (int j = q4; j < area; j += 4) {
-        const int cls = tile_class(v, a.x, a.y, a.z, a.w, tx, ty);
-        if (cls == 2 || (cls == 1 && depth)) {  // tail slots are written only with depth gradients
+    const Cnt2 cn = counts[i], of = offsets[i];
+    cnt = cn.v != 0 ? 1u : 0u;  // any kept tile (core or tail)
+    const long long bc = (long long)of.c(), bt = Kc + (long long)of.t();
+    const float* srcc = staged ? sP + (bc * NPART - fc) : partials + bc * NPART;
+    for (int j = q4; j < (int)cn.c(); j += 4)
 #pragma unroll
-          for (int q = 0; q < NPART; ++q) S[q] += (double)src[j * NPART + q];
-        }
-        tx += 4;
-        while (tx > r.z) {
-          tx -= w;
-          ++ty;
-        }
-      }
+      for (int q = 0; q < NPART; ++q) S[q] += (double)srcc[j * NPART + q];
+    if (depth) {
+      const float* srct = staged ? sT + (bt * NPART - ft) : partials + bt * NPART;
+      for (int j = q4; j < (int)cn.t(); j += 4)
+#pragma unroll
+        for (int q = 0; q < NPART; ++q) S[q] += (double)srct[j * NPART + q];
     }
   }
 #pragma unroll
@@ -1569,6 +1594,74 @@ __global__ __launch_bounds__(256) void k_patch_depth(int64_t K, uint64_t* keys, 
   if (k < K) keys[k] |= (uint64_t)dk[ids[k]];
 }
 
+// ------------------------------------------------------------------------------------------------
+// Fit-loop loss (the caller's side of the render op): loss = mean|a - b| + w2 * mean|c - d|, the
+// photometric L1 and the silhouette L1 of fit_multiview_stub.py:292-299, in two kernels per
+// direction instead of torch's chain of elementwise + reduction launches.  Deterministic: a fixed
+// grid, fixed per-thread strides, block tree sums, and an in-order final sum in double.
+// ------------------------------------------------------------------------------------------------
+constexpr int LOSS_BLOCKS = 512;
+
+__global__ __launch_bounds__(256) void k_l1_partial(const float* __restrict__ a, const float* __restrict__ b, int64_t n1,
+                                                    const float* __restrict__ c, const float* __restrict__ d, int64_t n2,
+                                                    float* __restrict__ partial) {
+  __shared__ float red[256];
+  const bool second = blockIdx.y == 1;
+  const float* x = second ? c : a;
+  const float* y = second ? d : b;
+  const int64_t n = second ? n2 : n1;
+  float acc = 0.0f;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)LOSS_BLOCKS * 256) acc += fabsf(x[e] - y[e]);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.y * LOSS_BLOCKS + blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(256) void k_l1_final(const float* __restrict__ partial, int64_t n1, int64_t n2, float w2,
+                                                  float* __restrict__ loss) {
+  __shared__ double r1[256], r2[256];
+  const int t = threadIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = t; i < LOSS_BLOCKS; i += 256) {
+    s1 += (double)partial[i];
+    s2 += (double)partial[LOSS_BLOCKS + i];
+  }
+  r1[t] = s1;
+  r2[t] = s2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) {
+      r1[t] += r1[t + w];
+      r2[t] += r2[t + w];
+    }
+    __syncthreads();
+  }
+  if (t != 0) return;
+  const float m1 = (float)(r1[0] / (double)n1);
+  *loss = n2 > 0 ? m1 + w2 * (float)(r2[0] / (double)n2) : m1;
+}
+
+// d/da = g sign(a - b) / n1, d/dc = (w2 g) sign(c - d) / n2 (torch: abs' = sign, sign(0) = 0).
+__global__ __launch_bounds__(256) void k_l1_grad(const float* __restrict__ a, const float* __restrict__ b, int64_t n1,
+                                                 const float* __restrict__ c, const float* __restrict__ d, int64_t n2,
+                                                 float w2, const float* __restrict__ g_loss, float* __restrict__ ga,
+                                                 float* __restrict__ gc) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const float g = *g_loss;
+  if (e < n1) {
+    const float t = a[e] - b[e];
+    ga[e] = (t > 0.0f ? 1.0f : (t < 0.0f ? -1.0f : 0.0f)) * (g / (float)n1);
+  }
+  if (e < n2) {
+    const float t = c[e] - d[e];
+    gc[e] = (t > 0.0f ? 1.0f : (t < 0.0f ? -1.0f : 0.0f)) * ((w2 * g) / (float)n2);
+  }
+}
+
 // Optional per-kernel timing with HIP events on the launch stream (gr_profile_begin/end), used by
 // bench.py to time the dominant kernels live.  Off by default; host-side state only.
 enum { PROF_RASTER_FWD = 0, PROF_RASTER_BWD = 1, PROF_REDUCE = 2, PROF_BINNING = 3, PROF_SLOTS = 4 };
@@ -1665,7 +1758,7 @@ size_t gr_bins_bytes(const gr_view* v, int n, const gr_plan* plan) {
 size_t gr_fwd_scratch_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
   const int vtiles = vtiles_of(v);
-  size_t off[3];
+  size_t off[4];
   return scratch_fixed(vtiles, plan->num_pairs, off) + align_up(tile_sort_tmp_bytes(plan->num_pairs, vtiles));
 }
 
@@ -1678,16 +1771,25 @@ size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan) {
          align_up(tiles * UL * sizeof(float));
 }
 
-// Decode the scanned total (high word: partial-sum slots, low word: pairs) into the plan; a count
-// that does not fit int32 is flagged as num_pairs = -1 (gr_fwd_render then reports the overflow).
-__global__ void k_plan(const unsigned long long* __restrict__ total, const unsigned* __restrict__ ttotal, gr_plan* plan) {
-  const unsigned long long t = *total;
-  const long long core = (long long)(t & 0xffffffffull), slots = (long long)(t >> 32);
-  const long long pairs = core + (long long)*ttotal;
-  const bool ok = pairs < (1ll << 31) && slots < (1ll << 31);
-  plan->num_pairs = ok ? pairs : -1;
-  plan->num_slots = ok ? slots : -1;
-  plan->num_core_pairs = ok ? core : -1;
+// Decode the scanned totals (core, tail pairs) into the plan; a count that does not fit int32 is
+// flagged as num_pairs = -1 (gr_fwd_render then reports the overflow).
+__global__ __launch_bounds__(256) void k_plan(const Cnt2* __restrict__ scanned, const unsigned long long* __restrict__ total,
+                                              int blocks, gr_plan* plan) {
+  __shared__ unsigned long long red[256];
+  unsigned long long acc = 0;
+  for (int b = threadIdx.x; b < blocks; b += 256) acc += total[b];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const unsigned long long pairs = red[0];
+  const bool ok = pairs < (1ull << 31);  // then neither packed word of the scan carried
+  plan->num_pairs = ok ? (long long)pairs : -1;
+  plan->num_slots = ok ? (long long)pairs : -1;  // one partial-sum slot per pair
+  plan->num_core_pairs = ok ? (long long)scanned->c() : -1;
 }
 
 gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, const float* scales, const float* colors,
@@ -1716,10 +1818,8 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
   GR_HIP_TRY(hipGetLastError());
   size_t tmp = scan_tmp_bytes(n);
   GR_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(g.scan_tmp, tmp, g.counts, g.offsets, n + 1, s));
-  tmp = scan_tmp_bytes(n);
-  GR_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(g.scan_tmp, tmp, g.tcounts, g.toffsets, n + 1, s));
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1), 0, s, (const unsigned long long*)(g.offsets + n),
-                     (const unsigned*)(g.toffsets + n), g.plan);
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(256), 0, s, (const Cnt2*)(g.offsets + n), (const unsigned long long*)g.total,
+                     blocks_for(n + 1), g.plan);
   GR_HIP_TRY(hipGetLastError());
   GR_HIP_TRY(hipMemcpyAsync(plan, g.plan, sizeof(gr_plan), hipMemcpyDeviceToHost, s));
   return GR_OK;
@@ -1761,14 +1861,13 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
   prof_mark(PROF_BINNING, s);
   if (n > 0 && num_pairs > 0) {
     Geom g = geom_view((void*)geom, n);
-    const auto* cnt = (const unsigned long long*)g.counts;
-    const auto* offs = (const unsigned long long*)g.offsets;
+    const Cnt2* cnt = (const Cnt2*)g.counts;
+    const Cnt2* offs = (const Cnt2*)g.offsets;
     if (short_keys(vtiles)) {
       // counting sort of each region (core pairs [0, Kc), tail pairs [Kc, K)) on 16-bit tile keys
       const int64_t Kc = plan->num_core_pairs, Kr[2] = {Kc, num_pairs - Kc};
       hipLaunchKernelGGL((k_emit_zones<uint16_t, false>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
-                         (const int4*)g.rect, cnt, offs, (const unsigned*)g.toffsets, g.rec, (uint16_t*)sc.keys_in,
-                         sc.ids_in);
+                         (const int4*)g.rect, cnt, offs, (const float4*)g.rec, (uint16_t*)sc.keys_in, sc.ids_in);
       GR_HIP_TRY(hipGetLastError());
       TSortPlan tp[2];
       int* Sz[2];
@@ -1805,18 +1904,21 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
         if (Kr[z] == 0) continue;
         hipLaunchKernelGGL(k_tile_place, dim3(tp[z].cols), dim3(64 * tp[z].waves), (size_t)tiles * sizeof(int) * tp[z].waves,
                            s, Kr[z], tp[z].cw, tp[z].cols, tiles, bits_for((uint32_t)tiles), kz[z], iz[z],
-                           (const int*)Sz[z], (const int2*)b.ranges, z, b.ids);
+                           (const int*)Sz[z], (const int2*)b.ranges, z, z == 0 ? 0 : (int)Kc, b.pairs);
         GR_HIP_TRY(hipGetLastError());
       }
     } else {
       // radix sort of the whole pair array on virtual-tile keys (> TSORT_MAX_TILES tiles)
       hipLaunchKernelGGL((k_emit_zones<uint32_t, true>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
-                         (const int4*)g.rect, cnt, offs, (const unsigned*)g.toffsets, g.rec, sc.keys_in, sc.ids_in);
+                         (const int4*)g.rect, cnt, offs, (const float4*)g.rec, sc.keys_in, sc.ids_in);
+      GR_HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_pair_values, dim3(blocks_for(num_pairs)), dim3(256), 0, s, num_pairs, (const int*)sc.ids_in,
+                         sc.pairs_in);
       GR_HIP_TRY(hipGetLastError());
       GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * vtiles, s));
       const int bits = bits_for((uint32_t)vtiles);
       size_t tmp = tile_sort_tmp_bytes(num_pairs, vtiles);
-      GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp, tmp, sc.keys_in, b.keys, sc.ids_in, b.ids,
+      GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp, tmp, sc.keys_in, b.keys, sc.pairs_in, b.pairs,
                                                     (int)num_pairs, 0, bits, s));
       hipLaunchKernelGGL(k_ranges<uint32_t>, dim3(blocks_for(num_pairs)), dim3(256), 0, s, num_pairs, b.keys, b.ranges);
       GR_HIP_TRY(hipGetLastError());
@@ -1836,7 +1938,7 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
   if (num_pairs > 0) {
     prof_mark(PROF_RASTER_FWD, s);
     hipLaunchKernelGGL(k_raster_fwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
-                       (const int*)b.num_items, (const int2*)b.ranges, (const int*)b.ids, (const float4*)g.rec,
+                       (const int*)b.num_items, (const int2*)b.ranges, (const int2*)b.pairs, (const float4*)g.rec,
                        sc.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_FWD, s);
@@ -1876,7 +1978,7 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
     const int64_t cap = item_cap(2 * tiles, num_pairs);
     prof_mark(PROF_RASTER_BWD, s);
     hipLaunchKernelGGL(k_raster_bwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
-                       (const int*)b.num_items, (const int*)b.ids, (const float4*)g.rec, (const float*)U, partials,
+                       (const int*)b.num_items, (const int2*)b.pairs, (const float4*)g.rec, (const float*)U, partials,
                        g_depth != nullptr ? 1 : 0);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_BWD, s);
@@ -1884,13 +1986,11 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
   prof_mark(PROF_REDUCE, s);
   if (color_dim == 3)
     hipLaunchKernelGGL(k_reduce_bwd<3>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
-                       (const float4*)g.rec, (const int4*)g.rect, (const unsigned long long*)g.counts,
-                       (const unsigned long long*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
+                       (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
                        d_opacities, g_depth != nullptr ? 1 : 0);
   else
     hipLaunchKernelGGL(k_reduce_bwd<12>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
-                       (const float4*)g.rec, (const int4*)g.rect, (const unsigned long long*)g.counts,
-                       (const unsigned long long*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
+                       (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
                        d_opacities, g_depth != nullptr ? 1 : 0);
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_REDUCE, s);
@@ -2015,6 +2115,32 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
                        lr.box, img);
   GR_HIP_TRY(hipGetLastError());
   GR_HIP_TRY(hipMemcpy(rgba, img, HW * 4, hipMemcpyDeviceToHost));
+  return GR_OK;
+}
+
+size_t gr_l1_loss_ws_bytes(void) { return (size_t)2 * LOSS_BLOCKS * sizeof(float); }
+
+gr_status gr_l1_loss_fwd(const float* a, const float* b, int64_t n1, const float* c, const float* d, int64_t n2, float w2,
+                         float* loss, void* ws, size_t ws_bytes, void* stream) {
+  if (n1 <= 0 || n2 < 0 || !a || !b || !loss || (n2 > 0 && (!c || !d)))
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_l1_loss_fwd: bad arguments");
+  if (!ws || ws_bytes < gr_l1_loss_ws_bytes()) return set_error(GR_ERR_WORKSPACE, "gr_l1_loss_fwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_l1_partial, dim3(LOSS_BLOCKS, 2), dim3(256), 0, s, a, b, n1, c, d, n2, (float*)ws);
+  GR_HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_l1_final, dim3(1), dim3(256), 0, s, (const float*)ws, n1, n2, w2, loss);
+  GR_HIP_TRY(hipGetLastError());
+  return GR_OK;
+}
+
+gr_status gr_l1_loss_bwd(const float* a, const float* b, int64_t n1, const float* c, const float* d, int64_t n2, float w2,
+                         const float* g_loss, float* g_a, float* g_c, void* stream) {
+  if (n1 <= 0 || n2 < 0 || !a || !b || !g_loss || !g_a || (n2 > 0 && (!c || !d || !g_c)))
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_l1_loss_bwd: bad arguments");
+  const int64_t nm = n1 > n2 ? n1 : n2;
+  hipLaunchKernelGGL(k_l1_grad, dim3(blocks_for(nm)), dim3(256), 0, (hipStream_t)stream, a, b, n1, c, d, n2, w2, g_loss,
+                     g_a, g_c);
+  GR_HIP_TRY(hipGetLastError());
   return GR_OK;
 }
 

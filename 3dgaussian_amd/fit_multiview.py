@@ -35,11 +35,14 @@ import torch.distributed as dist
 
 if __package__ in (None, ""):
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import losses  # type: ignore
     import torch_renderer as tr  # type: ignore
 else:
+    from . import losses
     from . import torch_renderer as tr
 
 RenderFn = Callable[..., tuple]
+FUSED_LOSS = os.environ.get("GR_FUSED_LOSS", "1") != "0"  # losses.l1_loss for the L1 terms (A/B switch)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -149,9 +152,15 @@ class ViewShardedFitter:
         kw = {} if prepared is None else {"prepared": prepared}
         pred, alpha, depth = self.render_fn(means, scales, colors, opacities, self.cams[i], self.width, self.height,
                                             self._background(device), **kw)
-        loss = torch.mean(torch.abs(pred - self.targets[i]))
-        if self.masks is not None and self.w_sil > 0.0:
-            loss = loss + self.w_sil * torch.mean(torch.abs(alpha - self.masks[i]))
+        use_sil = self.masks is not None and self.w_sil > 0.0
+        if self.render_fn is hip_render and pred.device.type == "cuda" and FUSED_LOSS:
+            # photometric + silhouette L1 fused on the device (losses.l1_loss); same value and gradient
+            loss = losses.l1_loss(pred, self.targets[i], alpha if use_sil else None,
+                                  self.masks[i] if use_sil else None, self.w_sil if use_sil else 0.0)
+        else:
+            loss = torch.mean(torch.abs(pred - self.targets[i]))
+            if use_sil:
+                loss = loss + self.w_sil * torch.mean(torch.abs(alpha - self.masks[i]))
         if self.depths is not None and self.w_depth > 0.0:
             d_pred = depth / (depth.max() + 1e-6)
             loss = loss + self.w_depth * torch.mean(torch.abs(d_pred - self.depths[i]))

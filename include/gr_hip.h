@@ -146,21 +146,33 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
                        const float* colors, const float* opacities, uint8_t* rgba);
 
 /* ------------------------------------------------------------------------------------------ */
+/* Fit-loop loss, the caller's side of the render op (fit_multiview_stub.py:292-299):         */
+/*   loss = mean|a - b| + w2 * mean|c - d|   (photometric L1 + weighted silhouette L1)        */
+/* Device pointers, float32, stream-ordered, deterministic.  c, d may be NULL with n2 = 0.     */
+/* The backward writes g_a = g sign(a-b)/n1 and g_c = (w2 g) sign(c-d)/n2, g = *g_loss.        */
+/* ------------------------------------------------------------------------------------------ */
+size_t gr_l1_loss_ws_bytes(void);
+gr_status gr_l1_loss_fwd(const float* a, const float* b, int64_t n1, const float* c, const float* d,
+                         int64_t n2, float w2, float* loss, void* ws, size_t ws_bytes, void* stream);
+gr_status gr_l1_loss_bwd(const float* a, const float* b, int64_t n1, const float* c, const float* d,
+                         int64_t n2, float w2, const float* g_loss, float* g_a, float* g_c,
+                         void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
 /* Introspection (host-only, no GPU needed).                                                  */
 /* ------------------------------------------------------------------------------------------ */
 
 /* Byte offsets of the sub-buffers inside geom / bins, for debugging and bit-exact tests.
  *   geom: [0] records float4[n+1][4], 64 bytes per Gaussian (record n: padding, o = 0):
- *             A = (px, py, qx, qy), B = (o, r, g, b), C = (z, first slot as int bits,
- *             tx0 | ty0 << 16 as uint bits, rectangle width as int bits), D = 0
+ *             A = (px, py, qx, qy), B = (o, r, g, b), C = (z, 0, 0, 0), D = 0
  *         [1] rect int4[n] (tx0,ty0,tx1,ty1) [2] counts u64[n+1] [3] offsets u64[n+1]
- *         [4] device copy of the plan (gr_plan) [5] tail counts u32[n+1] [6] tail offsets u32[n+1]
- *         [7] end of the fixed part (scan temp follows)
- *         (counts/offsets packed: rectangle area / first slot in the high word, core tiles / first
- *         core pair in the low word; tail pairs follow the num_core_pairs core pairs)
- *   bins: [0] keys (radix-sort fallback only, > 8192 tiles) [1] gaussian ids int32[K]
+ *         [4] device copy of the plan (gr_plan) and the exact pair total [5] end of the fixed part
+ *         (counts/offsets packed: core tiles / first core pair in the low word, tail tiles / first
+ *         tail pair after the num_core_pairs core pairs in the high word)
+ *   bins: [0] keys (radix-sort fallback only, > 8192 tiles) [1] pairs int2[K] (gaussian id,
+ *         emission index = backward partial-sum slot)
  *         [2] ranges int2[2 * tiles]: per virtual tile (2t: core list of tile t, 2t+1: its tail list) */
-#define GR_GEOM_PARTS 8
+#define GR_GEOM_PARTS 6
 void gr_geom_layout(int n, size_t offsets_out[GR_GEOM_PARTS]);
 void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[3]);
 

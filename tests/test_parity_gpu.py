@@ -113,27 +113,21 @@ def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=CUTOFF)
     n = m.shape[0]
     g_off = nat.geom_layout(n)
     geom = st.geom.cpu().numpy()
-    rec = geom[g_off[0]: g_off[0] + 64 * n].view(np.float32).reshape(n, 16)  # 64-byte records A|B|C|D
-    recA = rec[:, 0:4]
-    recC = rec[:, 8:12].view(np.uint32)
+    rec = geom[g_off[0]: g_off[0] + 64 * (n + 1)].view(np.float32).reshape(n + 1, 16)  # 64-byte records A|B|C|D
     rect = geom[g_off[1]: g_off[1] + 16 * n].view(np.int32).reshape(n, 4)
-    # packed u64: low word = kept tiles / first pair, high word = rectangle area / first slot
-    counts64 = geom[g_off[2]: g_off[2] + 8 * n].view(np.uint64)
-    offsets64 = geom[g_off[3]: g_off[3] + 8 * (n + 1)].view(np.uint64)
-    core = (counts64 & 0xFFFFFFFF).astype(np.int32)  # core tiles; tail tiles counted apart
-    tail = geom[g_off[5]: g_off[5] + 4 * n].view(np.uint32).astype(np.int32)
-    counts = core + tail
-    offsets = (offsets64 & 0xFFFFFFFF).astype(np.int32)
-    areas = (counts64 >> 32).astype(np.int64)
+    # packed u64 per Gaussian: core count | tail count << 32 (and their exclusive scan)
+    c64 = geom[g_off[2]: g_off[2] + 8 * n].view(np.uint64)
+    o64 = geom[g_off[3]: g_off[3] + 8 * (n + 1)].view(np.uint64)
+    cnt = np.stack([c64 & 0xFFFFFFFF, c64 >> 32], 1).astype(np.int64)
+    off = np.stack([o64 & 0xFFFFFFFF, o64 >> 32], 1).astype(np.int64)
     b_off = nat.bins_layout(gv, n, st.num_pairs)
     bins = st.bins.cpu().numpy()
     K = st.num_pairs
     tiles = ((W + 15) // 16) * ((H + 15) // 16)
-    ids = bins[b_off[1]: b_off[1] + 4 * K].view(np.int32)
+    pairs = bins[b_off[1]: b_off[1] + 8 * K].view(np.int32).reshape(K, 2)  # (gaussian id, emission index)
     ranges = bins[b_off[2]: b_off[2] + 16 * tiles].view(np.int32).reshape(2 * tiles, 2)  # per virtual tile
-    return dict(recA=recA, recC=recC, offsets64=offsets64, rect=rect, counts=counts, core=core, tail=tail,
-                offsets=offsets, ids=ids, ranges=ranges, K=K, Kc=int(st.plan.num_core_pairs), areas=areas,
-                slots=int(st.plan.num_slots))
+    return dict(rec=rec, rect=rect, core=cnt[:, 0], tail=cnt[:, 1], off=off, pairs=pairs, ranges=ranges, K=K,
+                Kc=int(st.plan.num_core_pairs), slots=int(st.plan.num_slots))
 
 
 @pytest.mark.parametrize("case", ["f1_n300_64x48", "f2_c1_view1", "c2_100k_512", "edge_big_sigma", "hd_1920x1080",
@@ -159,36 +153,35 @@ def test_bins_bit_exact(pkg, cuda, case):
     g = _native_bins(pkg, scene, view, proj, W, H, cuda)
     v = orc.make_view(view, proj, W, H, None, cutoff=CUTOFF, core_cutoff=CORE)
     rec, rect, counts = orc.preprocess(v, scene)
+    n = len(counts)
     # projected centres are float32-identical (same operation sequence, no FMA contraction)
-    np.testing.assert_array_equal(g["recA"][:, 0].view(np.int32), rec[:, 0].view(np.int32))
-    np.testing.assert_array_equal(g["recA"][:, 1].view(np.int32), rec[:, 1].view(np.int32))
-    np.testing.assert_array_equal(g["recA"][:, 2].view(np.int32), rec[:, 9].view(np.int32))  # qx
-    np.testing.assert_array_equal(g["recA"][:, 3].view(np.int32), rec[:, 10].view(np.int32))  # qy
-    np.testing.assert_array_equal(g["counts"], counts)
-    np.testing.assert_array_equal(g["rect"], rect)
-    kept = counts > 0
-    area = (rect[:, 2] - rect[:, 0] + 1) * (rect[:, 3] - rect[:, 1] + 1)
-    np.testing.assert_array_equal(g["areas"], np.where(kept, area, 0))
-    assert g["slots"] == int(np.where(kept, area, 0).sum())
-    # record word C of kept Gaussians: first slot, packed rectangle origin, rectangle width
-    C = g["recC"][kept]
-    np.testing.assert_array_equal(C[:, 1], (g["offsets64"][:-1][kept] >> 32).astype(np.uint32))
-    np.testing.assert_array_equal(C[:, 2], (rect[kept, 0] | (rect[kept, 1] << 16)).astype(np.uint32))
-    np.testing.assert_array_equal(C[:, 3], (rect[kept, 2] - rect[kept, 0] + 1).astype(np.uint32))
+    for col, ocol in ((0, 0), (1, 1), (2, 9), (3, 10)):  # px, py, qx, qy
+        np.testing.assert_array_equal(g["rec"][:n, col].view(np.int32), rec[:, ocol].view(np.int32))
+    assert g["rec"][n, 4] == 0.0 and g["rec"][n, 0] > 1e29  # the padding record
+    np.testing.assert_array_equal(g["core"] + g["tail"], counts)
+    np.testing.assert_array_equal(g["rect"][counts > 0], rect[counts > 0])
     _, keys, vals, ranges = orc.bin_pairs(v, rec, rect, counts)
-    assert g["K"] == len(vals)
-    # core pairs first (Gaussian order, per-Gaussian offsets = scan of the core counts), tail after
+    K = len(vals)
+    assert g["K"] == K == g["slots"]
     tail_pair = (keys & 1).astype(bool)
     assert g["Kc"] == int((~tail_pair).sum())
-    np.testing.assert_array_equal(g["core"], np.bincount(vals[~tail_pair], minlength=len(counts)))
-    np.testing.assert_array_equal(g["offsets"], np.concatenate([[0], np.cumsum(g["core"])]).astype(np.int32))
-    # every virtual tile's Gaussian list is bit-exact (ascending Gaussian index): the HIP lists sit
-    # in the core / tail regions of the pair array, the oracle's in virtual-tile order
+    np.testing.assert_array_equal(g["core"], np.bincount(vals[~tail_pair], minlength=n))
+    np.testing.assert_array_equal(g["off"][:, 0], np.concatenate([[0], np.cumsum(g["core"])]))
+    np.testing.assert_array_equal(g["off"][:, 1], np.concatenate([[0], np.cumsum(g["tail"])]))
+    # emission index of every oracle pair: Gaussian-major, tiles in raster order, core zone first
+    order = np.lexsort((keys >> 1, vals, tail_pair))
+    emit = np.empty(K, np.int64)
+    emit[order] = np.arange(K)
+    # every virtual tile's list is bit-exact (ascending Gaussian index, with each pair's emission
+    # index = its partial-sum slot): the HIP lists sit in the core / tail regions of the pair array
+    # (counting sort) or in virtual-tile order (radix sort), the oracle's in virtual-tile order
     lens = ranges[:, 1] - ranges[:, 0]
     glens = np.maximum(g["ranges"][:, 1] - g["ranges"][:, 0], 0)
     np.testing.assert_array_equal(glens, lens)
     for t in np.nonzero(lens)[0]:
-        np.testing.assert_array_equal(g["ids"][g["ranges"][t, 0]:g["ranges"][t, 1]], vals[ranges[t, 0]:ranges[t, 1]])
+        seg = g["pairs"][g["ranges"][t, 0]:g["ranges"][t, 1]]
+        np.testing.assert_array_equal(seg[:, 0], vals[ranges[t, 0]:ranges[t, 1]])
+        np.testing.assert_array_equal(seg[:, 1], emit[ranges[t, 0]:ranges[t, 1]])
         if len(lens) <= 16384:  # counting-sort path: tail lists in the tail region (radix: by virtual tile)
             assert (g["ranges"][t, 0] >= g["Kc"]) == bool(t & 1)
 
