@@ -693,12 +693,12 @@ __global__ __launch_bounds__(1024) void k_work_items_zones(int tiles, int Kc, co
 // and the Gaussian ids of batch b+2 are in flight in a register, so neither the id load nor the
 // dependent record gathers sit on the critical path.  The __syncthreads() at the top of each batch
 // waits for this wave's DMA (vmcnt(0)) and, as a barrier, for every other wave's.
-// Unconditional load (index clamped into the item, k1 > k0): a predicated load would make the
-// compiler wait for all outstanding memory operations, the in-flight DMA included, at the join.
-__device__ __forceinline__ int2 stage_id(int k, int k1, const int2* __restrict__ pairs) {
-  const int2 p = pairs[min(k, k1 - 1)];
-  return k < k1 ? p : make_int2(-1, -1);
-}
+// Unconditional load (index clamped into the item, k1 > k0); the padding select (k >= k1) is made
+// only when the pair is consumed, a batch later (stage_pair): selecting here lets the compiler turn
+// the load into a predicated one, and the join after it waits for every outstanding memory
+// operation, the in-flight DMA included.
+__device__ __forceinline__ int2 stage_id(int k, int k1, const int2* __restrict__ pairs) { return pairs[min(k, k1 - 1)]; }
+__device__ __forceinline__ int2 stage_pair(int2 raw, int k, int k1) { return k < k1 ? raw : make_int2(-1, -1); }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -913,13 +913,13 @@ __device__ __forceinline__ void fwd_accumulate(float* smem, int n, int k0, int k
     glds16(p + 1, sA + TP + 64 * wave);
     glds4(p + 2, reinterpret_cast<float*>(sA + 2 * TP) + 64 * wave);  // z = word C .x
   };
-  stage(stage_id(k0 + tid, k1, pairs).x, 0);
-  int2 idn = stage_id(k0 + TP + tid, k1, pairs);
+  stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1).x, 0);
+  int2 idn = stage_id(k0 + TP + tid, k1, pairs);  // raw: batch base + TP
   int buf = 0;
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
     stage_wait();
     __syncthreads();  // batch `buf` has landed; the other buffer's readers (previous batch) are done
-    if (base + TP < k1) stage(idn.x, buf ^ 1);
+    if (base + TP < k1) stage(stage_pair(idn, base + TP + tid, k1).x, buf ^ 1);
     idn = stage_id(base + 2 * TP + tid, k1, pairs);
     const float4* sA = reinterpret_cast<const float4*>(smem) + buf * BUF;
     const float4* sB = sA + TP;
@@ -1054,14 +1054,37 @@ __global__ __launch_bounds__(256) void k_fwd_finalize(ViewK v, const int2* __res
   write_pixel(v, y * v.W + x, acc, out_rgb, out_alpha, out_depth, saved4, savedD);
 }
 
-constexpr int UL = 5 * 2 * TP;  // floats of backward operands per tile (k_pixel_grads)
+constexpr int UL = 5 * 2 * TP;  // floats of backward operands per tile (k_pixel_grads, f32 kernel)
+// bf16 split-precision backward (k_raster_bwd_bf16): per tile, A fragments of v_mfma_f32_32x32x16_bf16
+// for 2 sides (T: contraction over x, R: over y) x 3 channel pairs x 3 bf16 pieces x 64 lanes, 16 B each.
+constexpr int UF_FRAGS = 2 * 3 * 3 * 64;  // uint4 per tile
+// channel pairs on the 32 MFMA rows (16 per channel): (dC_r, dC_g), (dC_b, -), (dW, dD); tail items
+// (depth-coupled terms only) need just the last pair
+__device__ __forceinline__ int pair_channel(int pr, int c) { return pr == 0 ? c : (pr == 1 ? (c == 0 ? 2 : -1) : 3 + c); }
+// contracted coordinate of k-slot 8h + j of the 32x32x16 operands: the 8 pixels a lane half h owns,
+// {4h..4h+3, 8+4h..8+4h+3}, which are also the output rows that lane half holds (C map, row =
+// (reg&3) + 8 (reg>>2) + 4h): one set of exponentials per lane serves both contractions.
+__device__ __forceinline__ int kslot_pixel(int h, int j) { return (j < 4) ? 4 * h + j : 8 + 4 * h + (j - 4); }
+
+// Exact three-way bf16 split: x = hi + mid + lo, each a truncated bf16 (hi keeps 8 significant bits,
+// the f32 remainders are exact), returned as f32 values whose low 16 bits are zero.
+__device__ __forceinline__ void split3(float x, float& hi, float& mid, float& lo) {
+  hi = __uint_as_float(__float_as_uint(x) & 0xffff0000u);
+  const float r1 = x - hi;
+  mid = __uint_as_float(__float_as_uint(r1) & 0xffff0000u);
+  lo = r1 - mid;  // <= 8 significant bits: exactly a bf16
+}
+// two bf16 (high halves of a, b) into one dword: low half = a, high half = b
+__device__ __forceinline__ unsigned pack_bf16(float a, float b) {
+  return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
+}
 
 // Per-pixel upstream vector U = (dC_r, dC_g, dC_b, dW, dD) of the OIT finalize
 // (torch_renderer.py:192-203), laid out [tile][channel][256] for the backward work items.
 __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __restrict__ saved4,
                                                      const float* __restrict__ savedD, const float* __restrict__ g_rgb,
                                                      const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
-                                                     float* __restrict__ U) {
+                                                     float* __restrict__ U, uint4* __restrict__ UF) {
   const int tile = blockIdx.x, tid = threadIdx.x;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
@@ -1096,6 +1119,30 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
   }
   // operand layout of k_raster_bwd_mfma (UL floats per tile): per channel k, AT[l][s] = U_k(x = 4xs+s,
   // y = li) and then AR[l][s] = U_k(x = li, y = 4xs+s), l = li + 16 xs: lane l reads one float4 each
+  if (UF) {  // bf16 fragments: stage u in LDS, then 384 (side, pair, lane) fragment triples
+    __shared__ float sU[5][TP];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) sU[k][tid] = u[k];
+    __syncthreads();
+    uint4* fr = reinterpret_cast<uint4*>(UF) + (size_t)tile * UF_FRAGS;
+    for (int cmb = tid; cmb < 2 * 3 * 64; cmb += 256) {
+      const int side = cmb / 192, pr = (cmb / 64) % 3, l = cmb & 63;
+      const int r = l & 31, h = l >> 5, ch = pair_channel(pr, r >> 4), i = r & 15;
+      float hi[8], mid[8], lo[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kk = kslot_pixel(h, j);
+        const float val = ch < 0 ? 0.0f : (side == 0 ? sU[ch][i * T + kk] : sU[ch][kk * T + i]);
+        split3(val, hi[j], mid[j], lo[j]);
+      }
+      uint4* o = fr + ((side * 3 + pr) * 3) * 64 + l;
+      o[0] = make_uint4(pack_bf16(hi[0], hi[1]), pack_bf16(hi[2], hi[3]), pack_bf16(hi[4], hi[5]), pack_bf16(hi[6], hi[7]));
+      o[64] = make_uint4(pack_bf16(mid[0], mid[1]), pack_bf16(mid[2], mid[3]), pack_bf16(mid[4], mid[5]),
+                         pack_bf16(mid[6], mid[7]));
+      o[128] = make_uint4(pack_bf16(lo[0], lo[1]), pack_bf16(lo[2], lo[3]), pack_bf16(lo[4], lo[5]), pack_bf16(lo[6], lo[7]));
+    }
+    return;
+  }
   float* dst = U + (size_t)tile * UL;
   const int px = tid & (T - 1), py = tid >> 4;
   const int at = (py + 16 * (px >> 2)) * 4 + (px & 3), ar = TP + (px + 16 * (py >> 2)) * 4 + (py & 3);
@@ -1162,13 +1209,13 @@ __device__ __forceinline__ void bwd_item(int n, int tile, int k0, int k1, int ti
     glds4(p + 2, &sZ[b][64 * wave]);
     sSlot[b][tid] = pr.y;
   };
-  stage(stage_id(k0 + tid, k1, pairs), 0);
-  int2 idn = stage_id(k0 + TP + tid, k1, pairs);
+  stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1), 0);
+  int2 idn = stage_id(k0 + TP + tid, k1, pairs);  // raw: batch base + TP
   int buf = 0;
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
     stage_wait();
     __syncthreads();  // batch `buf` has landed; the other buffer's readers (previous batch) are done
-    if (base + TP < k1) stage(idn, buf ^ 1);
+    if (base + TP < k1) stage(stage_pair(idn, base + TP + tid, k1), buf ^ 1);
     idn = stage_id(base + 2 * TP + tid, k1, pairs);
     const int nb = min(TP, k1 - base);  // Gaussians of this batch
     const int cnt = nb - wave * 64;
@@ -1266,6 +1313,198 @@ __global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
     bwd_item<true>(n, tile, k0, k1, tid, wave, li, xs, tx, ty, U, pairs, rec, partials, sA, sB, sZ, sSlot, sU);
   else
     bwd_item<false>(n, tile, k0, k1, tid, wave, li, xs, tx, ty, U, pairs, rec, partials, sA, sB, sZ, sSlot, sU);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Backward, split-precision form.  The same two contractions as k_raster_bwd_mfma,
+//   T_k[y][g] = sum_x U_k[x][y] ex_g(x),   R_k[x][g] = sum_y U_k[x][y] ey_g(y),
+// on v_mfma_f32_32x32x16_bf16 (K = the 16 pixels of a tile row / column, N = 32 Gaussians, M = two
+// channels x 16 pixels) with both operands split exactly into three bf16 pieces, x = x0 + x1 + x2,
+// and the six products of weight >= 2^-16 accumulated in f32 (smallest first): every dropped
+// cross term is below 2^-23 of its product, so the result is as accurate as the f32 contraction.
+// An f32 MFMA runs on the vector ALU's issue cycles (it cannot overlap VALU work); a bf16 MFMA is
+// 16x the rate and overlaps, so the splitting VALU work is bought back many times.
+// A = the tile's upstream vectors, pre-split by k_pixel_grads (UF); B = the Gaussian's exponentials,
+// split here.  Lane l (r = l & 31, h = l >> 5) owns Gaussian r of the group and pixels
+// kslot_pixel(h, 0..7) on both axes: its B operand for T is ex at those x, for R ey at those y, and
+// its accumulator rows of T (R) are exactly those y (x), so each exponential is computed once.
+// ------------------------------------------------------------------------------------------------
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ s16x8 as_frag(uint4 u) {
+  s16x8 f;
+  __builtin_memcpy(&f, &u, sizeof(f));
+  return f;
+}
+
+// A * B over the six significant piece products, smallest first.  A's pieces are read from LDS
+// (lane-linear fragments, one ds_read_b128 each) next to their use rather than held in registers:
+// that keeps the kernel at 4 waves per SIMD.
+__device__ __forceinline__ f32x16 mfma_split(const uint4* __restrict__ A, int lane, const s16x8 (&B)[3]) {
+  f32x16 c = {};
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(A[128 + lane]), B[0], c, 0, 0, 0);
+  const s16x8 a1 = as_frag(A[64 + lane]);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, B[1], c, 0, 0, 0);
+  const s16x8 a0 = as_frag(A[lane]);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, B[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, B[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, B[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, B[0], c, 0, 0, 0);
+  return c;
+}
+
+// eight f32 values -> three bf16x8 operand fragments (exact split)
+__device__ __forceinline__ void split_frag(const float (&v)[8], s16x8 (&f)[3]) {
+  float hi[8], mid[8], lo[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) split3(v[j], hi[j], mid[j], lo[j]);
+  f[0] = as_frag(make_uint4(pack_bf16(hi[0], hi[1]), pack_bf16(hi[2], hi[3]), pack_bf16(hi[4], hi[5]), pack_bf16(hi[6], hi[7])));
+  f[1] = as_frag(make_uint4(pack_bf16(mid[0], mid[1]), pack_bf16(mid[2], mid[3]), pack_bf16(mid[4], mid[5]),
+                            pack_bf16(mid[6], mid[7])));
+  f[2] = as_frag(make_uint4(pack_bf16(lo[0], lo[1]), pack_bf16(lo[2], lo[3]), pack_bf16(lo[4], lo[5]), pack_bf16(lo[6], lo[7])));
+}
+
+template <bool TAIL>
+__device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, int wave, int tx, int ty,
+                                              const int2* __restrict__ pairs, const float4* __restrict__ rec,
+                                              float* __restrict__ partials, float4 (*sA)[TP], float4 (*sB)[TP],
+                                              float (*sZ)[TP], int (*sSlot)[TP], const uint4* sUF) {
+  constexpr int P0 = TAIL ? 2 : 0;  // first channel pair contracted
+  const int lane = tid & 63, r = lane & 31, h = lane >> 5;
+  // pixel centres of the lane's 8 contraction slots (x for T, y for R): base + compile-time offset
+  const float pxb = (float)(tx * T + 4 * h) + 0.5f, pyb = (float)(ty * T + 4 * h) + 0.5f;
+#define PX0(q) (pxb + (float)((q) < 4 ? (q) : (q) + 4))
+#define PY0(q) (pyb + (float)((q) < 4 ? (q) : (q) + 4))
+  auto stage = [&](int2 pr, int b) {
+    const float4* p = rec_of(pr.x, n, rec);
+    glds16(p, &sA[b][64 * wave]);
+    glds16(p + 1, &sB[b][64 * wave]);
+    glds4(p + 2, &sZ[b][64 * wave]);
+    sSlot[b][tid] = pr.y;
+  };
+  stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1), 0);
+  int2 idn = stage_id(k0 + TP + tid, k1, pairs);  // raw: batch base + TP
+  int buf = 0;
+  for (int base = k0; base < k1; base += TP, buf ^= 1) {
+    stage_wait();
+    __syncthreads();  // batch `buf` has landed; the other buffer's readers (previous batch) are done
+    if (base + TP < k1) stage(stage_pair(idn, base + TP + tid, k1), buf ^ 1);
+    idn = stage_id(base + 2 * TP + tid, k1, pairs);
+    const int nb = min(TP, k1 - base);
+    for (int gi = 0; gi < 2; ++gi) {
+      const int g0 = wave * 64 + gi * 32;
+      if (g0 >= nb) break;  // wave-uniform
+      const int j = g0 + r;
+      const float4 a = sA[buf][j];
+      const float4 b = sB[buf][j];
+      const float z = sZ[buf][j];
+      const int myslot = sSlot[buf][j];  // -1 for padding
+      float ex[8], ey[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float dx = PX0(q) - a.x, dy = PY0(q) - a.y;
+        ex[q] = __builtin_amdgcn_exp2f(dx * a.z * dx);  // exactly 0 for padding
+        ey[q] = __builtin_amdgcn_exp2f(dy * a.w * dy);
+      }
+      // both contractions are issued before either epilogue, so the T epilogue's VALU work runs while
+      // the R MFMAs execute
+      s16x8 BT[3], BR[3];
+      split_frag(ex, BT);
+      split_frag(ey, BR);
+      f32x16 DT[3], DR[3];
+#pragma unroll
+      for (int pr = P0; pr < 3; ++pr) DT[pr] = mfma_split(sUF + (0 * 3 + pr) * 3 * 64, lane, BT);
+#pragma unroll
+      for (int pr = P0; pr < 3; ++pr) DR[pr] = mfma_split(sUF + (1 * 3 + pr) * 3 * 64, lane, BR);
+      float S[NPART] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      // T: rows y = kslot_pixel(h, q) of channels pair_channel(pr, c) at register 8c + q
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float dy = PY0(q) - a.y;
+        const float T3 = DT[2][q], T4 = DT[2][8 + q];
+        float GT;
+        if constexpr (TAIL) {
+          GT = fmaf(z, T4, T3);
+        } else {
+          const float T0 = DT[0][q], T1 = DT[0][8 + q], T2 = DT[1][q];
+          S[0] = fmaf(ey[q], T0, S[0]);
+          S[1] = fmaf(ey[q], T1, S[1]);
+          S[2] = fmaf(ey[q], T2, S[2]);
+          GT = fmaf(z, T4, fmaf(b.w, T2, fmaf(b.z, T1, fmaf(b.y, T0, T3))));
+        }
+        S[3] = fmaf(ey[q], T4, S[3]);
+        const float t = ey[q] * GT;
+        S[4] += t;
+        const float tdy = t * dy;
+        S[6] += tdy;
+        S[8] = fmaf(tdy, dy, S[8]);
+      }
+      // R: rows x = kslot_pixel(h, q)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float dx = PX0(q) - a.x;
+        const float R3 = DR[2][q], R4 = DR[2][8 + q];
+        float GR;
+        if constexpr (TAIL) {
+          GR = fmaf(z, R4, R3);
+        } else {
+          GR = fmaf(z, R4, fmaf(b.w, DR[1][q], fmaf(b.z, DR[0][8 + q], fmaf(b.y, DR[0][q], R3))));
+        }
+        const float tdx = (ex[q] * GR) * dx;  // (0 * G) * dx: padding stays 0, never 0 * inf
+        S[5] += tdx;
+        S[7] = fmaf(tdx, dx, S[7]);
+      }
+      // lanes r and r + 32 hold the two halves of Gaussian r's pixels: half 0 ends with the totals of
+      // S0, S2, S4, S6, S8, half 1 with S1, S3, S5, S7
+      const float P01 = pair32(S[0], S[1]), P23 = pair32(S[2], S[3]), P45 = pair32(S[4], S[5]);
+      const float P67 = pair32(S[6], S[7]), P8 = pair32(S[8], S[8]);
+      if (myslot >= 0) {
+        float* dst = partials + (size_t)myslot * NPART + h;
+        dst[0] = b.x * P01;  // colour / depth sums carry the opacity
+        dst[2] = b.x * P23;
+        dst[4] = P45;
+        dst[6] = P67;
+        if (h == 0) dst[8] = P8;
+      }
+    }
+  }
+#undef PX0
+#undef PY0
+}
+
+#ifndef GR_BF16_WAVES
+#define GR_BF16_WAVES 2
+#endif
+
+__global__ __launch_bounds__(256, GR_BF16_WAVES) void k_raster_bwd_bf16(ViewK v, int n, const int4* __restrict__ items,
+                                                           const int* __restrict__ num_items, const int2* __restrict__ pairs,
+                                                           const float4* __restrict__ rec, const uint4* __restrict__ UF,
+                                                           float* __restrict__ partials, int depth) {
+  __shared__ __attribute__((aligned(16))) float4 sA[2][TP];
+  __shared__ __attribute__((aligned(16))) float4 sB[2][TP];
+  __shared__ float sZ[2][TP];
+  __shared__ int sSlot[2][TP];
+  __shared__ __attribute__((aligned(16))) uint4 sUF[UF_FRAGS];
+  const int nitems = *num_items;
+  if ((int)blockIdx.x >= nitems) return;
+  const int item = xcd_item(blockIdx.x, nitems);
+  const int4 it = items[item];
+  const bool tail = it.x & 1;
+  if (tail && !depth) return;
+  const int tile = it.x >> 1, k0 = it.y, k1 = it.z;
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  {  // the tile's A fragments -> LDS (DMA), then this lane's into registers
+    const uint4* src = UF + (size_t)tile * UF_FRAGS;
+    for (int c = wave; c < UF_FRAGS / 64; c += 4) glds16(src + 64 * c + lane, sUF + 64 * c);
+    stage_wait();
+    __syncthreads();
+  }
+  if (tail)
+    bwd_item_bf16<true>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sSlot, sUF);
+  else
+    bwd_item_bf16<false>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sSlot, sUF);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1687,6 +1926,16 @@ void prof_mark(int which, hipStream_t s) {
 
 inline int blocks_for(int64_t n, int bs = 256) { return (int)((n + bs - 1) / bs); }
 
+// Backward splat kernel: the bf16 split-precision one (default) or the f32 one (GR_BWD_F32=1, kept
+// as the reference form and for A/B timing).  Both meet the same tests.
+bool bwd_split_precision() {
+  static const bool f32 = [] {
+    const char* e = std::getenv("GR_BWD_F32");
+    return e && e[0] == '1';
+  }();
+  return !f32;
+}
+
 gr_status check_view(const gr_view* v) {
   if (!v) return set_error(GR_ERR_INVALID_ARGUMENT, "view is null");
   if (v->width <= 0 || v->height <= 0) return set_error(GR_ERR_INVALID_ARGUMENT, "width/height must be positive");
@@ -1767,8 +2016,8 @@ size_t gr_fwd_scratch_bytes(const gr_view* v, int n, const gr_plan* plan) {
 size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
   const size_t tiles = (size_t)tiles_x_of(v->width) * tiles_y_of(v->height);
-  return align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)) +
-         align_up(tiles * UL * sizeof(float));
+  const size_t per_tile = UL * sizeof(float) > UF_FRAGS * sizeof(uint4) ? UL * sizeof(float) : UF_FRAGS * sizeof(uint4);
+  return align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)) + align_up(tiles * per_tile);
 }
 
 // Decode the scanned totals (core, tail pairs) into the plan; a count that does not fit int32 is
@@ -1972,14 +2221,20 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
   float* partials = (float*)ws;
   if (num_pairs > 0) {
     float* U = (float*)((char*)ws + align_up((size_t)plan->num_slots * NPART * sizeof(float)));
+    const bool split = bwd_split_precision();
     hipLaunchKernelGGL(k_pixel_grads, dim3(tiles), dim3(256), 0, s, vk, (const float4*)saved, saved + 4 * HW, g_rgb,
-                       g_alpha, g_depth, U);
+                       g_alpha, g_depth, U, split ? (uint4*)U : (uint4*)nullptr);
     GR_HIP_TRY(hipGetLastError());
     const int64_t cap = item_cap(2 * tiles, num_pairs);
     prof_mark(PROF_RASTER_BWD, s);
-    hipLaunchKernelGGL(k_raster_bwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
-                       (const int*)b.num_items, (const int2*)b.pairs, (const float4*)g.rec, (const float*)U, partials,
-                       g_depth != nullptr ? 1 : 0);
+    if (split)
+      hipLaunchKernelGGL(k_raster_bwd_bf16, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
+                         (const int*)b.num_items, (const int2*)b.pairs, (const float4*)g.rec, (const uint4*)U, partials,
+                         g_depth != nullptr ? 1 : 0);
+    else
+      hipLaunchKernelGGL(k_raster_bwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
+                         (const int*)b.num_items, (const int2*)b.pairs, (const float4*)g.rec, (const float*)U, partials,
+                         g_depth != nullptr ? 1 : 0);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_BWD, s);
   }
