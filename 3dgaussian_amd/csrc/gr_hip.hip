@@ -132,7 +132,57 @@ __device__ __forceinline__ void project(const ViewK& v, float x, float y, float 
   o.sy = o.syr < 1.0f ? 1.0f : o.syr;
 }
 
-// Colour before clamp (torch_renderer.py:86-106).
+// Degree-3 extension of the reference's direction basis (torch_renderer.py:94-106 has degree 1:
+// col = k0 + k1 x + k2 y + k3 z with d = (x, y, z) the unit view direction).  The basis is the real
+// spherical-harmonic polynomials up to degree 3 without normalisation constants, continuing the
+// reference's unnormalised degree-1 terms: 1 | x y z | xy yz 3z^2-1 xz x^2-y^2 | y(3x^2-y^2) xyz
+// y(5z^2-1) z(5z^2-3) x(5z^2-1) z(x^2-y^2) x(x^2-3y^2).  With the degree-2/3 coefficients zero it is
+// the reference's degree-1 colour (same float operations for the first four terms).
+template <typename F>
+__host__ __device__ __forceinline__ void sh3_basis(F x, F y, F z, F (&Y)[16]) {
+  Y[0] = F(1);
+  Y[1] = x;
+  Y[2] = y;
+  Y[3] = z;
+  Y[4] = x * y;
+  Y[5] = y * z;
+  Y[6] = F(3) * z * z - F(1);
+  Y[7] = x * z;
+  Y[8] = x * x - y * y;
+  Y[9] = y * (F(3) * x * x - y * y);
+  Y[10] = x * y * z;
+  Y[11] = y * (F(5) * z * z - F(1));
+  Y[12] = z * (F(5) * z * z - F(3));
+  Y[13] = x * (F(5) * z * z - F(1));
+  Y[14] = z * (x * x - y * y);
+  Y[15] = x * (x * x - F(3) * y * y);
+}
+// d Y_i / d(x, y, z)
+template <typename F>
+__host__ __device__ __forceinline__ void sh3_basis_grad(F x, F y, F z, F (&G)[16][3]) {
+  const F xx = x * x, yy = y * y, zz = z * z;
+  const F g[16][3] = {{0, 0, 0},
+                      {1, 0, 0},
+                      {0, 1, 0},
+                      {0, 0, 1},
+                      {y, x, 0},
+                      {0, z, y},
+                      {0, 0, F(6) * z},
+                      {z, 0, x},
+                      {F(2) * x, F(-2) * y, 0},
+                      {F(6) * x * y, F(3) * xx - F(3) * yy, 0},
+                      {y * z, x * z, x * y},
+                      {0, F(5) * zz - F(1), F(10) * y * z},
+                      {0, 0, F(15) * zz - F(3)},
+                      {F(5) * zz - F(1), 0, F(10) * x * z},
+                      {F(2) * x * z, F(-2) * y * z, xx - yy},
+                      {F(3) * xx - F(3) * yy, F(-6) * x * y, 0}};
+  for (int i = 0; i < 16; ++i)
+    for (int j = 0; j < 3; ++j) G[i][j] = g[i][j];
+}
+
+// Colour before clamp (torch_renderer.py:86-106): RGB (CD = 3), the reference's degree-1 basis
+// (CD = 12) or its degree-3 extension (CD = 48).
 template <int CD>
 __device__ __forceinline__ void eval_color(const ViewK& v, float mx, float my, float mz, const float* col, float out[3]) {
   if constexpr (CD == 3) {
@@ -147,6 +197,14 @@ __device__ __forceinline__ void eval_color(const ViewK& v, float mx, float my, f
     d2 /= nrm;
 #pragma unroll
     for (int k = 0; k < 3; ++k) out[k] = ((col[k] + col[3 + k] * d0) + col[6 + k] * d1) + col[9 + k] * d2;
+    if constexpr (CD == 48) {
+      float Y[16];
+      sh3_basis(d0, d1, d2, Y);
+#pragma unroll
+      for (int i = 4; i < 16; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) out[k] += col[3 * i + k] * Y[i];
+    }
   }
 }
 
@@ -1674,14 +1732,28 @@ __device__ void chain_rule(const ViewK& v, int i, const double* S, unsigned cnt,
     const double ne = nn + 1e-8;
     const double d[3] = {vv[0] / ne, vv[1] / ne, vv[2] / ne};
     double gd[3] = {0.0, 0.0, 0.0};
+    if constexpr (CD == 12) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      dc[k] = (float)dcol[k];
+      for (int k = 0; k < 3; ++k) {
+        dc[k] = (float)dcol[k];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        dc[(1 + j) * 3 + k] = (float)(dcol[k] * d[j]);
-        gd[j] += dcol[k] * (double)col[(1 + j) * 3 + k];
+        for (int j = 0; j < 3; ++j) {
+          dc[(1 + j) * 3 + k] = (float)(dcol[k] * d[j]);
+          gd[j] += dcol[k] * (double)col[(1 + j) * 3 + k];
+        }
       }
+    } else {  // degree 3: d col / d k_i = Y_i(d), d col / d d = sum_i k_i dY_i/dd
+      double Y[16], G[16][3];
+      sh3_basis(d[0], d[1], d[2], Y);
+      sh3_basis_grad(d[0], d[1], d[2], G);
+      for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          dc[3 * i + k] = (float)(dcol[k] * Y[i]);
+          const double t = dcol[k] * (double)col[3 * i + k];
+#pragma unroll
+          for (int j = 0; j < 3; ++j) gd[j] += t * G[i][j];
+        }
     }
     if (nn > 0.0) {
       const double vg = vv[0] * gd[0] + vv[1] * gd[1] + vv[2] * gd[2];
@@ -2047,7 +2119,8 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
   if (n < 0) return set_error(GR_ERR_INVALID_ARGUMENT, "n must be >= 0");
-  if (color_dim != 3 && color_dim != 12) return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3)");
+  if (color_dim != 3 && color_dim != 12 && color_dim != 48)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");
   if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
   if (n == 0) {
     plan->num_pairs = 0;
@@ -2062,8 +2135,10 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
   Geom g = geom_view(geom, n);
   if (color_dim == 3)
     hipLaunchKernelGGL(k_preprocess<3>, dim3(blocks_for(n + 1)), dim3(256), 0, s, vk, n, means, scales, colors, opacities, g);
-  else
+  else if (color_dim == 12)
     hipLaunchKernelGGL(k_preprocess<12>, dim3(blocks_for(n + 1)), dim3(256), 0, s, vk, n, means, scales, colors, opacities, g);
+  else
+    hipLaunchKernelGGL(k_preprocess<48>, dim3(blocks_for(n + 1)), dim3(256), 0, s, vk, n, means, scales, colors, opacities, g);
   GR_HIP_TRY(hipGetLastError());
   size_t tmp = scan_tmp_bytes(n);
   GR_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(g.scan_tmp, tmp, g.counts, g.offsets, n + 1, s));
@@ -2205,7 +2280,8 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
   if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
-  if (color_dim != 3 && color_dim != 12) return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3)");
+  if (color_dim != 3 && color_dim != 12 && color_dim != 48)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");
   if (n == 0) return GR_OK;
   if (!g_rgb || !saved || !geom || !bins || !d_means || !d_scales || !d_colors || !d_opacities)
     return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
@@ -2243,8 +2319,12 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
     hipLaunchKernelGGL(k_reduce_bwd<3>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
                        (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
                        d_opacities, g_depth != nullptr ? 1 : 0);
-  else
+  else if (color_dim == 12)
     hipLaunchKernelGGL(k_reduce_bwd<12>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
+                       (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
+                       d_opacities, g_depth != nullptr ? 1 : 0);
+  else
+    hipLaunchKernelGGL(k_reduce_bwd<48>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
                        (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
                        d_opacities, g_depth != nullptr ? 1 : 0);
   GR_HIP_TRY(hipGetLastError());

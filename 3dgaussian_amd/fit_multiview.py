@@ -48,13 +48,15 @@ FUSED_LOSS = os.environ.get("GR_FUSED_LOSS", "1") != "0"  # losses.l1_loss for t
 # ------------------------------------------------------------------------------------------------
 # Parameters (fit_multiview_stub.py:114-137) — CPU RNG, then moved to the device.
 # ------------------------------------------------------------------------------------------------
-def build_params(n: int, device: torch.device, use_sh: bool) -> dict:
+def build_params(n: int, device: torch.device, use_sh: bool, sh_degree: int = 1) -> dict:
+    """sh_degree 3 (extension, config C3): (N,16,3) coefficients, the degree-1 init of the stub plus
+    zero degree-2/3 terms."""
     means = (torch.rand((n, 3)) - 0.5) * 1.2
     scales_raw = torch.full((n, 3), -2.2)
     opacities_raw = torch.full((n,), -2.2)
     params = {"means": means, "scales_raw": scales_raw, "opacities_raw": opacities_raw}
     if use_sh:
-        sh = torch.zeros((n, 4, 3))
+        sh = torch.zeros((n, 16 if sh_degree == 3 else 4, 3))
         sh[:, 0, :] = 0.1 * torch.rand((n, 3))
         params["sh_raw"] = sh
     else:
@@ -262,6 +264,7 @@ def main(argv=None) -> None:
     ap.add_argument("--num_gaussians", type=int, default=800)
     ap.add_argument("--max_gaussians", type=int, default=3000)
     ap.add_argument("--use_sh", action="store_true")
+    ap.add_argument("--sh_degree", type=int, default=1, choices=(1, 3), help="with --use_sh: 1 (reference) or 3 (extension)")
     ap.add_argument("--densify_interval", type=int, default=80)
     ap.add_argument("--prune_interval", type=int, default=80)
     ap.add_argument("--densify_ratio", type=float, default=0.15)
@@ -315,7 +318,7 @@ def main(argv=None) -> None:
     else:
         cams = orbit_cameras(len(targets), args.width, args.height, device)
 
-    params = build_params(args.num_gaussians, device, args.use_sh)
+    params = build_params(args.num_gaussians, device, args.use_sh, args.sh_degree)
     fitter = ViewShardedFitter(params, cams, targets, args.width, args.height, lr=args.lr, masks=masks, depths=depths,
                                silhouette_weight=args.silhouette_weight, depth_weight=args.depth_weight,
                                reg_opacity=args.reg_opacity, reg_scale=args.reg_scale)

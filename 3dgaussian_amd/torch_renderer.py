@@ -135,6 +135,13 @@ def make_view(view, proj, width: int, height: int, background=None, cutoff: floa
     return gv
 
 
+def _color_dim(colors: torch.Tensor) -> int:
+    """gr_hip.h color_dim: 3 (RGB), 12 (the reference's degree-1 basis, (N,4,3)) or 48 (the degree-3
+    extension, (N,16,3): unnormalised real spherical-harmonic polynomials continuing the reference's
+    degree-1 terms)."""
+    return 3 if colors.dim() == 2 else 3 * int(colors.shape[1])
+
+
 def _stream(device: torch.device) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
@@ -177,7 +184,7 @@ def prepare_native(means, scales, colors, opacities, gv: _native.GrView) -> Prep
     L = _native.lib()
     dev = means.device
     n = int(means.shape[0])
-    cd = 3 if colors.dim() == 2 else 12
+    cd = _color_dim(colors)
     geom = torch.empty((int(L.gr_geom_bytes(n)),), dtype=torch.uint8, device=dev)
     plan_host = torch.zeros(3, dtype=torch.int64, pin_memory=True)  # gr_plan {num_pairs, num_slots, num_core_pairs}
     _native.check(L.gr_fwd_prepare_async(ctypes.byref(gv), n, _native.ptr(means), _native.ptr(scales),
@@ -221,7 +228,7 @@ def backward_native(means, scales, colors, opacities, st: RenderState, g_out, g_
     """Run gr_bwd.  Returns (d_means, d_scales, d_colors, d_opacities)."""
     L = _native.lib()
     dev = means.device
-    cd = 3 if colors.dim() == 2 else 12
+    cd = _color_dim(colors)
     ws = torch.empty((int(L.gr_bwd_bytes(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan))),), dtype=torch.uint8, device=dev)
     dm = torch.empty_like(means)
     ds = torch.empty_like(scales)
@@ -304,7 +311,7 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
 def render_gaussians_torch(
     means: torch.Tensor,  # (N,3) float32
     scales: torch.Tensor,  # (N,3) float32
-    colors: torch.Tensor,  # (N,3) or SH coeffs (N,4,3)
+    colors: torch.Tensor,  # (N,3) or SH coeffs (N,4,3); extension: degree-3 coefficients (N,16,3)
     opacities: torch.Tensor,  # (N,)  float32
     camera: Camera,
     width: int,
@@ -334,7 +341,7 @@ def render_gaussians_torch(
         return torch.zeros((height, width, 3), dtype=torch.float32, device=means.device)
     if n > max_gaussians:
         raise ValueError(f"N={n} too large for torch reference renderer. Increase max_gaussians or downsample.")
-    if not ((colors.ndim == 2 and colors.shape[1] == 3) or (colors.ndim == 3 and colors.shape[1] == 4 and colors.shape[2] == 3)):
+    if not ((colors.ndim == 2 and colors.shape[1] == 3) or (colors.ndim == 3 and colors.shape[1] in (4, 16) and colors.shape[2] == 3)):
         raise ValueError("colors must be (N,3) or SH coeffs (N,4,3)")
 
     out, alpha, depth = rasterize(means, scales, colors, opacities, camera.view, camera.proj, width, height,

@@ -79,7 +79,8 @@ typedef struct gr_view {
 
 /* ------------------------------------------------------------------------------------------ */
 /* Differentiable path (device pointers).                                                     */
-/*   means (N,3), scales (N,3), colors (N,3) [color_dim 3] or SH deg-1 (N,4,3) [color_dim 12], */
+/*   means (N,3), scales (N,3), colors (N,3) [color_dim 3] or SH deg-1 (N,4,3) [color_dim 12]   */
+/*   (extension: degree-3 coefficients (N,16,3) [color_dim 48], basis in DESIGN.md §2),           */
 /*   opacities (N,), all float32 contiguous.                                                   */
 /* ------------------------------------------------------------------------------------------ */
 
@@ -129,7 +130,7 @@ size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan);
 
 /* Backward of gr_fwd_render.  g_rgb (H,W,3) required; g_alpha, g_depth may be NULL (zero).
  * Writes (overwrites) d_means (N,3), d_scales (N,3) (column 2 is always 0),
- * d_colors (N,3) or (N,4,3), d_opacities (N,). */
+ * d_colors (N,3), (N,4,3) or (N,16,3), d_opacities (N,). */
 gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* means,
                  const float* scales, const float* colors, int color_dim, const float* opacities,
                  const void* geom, const void* bins, const float* saved, const float* g_rgb,

@@ -122,6 +122,8 @@ def color_dim(colors: np.ndarray) -> int:
         return 3
     if colors.ndim == 3 and colors.shape[1:] == (4, 3):
         return 12
+    if colors.ndim == 3 and colors.shape[1:] == (16, 3):  # degree-3 extension (build only)
+        return 48
     raise ValueError("colors must be (N,3) or SH coeffs (N,4,3)")
 
 
