@@ -417,7 +417,13 @@ inline TSortPlan tsort_plan(int64_t K, int tiles) {
   p.waves = tsort_waves(tiles);
   int64_t pw = 2048 * GR_TSORT_NSEG;
   const int64_t kk = K > 0 ? K : 1;
-  while ((int64_t)tiles * ((kk + pw * p.waves - 1) / (pw * p.waves)) > (1ll << 28)) pw *= 2;
+  // Wider columns (more 2048-pair segments per wave) while the count matrix would outweigh half the
+  // keys and there are columns to spare: at many tiles (1080p: 8160) and many pairs the matrices
+  // (M and its scan, tiles x columns ints, each read and written) otherwise dominate the sort.
+  auto cols_of = [&](int64_t w) { return (kk + w * p.waves - 1) / (w * p.waves); };
+  while ((int64_t)tiles * cols_of(pw) > (1ll << 28) ||
+         ((int64_t)tiles * cols_of(pw) > kk / 2 && cols_of(2 * pw) >= 1024))
+    pw *= 2;
   p.cw = (int)(pw * p.waves);
   p.cols = (int)((kk + p.cw - 1) / p.cw);
   p.cells = (size_t)tiles * p.cols;

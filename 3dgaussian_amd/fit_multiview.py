@@ -42,6 +42,7 @@ else:
     from . import torch_renderer as tr
 
 RenderFn = Callable[..., tuple]
+DEVICE_DENSIFY_MIN = 100_000  # Gaussians from which densify/prune runs on the device (C5 scale)
 FUSED_LOSS = os.environ.get("GR_FUSED_LOSS", "1") != "0"  # losses.l1_loss for the L1 terms (A/B switch)
 
 
@@ -109,6 +110,39 @@ def densify_and_prune(params: dict, max_gaussians: int, densify_ratio: float, pr
     return {k: torch.nn.Parameter(v.to(device)) for k, v in out.items()}
 
 
+def densify_and_prune_device(params: dict, max_gaussians: int, densify_ratio: float, prune_opacity: float,
+                             generator: torch.Generator) -> dict:
+    """The same rule as densify_and_prune (fit_multiview_stub.py:140-197) evaluated on the device, for
+    fits at scale (config C5: millions of Gaussians), with the jitter drawn from a device generator:
+    no host round trip of the parameters.  Same keep / top-k / jitter / -0.1 opacity / colour
+    duplication; only the random stream differs from the stub's CPU one."""
+    with torch.no_grad():
+        means, scales_raw, op_raw = params["means"].detach(), params["scales_raw"].detach(), params["opacities_raw"].detach()
+        key = "sh_raw" if "sh_raw" in params else "colors_raw"
+        col = params[key].detach()
+        op = torch.sigmoid(op_raw)
+        keep = op > prune_opacity
+        if int(keep.sum()) < 64:
+            top_keep = torch.topk(op, k=min(64, op.shape[0]), largest=True).indices
+            keep = torch.zeros_like(keep, dtype=torch.bool)
+            keep[top_keep] = True
+        means, scales_raw, op_raw, col = means[keep], scales_raw[keep], op_raw[keep], col[keep]
+        n = means.shape[0]
+        room = max(0, max_gaussians - n)
+        add_n = min(room, max(0, int(n * densify_ratio)))
+        if add_n > 0 and n > 0:
+            idx = torch.topk(torch.sigmoid(op_raw), k=min(n, add_n), largest=True).indices
+            scales = torch.nn.functional.softplus(scales_raw[idx]) + 1e-3
+            jitter = 0.25 * scales * torch.randn(means[idx].shape, generator=generator, device=means.device,
+                                                 dtype=means.dtype)
+            means = torch.cat([means, means[idx] + jitter], dim=0)
+            scales_raw = torch.cat([scales_raw, scales_raw[idx]], dim=0)
+            col = torch.cat([col, col[idx]], dim=0)
+            op_raw = torch.cat([op_raw, op_raw[idx] - 0.1], dim=0)
+        out = {"means": means, "scales_raw": scales_raw, "opacities_raw": op_raw, key: col}
+    return {k: torch.nn.Parameter(v.contiguous()) for k, v in out.items()}
+
+
 def hip_render(means, scales, colors, opacities, cam, width, height, background, prepared=None):
     return tr.render_gaussians_torch(means, scales, colors, opacities, cam, width=width, height=height,
                                      background=background, max_gaussians=max(10000, int(means.shape[0])), return_aux=True,
@@ -134,6 +168,7 @@ class ViewShardedFitter:
         self.world = dist.get_world_size(group) if self.distributed else 1
         self.my_views = list(range(self.rank, len(targets), self.world))
         self.opt = torch.optim.Adam(list(self.params.values()), lr=lr)
+        self.densify_seed = 1234
 
     def reset_optimizer(self) -> None:
         self.opt = torch.optim.Adam(list(self.params.values()), lr=self.lr)
@@ -206,11 +241,25 @@ class ViewShardedFitter:
         self.opt.step()
         return loss_all
 
-    def densify_and_prune(self, max_gaussians: int, densify_ratio: float, prune_opacity: float) -> None:
+    def densify_and_prune(self, max_gaussians: int, densify_ratio: float, prune_opacity: float,
+                          on_device: Optional[bool] = None) -> None:
+        """on_device (default: N >= DEVICE_DENSIFY_MIN): the device-side rule with a device generator
+        (densify_and_prune_device); otherwise the host rule with the stub's CPU random stream."""
+        n_now = int(self.params["means"].shape[0])
+        if on_device is None:
+            on_device = self.params["means"].device.type == "cuda" and n_now >= DEVICE_DENSIFY_MIN
+        if on_device and getattr(self, "_dgen", None) is None:
+            self._dgen = torch.Generator(device=self.params["means"].device).manual_seed(self.densify_seed)
+
+        def decide():
+            if on_device:
+                return densify_and_prune_device(self.params, max_gaussians, densify_ratio, prune_opacity, self._dgen)
+            return densify_and_prune(self.params, max_gaussians, densify_ratio, prune_opacity)
+
         if self.world > 1:
-            # rank 0 decides (host RNG), everyone receives the new tensors
+            # rank 0 decides, everyone receives the new tensors
             if self.rank == 0:
-                newp = densify_and_prune(self.params, max_gaussians, densify_ratio, prune_opacity)
+                newp = decide()
                 n = torch.tensor([newp["means"].shape[0]], device=self.params["means"].device)
             else:
                 n = torch.zeros(1, dtype=torch.int64, device=self.params["means"].device)
@@ -222,7 +271,7 @@ class ViewShardedFitter:
                 dist.broadcast(newp[k].data, 0, group=self.group)
             self.params = newp
         else:
-            self.params = densify_and_prune(self.params, max_gaussians, densify_ratio, prune_opacity)
+            self.params = decide()
         self.reset_optimizer()
 
 
