@@ -143,6 +143,38 @@ def densify_and_prune_device(params: dict, max_gaussians: int, densify_ratio: fl
     return {k: torch.nn.Parameter(v.contiguous()) for k, v in out.items()}
 
 
+def _spread3(v: torch.Tensor) -> torch.Tensor:
+    """Bits 0..9 of v moved to bits 0, 3, 6, .. 27 (Morton interleave of one axis)."""
+    v = (v | (v << 16)) & 0x030000FF
+    v = (v | (v << 8)) & 0x0300F00F
+    v = (v | (v << 4)) & 0x030C30C3
+    return (v | (v << 2)) & 0x09249249
+
+
+def morton_order(means: torch.Tensor) -> torch.Tensor:
+    """Permutation that puts the Gaussians in 3-D Morton (Z-curve) order of their centres, 10 bits per
+    axis over the bounding box; stable, so every rank computes the same permutation from the same
+    means.  Neighbours in this order are neighbours in space, hence on screen in every view: the
+    pairs one wave emits land in few tiles (the tile sort writes runs instead of scattered 8-byte
+    pairs) and a tile's records are gathered from few cache lines."""
+    with torch.no_grad():
+        m = means.detach()
+        lo = m.amin(0)
+        ext = (m.amax(0) - lo).clamp_min(1e-20)
+        q = ((m - lo) / ext * 1023.0).round().to(torch.int64).clamp_(0, 1023)
+        key = _spread3(q[:, 0]) | (_spread3(q[:, 1]) << 1) | (_spread3(q[:, 2]) << 2)
+        return torch.argsort(key, stable=True)
+
+
+def spatial_order(params: dict) -> dict:
+    """The same Gaussians, permuted into morton_order (a layout choice of the trainer: the rendered
+    images and the loss do not depend on the order of the Gaussians beyond float summation order)."""
+    if params["means"].shape[0] < 2:
+        return params
+    perm = morton_order(params["means"])
+    return {k: torch.nn.Parameter(v.detach()[perm].contiguous()) for k, v in params.items()}
+
+
 def hip_render(means, scales, colors, opacities, cam, width, height, background, prepared=None):
     return tr.render_gaussians_torch(means, scales, colors, opacities, cam, width=width, height=height,
                                      background=background, max_gaussians=max(10000, int(means.shape[0])), return_aux=True,
@@ -155,8 +187,11 @@ class ViewShardedFitter:
     def __init__(self, params: dict, cams: list, targets: list, width: int, height: int, lr: float = 0.02,
                  masks: Optional[list] = None, depths: Optional[list] = None, silhouette_weight: float = 0.2,
                  depth_weight: float = 0.05, reg_opacity: float = 1e-3, reg_scale: float = 1e-3,
-                 render_fn: RenderFn = hip_render, group=None):
-        self.params = params
+                 render_fn: RenderFn = hip_render, group=None, reorder: bool = True):
+        # reorder: keep the Gaussians in spatial (Morton) order, re-established after every
+        # densify/prune (spatial_order); off only to compare with an unpermuted run
+        self.reorder = reorder
+        self.params = spatial_order(params) if reorder else params
         self.cams, self.targets, self.masks, self.depths = cams, targets, masks, depths
         self.width, self.height, self.lr = width, height, lr
         self.w_sil, self.w_depth = silhouette_weight, depth_weight
@@ -253,8 +288,10 @@ class ViewShardedFitter:
 
         def decide():
             if on_device:
-                return densify_and_prune_device(self.params, max_gaussians, densify_ratio, prune_opacity, self._dgen)
-            return densify_and_prune(self.params, max_gaussians, densify_ratio, prune_opacity)
+                newp = densify_and_prune_device(self.params, max_gaussians, densify_ratio, prune_opacity, self._dgen)
+            else:
+                newp = densify_and_prune(self.params, max_gaussians, densify_ratio, prune_opacity)
+            return spatial_order(newp) if self.reorder else newp
 
         if self.world > 1:
             # rank 0 decides, everyone receives the new tensors

@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--views", type=int, default=50)
     ap.add_argument("--res", type=int, default=800)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-reorder", action="store_true",
+                    help="keep the synthetic Gaussians in their random order (A/B of the trainer's Morton order)")
     return ap.parse_args()
 
 
@@ -116,7 +118,7 @@ def main():
     g = torch.Generator(device=device).manual_seed(1)
     targets = [torch.rand((R, R, 3), generator=g, device=device) for _ in range(V)]
     masks = [(t.mean(dim=2) > 0.5).to(torch.float32) for t in targets]
-    fitter = fm.ViewShardedFitter(params, cams, targets, R, R, lr=0.02, masks=masks)
+    fitter = fm.ViewShardedFitter(params, cams, targets, R, R, lr=0.02, masks=masks, reorder=not args.no_reorder)
 
     for _ in range(args.warmup):
         fitter.step()
@@ -179,7 +181,8 @@ def main():
                        "core_cutoff_sigma": tr.DEFAULT_CORE_CUTOFF,
                        "scale": round(0.1061 * (1200.0 / n) ** (1.0 / 3.0), 5), "seed": 0,
                        "parallelism": f"view-sharded dp{world}", "pairs_per_view": int(avg_pairs),
-                       "core_pairs_per_view": int(avg_core)},
+                       "core_pairs_per_view": int(avg_core),
+                       "gaussian_order": "random" if args.no_reorder else "morton (trainer layout, fit_multiview.spatial_order)"},
             # achieved = algorithmic (f32-accurate contraction) FLOP/s of the backward splat against the
             # native f32 MFMA peak; the bf16-split kernel's executed MFMA rate is reported beside it
             "roofline": {"bound": "mfma", "kernel": BWD_KERNEL, "achieved": round(achieved, 2),
