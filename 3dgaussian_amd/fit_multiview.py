@@ -190,8 +190,14 @@ class ViewShardedFitter:
                  render_fn: RenderFn = hip_render, group=None, reorder: bool = True):
         # reorder: keep the Gaussians in spatial (Morton) order, re-established after every
         # densify/prune (spatial_order); off only to compare with an unpermuted run
+        # perm: self.params[k][i] = canonical[k][perm[i]], the canonical order being the stub's (the
+        # order densify_and_prune and gaussians_fitted.npz see: top-k ties and jitter draws follow it)
         self.reorder = reorder
-        self.params = spatial_order(params) if reorder else params
+        self.perm = None
+        if reorder and params["means"].shape[0] >= 2:
+            self.perm = morton_order(params["means"])
+            params = {k: torch.nn.Parameter(v.detach()[self.perm].contiguous()) for k, v in params.items()}
+        self.params = params
         self.cams, self.targets, self.masks, self.depths = cams, targets, masks, depths
         self.width, self.height, self.lr = width, height, lr
         self.w_sil, self.w_depth = silhouette_weight, depth_weight
@@ -204,6 +210,17 @@ class ViewShardedFitter:
         self.my_views = list(range(self.rank, len(targets), self.world))
         self.opt = torch.optim.Adam(list(self.params.values()), lr=lr)
         self.densify_seed = 1234
+
+    def canonical_params(self) -> dict:
+        """The parameters in the stub's order (undoes the trainer's Morton permutation)."""
+        if self.perm is None:
+            return self.params
+        out = {}
+        for k, v in self.params.items():
+            c = torch.empty_like(v.detach())
+            c[self.perm] = v.detach()
+            out[k] = torch.nn.Parameter(c)
+        return out
 
     def reset_optimizer(self) -> None:
         self.opt = torch.optim.Adam(list(self.params.values()), lr=self.lr)
@@ -287,28 +304,38 @@ class ViewShardedFitter:
             self._dgen = torch.Generator(device=self.params["means"].device).manual_seed(self.densify_seed)
 
         def decide():
+            base = self.canonical_params()
             if on_device:
-                newp = densify_and_prune_device(self.params, max_gaussians, densify_ratio, prune_opacity, self._dgen)
+                newp = densify_and_prune_device(base, max_gaussians, densify_ratio, prune_opacity, self._dgen)
             else:
-                newp = densify_and_prune(self.params, max_gaussians, densify_ratio, prune_opacity)
-            return spatial_order(newp) if self.reorder else newp
+                newp = densify_and_prune(base, max_gaussians, densify_ratio, prune_opacity)
+            perm = None
+            if self.reorder and newp["means"].shape[0] >= 2:
+                perm = morton_order(newp["means"])
+                newp = {k: torch.nn.Parameter(v.detach()[perm].contiguous()) for k, v in newp.items()}
+            return newp, perm
 
         if self.world > 1:
             # rank 0 decides, everyone receives the new tensors
+            dev = self.params["means"].device
             if self.rank == 0:
-                newp = decide()
-                n = torch.tensor([newp["means"].shape[0]], device=self.params["means"].device)
+                newp, perm = decide()
+                n = torch.tensor([newp["means"].shape[0], int(perm is not None)], device=dev)
             else:
-                n = torch.zeros(1, dtype=torch.int64, device=self.params["means"].device)
+                n = torch.zeros(2, dtype=torch.int64, device=dev)
             dist.broadcast(n, 0, group=self.group)
+            n_new, has_perm = int(n[0].item()), bool(n[1].item())
             if self.rank != 0:
-                newp = {k: torch.nn.Parameter(torch.empty((int(n.item()),) + tuple(v.shape[1:]), device=v.device))
+                newp = {k: torch.nn.Parameter(torch.empty((n_new,) + tuple(v.shape[1:]), device=v.device))
                         for k, v in self.params.items()}
+                perm = torch.empty(n_new, dtype=torch.int64, device=dev) if has_perm else None
             for k in sorted(newp):
                 dist.broadcast(newp[k].data, 0, group=self.group)
-            self.params = newp
+            if has_perm:
+                dist.broadcast(perm, 0, group=self.group)
+            self.params, self.perm = newp, perm
         else:
-            self.params = decide()
+            self.params, self.perm = decide()
         self.reset_optimizer()
 
 
@@ -430,7 +457,7 @@ def save_outputs(fitter: ViewShardedFitter, cams, args, out_dir: Path, loss_log)
     from PIL import Image
 
     out_dir.mkdir(parents=True, exist_ok=True)
-    p = fitter.params
+    p = fitter.canonical_params()
     means = p["means"]
     scales = torch.nn.functional.softplus(p["scales_raw"]) + 1e-3
     opacities = torch.sigmoid(p["opacities_raw"])

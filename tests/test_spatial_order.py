@@ -64,3 +64,29 @@ def test_fit_loss_independent_of_order():
     assert abs(la - lb) <= 1e-6 * max(1.0, abs(la))
     for k in params:
         torch.testing.assert_close(a.params[k].detach()[perm], b.params[k].detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_densify_sees_the_stub_order():
+    """The trainer's permutation is invisible to densify/prune and to gaussians_fitted.npz: densify runs
+    on canonical_params() (the stub's order, so top-k ties and jitter draws match the stub) and the
+    result is re-permuted."""
+    torch.manual_seed(11)
+    params = fm.build_params(200, torch.device("cpu"), use_sh=False)
+    with torch.no_grad():  # many exact ties in opacity, as after a few Adam steps
+        params["opacities_raw"].copy_(-2.2 + 0.02 * torch.randint(-2, 3, (200,)).float())
+    W, H = 16, 12
+    cams = fm.orbit_cameras(2, W, H, torch.device("cpu"))
+    targets = [torch.zeros((H, W, 3)) for _ in range(2)]
+    f = fm.ViewShardedFitter({k: torch.nn.Parameter(v.detach().clone()) for k, v in params.items()}, cams, targets, W, H,
+                             reorder=True)
+    canon = f.canonical_params()
+    for k in params:
+        assert torch.equal(canon[k].detach(), params[k].detach())
+    torch.manual_seed(5)
+    ref = fm.densify_and_prune({k: torch.nn.Parameter(v.detach().clone()) for k, v in params.items()}, 400, 0.15, 0.05)
+    torch.manual_seed(5)
+    f.densify_and_prune(400, 0.15, 0.05, on_device=False)
+    got = f.canonical_params()
+    for k in ref:
+        assert torch.equal(got[k].detach(), ref[k].detach()), k
+    assert torch.equal(torch.sort(f.perm).values, torch.arange(ref["means"].shape[0]))
