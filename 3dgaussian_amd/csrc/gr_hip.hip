@@ -334,7 +334,10 @@ Geom geom_view(void* base, int n) {
 // ------------------------------------------------------------------------------------------------
 // Bins buffer layout.
 // ------------------------------------------------------------------------------------------------
-constexpr int CH = 1024;  // Gaussians per raster work item (one chunk of one tile's list)
+#ifndef GR_CH
+#define GR_CH 1024
+#endif
+constexpr int CH = GR_CH;  // Gaussians per raster work item (one chunk of one tile's list)
 constexpr int NPART = 9;  // backward partial sums per (Gaussian, tile) pair
 
 // Virtual tiles up to which the pairs are grouped by the stable counting sort (16-bit keys; see
@@ -1124,7 +1127,12 @@ constexpr int UL = 5 * 2 * TP;  // floats of backward operands per tile (k_pixel
 constexpr int UF_FRAGS = 2 * 3 * 3 * 64;  // uint4 per tile
 // channel pairs on the 32 MFMA rows (16 per channel): (dC_r, dC_g), (dC_b, -), (dW, dD); tail items
 // (depth-coupled terms only) need just the last pair
-__device__ __forceinline__ int pair_channel(int pr, int c) { return pr == 0 ? c : (pr == 1 ? (c == 0 ? 2 : -1) : 3 + c); }
+// Without an upstream depth gradient dD is identically zero, so the four live channels fill two pairs:
+// (dC_r, dC_g), (dC_b, dW) and the third pair is never contracted (two thirds of the MFMA work).
+__device__ __forceinline__ int pair_channel(int pr, int c, bool depth) {
+  if (!depth) return pr == 0 ? c : (pr == 1 ? 2 + c : -1);
+  return pr == 0 ? c : (pr == 1 ? (c == 0 ? 2 : -1) : 3 + c);
+}
 // contracted coordinate of k-slot 8h + j of the 32x32x16 operands: the 8 pixels a lane half h owns,
 // {4h..4h+3, 8+4h..8+4h+3}, which are also the output rows that lane half holds (C map, row =
 // (reg&3) + 8 (reg>>2) + 4h): one set of exponentials per lane serves both contractions.
@@ -1189,9 +1197,11 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
     for (int k = 0; k < 5; ++k) sU[k][tid] = u[k];
     __syncthreads();
     uint4* fr = reinterpret_cast<uint4*>(UF) + (size_t)tile * UF_FRAGS;
+    const bool depth = g_depth != nullptr;
     for (int cmb = tid; cmb < 2 * 3 * 64; cmb += 256) {
       const int side = cmb / 192, pr = (cmb / 64) % 3, l = cmb & 63;
-      const int r = l & 31, h = l >> 5, ch = pair_channel(pr, r >> 4), i = r & 15;
+      if (!depth && pr == 2) continue;  // never read
+      const int r = l & 31, h = l >> 5, ch = pair_channel(pr, r >> 4, depth), i = r & 15;
       float hi[8], mid[8], lo[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -1429,12 +1439,14 @@ __device__ __forceinline__ void split_frag(const float (&v)[8], s16x8 (&f)[3]) {
   f[2] = as_frag(make_uint4(pack_bf16(lo[0], lo[1]), pack_bf16(lo[2], lo[3]), pack_bf16(lo[4], lo[5]), pack_bf16(lo[6], lo[7])));
 }
 
-template <bool TAIL>
+template <bool TAIL, bool DEPTH>
 __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, int wave, int tx, int ty,
                                               const int2* __restrict__ pairs, const float4* __restrict__ rec,
                                               float* __restrict__ partials, float4 (*sA)[TP], float4 (*sB)[TP],
                                               float (*sZ)[TP], int (*sSlot)[TP], const uint4* sUF) {
-  constexpr int P0 = TAIL ? 2 : 0;  // first channel pair contracted
+  static_assert(DEPTH || !TAIL, "tail items carry only depth-coupled terms");
+  constexpr int P0 = TAIL ? 2 : 0;      // first channel pair contracted
+  constexpr int P1 = DEPTH ? 3 : 2;     // one past the last (pair_channel)
   const int lane = tid & 63, r = lane & 31, h = lane >> 5;
   // pixel centres of the lane's 8 contraction slots (x for T, y for R): base + compile-time offset
   const float pxb = (float)(tx * T + 4 * h) + 0.5f, pyb = (float)(ty * T + 4 * h) + 0.5f;
@@ -1478,26 +1490,33 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
       split_frag(ey, BR);
       f32x16 DT[3], DR[3];
 #pragma unroll
-      for (int pr = P0; pr < 3; ++pr) DT[pr] = mfma_split(sUF + (0 * 3 + pr) * 3 * 64, lane, BT);
+      for (int pr = P0; pr < P1; ++pr) DT[pr] = mfma_split(sUF + (0 * 3 + pr) * 3 * 64, lane, BT);
 #pragma unroll
-      for (int pr = P0; pr < 3; ++pr) DR[pr] = mfma_split(sUF + (1 * 3 + pr) * 3 * 64, lane, BR);
+      for (int pr = P0; pr < P1; ++pr) DR[pr] = mfma_split(sUF + (1 * 3 + pr) * 3 * 64, lane, BR);
       float S[NPART] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       // T: rows y = kslot_pixel(h, q) of channels pair_channel(pr, c) at register 8c + q
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const float dy = PY0(q) - a.y;
-        const float T3 = DT[2][q], T4 = DT[2][8 + q];
         float GT;
-        if constexpr (TAIL) {
+        if constexpr (!DEPTH) {  // T4 = 0
+          const float T0 = DT[0][q], T1 = DT[0][8 + q], T2 = DT[1][q], T3 = DT[1][8 + q];
+          S[0] = fmaf(ey[q], T0, S[0]);
+          S[1] = fmaf(ey[q], T1, S[1]);
+          S[2] = fmaf(ey[q], T2, S[2]);
+          GT = fmaf(b.w, T2, fmaf(b.z, T1, fmaf(b.y, T0, T3)));
+        } else if constexpr (TAIL) {
+          const float T3 = DT[2][q], T4 = DT[2][8 + q];
           GT = fmaf(z, T4, T3);
+          S[3] = fmaf(ey[q], T4, S[3]);
         } else {
-          const float T0 = DT[0][q], T1 = DT[0][8 + q], T2 = DT[1][q];
+          const float T0 = DT[0][q], T1 = DT[0][8 + q], T2 = DT[1][q], T3 = DT[2][q], T4 = DT[2][8 + q];
           S[0] = fmaf(ey[q], T0, S[0]);
           S[1] = fmaf(ey[q], T1, S[1]);
           S[2] = fmaf(ey[q], T2, S[2]);
           GT = fmaf(z, T4, fmaf(b.w, T2, fmaf(b.z, T1, fmaf(b.y, T0, T3))));
+          S[3] = fmaf(ey[q], T4, S[3]);
         }
-        S[3] = fmaf(ey[q], T4, S[3]);
         const float t = ey[q] * GT;
         S[4] += t;
         const float tdy = t * dy;
@@ -1508,12 +1527,13 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const float dx = PX0(q) - a.x;
-        const float R3 = DR[2][q], R4 = DR[2][8 + q];
         float GR;
-        if constexpr (TAIL) {
-          GR = fmaf(z, R4, R3);
+        if constexpr (!DEPTH) {
+          GR = fmaf(b.w, DR[1][q], fmaf(b.z, DR[0][8 + q], fmaf(b.y, DR[0][q], DR[1][8 + q])));
+        } else if constexpr (TAIL) {
+          GR = fmaf(z, DR[2][8 + q], DR[2][q]);
         } else {
-          GR = fmaf(z, R4, fmaf(b.w, DR[1][q], fmaf(b.z, DR[0][8 + q], fmaf(b.y, DR[0][q], R3))));
+          GR = fmaf(z, DR[2][8 + q], fmaf(b.w, DR[1][q], fmaf(b.z, DR[0][8 + q], fmaf(b.y, DR[0][q], DR[2][q]))));
         }
         const float tdx = (ex[q] * GR) * dx;  // (0 * G) * dx: padding stays 0, never 0 * inf
         S[5] += tdx;
@@ -1565,23 +1585,25 @@ __global__ __launch_bounds__(256, GR_BF16_WAVES) void k_raster_bwd_bf16(ViewK v,
     stage_wait();
     __syncthreads();
   }
-  if (tail)
-    bwd_item_bf16<true>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sSlot, sUF);
+  if (!depth)
+    bwd_item_bf16<false, false>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sSlot, sUF);
+  else if (tail)
+    bwd_item_bf16<true, true>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sSlot, sUF);
   else
-    bwd_item_bf16<false>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sSlot, sUF);
+    bwd_item_bf16<false, true>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sSlot, sUF);
 }
 
 // ------------------------------------------------------------------------------------------------
 // Per-Gaussian reduction of pair partials + chain rule.  Deterministic.
 // ------------------------------------------------------------------------------------------------
 #ifndef GR_RG
-#define GR_RG 32
+#define GR_RG 64
 #endif
-constexpr int RG = GR_RG;        // Gaussians per reduce block (4 lanes each)
-constexpr int RWIN = 18 * GR_RG;  // partial-sum slots staged in LDS per block (18 per Gaussian, both zones)
+constexpr int RG = GR_RG;        // Gaussians per reduce block (4 lanes each; one wave runs the chain rule)
+constexpr int RWIN = 14 * GR_RG;  // partial-sum slots staged in LDS per block (14 per Gaussian, both zones)
 
-template <int CD>
-__device__ void chain_rule(const ViewK& v, int i, const double* S, unsigned cnt, const float* __restrict__ means,
+template <int CD, typename F>
+__device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, const float* __restrict__ means,
                            const float* __restrict__ scales, const float* __restrict__ colors,
                            const float* __restrict__ opac, float* __restrict__ d_means, float* __restrict__ d_scales,
                            float* __restrict__ d_colors, float* __restrict__ d_opac);
@@ -1661,12 +1683,25 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
     S[q] += __shfl_xor(S[q], 1);
     S[q] += __shfl_xor(S[q], 2);
   }
-  if (q4 != 0 || i >= n) return;
-  chain_rule<CD>(v, i, S, cnt, means, scales, colors, opac, d_means, d_scales, d_colors, d_opac);
+  // the block's sums -> LDS; then one lane per Gaussian (wave 0, every lane busy) runs the chain rule
+  // in f32 (the reference's autograd precision)
+  __shared__ float sS[RG][NPART + 1];
+  if (q4 == 0) {
+#pragma unroll
+    for (int q = 0; q < NPART; ++q) sS[tid >> 2][q] = (float)S[q];
+    sS[tid >> 2][NPART] = cnt ? 1.0f : 0.0f;
+  }
+  __syncthreads();
+  if (tid >= RG || g0 + tid >= n) return;
+  float Sf[NPART];
+#pragma unroll
+  for (int q = 0; q < NPART; ++q) Sf[q] = sS[tid][q];
+  chain_rule<CD, float>(v, g0 + tid, Sf, sS[tid][NPART] != 0.0f ? 1u : 0u, means, scales, colors, opac, d_means, d_scales,
+                        d_colors, d_opac);
 }
 
-template <int CD>
-__device__ void chain_rule(const ViewK& v, int i, const double* S, unsigned cnt, const float* __restrict__ means,
+template <int CD, typename F>
+__device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, const float* __restrict__ means,
                            const float* __restrict__ scales, const float* __restrict__ colors,
                            const float* __restrict__ opac, float* __restrict__ d_means, float* __restrict__ d_scales,
                            float* __restrict__ d_colors, float* __restrict__ d_opac) {
@@ -1688,56 +1723,56 @@ __device__ void chain_rule(const ViewK& v, int i, const double* S, unsigned cnt,
   }
   Proj p;
   project(v, mx, my, mz, s0, s1, p);
-  const double o = op < 0.0f ? 0.0 : (double)op;
-  const double sx = p.sx, sy = p.sy;
+  const F o = op < 0.0f ? F(0) : (F)op;
+  const F sx = p.sx, sy = p.sy;
   // ge = o * gw * E  ->  sums over ge carry a factor o.
-  const double dpx = o * S[5] / (sx * sx), dpy = o * S[6] / (sy * sy);
-  double dsx = o * S[7] / (sx * sx * sx), dsy = o * S[8] / (sy * sy * sy);
-  if (!(p.sxr >= 1.0f)) dsx = 0.0;
-  if (!(p.syr >= 1.0f)) dsy = 0.0;
-  const double fx = fabs((double)v.P[0]), fy = fabs((double)v.P[5]);
-  const double kx = 0.5 * v.W * fx / p.za, ky = 0.5 * v.H * fy / p.za;
-  const double sgx = s0 > 0.f ? 1.0 : (s0 < 0.f ? -1.0 : 0.0);
-  const double sgy = s1 > 0.f ? 1.0 : (s1 < 0.f ? -1.0 : 0.0);
+  const F dpx = o * S[5] / (sx * sx), dpy = o * S[6] / (sy * sy);
+  F dsx = o * S[7] / (sx * sx * sx), dsy = o * S[8] / (sy * sy * sy);
+  if (!(p.sxr >= 1.0f)) dsx = F(0);
+  if (!(p.syr >= 1.0f)) dsy = F(0);
+  const F fx = fabsf(v.P[0]), fy = fabsf(v.P[5]);
+  const F kx = F(0.5) * v.W * fx / p.za, ky = F(0.5) * v.H * fy / p.za;
+  const F sgx = s0 > 0.f ? F(1) : (s0 < 0.f ? F(-1) : F(0));
+  const F sgy = s1 > 0.f ? F(1) : (s1 < 0.f ? F(-1) : F(0));
   d_scales[3 * i + 0] = (float)(dsx * kx * sgx);
   d_scales[3 * i + 1] = (float)(dsy * ky * sgy);
   d_scales[3 * i + 2] = 0.f;
-  const double dza = S[3] - dsx * p.sxr / p.za - dsy * p.syr / p.za;
-  double dpc[4] = {0.0, 0.0, 0.0, 0.0};
-  if (fabsf(p.pc[2]) >= 1e-6f) dpc[2] += dza * (p.pc[2] > 0.f ? 1.0 : (p.pc[2] < 0.f ? -1.0 : 0.0));
-  const double dndx = dpx * 0.5 * (v.W - 1);
-  const double dndy = -dpy * 0.5 * (v.H - 1);
-  double dclip[4];
+  const F dza = S[3] - dsx * p.sxr / p.za - dsy * p.syr / p.za;
+  F dpc[4] = {F(0), F(0), F(0), F(0)};
+  if (fabsf(p.pc[2]) >= 1e-6f) dpc[2] += dza * (p.pc[2] > 0.f ? F(1) : (p.pc[2] < 0.f ? F(-1) : F(0)));
+  const F dndx = dpx * F(0.5) * (v.W - 1);
+  const F dndy = -dpy * F(0.5) * (v.H - 1);
+  F dclip[4];
   dclip[0] = dndx / p.ws;
   dclip[1] = dndy / p.ws;
-  dclip[2] = 0.0;
-  dclip[3] = (fabsf(p.clip[3]) < 1e-8f) ? 0.0 : -(dndx * p.clip[0] + dndy * p.clip[1]) / ((double)p.ws * p.ws);
+  dclip[2] = F(0);
+  dclip[3] = (fabsf(p.clip[3]) < 1e-8f) ? F(0) : -(dndx * p.clip[0] + dndy * p.clip[1]) / ((F)p.ws * p.ws);
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) dpc[j] += (double)v.P[r * 4 + j] * dclip[r];
-  double dm[3];
+    for (int r = 0; r < 4; ++r) dpc[j] += (F)v.P[r * 4 + j] * dclip[r];
+  F dm[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    dm[j] = 0.0;
+    dm[j] = F(0);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) dm[j] += (double)v.V[r * 4 + j] * dpc[r];
+    for (int r = 0; r < 4; ++r) dm[j] += (F)v.V[r * 4 + j] * dpc[r];
   }
-  d_opac[i] = (float)((op >= 0.0f) ? S[4] : 0.0);
+  d_opac[i] = (float)((op >= 0.0f) ? S[4] : F(0));
   float cpre[3];
   eval_color<CD>(v, mx, my, mz, col, cpre);
-  double dcol[3];
+  F dcol[3];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) dcol[k] = (cpre[k] >= 0.0f && cpre[k] <= 1.0f) ? S[k] : 0.0;
+  for (int k = 0; k < 3; ++k) dcol[k] = (cpre[k] >= 0.0f && cpre[k] <= 1.0f) ? S[k] : F(0);
   if constexpr (CD == 3) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) dc[k] = (float)dcol[k];
   } else {
-    const double vv[3] = {(double)v.cam[0] - mx, (double)v.cam[1] - my, (double)v.cam[2] - mz};
-    const double nn = sqrt(vv[0] * vv[0] + vv[1] * vv[1] + vv[2] * vv[2]);
-    const double ne = nn + 1e-8;
-    const double d[3] = {vv[0] / ne, vv[1] / ne, vv[2] / ne};
-    double gd[3] = {0.0, 0.0, 0.0};
+    const F vv[3] = {(F)v.cam[0] - mx, (F)v.cam[1] - my, (F)v.cam[2] - mz};
+    const F nn = std::sqrt(vv[0] * vv[0] + vv[1] * vv[1] + vv[2] * vv[2]);
+    const F ne = nn + F(1e-8);
+    const F d[3] = {vv[0] / ne, vv[1] / ne, vv[2] / ne};
+    F gd[3] = {F(0), F(0), F(0)};
     if constexpr (CD == 12) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -1745,24 +1780,24 @@ __device__ void chain_rule(const ViewK& v, int i, const double* S, unsigned cnt,
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           dc[(1 + j) * 3 + k] = (float)(dcol[k] * d[j]);
-          gd[j] += dcol[k] * (double)col[(1 + j) * 3 + k];
+          gd[j] += dcol[k] * (F)col[(1 + j) * 3 + k];
         }
       }
     } else {  // degree 3: d col / d k_i = Y_i(d), d col / d d = sum_i k_i dY_i/dd
-      double Y[16], G[16][3];
+      F Y[16], G[16][3];
       sh3_basis(d[0], d[1], d[2], Y);
       sh3_basis_grad(d[0], d[1], d[2], G);
       for (int i = 0; i < 16; ++i)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           dc[3 * i + k] = (float)(dcol[k] * Y[i]);
-          const double t = dcol[k] * (double)col[3 * i + k];
+          const F t = dcol[k] * (F)col[3 * i + k];
 #pragma unroll
           for (int j = 0; j < 3; ++j) gd[j] += t * G[i][j];
         }
     }
-    if (nn > 0.0) {
-      const double vg = vv[0] * gd[0] + vv[1] * gd[1] + vv[2] * gd[2];
+    if (nn > F(0)) {
+      const F vg = vv[0] * gd[0] + vv[1] * gd[1] + vv[2] * gd[2];
 #pragma unroll
       for (int j = 0; j < 3; ++j) dm[j] -= gd[j] / ne - vv[j] * vg / (nn * ne * ne);
     }

@@ -11,7 +11,11 @@ reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 dev = torch.device("cuda:0")
 scene = orc.synthetic_scene(N, seed=0)
 view, proj = orc.orbit_cameras(50, R, R)[0]
-t = [torch.from_numpy(a).to(dev).requires_grad_(True) for a in scene.arrays()]
+t = [torch.from_numpy(a).to(dev) for a in scene.arrays()]
+if os.environ.get("PROBE_RANDOM_ORDER") != "1":  # the trainer's layout (fit_multiview.morton_order)
+    perm = importlib.import_module("3dgaussian_amd.fit_multiview").morton_order(t[0])
+    t = [x[perm].contiguous() for x in t]
+t = [x.requires_grad_(True) for x in t]
 g = torch.randn(R, R, 3, device=dev)
 for _ in range(reps):
     out, a, d = tr.rasterize(*t, view, proj, R, R)
