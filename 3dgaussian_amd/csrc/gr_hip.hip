@@ -354,6 +354,7 @@ struct Bins {
   int4* items;         // [cap] work items (tile, k0, k1, chunk)
   int* num_items;      // [1]
   int* tile_item0;     // [tiles] first work item of each tile
+  int* pos_of;         // [K] sorted position of each pair, by emission index (k_reduce_bwd's map)
 };
 
 // Forward-only scratch (freed by the caller after gr_fwd_render).
@@ -368,7 +369,7 @@ struct Scratch {
 inline int64_t item_cap(int tiles, int64_t K) { return (K + CH - 1) / CH + tiles; }
 
 // `vtiles` = 2 x tiles (core and tail lists of each tile) on the differentiable path.
-size_t bins_fixed(int vtiles, int64_t K, size_t off[6]) {
+size_t bins_fixed(int vtiles, int64_t K, size_t off[7]) {
   const int tiles = vtiles;
   const size_t kk = (size_t)(K > 0 ? K : 1);
   const size_t cap = (size_t)item_cap(tiles, K);
@@ -379,6 +380,7 @@ size_t bins_fixed(int vtiles, int64_t K, size_t off[6]) {
   off[3] = o; o = align_up(o + cap * sizeof(int4));
   off[4] = o; o = align_up(o + sizeof(int));
   off[5] = o; o = align_up(o + (size_t)tiles * sizeof(int));
+  off[6] = o; o = align_up(o + kk * sizeof(int));
   return o;
 }
 
@@ -463,7 +465,7 @@ size_t sort_tmp_bytes(int64_t K, int bits) {
 }
 
 Bins bins_view(void* base, int tiles, int64_t K) {
-  size_t off[6];
+  size_t off[7];
   bins_fixed(tiles, K, off);
   char* b = (char*)base;
   Bins r;
@@ -473,6 +475,7 @@ Bins bins_view(void* base, int tiles, int64_t K) {
   r.items = (int4*)(b + off[3]);
   r.num_items = (int*)(b + off[4]);
   r.tile_item0 = (int*)(b + off[5]);
+  r.pos_of = (int*)(b + off[6]);
   return r;
 }
 
@@ -647,6 +650,13 @@ __global__ __launch_bounds__(256) void k_emit_zones(ViewK v, int n, const int4* 
     keys[k] = sK[e];
     ids[k] = sI[e];
   }
+}
+
+// Radix-sort path: sorted position of each pair by emission index (the counting sort writes it in
+// k_tile_place).
+__global__ __launch_bounds__(256) void k_pos_of(int64_t K, const int2* __restrict__ pairs, int* __restrict__ pos_of) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < K) pos_of[pairs[k].y] = (int)k;
 }
 
 // Radix-sort path: the sort's values, (gaussian id, emission index).
@@ -897,7 +907,7 @@ __device__ __forceinline__ void ts_load(int64_t kb, int64_t k1, int64_t klast, i
 // One register-resident segment of k_tile_place: 32 steps of 64 pairs, in pair order.
 // kseg: emission index of the segment's first pair (the slot written next to the Gaussian id).
 __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int (&d)[TS_SEG], const int (&id)[TS_SEG],
-                                         int kseg, int2* __restrict__ pairs_out) {
+                                         int kseg, int2* __restrict__ pairs_out, int* __restrict__ pos_of) {
   const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
   for (int j = 0; j < TS_SEG; ++j) {
@@ -912,6 +922,7 @@ __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int 
     if (ok) {
       const int pos = my[d[j]] + __popcll(m & below);
       pairs_out[pos] = make_int2(id[j], kseg + j * 64 + lane);
+      pos_of[kseg + j * 64 + lane] = pos;  // emission order: coalesced
       __builtin_amdgcn_wave_barrier();  // every lane has read the cursor before it moves
       if ((m >> lane) == 1ull) my[d[j]] = pos + 1;  // highest lane of its group
     }
@@ -922,7 +933,8 @@ __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int 
 __global__ __launch_bounds__(256) void k_tile_place(int64_t K, int cw, int cols, int tiles, int bits,
                                                     const uint16_t* __restrict__ keys, const int* __restrict__ ids_in,
                                                     const int* __restrict__ S, const int2* __restrict__ ranges,
-                                                    int zone, int zbase, int2* __restrict__ pairs_out) {
+                                                    int zone, int zbase, int2* __restrict__ pairs_out,
+                                                    int* __restrict__ pos_of) {
   extern __shared__ int cur[];  // [waves][tiles]
   const int c = xcd_item(blockIdx.x, cols);
   const int waves = (int)blockDim.x >> 6, w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
@@ -954,11 +966,11 @@ __global__ __launch_bounds__(256) void k_tile_place(int64_t K, int cw, int cols,
   }
   __syncthreads();
   if (nseg == 1) {
-    ts_place(lane, bits, my, d, id, zbase + (int)k0, pairs_out);  // keys and ids are still in registers
+    ts_place(lane, bits, my, d, id, zbase + (int)k0, pairs_out, pos_of);  // keys and ids are still in registers
   } else {
     for (int seg = 0; seg < nseg; ++seg) {
       ts_load(k0 + (int64_t)seg * 64 * TS_SEG, k1, K - 1, lane, keys, ids_in, d, id);
-      ts_place(lane, bits, my, d, id, zbase + (int)(k0 + (int64_t)seg * 64 * TS_SEG), pairs_out);
+      ts_place(lane, bits, my, d, id, zbase + (int)(k0 + (int64_t)seg * 64 * TS_SEG), pairs_out, pos_of);
     }
   }
 }
@@ -1264,7 +1276,7 @@ template <bool TAIL>
 __device__ __forceinline__ void bwd_item(int n, int tile, int k0, int k1, int tid, int wave, int li, int xs, int tx, int ty,
                                          const float* __restrict__ U, const int2* __restrict__ pairs,
                                          const float4* __restrict__ rec, float* __restrict__ partials,
-                                         float4 (*sA)[TP], float4 (*sB)[TP], float (*sZ)[TP], int (*sSlot)[TP],
+                                         float4 (*sA)[TP], float4 (*sB)[TP], float (*sZ)[TP],
                                          float4* sU) {
   constexpr int KLO = TAIL ? 3 : 0;  // first upstream channel contracted
   const int lane = tid & 63;
@@ -1281,7 +1293,6 @@ __device__ __forceinline__ void bwd_item(int n, int tile, int k0, int k1, int ti
     glds16(p, &sA[b][64 * wave]);
     glds16(p + 1, &sB[b][64 * wave]);
     glds4(p + 2, &sZ[b][64 * wave]);
-    sSlot[b][tid] = pr.y;
   };
   stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1), 0);
   int2 idn = stage_id(k0 + TP + tid, k1, pairs);  // raw: batch base + TP
@@ -1299,7 +1310,7 @@ __device__ __forceinline__ void bwd_item(int n, int tile, int k0, int k1, int ti
       const float4 a = sA[buf][j];
       const float4 b = sB[buf][j];
       const float z = sZ[buf][j];
-      const int myslot = sSlot[buf][j];  // -1 for padding
+      const int myslot = j < nb ? base + j : -1;  // the pair's sorted position = its partial-sum row
       float ex[4], ey[4], dx[4], dy[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -1371,7 +1382,6 @@ __global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
   __shared__ __attribute__((aligned(16))) float4 sA[2][TP];
   __shared__ __attribute__((aligned(16))) float4 sB[2][TP];
   __shared__ float sZ[2][TP];
-  __shared__ int sSlot[2][TP];
   __shared__ __attribute__((aligned(16))) float4 sU[UL / 4];
   const int nitems = *num_items;
   if ((int)blockIdx.x >= nitems) return;
@@ -1384,9 +1394,9 @@ __global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int li = lane & 15, xs = lane >> 4;
   if (tail)
-    bwd_item<true>(n, tile, k0, k1, tid, wave, li, xs, tx, ty, U, pairs, rec, partials, sA, sB, sZ, sSlot, sU);
+    bwd_item<true>(n, tile, k0, k1, tid, wave, li, xs, tx, ty, U, pairs, rec, partials, sA, sB, sZ, sU);
   else
-    bwd_item<false>(n, tile, k0, k1, tid, wave, li, xs, tx, ty, U, pairs, rec, partials, sA, sB, sZ, sSlot, sU);
+    bwd_item<false>(n, tile, k0, k1, tid, wave, li, xs, tx, ty, U, pairs, rec, partials, sA, sB, sZ, sU);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1417,6 +1427,15 @@ __device__ __forceinline__ s16x8 as_frag(uint4 u) {
 // that keeps the kernel at 4 waves per SIMD.
 __device__ __forceinline__ f32x16 mfma_split(const uint4* __restrict__ A, int lane, const s16x8 (&B)[3]) {
   f32x16 c = {};
+#ifdef GR_DIAG_NOMFMA
+  {
+    const uint4 u = A[lane];
+    const float f = __uint_as_float(u.x) + __uint_as_float((unsigned)B[0][0] << 16);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) c[i] = f;
+    return c;
+  }
+#endif
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(A[128 + lane]), B[0], c, 0, 0, 0);
   const s16x8 a1 = as_frag(A[64 + lane]);
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, B[1], c, 0, 0, 0);
@@ -1443,7 +1462,7 @@ template <bool TAIL, bool DEPTH>
 __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, int wave, int tx, int ty,
                                               const int2* __restrict__ pairs, const float4* __restrict__ rec,
                                               float* __restrict__ partials, float4 (*sA)[TP], float4 (*sB)[TP],
-                                              float (*sZ)[TP], int (*sSlot)[TP], const uint4* sUF) {
+                                              float (*sZ)[TP], const uint4* sUF) {
   static_assert(DEPTH || !TAIL, "tail items carry only depth-coupled terms");
   constexpr int P0 = TAIL ? 2 : 0;      // first channel pair contracted
   constexpr int P1 = DEPTH ? 3 : 2;     // one past the last (pair_channel)
@@ -1453,11 +1472,14 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
 #define PX0(q) (pxb + (float)((q) < 4 ? (q) : (q) + 4))
 #define PY0(q) (pyb + (float)((q) < 4 ? (q) : (q) + 4))
   auto stage = [&](int2 pr, int b) {
+#ifdef GR_DIAG_SAMEREC
+    const float4* p = rec_of(pr.x < 0 ? -1 : (pr.x & 63), n, rec);
+#else
     const float4* p = rec_of(pr.x, n, rec);
+#endif
     glds16(p, &sA[b][64 * wave]);
     glds16(p + 1, &sB[b][64 * wave]);
     glds4(p + 2, &sZ[b][64 * wave]);
-    sSlot[b][tid] = pr.y;
   };
   stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1), 0);
   int2 idn = stage_id(k0 + TP + tid, k1, pairs);  // raw: batch base + TP
@@ -1475,13 +1497,18 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
       const float4 a = sA[buf][j];
       const float4 b = sB[buf][j];
       const float z = sZ[buf][j];
-      const int myslot = sSlot[buf][j];  // -1 for padding
+      const int myslot = j < nb ? base + j : -1;  // the pair's sorted position = its partial-sum row
       float ex[8], ey[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const float dx = PX0(q) - a.x, dy = PY0(q) - a.y;
+#ifdef GR_DIAG_NOEXP
+        ex[q] = dx * a.z * dx;
+        ey[q] = dy * a.w * dy;
+#else
         ex[q] = __builtin_amdgcn_exp2f(dx * a.z * dx);  // exactly 0 for padding
         ey[q] = __builtin_amdgcn_exp2f(dy * a.w * dy);
+#endif
       }
       // both contractions are issued before either epilogue, so the T epilogue's VALU work runs while
       // the R MFMAs execute
@@ -1494,6 +1521,11 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
 #pragma unroll
       for (int pr = P0; pr < P1; ++pr) DR[pr] = mfma_split(sUF + (1 * 3 + pr) * 3 * 64, lane, BR);
       float S[NPART] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#ifdef GR_DIAG_NOEPI
+      S[0] = DT[0][0] + DR[0][1]; S[4] = DT[1][3] + DR[1][5]; S[5] = DT[0][9];
+      if (0)
+#endif
+      {
       // T: rows y = kslot_pixel(h, q) of channels pair_channel(pr, c) at register 8c + q
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -1539,11 +1571,16 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
         S[5] += tdx;
         S[7] = fmaf(tdx, dx, S[7]);
       }
+      }
       // lanes r and r + 32 hold the two halves of Gaussian r's pixels: half 0 ends with the totals of
       // S0, S2, S4, S6, S8, half 1 with S1, S3, S5, S7
       const float P01 = pair32(S[0], S[1]), P23 = pair32(S[2], S[3]), P45 = pair32(S[4], S[5]);
       const float P67 = pair32(S[6], S[7]), P8 = pair32(S[8], S[8]);
+#ifdef GR_DIAG_NOSTORE
+      if (myslot == -12345) {
+#else
       if (myslot >= 0) {
+#endif
         float* dst = partials + (size_t)myslot * NPART + h;
         dst[0] = b.x * P01;  // colour / depth sums carry the opacity
         dst[2] = b.x * P23;
@@ -1560,22 +1597,27 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
 #ifndef GR_BF16_WAVES
 #define GR_BF16_WAVES 2
 #endif
+#ifndef GR_BF16_WAVES_ND
+#define GR_BF16_WAVES_ND 2
+#endif
 
-__global__ __launch_bounds__(256, GR_BF16_WAVES) void k_raster_bwd_bf16(ViewK v, int n, const int4* __restrict__ items,
+// DEPTH = 0: no upstream depth gradient (4 channels, tail items skipped) — its own kernel, so its
+// register budget is not set by the 5-channel form's.
+template <bool DEPTH>
+__global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void k_raster_bwd_bf16(ViewK v, int n, const int4* __restrict__ items,
                                                            const int* __restrict__ num_items, const int2* __restrict__ pairs,
                                                            const float4* __restrict__ rec, const uint4* __restrict__ UF,
-                                                           float* __restrict__ partials, int depth) {
+                                                           float* __restrict__ partials) {
   __shared__ __attribute__((aligned(16))) float4 sA[2][TP];
   __shared__ __attribute__((aligned(16))) float4 sB[2][TP];
   __shared__ float sZ[2][TP];
-  __shared__ int sSlot[2][TP];
   __shared__ __attribute__((aligned(16))) uint4 sUF[UF_FRAGS];
   const int nitems = *num_items;
   if ((int)blockIdx.x >= nitems) return;
   const int item = xcd_item(blockIdx.x, nitems);
   const int4 it = items[item];
   const bool tail = it.x & 1;
-  if (tail && !depth) return;
+  if (tail && !DEPTH) return;
   const int tile = it.x >> 1, k0 = it.y, k1 = it.z;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1585,12 +1627,12 @@ __global__ __launch_bounds__(256, GR_BF16_WAVES) void k_raster_bwd_bf16(ViewK v,
     stage_wait();
     __syncthreads();
   }
-  if (!depth)
-    bwd_item_bf16<false, false>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sSlot, sUF);
+  if constexpr (!DEPTH)
+    bwd_item_bf16<false, false>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sUF);
   else if (tail)
-    bwd_item_bf16<true, true>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sSlot, sUF);
+    bwd_item_bf16<true, true>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sUF);
   else
-    bwd_item_bf16<false, true>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sSlot, sUF);
+    bwd_item_bf16<false, true>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sUF);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1600,7 +1642,6 @@ __global__ __launch_bounds__(256, GR_BF16_WAVES) void k_raster_bwd_bf16(ViewK v,
 #define GR_RG 64
 #endif
 constexpr int RG = GR_RG;        // Gaussians per reduce block (4 lanes each; one wave runs the chain rule)
-constexpr int RWIN = 14 * GR_RG;  // partial-sum slots staged in LDS per block (14 per Gaussian, both zones)
 
 template <int CD, typename F>
 __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, const float* __restrict__ means,
@@ -1608,57 +1649,24 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
                            const float* __restrict__ opac, float* __restrict__ d_means, float* __restrict__ d_scales,
                            float* __restrict__ d_colors, float* __restrict__ d_opac);
 
-// Copy partial-sum slots [s0, s1) into LDS at dst (coalesced float4 loads, 4 in flight per lane);
-// returns the first float staged (s0 * NPART rounded down to a float4).
-__device__ __forceinline__ long long stage_slots(long long s0, long long s1, const float* __restrict__ partials, float* dst,
-                                                 int tid) {
-  const long long fa = (s0 * NPART) & ~3ll, fe = s1 * NPART;
-  const int nv = (int)((fe - fa + 3) >> 2);
-  const float4* src = reinterpret_cast<const float4*>(partials + fa);
-  float4* d4 = reinterpret_cast<float4*>(dst);
-  constexpr int NT = 4 * RG;
-  int e = tid;
-  for (; e + 3 * NT < nv; e += 4 * NT) {
-    const float4 x0 = src[e], x1 = src[e + NT], x2 = src[e + 2 * NT], x3 = src[e + 3 * NT];
-    d4[e] = x0;
-    d4[e + NT] = x1;
-    d4[e + 2 * NT] = x2;
-    d4[e + 3 * NT] = x3;
-  }
-  for (; e < nv; e += NT) d4[e] = src[e];
-  return fa;
-}
-
-// Block of RG Gaussians, 4 lanes each.  A Gaussian's partial-sum slots are its pairs' emission
-// indices: its core pairs [c_i, c_i + core_i) and (only with an upstream depth gradient; otherwise
-// the backward skipped them) its tail pairs Kc + [t_i, t_i + tail_i), each contiguous and, over the
-// block, one contiguous range per zone, staged into LDS.  Lane q sums slots q, q+4, ... (core, then
-// tail), the 4 sums are combined in a fixed order (deterministic, no atomics), and lane 0 applies
-// the chain rule.
+// Block of RG Gaussians, 4 lanes each.  A Gaussian's pairs are its emission indices: core pairs
+// [c_i, c_i + core_i) and (only with an upstream depth gradient; otherwise the backward skipped them)
+// tail pairs Kc + [t_i, t_i + tail_i); their partial sums sit at the pairs' sorted positions
+// (pos_of), where the backward splat wrote them with coalesced stores.  Lane q sums pairs q, q+4, ...
+// (core, then tail), the 4 sums are combined in a fixed order (deterministic, no atomics), and one
+// lane per Gaussian applies the chain rule.
 template <int CD>
 __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const float* __restrict__ means,
                                                     const float* __restrict__ scales, const float* __restrict__ colors,
                                                     const float* __restrict__ opac, const Cnt2* __restrict__ counts,
-                                                    const Cnt2* __restrict__ offsets, const float* __restrict__ partials,
-                                                    float* __restrict__ d_means, float* __restrict__ d_scales,
-                                                    float* __restrict__ d_colors, float* __restrict__ d_opac, int depth) {
-  __shared__ __attribute__((aligned(16))) float sP[RWIN * NPART + 16];
+                                                    const Cnt2* __restrict__ offsets, const int* __restrict__ pos_of,
+                                                    const float* __restrict__ partials, float* __restrict__ d_means,
+                                                    float* __restrict__ d_scales, float* __restrict__ d_colors,
+                                                    float* __restrict__ d_opac, int depth) {
   const int g0 = blockIdx.x * RG;
   const int tid = threadIdx.x, q4 = tid & 3;
   const int i = g0 + (tid >> 2);
-  const int gend = min(n, g0 + RG);
   const long long Kc = (long long)offsets[n].c();
-  const long long c0 = (long long)offsets[g0].c(), c1 = (long long)offsets[gend].c();
-  const long long t0 = depth ? Kc + (long long)offsets[g0].t() : 0, t1 = depth ? Kc + (long long)offsets[gend].t() : 0;
-  const bool staged = (c1 - c0) + (t1 - t0) <= RWIN;  // block-uniform
-  long long fc = 0, ft = 0;
-  // tail window after the core one: the core copy spans at most (c1 - c0) * NPART + 6 floats
-  float* sT = sP + (((c1 - c0) * NPART + 9) & ~3ll);
-  if (staged) {
-    fc = stage_slots(c0, c1, partials, sP, tid);
-    if (t1 > t0) ft = stage_slots(t0, t1, partials, sT, tid);
-  }
-  __syncthreads();
   double S[NPART];
 #pragma unroll
   for (int q = 0; q < NPART; ++q) S[q] = 0.0;
@@ -1666,16 +1674,22 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
   if (i < n) {
     const Cnt2 cn = counts[i], of = offsets[i];
     cnt = cn.v != 0 ? 1u : 0u;  // any kept tile (core or tail)
-    const long long bc = (long long)of.c(), bt = Kc + (long long)of.t();
-    const float* srcc = staged ? sP + (bc * NPART - fc) : partials + bc * NPART;
-    for (int j = q4; j < (int)cn.c(); j += 4)
+    // pair e of this Gaussian (emission index) was written by the backward splat at its sorted
+    // position pos_of[e]: the block's Gaussians are consecutive, so within each tile their rows are
+    // one contiguous run of the sorted array
+    const int* pc = pos_of + (long long)of.c();
+    for (int j = q4; j < (int)cn.c(); j += 4) {
+      const float* src = partials + (size_t)pc[j] * NPART;
 #pragma unroll
-      for (int q = 0; q < NPART; ++q) S[q] += (double)srcc[j * NPART + q];
+      for (int q = 0; q < NPART; ++q) S[q] += (double)src[q];
+    }
     if (depth) {
-      const float* srct = staged ? sT + (bt * NPART - ft) : partials + bt * NPART;
-      for (int j = q4; j < (int)cn.t(); j += 4)
+      const int* pt = pos_of + Kc + (long long)of.t();
+      for (int j = q4; j < (int)cn.t(); j += 4) {
+        const float* src = partials + (size_t)pt[j] * NPART;
 #pragma unroll
-        for (int q = 0; q < NPART; ++q) S[q] += (double)srct[j * NPART + q];
+        for (int q = 0; q < NPART; ++q) S[q] += (double)src[q];
+      }
     }
   }
 #pragma unroll
@@ -2097,7 +2111,7 @@ void gr_geom_layout(int n, size_t offsets_out[GR_GEOM_PARTS]) { geom_fixed(n, of
 
 void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[3]) {
   (void)n;
-  size_t off[6];
+  size_t off[7];
   bins_fixed(vtiles_of(v), plan ? plan->num_pairs : 0, off);
   offsets_out[0] = off[0];
   offsets_out[1] = off[1];
@@ -2113,7 +2127,7 @@ size_t gr_saved_floats(const gr_view* v) { return (size_t)5 * v->width * v->heig
 
 size_t gr_bins_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
-  size_t off[6];
+  size_t off[7];
   return bins_fixed(vtiles_of(v), plan->num_pairs, off);
 }
 
@@ -2269,7 +2283,7 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
         if (Kr[z] == 0) continue;
         hipLaunchKernelGGL(k_tile_place, dim3(tp[z].cols), dim3(64 * tp[z].waves), (size_t)tiles * sizeof(int) * tp[z].waves,
                            s, Kr[z], tp[z].cw, tp[z].cols, tiles, bits_for((uint32_t)tiles), kz[z], iz[z],
-                           (const int*)Sz[z], (const int2*)b.ranges, z, z == 0 ? 0 : (int)Kc, b.pairs);
+                           (const int*)Sz[z], (const int2*)b.ranges, z, z == 0 ? 0 : (int)Kc, b.pairs, b.pos_of);
         GR_HIP_TRY(hipGetLastError());
       }
     } else {
@@ -2286,6 +2300,8 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
       GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp, tmp, sc.keys_in, b.keys, sc.pairs_in, b.pairs,
                                                     (int)num_pairs, 0, bits, s));
       hipLaunchKernelGGL(k_ranges<uint32_t>, dim3(blocks_for(num_pairs)), dim3(256), 0, s, num_pairs, b.keys, b.ranges);
+      GR_HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_pos_of, dim3(blocks_for(num_pairs)), dim3(256), 0, s, num_pairs, (const int2*)b.pairs, b.pos_of);
       GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
                          b.tile_item0);
@@ -2345,9 +2361,9 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
     const int64_t cap = item_cap(2 * tiles, num_pairs);
     prof_mark(PROF_RASTER_BWD, s);
     if (split)
-      hipLaunchKernelGGL(k_raster_bwd_bf16, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
-                         (const int*)b.num_items, (const int2*)b.pairs, (const float4*)g.rec, (const uint4*)U, partials,
-                         g_depth != nullptr ? 1 : 0);
+      hipLaunchKernelGGL(g_depth != nullptr ? k_raster_bwd_bf16<true> : k_raster_bwd_bf16<false>, dim3((unsigned)cap),
+                         dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items, (const int2*)b.pairs,
+                         (const float4*)g.rec, (const uint4*)U, partials);
     else
       hipLaunchKernelGGL(k_raster_bwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
                          (const int*)b.num_items, (const int2*)b.pairs, (const float4*)g.rec, (const float*)U, partials,
@@ -2358,15 +2374,15 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
   prof_mark(PROF_REDUCE, s);
   if (color_dim == 3)
     hipLaunchKernelGGL(k_reduce_bwd<3>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
-                       (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
+                       (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const int*)b.pos_of, (const float*)partials, d_means, d_scales, d_colors,
                        d_opacities, g_depth != nullptr ? 1 : 0);
   else if (color_dim == 12)
     hipLaunchKernelGGL(k_reduce_bwd<12>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
-                       (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
+                       (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const int*)b.pos_of, (const float*)partials, d_means, d_scales, d_colors,
                        d_opacities, g_depth != nullptr ? 1 : 0);
   else
     hipLaunchKernelGGL(k_reduce_bwd<48>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
-                       (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const float*)partials, d_means, d_scales, d_colors,
+                       (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const int*)b.pos_of, (const float*)partials, d_means, d_scales, d_colors,
                        d_opacities, g_depth != nullptr ? 1 : 0);
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_REDUCE, s);

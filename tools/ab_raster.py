@@ -11,7 +11,11 @@ reps = int(sys.argv[3]) if len(sys.argv) > 3 else 6
 dev = torch.device("cuda:0")
 scene = orc.synthetic_scene(N, seed=0)
 views = orc.orbit_cameras(50, R, R)
-t = [torch.from_numpy(a).to(dev).requires_grad_(True) for a in scene.arrays()]
+t = [torch.from_numpy(a).to(dev) for a in scene.arrays()]
+if os.environ.get("AB_RANDOM_ORDER") != "1":  # the trainer's layout (fit_multiview.morton_order)
+    perm = importlib.import_module("3dgaussian_amd.fit_multiview").morton_order(t[0])
+    t = [x[perm].contiguous() for x in t]
+t = [x.requires_grad_(True) for x in t]
 g = torch.randn(R, R, 3, device=dev)
 gd = torch.randn(R, R, device=dev) if os.environ.get("AB_DEPTH") == "1" else None
 CORE = float(os.environ.get("AB_CORE", tr.DEFAULT_CORE_CUTOFF))  # 0: one zone

@@ -7,5 +7,6 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 DST=$ROOT/ab/$NAME
 rm -rf "$DST" && mkdir -p "$DST"
 tar -C "$ROOT" --exclude=./ab --exclude=./.git --exclude=./gpurun_out --exclude=./tests/golden -cf - . | tar -x -C "$DST"
-make -s -C "$DST/3dgaussian_amd/csrc" EXTRA="$FLAGS" >/dev/null
+rm -f "$DST/3dgaussian_amd/libgr_hip.so"  # the copied library is newer than its source: force the rebuild
+make -s -B -C "$DST/3dgaussian_amd/csrc" EXTRA="$FLAGS" >/dev/null
 echo "built $DST ($FLAGS)"
