@@ -722,7 +722,7 @@ __global__ __launch_bounds__(1024) void k_work_items(int vtiles, const int2* __r
 
 // Counting-sort path: per-tile pair totals of the core region (Tc) and of the tail region (Tt,
 // starting at Kc) are scanned into the virtual-tile ranges (2t: core, 2t+1: tail), then cut.
-__global__ __launch_bounds__(1024) void k_work_items_zones(int tiles, int Kc, const int* __restrict__ Tc,
+__global__ __launch_bounds__(1024) void k_work_items_zones(int tiles, int tiles_x, int Kc, const int* __restrict__ Tc,
                                                            const int* __restrict__ Tt, int2* __restrict__ ranges,
                                                            int4* __restrict__ items, int* __restrict__ num_items,
                                                            int* __restrict__ tile_item0) {
@@ -975,6 +975,161 @@ __global__ __launch_bounds__(256) void k_tile_place(int64_t K, int cw, int cols,
   }
 }
 
+// Exact three-way bf16 split: x = hi + mid + lo, each a truncated bf16 (hi keeps 8 significant bits,
+// the f32 remainders are exact), returned as f32 values whose low 16 bits are zero.
+__device__ __forceinline__ void split3(float x, float& hi, float& mid, float& lo) {
+  hi = __uint_as_float(__float_as_uint(x) & 0xffff0000u);
+  const float r1 = x - hi;
+  mid = __uint_as_float(__float_as_uint(r1) & 0xffff0000u);
+  lo = r1 - mid;  // <= 8 significant bits: exactly a bf16
+}
+// two bf16 (high halves of a, b) into one dword: low half = a, high half = b
+__device__ __forceinline__ unsigned pack_bf16(float a, float b) {
+  return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
+}
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ s16x8 as_frag(uint4 u) {
+  s16x8 f;
+  __builtin_memcpy(&f, &u, sizeof(f));
+  return f;
+}
+
+// Split-precision forward (k_raster_fwd_mfma<true>): the same contraction on v_mfma_f32_16x16x32_bf16
+// (K = 32 Gaussians per instruction).  B = ey and the W / D operands (o ex, o z ex) are split exactly
+// into three bf16 pieces and multiplied with the six products of weight >= 2^-16 (f32-grade, as the
+// backward): the depth gradient d depth / d w = (z - depth) / (W + 1e-6) cancels catastrophically on
+// thin pixels, so W and D must carry full f32 accuracy.  The colour operands (o c ex) take two pieces,
+// hi = truncated bf16, lo = bf16(x - hi) rounded to nearest, and three products: each colour
+// accumulator is a sum of non-negative terms, each within 2^-16 of exact, so its relative error stays
+// below that (no cancellation) — far inside the 1e-4 parity bar.
+// Lane l supplies A[x = l&15][g = 8(l>>4) + j] and B[g][y = l&15], j = 0..7, and receives
+// C[x = 4(l>>4) + r][y = l&15] (the f32 kernel's output map).
+__device__ __forceinline__ void split3_frag(const float (&v)[8], s16x8 (&f)[3]) {
+  float hi[8], mid[8], lo[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) split3(v[j], hi[j], mid[j], lo[j]);
+  f[0] = as_frag(make_uint4(pack_bf16(hi[0], hi[1]), pack_bf16(hi[2], hi[3]), pack_bf16(hi[4], hi[5]), pack_bf16(hi[6], hi[7])));
+  f[1] = as_frag(make_uint4(pack_bf16(mid[0], mid[1]), pack_bf16(mid[2], mid[3]), pack_bf16(mid[4], mid[5]),
+                            pack_bf16(mid[6], mid[7])));
+  f[2] = as_frag(make_uint4(pack_bf16(lo[0], lo[1]), pack_bf16(lo[2], lo[3]), pack_bf16(lo[4], lo[5]), pack_bf16(lo[6], lo[7])));
+}
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+// two pieces: hi = truncated bf16, lo = bf16(x - hi) rounded to nearest (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ void split2_frag(const float (&v)[8], s16x8 (&f)[2]) {
+  unsigned h[4], l[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float h0 = __uint_as_float(__float_as_uint(v[2 * p]) & 0xffff0000u);
+    const float h1 = __uint_as_float(__float_as_uint(v[2 * p + 1]) & 0xffff0000u);
+    h[p] = pack_bf16(h0, h1);
+    const f32x2_t r = {v[2 * p] - h0, v[2 * p + 1] - h1};
+    const bf16x2_t lb = __builtin_convertvector(r, bf16x2_t);
+    __builtin_memcpy(&l[p], &lb, 4);
+  }
+  f[0] = as_frag(make_uint4(h[0], h[1], h[2], h[3]));
+  f[1] = as_frag(make_uint4(l[0], l[1], l[2], l[3]));
+}
+__device__ __forceinline__ f32x4 mfma16(const s16x8& a, const s16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// sum over the six significant piece products, smallest first
+__device__ __forceinline__ f32x4 mfma16_split3(const s16x8 (&a)[3], const s16x8 (&b)[3], f32x4 c) {
+  c = mfma16(a[2], b[0], c);
+  c = mfma16(a[1], b[1], c);
+  c = mfma16(a[0], b[2], c);
+  c = mfma16(a[1], b[0], c);
+  c = mfma16(a[0], b[1], c);
+  return mfma16(a[0], b[0], c);
+}
+__device__ __forceinline__ f32x4 mfma16_split2(const s16x8 (&a)[2], const s16x8 (&b)[3], f32x4 c) {
+  c = mfma16(a[1], b[0], c);
+  c = mfma16(a[0], b[1], c);
+  return mfma16(a[0], b[0], c);
+}
+
+template <bool TAIL>
+__device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, int k1, int tid, int wave, float xc, float yc,
+                                                    int gq, const int2* __restrict__ pairs, const float4* __restrict__ rec,
+                                                    f32x4& cW, f32x4& cR, f32x4& cG, f32x4& cB, f32x4& cD) {
+  constexpr int BUF = 2 * TP + TP / 4;  // float4 units per buffer (fwd_accumulate's staging layout)
+  auto stage = [&](int g, int b) {
+    const float4* p = rec_of(g, n, rec);
+    float4* sA = reinterpret_cast<float4*>(smem) + b * BUF;
+    glds16(p, sA + 64 * wave);
+    glds16(p + 1, sA + TP + 64 * wave);
+    glds4(p + 2, reinterpret_cast<float*>(sA + 2 * TP) + 64 * wave);
+  };
+  stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1).x, 0);
+  int2 idn = stage_id(k0 + TP + tid, k1, pairs);
+  int buf = 0;
+  for (int base = k0; base < k1; base += TP, buf ^= 1) {
+    stage_wait();
+    __syncthreads();
+    if (base + TP < k1) stage(stage_pair(idn, base + TP + tid, k1).x, buf ^ 1);
+    idn = stage_id(base + 2 * TP + tid, k1, pairs);
+    const float4* sA = reinterpret_cast<const float4*>(smem) + buf * BUF;
+    const float4* sB = sA + TP;
+    const float* sZ = reinterpret_cast<const float*>(sB + TP);
+    const int cnt = min(TP, k1 - base) - wave * 64;           // Gaussians of this batch for this wave
+    const int nst = cnt <= 0 ? 0 : min(2, (cnt + 31) >> 5);  // steps of 32 (padding records are zero)
+    for (int st = 0; st < nst; ++st) {
+      float aW[8], aR[8], aG[8], aB[8], aD[8], bv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int g = wave * 64 + st * 32 + 8 * gq + j;
+        const float4 a = sA[g];
+        const float z = sZ[g];
+        const float dx = xc - a.x, dy = yc - a.y;
+        const float ex = __builtin_amdgcn_exp2f(dx * a.z * dx);
+        bv[j] = __builtin_amdgcn_exp2f(dy * a.w * dy);
+        if constexpr (TAIL) {
+          const float oe = sB[g].x * ex;
+          aW[j] = oe;
+          aD[j] = oe * z;
+        } else {
+          const float4 b = sB[g];
+          const float oe = b.x * ex;
+          aW[j] = oe;
+          aR[j] = oe * b.y;
+          aG[j] = oe * b.z;
+          aB[j] = oe * b.w;
+          aD[j] = oe * z;
+        }
+      }
+      s16x8 fb[3], f3[3];
+      split3_frag(bv, fb);
+      split3_frag(aW, f3);
+      cW = mfma16_split3(f3, fb, cW);
+      split3_frag(aD, f3);
+      cD = mfma16_split3(f3, fb, cD);
+      if constexpr (!TAIL) {
+#ifdef GR_FWD_RGB3
+        split3_frag(aR, f3);
+        cR = mfma16_split3(f3, fb, cR);
+        split3_frag(aG, f3);
+        cG = mfma16_split3(f3, fb, cG);
+        split3_frag(aB, f3);
+        cB = mfma16_split3(f3, fb, cB);
+        if (false)
+#endif
+        {
+        s16x8 f2[2];
+        split2_frag(aR, f2);
+        cR = mfma16_split2(f2, fb, cR);
+        split2_frag(aG, f2);
+        cG = mfma16_split2(f2, fb, cG);
+        split2_frag(aB, f2);
+        cB = mfma16_split2(f2, fb, cB);
+        }
+      }
+    }
+  }
+}
+
 // Forward: one workgroup (4 waves) per work item.  Batches of 256 Gaussians go through a double-
 // buffered LDS stage; wave w takes Gaussians [64w, 64w+64) of each batch in blocks of 4 steps of 4
 // (the MFMA K dimension).  Padding entries are exact zeros, so whole blocks are processed.
@@ -1062,6 +1217,7 @@ __device__ __forceinline__ void write_pixel(const ViewK& v, int p, const float* 
   savedD[p] = acc[4];
 }
 
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, int n, const int4* __restrict__ items,
                                                          const int* __restrict__ num_items, const int2* __restrict__ ranges,
                                                          const int2* __restrict__ pairs, const float4* __restrict__ rec,
@@ -1081,10 +1237,17 @@ __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, int n, const i
   const float xc = (float)(tx * T + li) + 0.5f;  // A row = x
   const float yc = (float)(ty * T + li) + 0.5f;  // B col = y
   f32x4 cW = {0.f, 0.f, 0.f, 0.f}, cR = cW, cG = cW, cB = cW, cD = cW;
-  if (it.x & 1)
-    fwd_accumulate<true>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
-  else
-    fwd_accumulate<false>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
+  if constexpr (SPLIT) {
+    if (it.x & 1)
+      fwd_accumulate_bf16<true>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
+    else
+      fwd_accumulate_bf16<false>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
+  } else {
+    if (it.x & 1)
+      fwd_accumulate<true>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
+    else
+      fwd_accumulate<false>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
+  }
   __syncthreads();
   {  // lane holds C[x = 4*gs + r][y = li]: pixel index y*16 + x, 4 consecutive x
     float* rw = smem + wave * 5 * TP + li * T + 4 * gs;
@@ -1150,18 +1313,6 @@ __device__ __forceinline__ int pair_channel(int pr, int c, bool depth) {
 // (reg&3) + 8 (reg>>2) + 4h): one set of exponentials per lane serves both contractions.
 __device__ __forceinline__ int kslot_pixel(int h, int j) { return (j < 4) ? 4 * h + j : 8 + 4 * h + (j - 4); }
 
-// Exact three-way bf16 split: x = hi + mid + lo, each a truncated bf16 (hi keeps 8 significant bits,
-// the f32 remainders are exact), returned as f32 values whose low 16 bits are zero.
-__device__ __forceinline__ void split3(float x, float& hi, float& mid, float& lo) {
-  hi = __uint_as_float(__float_as_uint(x) & 0xffff0000u);
-  const float r1 = x - hi;
-  mid = __uint_as_float(__float_as_uint(r1) & 0xffff0000u);
-  lo = r1 - mid;  // <= 8 significant bits: exactly a bf16
-}
-// two bf16 (high halves of a, b) into one dword: low half = a, high half = b
-__device__ __forceinline__ unsigned pack_bf16(float a, float b) {
-  return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
-}
 
 // Per-pixel upstream vector U = (dC_r, dC_g, dC_b, dW, dD) of the OIT finalize
 // (torch_renderer.py:192-203), laid out [tile][channel][256] for the backward work items.
@@ -1413,14 +1564,6 @@ __global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
 // kslot_pixel(h, 0..7) on both axes: its B operand for T is ex at those x, for R ey at those y, and
 // its accumulator rows of T (R) are exactly those y (x), so each exponential is computed once.
 // ------------------------------------------------------------------------------------------------
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ s16x8 as_frag(uint4 u) {
-  s16x8 f;
-  __builtin_memcpy(&f, &u, sizeof(f));
-  return f;
-}
 
 // A * B over the six significant piece products, smallest first.  A's pieces are read from LDS
 // (lane-linear fragments, one ds_read_b128 each) next to their use rather than held in registers:
@@ -1479,7 +1622,7 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
 #endif
     glds16(p, &sA[b][64 * wave]);
     glds16(p + 1, &sB[b][64 * wave]);
-    glds4(p + 2, &sZ[b][64 * wave]);
+    if constexpr (DEPTH) glds4(p + 2, &sZ[b][64 * wave]);  // z enters only the depth-coupled terms
   };
   stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1), 0);
   int2 idn = stage_id(k0 + TP + tid, k1, pairs);  // raw: batch base + TP
@@ -1496,7 +1639,7 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
       const int j = g0 + r;
       const float4 a = sA[buf][j];
       const float4 b = sB[buf][j];
-      const float z = sZ[buf][j];
+      const float z = DEPTH ? sZ[buf][j] : 0.0f;
       const int myslot = j < nb ? base + j : -1;  // the pair's sorted position = its partial-sum row
       float ex[8], ey[8];
 #pragma unroll
@@ -2063,6 +2206,16 @@ bool bwd_split_precision() {
   return !f32;
 }
 
+// Forward splat kernel: the split bf16 one (default) or the f32 one (GR_FWD_F32=1, kept as the
+// reference form and for A/B timing).  Both meet the same tests.
+bool fwd_split_precision() {
+  static const bool f32 = [] {
+    const char* e = std::getenv("GR_FWD_F32");
+    return e && e[0] == '1';
+  }();
+  return !f32;
+}
+
 gr_status check_view(const gr_view* v) {
   if (!v) return set_error(GR_ERR_INVALID_ARGUMENT, "view is null");
   if (v->width <= 0 || v->height <= 0) return set_error(GR_ERR_INVALID_ARGUMENT, "width/height must be positive");
@@ -2276,7 +2429,7 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
         }
         GR_HIP_TRY(hipGetLastError());
       }
-      hipLaunchKernelGGL(k_work_items_zones, dim3(1), dim3(1024), 0, s, tiles, (int)Kc, (const int*)Tz[0],
+      hipLaunchKernelGGL(k_work_items_zones, dim3(1), dim3(1024), 0, s, tiles, vk.tiles_x, (int)Kc, (const int*)Tz[0],
                          (const int*)Tz[1], b.ranges, b.items, b.num_items, b.tile_item0);
       GR_HIP_TRY(hipGetLastError());
       for (int z = 0; z < 2; ++z) {
@@ -2318,7 +2471,7 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
   const int64_t cap = item_cap(vtiles, num_pairs);
   if (num_pairs > 0) {
     prof_mark(PROF_RASTER_FWD, s);
-    hipLaunchKernelGGL(k_raster_fwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
+    hipLaunchKernelGGL(fwd_split_precision() ? k_raster_fwd_mfma<true> : k_raster_fwd_mfma<false>, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
                        (const int*)b.num_items, (const int2*)b.ranges, (const int2*)b.pairs, (const float4*)g.rec,
                        sc.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
     GR_HIP_TRY(hipGetLastError());
