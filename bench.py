@@ -13,10 +13,13 @@ Synthetic data (no network): means ~ U(-0.6,0.6)^3, opacity sigmoid(-2.2), colou
 density-matched scale 0.1061*(1200/N)^(1/3); targets are seeded random images.
 
 Also reported on rank 0:
-  roofline      the dominant kernel (k_raster_bwd_mfma), timed live with HIP events on its launch
-                stream: algorithmic FLOP per launch (MFMA formulation) / average
-                launch time, against the f32 MFMA dense peak; plus its HBM traffic from rocprofv3
-                PMC counters when profiles/pmc_traffic.json exists (tools/pmc_traffic.py).
+  roofline      the dominant kernel (k_raster_bwd_bf16, the backward splat), timed live with HIP events
+                on its launch stream (gr_profile_begin/end): MFMA FLOP per launch (split-bf16
+                formulation) / average launch time, against the bf16 dense peak, with the
+                f32-equivalent rate beside it; plus its HBM traffic from rocprofv3 PMC counters when
+                profiles/pmc_traffic.json exists (tools/pmc_traffic.py).
+  hbm_model     the north_star's framing: SURVEY.md §8(d)'s byte model of the tile-binned path at the
+                measured pairs per view, and the bench value as a fraction of its 8 TB/s roofline.
   cpu_baseline  the CPU oracle (oracle/gr_oracle.c, OpenMP) on one view of the same workload.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
@@ -47,16 +50,22 @@ fm = importlib.import_module("3dgaussian_amd.fit_multiview")
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 (f32-in MFMA) dense peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense peak
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak (spec)
-MFMA_FLOP = 2 * 16 * 16 * 4  # one v_mfma_f32_16x16x4_f32
-# algorithmic FLOP per (Gaussian, tile) pair: core pairs carry every channel, tail pairs
-# (two-zone footprint) W and D only; the bench's loss has no depth term, so the backward skips tails
-FLOP_PER_CORE_PAIR_FWD = 5 / 4 * MFMA_FLOP  # 5 MFMA per 4 Gaussians
-FLOP_PER_TAIL_PAIR_FWD = 2 / 4 * MFMA_FLOP  # 2 MFMA per 4 Gaussians
-FLOP_PER_CORE_PAIR_BWD = 40 / 16 * MFMA_FLOP  # 40 MFMA per 16 Gaussians (T + R contractions)
-# the default backward runs those contractions as exact 3-piece bf16 splits: 2 sides x 3 channel
-# pairs x 6 piece products of v_mfma_f32_32x32x16_bf16 per 32 Gaussians (executed, not algorithmic)
-HW_FLOP_PER_CORE_PAIR_BWD_BF16 = 2 * 3 * 6 * (2 * 32 * 32 * 16) / 32
+MFMA_32x32x16 = 2 * 32 * 32 * 16  # FLOP of one v_mfma_f32_32x32x16_bf16
+# Backward splat without an upstream depth gradient (the bench's loss: L1 + silhouette), per core pair
+# (DESIGN.md §5): two K = 16 contractions (over x and over y) of 4 upstream channels,
+#   f32-equivalent (algorithmic) FLOP = 2 sides x 4 channels x 16 x 16 x 2 = 4096,
+#   executed on the bf16 pipe as exact 3-piece splits: 2 sides x 2 channel pairs x 6 piece products
+#   of v_mfma_f32_32x32x16_bf16 per 32 pairs = 24,576 FLOP per pair.
+F32_FLOP_PER_CORE_PAIR_BWD = 2 * 4 * 16 * 16 * 2
+BF16_FLOP_PER_CORE_PAIR_BWD = 2 * 2 * 6 * MFMA_32x32x16 / 32
+# Forward splat, f32-equivalent: 5 channels (core) / 2 channels (tail) x 16 x 16 x 2 per pair.
+F32_FLOP_PER_CORE_PAIR_FWD = 5 * 16 * 16 * 2
+F32_FLOP_PER_TAIL_PAIR_FWD = 2 * 16 * 16 * 2
 BWD_KERNEL = "k_raster_bwd_mfma" if os.environ.get("GR_BWD_F32") == "1" else "k_raster_bwd_bf16"
+# SURVEY.md §8(d) HBM model of the tile-binned algorithm (the north_star's "fraction of the HBM
+# roofline" framing): bytes per view = N (3 B_in + 2 x 36) + K (2 x 12 + 2 x 36 + 2 x 36) + 60 H W
+# with B_in = 40 (RGB), K = pairs per view as binned here.
+B_IN_RGB = 40
 
 
 def parse():
@@ -143,7 +152,7 @@ def main():
     # pairs per view for the algorithmic FLOP count (same binning as the kernels)
     pairs, core = [], []
     with torch.no_grad():
-        means, scales, colors, opac = fm.activations(params)
+        means, scales, colors, opac = fm.activations(fitter.params)
         for i in fitter.my_views:
             gv = tr.make_view(cams[i].view, cams[i].proj, R, R, None, tr.DEFAULT_CUTOFF)
             _, _, _, st = tr.forward_native(means.contiguous(), scales.contiguous(), colors.contiguous(), opac.contiguous(), gv)
@@ -154,13 +163,17 @@ def main():
         fwd_ms, fwd_n = prof["raster_fwd"]
         avg_pairs, avg_core = float(np.mean(pairs)), float(np.mean(core))
         bwd_avg_s = bwd_ms / max(bwd_n, 1) / 1e3
-        achieved = FLOP_PER_CORE_PAIR_BWD * avg_core / bwd_avg_s / 1e12
-        fwd_flop = FLOP_PER_CORE_PAIR_FWD * avg_core + FLOP_PER_TAIL_PAIR_FWD * (avg_pairs - avg_core)
+        fwd_avg_s = fwd_ms / max(fwd_n, 1) / 1e3
+        bf16_tflops = BF16_FLOP_PER_CORE_PAIR_BWD * avg_core / bwd_avg_s / 1e12
+        f32eq_tflops = F32_FLOP_PER_CORE_PAIR_BWD * avg_core / bwd_avg_s / 1e12
+        fwd_flop = F32_FLOP_PER_CORE_PAIR_FWD * avg_core + F32_FLOP_PER_TAIL_PAIR_FWD * (avg_pairs - avg_core)
         traffic = None
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
                 traffic = json.load(f).get(BWD_KERNEL, {}).get("hbm_bytes_per_launch")
+        hbm_bytes_view = n * (3 * B_IN_RGB + 2 * 36) + avg_pairs * (2 * 12 + 2 * 36 + 2 * 36) + 60 * R * R
+        hbm_roof_mpx = HBM_PEAK_GBS * 1e9 / hbm_bytes_view * R * R / 1e6
         pixels = V * R * R * args.steps
         value = pixels / elapsed / 1e6
         out = {
@@ -183,16 +196,19 @@ def main():
                        "parallelism": f"view-sharded dp{world}", "pairs_per_view": int(avg_pairs),
                        "core_pairs_per_view": int(avg_core),
                        "gaussian_order": "random" if args.no_reorder else "morton (trainer layout, fit_multiview.spatial_order)"},
-            # achieved = algorithmic (f32-accurate contraction) FLOP/s of the backward splat against the
-            # native f32 MFMA peak; the bf16-split kernel's executed MFMA rate is reported beside it
-            "roofline": {"bound": "mfma", "kernel": BWD_KERNEL, "achieved": round(achieved, 2),
-                         "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
+            # achieved = the backward splat's MFMA FLOP/s as executed on the bf16 pipe (the split-precision
+            # algorithm's own FLOP: 6 piece products per contraction) against the bf16 dense peak; its
+            # f32-equivalent rate (the contraction's FLOP at f32) is reported beside it
+            "roofline": {"bound": "mfma", "kernel": BWD_KERNEL, "achieved": round(bf16_tflops, 1),
+                         "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(bf16_tflops / BF16_MFMA_PEAK_TFLOPS, 4),
                          "traffic": traffic, "avg_launch_us": round(bwd_avg_s * 1e6, 1), "launches": bwd_n,
-                         "executed_bf16_tflops": (round(HW_FLOP_PER_CORE_PAIR_BWD_BF16 * avg_core / bwd_avg_s / 1e12, 1)
-                                                  if BWD_KERNEL.endswith("bf16") else None),
-                         "bf16_peak": BF16_MFMA_PEAK_TFLOPS,
-                         "fwd_kernel_avg_us": round(fwd_ms / max(fwd_n, 1) * 1e3, 1),
-                         "fwd_achieved_tflops": round(fwd_flop / (fwd_ms / max(fwd_n, 1) / 1e3) / 1e12, 2)},
+                         "flop_per_pair_executed": BF16_FLOP_PER_CORE_PAIR_BWD, "pairs_per_launch": int(avg_core),
+                         "f32_equivalent_tflops": round(f32eq_tflops, 1), "f32_peak": F32_MFMA_PEAK_TFLOPS,
+                         "fwd_kernel_avg_us": round(fwd_avg_s * 1e6, 1),
+                         "fwd_f32_equivalent_tflops": round(fwd_flop / fwd_avg_s / 1e12, 1)},
+            "hbm_model": {"bytes_per_view": int(hbm_bytes_view), "roofline_mpx_per_s": round(hbm_roof_mpx, 1),
+                          "frac": round(value / (hbm_roof_mpx * world), 4),
+                          "source": "SURVEY.md 8(d) tile-binned byte model at the measured pairs/view, 8 TB/s"},
             "loss": float(loss),
         }
         if not args.no_cpu_baseline and world == 1:

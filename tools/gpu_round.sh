@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU-box pass: gpu tests, bench, rocprofv3 kernel stats, PMC HBM traffic.  Usage: bash tools/gpu_round.sh <tag>
+# One GPU-box pass: gpu tests, smoke, bench, rocprofv3 kernel stats, PMC HBM traffic.  Usage: bash tools/gpu_round.sh <tag>
 set -e
 TAG=${1:-r01}
 R=${GRAFT_REPO_ROOT:-$PWD}
@@ -7,6 +7,7 @@ O=gpurun_out/$TAG
 mkdir -p $R/$O
 cd $R
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 timeout -k 10 300 python bench.py > $O/bench.log 2>&1
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/stats -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $R/$O/bench_prof.log 2>&1
