@@ -23,6 +23,7 @@ Run on 8 GPUs:    python -m torch.distributed.run --nproc-per-node 8 --master-ad
 from __future__ import annotations
 
 import argparse
+import contextlib
 import math
 import os
 import sys
@@ -44,6 +45,7 @@ else:
 RenderFn = Callable[..., tuple]
 DEVICE_DENSIFY_MIN = 100_000  # Gaussians from which densify/prune runs on the device (C5 scale)
 FUSED_LOSS = os.environ.get("GR_FUSED_LOSS", "1") != "0"  # losses.l1_loss for the L1 terms (A/B switch)
+TWO_STREAMS = os.environ.get("GR_TWO_STREAMS", "1") != "0"  # views alternate over two HIP streams (A/B switch)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -260,17 +262,42 @@ class ViewShardedFitter:
         self.opt.zero_grad(set_to_none=True)
         means, scales, colors, opacities = activations(self.params)
         device = means.device
-        total = torch.zeros((), device=device)
         # HIP renderer: the next view's preparation is enqueued before this view renders, so the
-        # host reads each view's pair count while the device is still busy (no idle gap per view)
+        # host reads each view's pair count while the device is still busy (no idle gap per view);
+        # views alternate over two HIP streams, so one view's latency-bound binning kernels run beside
+        # the other's splat kernels (autograd runs each view's backward on its forward stream)
         prefetch = self.render_fn is hip_render and means.device.type == "cuda" and means.shape[0] > 0
+        streams = [None]
+        if prefetch and TWO_STREAMS and len(self.my_views) > 1:
+            main = torch.cuda.current_stream(device)
+            if getattr(self, "_side", None) is None or self._side.device != device:
+                self._side = torch.cuda.Stream(device)
+            self._side.wait_stream(main)  # the activations are produced on the main stream
+            streams = [main, self._side]
+        totals = [torch.zeros((), device=device) for _ in streams]
         views = self.my_views
-        nxt = self._prepare(views[0], means, scales, colors, opacities) if prefetch and views else None
+
+        def on(j):
+            s = streams[j % len(streams)]
+            return torch.cuda.stream(s) if s is not None else contextlib.nullcontext()
+
+        nxt = None
+        if prefetch and views:
+            with on(0):
+                nxt = self._prepare(views[0], means, scales, colors, opacities)
         for j, i in enumerate(views):
             cur = nxt
             if prefetch and j + 1 < len(views):
-                nxt = self._prepare(views[j + 1], means, scales, colors, opacities)
-            total = total + self.view_loss(i, means, scales, colors, opacities, prepared=cur)
+                with on(j + 1):
+                    nxt = self._prepare(views[j + 1], means, scales, colors, opacities)
+            with on(j):
+                totals[j % len(streams)] = totals[j % len(streams)] + self.view_loss(i, means, scales, colors, opacities,
+                                                                                   prepared=cur)
+        if len(streams) > 1:
+            streams[0].wait_stream(streams[1])
+        total = totals[0]
+        for t in totals[1:]:
+            total = total + t
         loss = total / len(self.targets)
         if self.rank == 0:
             loss = loss + self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean()
