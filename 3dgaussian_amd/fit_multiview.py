@@ -45,7 +45,7 @@ else:
 RenderFn = Callable[..., tuple]
 DEVICE_DENSIFY_MIN = 100_000  # Gaussians from which densify/prune runs on the device (C5 scale)
 FUSED_LOSS = os.environ.get("GR_FUSED_LOSS", "1") != "0"  # losses.l1_loss for the L1 terms (A/B switch)
-TWO_STREAMS = os.environ.get("GR_TWO_STREAMS", "1") != "0"  # views alternate over two HIP streams (A/B switch)
+NUM_STREAMS = max(1, int(os.environ.get("GR_STREAMS", "3")))  # HIP streams the views rotate over
 
 
 # ------------------------------------------------------------------------------------------------
@@ -264,16 +264,19 @@ class ViewShardedFitter:
         device = means.device
         # HIP renderer: the next view's preparation is enqueued before this view renders, so the
         # host reads each view's pair count while the device is still busy (no idle gap per view);
-        # views alternate over two HIP streams, so one view's latency-bound binning kernels run beside
-        # the other's splat kernels (autograd runs each view's backward on its forward stream)
+        # views rotate over NUM_STREAMS HIP streams, so one view's latency-bound binning kernels run
+        # beside another's splat kernels (autograd runs each view's backward on its forward stream)
         prefetch = self.render_fn is hip_render and means.device.type == "cuda" and means.shape[0] > 0
         streams = [None]
-        if prefetch and TWO_STREAMS and len(self.my_views) > 1:
+        ns = min(NUM_STREAMS, len(self.my_views))
+        if prefetch and ns > 1:
             main = torch.cuda.current_stream(device)
-            if getattr(self, "_side", None) is None or self._side.device != device:
-                self._side = torch.cuda.Stream(device)
-            self._side.wait_stream(main)  # the activations are produced on the main stream
-            streams = [main, self._side]
+            side = getattr(self, "_side", None)
+            if side is None or len(side) != ns - 1 or side[0].device != device:
+                self._side = side = [torch.cuda.Stream(device) for _ in range(ns - 1)]
+            for st in side:
+                st.wait_stream(main)  # the activations are produced on the main stream
+            streams = [main] + side
         totals = [torch.zeros((), device=device) for _ in streams]
         views = self.my_views
 
@@ -293,8 +296,8 @@ class ViewShardedFitter:
             with on(j):
                 totals[j % len(streams)] = totals[j % len(streams)] + self.view_loss(i, means, scales, colors, opacities,
                                                                                    prepared=cur)
-        if len(streams) > 1:
-            streams[0].wait_stream(streams[1])
+        for st in streams[1:]:
+            streams[0].wait_stream(st)
         total = totals[0]
         for t in totals[1:]:
             total = total + t
