@@ -40,6 +40,7 @@ class GrView(ctypes.Structure):
         ("cam_pos", ctypes.c_float * 3),
         ("cutoff", ctypes.c_float),
         ("core_cutoff", ctypes.c_float),
+        ("no_depth_grad", ctypes.c_int),
     ]
 
 

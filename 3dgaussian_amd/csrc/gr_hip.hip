@@ -1051,7 +1051,7 @@ __device__ __forceinline__ f32x4 mfma16_split2(const s16x8 (&a)[2], const s16x8 
   return mfma16(a[0], b[0], c);
 }
 
-template <bool TAIL>
+template <bool TAIL, bool PRECISE>
 __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, int k1, int tid, int wave, float xc, float yc,
                                                     int gq, const int2* __restrict__ pairs, const float4* __restrict__ rec,
                                                     f32x4& cW, f32x4& cR, f32x4& cG, f32x4& cB, f32x4& cD) {
@@ -1101,11 +1101,22 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
         }
       }
       s16x8 fb[3], f3[3];
-      split3_frag(bv, fb);
-      split3_frag(aW, f3);
-      cW = mfma16_split3(f3, fb, cW);
-      split3_frag(aD, f3);
-      cD = mfma16_split3(f3, fb, cD);
+      if constexpr (PRECISE) {
+        split3_frag(bv, fb);
+        split3_frag(aW, f3);
+        cW = mfma16_split3(f3, fb, cW);
+        split3_frag(aD, f3);
+        cD = mfma16_split3(f3, fb, cD);
+      } else {  // no depth gradient will follow: W and D need only what the colours need
+        s16x8 f2b[2], f2[2];
+        split2_frag(bv, f2b);
+        fb[0] = f2b[0];
+        fb[1] = f2b[1];
+        split2_frag(aW, f2);
+        cW = mfma16_split2(f2, fb, cW);
+        split2_frag(aD, f2);
+        cD = mfma16_split2(f2, fb, cD);
+      }
       if constexpr (!TAIL) {
 #ifdef GR_FWD_RGB3
         split3_frag(aR, f3);
@@ -1217,7 +1228,9 @@ __device__ __forceinline__ void write_pixel(const ViewK& v, int p, const float* 
   savedD[p] = acc[4];
 }
 
-template <bool SPLIT>
+// MODE 0: f32 MFMA (GR_FWD_F32=1); 1: split bf16, W and D f32-grade; 2: split bf16, W and D within
+// 2^-16 (views rendered with no_depth_grad).
+template <int MODE>
 __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, int n, const int4* __restrict__ items,
                                                          const int* __restrict__ num_items, const int2* __restrict__ ranges,
                                                          const int2* __restrict__ pairs, const float4* __restrict__ rec,
@@ -1237,11 +1250,11 @@ __global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, int n, const i
   const float xc = (float)(tx * T + li) + 0.5f;  // A row = x
   const float yc = (float)(ty * T + li) + 0.5f;  // B col = y
   f32x4 cW = {0.f, 0.f, 0.f, 0.f}, cR = cW, cG = cW, cB = cW, cD = cW;
-  if constexpr (SPLIT) {
+  if constexpr (MODE > 0) {
     if (it.x & 1)
-      fwd_accumulate_bf16<true>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
+      fwd_accumulate_bf16<true, MODE == 1>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
     else
-      fwd_accumulate_bf16<false>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
+      fwd_accumulate_bf16<false, MODE == 1>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
   } else {
     if (it.x & 1)
       fwd_accumulate<true>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
@@ -2471,7 +2484,8 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
   const int64_t cap = item_cap(vtiles, num_pairs);
   if (num_pairs > 0) {
     prof_mark(PROF_RASTER_FWD, s);
-    hipLaunchKernelGGL(fwd_split_precision() ? k_raster_fwd_mfma<true> : k_raster_fwd_mfma<false>, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
+    hipLaunchKernelGGL(!fwd_split_precision() ? k_raster_fwd_mfma<0> : (v->no_depth_grad ? k_raster_fwd_mfma<2> : k_raster_fwd_mfma<1>),
+                       dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
                        (const int*)b.num_items, (const int2*)b.ranges, (const int2*)b.pairs, (const float4*)g.rec,
                        sc.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
     GR_HIP_TRY(hipGetLastError());
@@ -2489,6 +2503,9 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
                  float* d_scales, float* d_colors, float* d_opacities, void* ws, size_t ws_bytes, void* stream) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
+  if (g_depth && v->no_depth_grad)
+    return set_error(GR_ERR_INVALID_ARGUMENT,
+                     "depth gradient for a view rendered with no_depth_grad (render it with depth_grad=True)");
   if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
   if (color_dim != 3 && color_dim != 12 && color_dim != 48)
     return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");

@@ -177,10 +177,10 @@ def spatial_order(params: dict) -> dict:
     return {k: torch.nn.Parameter(v.detach()[perm].contiguous()) for k, v in params.items()}
 
 
-def hip_render(means, scales, colors, opacities, cam, width, height, background, prepared=None):
+def hip_render(means, scales, colors, opacities, cam, width, height, background, prepared=None, depth_grad=True):
     return tr.render_gaussians_torch(means, scales, colors, opacities, cam, width=width, height=height,
                                      background=background, max_gaussians=max(10000, int(means.shape[0])), return_aux=True,
-                                     prepared=prepared)
+                                     prepared=prepared, depth_grad=depth_grad)
 
 
 class ViewShardedFitter:
@@ -241,6 +241,10 @@ class ViewShardedFitter:
     def view_loss(self, i: int, means, scales, colors, opacities, prepared=None) -> torch.Tensor:
         device = means.device
         kw = {} if prepared is None else {"prepared": prepared}
+        if self.render_fn is hip_render:
+            # without a depth loss the depth output gets no gradient: the forward may accumulate W and D
+            # at the colours' precision (gr_view.no_depth_grad)
+            kw["depth_grad"] = self.depths is not None and self.w_depth > 0.0
         pred, alpha, depth = self.render_fn(means, scales, colors, opacities, self.cams[i], self.width, self.height,
                                             self._background(device), **kw)
         use_sil = self.masks is not None and self.w_sil > 0.0

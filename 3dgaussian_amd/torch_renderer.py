@@ -110,8 +110,10 @@ def _host_matrix(t: torch.Tensor) -> np.ndarray:
 
 
 def make_view(view, proj, width: int, height: int, background=None, cutoff: float = DEFAULT_CUTOFF,
-              core_cutoff: float = DEFAULT_CORE_CUTOFF) -> _native.GrView:
-    """Build a gr_view from host (numpy / tensor) matrices."""
+              core_cutoff: float = DEFAULT_CORE_CUTOFF, depth_grad: bool = True) -> _native.GrView:
+    """Build a gr_view from host (numpy / tensor) matrices.  ``depth_grad=False`` promises that the
+    depth output will get no gradient (gr_view.no_depth_grad): W and D are then accumulated within
+    2^-16 relative instead of f32-grade, and a depth gradient raises in the backward."""
     V = view if isinstance(view, np.ndarray) else _host_matrix(view)
     P = proj if isinstance(proj, np.ndarray) else _host_matrix(proj)
     V = np.asarray(V, dtype=np.float32).reshape(4, 4)
@@ -132,6 +134,7 @@ def make_view(view, proj, width: int, height: int, background=None, cutoff: floa
     gv.cam_pos[:] = cam.astype(np.float32).tolist()
     gv.cutoff = float(cutoff)
     gv.core_cutoff = float(core_cutoff)
+    gv.no_depth_grad = 0 if depth_grad else 1
     return gv
 
 
@@ -272,6 +275,9 @@ class _RasterizeGaussians(torch.autograd.Function):
         g_out = g_out.contiguous().float()
         g_alpha = None if g_alpha is None else g_alpha.contiguous().float()
         g_depth = None if g_depth is None else g_depth.contiguous().float()
+        if g_depth is not None and st.gv.no_depth_grad:
+            raise RuntimeError("the depth output was rendered with depth_grad=False and cannot be differentiated; "
+                               "render with depth_grad=True")
         dm, ds, dc, do = backward_native(means, scales, colors, opacities, st, g_out, g_alpha, g_depth)
         dbg = _grad_background(st, background, g_out) if ctx.needs_input_grad[4] else None
         return dm, ds, dc, do, dbg, None, None
@@ -295,16 +301,17 @@ def prepare_view(means, scales, colors, opacities, view, proj, width, height, ba
 
 
 def rasterize(means, scales, colors, opacities, view, proj, width, height, background=None, cutoff=DEFAULT_CUTOFF,
-              prepared: Optional[Prepared] = None, core_cutoff=DEFAULT_CORE_CUTOFF):
+              prepared: Optional[Prepared] = None, core_cutoff=DEFAULT_CORE_CUTOFF, depth_grad: bool = True):
     """Differentiable render of one view on the HIP device: returns (rgb (H,W,3), alpha (H,W), depth (H,W)).
 
-    ``prepared`` (from ``prepare_view`` with the same inputs) skips the preparation step."""
+    ``prepared`` (from ``prepare_view`` with the same inputs) skips the preparation step;
+    ``depth_grad=False``: see ``make_view``."""
     dev = means.device
     m, s, c, o = _device_inputs(means, scales, colors, opacities)
     if background is None:
         background = torch.zeros(3, dtype=torch.float32, device=dev)
     background = background.to(dtype=torch.float32, device=dev)
-    gv = make_view(view, proj, width, height, background, cutoff, core_cutoff)
+    gv = make_view(view, proj, width, height, background, cutoff, core_cutoff, depth_grad)
     return _RasterizeGaussians.apply(m, s, c, o, background, gv, prepared)
 
 
@@ -323,12 +330,14 @@ def render_gaussians_torch(
     cutoff: float = DEFAULT_CUTOFF,
     prepared: Optional[Prepared] = None,
     core_cutoff: float = DEFAULT_CORE_CUTOFF,
+    depth_grad: bool = True,
 ):
     """Differentiable Gaussian splat; signature, results and errors of torch_renderer.py:109-203.
 
     Returns ``out`` (H,W,3) or ``(out, alpha, depth)`` when ``return_aux``; ``n == 0`` returns a
     single zero image even with ``return_aux`` (torch_renderer.py:135-136).  ``cutoff``,
-    ``core_cutoff`` and ``prepared`` (see ``prepare_view``) are extensions; the reference has none.
+    ``core_cutoff``, ``prepared`` (see ``prepare_view``) and ``depth_grad`` (see ``make_view``) are
+    extensions; the reference has none.
     """
     if background is None:
         background = torch.tensor([0.0, 0.0, 0.0], dtype=torch.float32, device=means.device)
@@ -345,7 +354,8 @@ def render_gaussians_torch(
         raise ValueError("colors must be (N,3) or SH coeffs (N,4,3)")
 
     out, alpha, depth = rasterize(means, scales, colors, opacities, camera.view, camera.proj, width, height,
-                                  background=background, cutoff=cutoff, prepared=prepared, core_cutoff=core_cutoff)
+                                  background=background, cutoff=cutoff, prepared=prepared, core_cutoff=core_cutoff,
+                                  depth_grad=depth_grad)
     if not return_aux:
         return out
     return out, alpha, depth

@@ -25,13 +25,15 @@ CUTOFF = 7.0  # product defaults (3dgaussian_amd/torch_renderer.py DEFAULT_CUTOF
 CORE = 5.5
 
 
-def _run_hip(pkg, d, device, cutoff=None, with_depth=True):
+def _run_hip(pkg, d, device, cutoff=None, with_depth=True, depth_grad=True):
     tr = pkg.torch_renderer
     W, H = int(d["width"]), int(d["height"])
     t = {k: torch.from_numpy(np.ascontiguousarray(d[k])).to(device).requires_grad_(True)
          for k in ("means", "scales", "colors", "opacities")}
     cam = tr.Camera(view=torch.from_numpy(d["view"]).to(device), proj=torch.from_numpy(d["proj"]).to(device))
     kw = {} if cutoff is None else {"cutoff": cutoff}
+    if not depth_grad:
+        kw["depth_grad"] = False
     res = tr.render_gaussians_torch(t["means"], t["scales"], t["colors"], t["opacities"], cam, W, H,
                                     background=torch.from_numpy(d["background"]).to(device),
                                     max_gaussians=max(10000, d["means"].shape[0]), return_aux=True, **kw)
@@ -89,18 +91,32 @@ def test_fwd_bwd_matches_binned_oracle(pkg, cuda, name):
         assert orc.rel_l2(hip[k], ora[k]) <= 1e-4, k
 
 
+@pytest.mark.parametrize("depth_grad", [True, False])
 @pytest.mark.parametrize("name", ["f1_n300_64x48", "f1_n64_32x32_sh", "f2_c1_view0", "f2_c1_view2"])
-def test_no_depth_gradient(pkg, cuda, name):
+def test_no_depth_gradient(pkg, cuda, name, depth_grad):
     """Loss without the depth output (the fit loop's L1 + silhouette): the backward gets no depth
     gradient and skips the tail pairs of the two-zone footprint.  Against the binned oracle with the
-    same semantics, and against the exact dense answer."""
+    same semantics, and against the exact dense answer.  depth_grad=False (gr_view.no_depth_grad, what
+    the fit driver passes without a depth loss) also accumulates W and D at the colours' precision:
+    outputs and gradients still meet the bar against the reference's own outputs."""
     d = golden(name)
-    hip = _run_hip(pkg, d, cuda, with_depth=False)
+    hip = _run_hip(pkg, d, cuda, with_depth=False, depth_grad=depth_grad)
     ora = _oracle(d, binned=True, with_depth=False)
     exact = _oracle(d, binned=False, with_depth=False)
+    for k in ("out_rgb", "out_alpha", "out_depth"):
+        assert orc.rel_l2(hip[k], d[k]) <= 1e-4, k
+        assert orc.psnr(hip[k], d[k]) >= 60.0 if k == "out_rgb" else True
     for k in GRAD_KEYS:
         assert orc.rel_l2(hip[k], ora[k]) <= 1e-4, k
         assert orc.rel_l2(hip[k], exact[k]) <= 1e-4, k
+
+
+def test_depth_gradient_needs_depth_grad(pkg, cuda):
+    """A view rendered with depth_grad=False refuses a depth gradient instead of returning a less
+    accurate one."""
+    d = golden("f1_n300_64x48")
+    with pytest.raises(RuntimeError, match="depth_grad"):
+        _run_hip(pkg, d, cuda, with_depth=True, depth_grad=False)
 
 
 def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=CUTOFF):
