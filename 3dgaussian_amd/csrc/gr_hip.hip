@@ -997,14 +997,15 @@ __device__ __forceinline__ s16x8 as_frag(uint4 u) {
   return f;
 }
 
-// Split-precision forward (k_raster_fwd_mfma<true>): the same contraction on v_mfma_f32_16x16x32_bf16
-// (K = 32 Gaussians per instruction).  B = ey and the W / D operands (o ex, o z ex) are split exactly
-// into three bf16 pieces and multiplied with the six products of weight >= 2^-16 (f32-grade, as the
-// backward): the depth gradient d depth / d w = (z - depth) / (W + 1e-6) cancels catastrophically on
-// thin pixels, so W and D must carry full f32 accuracy.  The colour operands (o c ex) take two pieces,
-// hi = truncated bf16, lo = bf16(x - hi) rounded to nearest, and three products: each colour
-// accumulator is a sum of non-negative terms, each within 2^-16 of exact, so its relative error stays
-// below that (no cancellation) — far inside the 1e-4 parity bar.
+// Split-precision forward (k_raster_fwd_mfma<1|2>): the same contraction on v_mfma_f32_16x16x32_bf16
+// (K = 32 Gaussians per instruction).  Mode 1: B = ey and the W / D operands (o ex, o z ex) are split
+// exactly into three bf16 pieces and multiplied with the six products of weight >= 2^-16 (f32-grade,
+// as the backward): the depth gradient d depth / d w = (z - depth) / (W + 1e-6) cancels
+// catastrophically on thin pixels, so W and D must carry full f32 accuracy.  The colour operands
+// (o c ex) take two round-to-nearest pieces and three products (split2_frag): each colour accumulator
+// is a sum of non-negative terms, each within ~2^-16 of exact with unbiased errors, so its relative
+// error stays below that (no cancellation) — far inside the 1e-4 parity bar.  Mode 2 (no_depth_grad
+// views): W and D take the colours' two pieces too.
 // Lane l supplies A[x = l&15][g = 8(l>>4) + j] and B[g][y = l&15], j = 0..7, and receives
 // C[x = 4(l>>4) + r][y = l&15] (the f32 kernel's output map).
 __device__ __forceinline__ void split3_frag(const float (&v)[8], s16x8 (&f)[3]) {
@@ -1018,15 +1019,18 @@ __device__ __forceinline__ void split3_frag(const float (&v)[8], s16x8 (&f)[3]) 
 }
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
-// two pieces: hi = truncated bf16, lo = bf16(x - hi) rounded to nearest (v_cvt_pk_bf16_f32)
+// two pieces, both rounded to nearest (v_cvt_pk_bf16_f32): hi = bf16(x), lo = bf16(x - hi).  |x - hi|
+// <= 2^-9 |x| and |x - hi - lo| <= 2^-17 |x|, so the dropped lo*lo product is <= 2^-18 of the
+// product and every error term is unbiased (a truncated hi would leave a residual of up to 2^-7 and
+// a one-signed lo*lo of up to 2^-14).
 __device__ __forceinline__ void split2_frag(const float (&v)[8], s16x8 (&f)[2]) {
   unsigned h[4], l[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    const float h0 = __uint_as_float(__float_as_uint(v[2 * p]) & 0xffff0000u);
-    const float h1 = __uint_as_float(__float_as_uint(v[2 * p + 1]) & 0xffff0000u);
-    h[p] = pack_bf16(h0, h1);
-    const f32x2_t r = {v[2 * p] - h0, v[2 * p + 1] - h1};
+    const f32x2_t x = {v[2 * p], v[2 * p + 1]};
+    const bf16x2_t hb = __builtin_convertvector(x, bf16x2_t);
+    __builtin_memcpy(&h[p], &hb, 4);
+    const f32x2_t r = {x.x - __uint_as_float(h[p] << 16), x.y - __uint_as_float(h[p] & 0xffff0000u)};
     const bf16x2_t lb = __builtin_convertvector(r, bf16x2_t);
     __builtin_memcpy(&l[p], &lb, 4);
   }
@@ -1332,7 +1336,7 @@ __device__ __forceinline__ int kslot_pixel(int h, int j) { return (j < 4) ? 4 * 
 __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __restrict__ saved4,
                                                      const float* __restrict__ savedD, const float* __restrict__ g_rgb,
                                                      const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
-                                                     float* __restrict__ U, uint4* __restrict__ UF) {
+                                                     float* __restrict__ U, uint4* __restrict__ UF, int pieces) {
   const int tile = blockIdx.x, tid = threadIdx.x;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
@@ -1378,6 +1382,20 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
       const int side = cmb / 192, pr = (cmb / 64) % 3, l = cmb & 63;
       if (!depth && pr == 2) continue;  // never read
       const int r = l & 31, h = l >> 5, ch = pair_channel(pr, r >> 4, depth), i = r & 15;
+      uint4* o = fr + ((side * 3 + pr) * 3) * 64 + l;
+      if (pieces == 2) {  // no_depth_grad views: two round-to-nearest pieces (split2_frag)
+        float val[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int kk = kslot_pixel(h, j);
+          val[j] = ch < 0 ? 0.0f : (side == 0 ? sU[ch][i * T + kk] : sU[ch][kk * T + i]);
+        }
+        s16x8 f2[2];
+        split2_frag(val, f2);
+        __builtin_memcpy(&o[0], &f2[0], 16);
+        __builtin_memcpy(&o[64], &f2[1], 16);
+        continue;
+      }
       float hi[8], mid[8], lo[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -1385,7 +1403,6 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
         const float val = ch < 0 ? 0.0f : (side == 0 ? sU[ch][i * T + kk] : sU[ch][kk * T + i]);
         split3(val, hi[j], mid[j], lo[j]);
       }
-      uint4* o = fr + ((side * 3 + pr) * 3) * 64 + l;
       o[0] = make_uint4(pack_bf16(hi[0], hi[1]), pack_bf16(hi[2], hi[3]), pack_bf16(hi[4], hi[5]), pack_bf16(hi[6], hi[7]));
       o[64] = make_uint4(pack_bf16(mid[0], mid[1]), pack_bf16(mid[2], mid[3]), pack_bf16(mid[4], mid[5]),
                          pack_bf16(mid[6], mid[7]));
@@ -1603,6 +1620,16 @@ __device__ __forceinline__ f32x16 mfma_split(const uint4* __restrict__ A, int la
   return c;
 }
 
+// A * B over two round-to-nearest pieces each (split2_frag; no_depth_grad views): three products.
+__device__ __forceinline__ f32x16 mfma_split2(const uint4* __restrict__ A, int lane, const s16x8 (&B)[2]) {
+  f32x16 c = {};
+  const s16x8 a0 = as_frag(A[lane]);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(A[64 + lane]), B[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, B[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, B[0], c, 0, 0, 0);
+  return c;
+}
+
 // eight f32 values -> three bf16x8 operand fragments (exact split)
 __device__ __forceinline__ void split_frag(const float (&v)[8], s16x8 (&f)[3]) {
   float hi[8], mid[8], lo[8];
@@ -1614,7 +1641,7 @@ __device__ __forceinline__ void split_frag(const float (&v)[8], s16x8 (&f)[3]) {
   f[2] = as_frag(make_uint4(pack_bf16(lo[0], lo[1]), pack_bf16(lo[2], lo[3]), pack_bf16(lo[4], lo[5]), pack_bf16(lo[6], lo[7])));
 }
 
-template <bool TAIL, bool DEPTH>
+template <bool TAIL, bool DEPTH, int PIECES>
 __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, int wave, int tx, int ty,
                                               const int2* __restrict__ pairs, const float4* __restrict__ rec,
                                               float* __restrict__ partials, float4 (*sA)[TP], float4 (*sB)[TP],
@@ -1668,14 +1695,24 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
       }
       // both contractions are issued before either epilogue, so the T epilogue's VALU work runs while
       // the R MFMAs execute
-      s16x8 BT[3], BR[3];
-      split_frag(ex, BT);
-      split_frag(ey, BR);
       f32x16 DT[3], DR[3];
+      if constexpr (PIECES == 3) {
+        s16x8 BT[3], BR[3];
+        split_frag(ex, BT);
+        split_frag(ey, BR);
 #pragma unroll
-      for (int pr = P0; pr < P1; ++pr) DT[pr] = mfma_split(sUF + (0 * 3 + pr) * 3 * 64, lane, BT);
+        for (int pr = P0; pr < P1; ++pr) DT[pr] = mfma_split(sUF + (0 * 3 + pr) * 3 * 64, lane, BT);
 #pragma unroll
-      for (int pr = P0; pr < P1; ++pr) DR[pr] = mfma_split(sUF + (1 * 3 + pr) * 3 * 64, lane, BR);
+        for (int pr = P0; pr < P1; ++pr) DR[pr] = mfma_split(sUF + (1 * 3 + pr) * 3 * 64, lane, BR);
+      } else {
+        s16x8 BT[2], BR[2];
+        split2_frag(ex, BT);
+        split2_frag(ey, BR);
+#pragma unroll
+        for (int pr = P0; pr < P1; ++pr) DT[pr] = mfma_split2(sUF + (0 * 3 + pr) * 3 * 64, lane, BT);
+#pragma unroll
+        for (int pr = P0; pr < P1; ++pr) DR[pr] = mfma_split2(sUF + (1 * 3 + pr) * 3 * 64, lane, BR);
+      }
       float S[NPART] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #ifdef GR_DIAG_NOEPI
       S[0] = DT[0][0] + DR[0][1]; S[4] = DT[1][3] + DR[1][5]; S[5] = DT[0][9];
@@ -1759,7 +1796,8 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
 
 // DEPTH = 0: no upstream depth gradient (4 channels, tail items skipped) — its own kernel, so its
 // register budget is not set by the 5-channel form's.
-template <bool DEPTH>
+// PIECES = 2: no_depth_grad views (two round-to-nearest pieces per operand, three products).
+template <bool DEPTH, int PIECES>
 __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void k_raster_bwd_bf16(ViewK v, int n, const int4* __restrict__ items,
                                                            const int* __restrict__ num_items, const int2* __restrict__ pairs,
                                                            const float4* __restrict__ rec, const uint4* __restrict__ UF,
@@ -1784,11 +1822,11 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
     __syncthreads();
   }
   if constexpr (!DEPTH)
-    bwd_item_bf16<false, false>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sUF);
+    bwd_item_bf16<false, false, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sUF);
   else if (tail)
-    bwd_item_bf16<true, true>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sUF);
+    bwd_item_bf16<true, true, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sUF);
   else
-    bwd_item_bf16<false, true>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sUF);
+    bwd_item_bf16<false, true, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sUF);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2526,15 +2564,16 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
     float* U = (float*)((char*)ws + align_up((size_t)plan->num_slots * NPART * sizeof(float)));
     const bool split = bwd_split_precision();
     hipLaunchKernelGGL(k_pixel_grads, dim3(tiles), dim3(256), 0, s, vk, (const float4*)saved, saved + 4 * HW, g_rgb,
-                       g_alpha, g_depth, U, split ? (uint4*)U : (uint4*)nullptr);
+                       g_alpha, g_depth, U, split ? (uint4*)U : (uint4*)nullptr, v->no_depth_grad ? 2 : 3);
     GR_HIP_TRY(hipGetLastError());
     const int64_t cap = item_cap(2 * tiles, num_pairs);
     prof_mark(PROF_RASTER_BWD, s);
-    if (split)
-      hipLaunchKernelGGL(g_depth != nullptr ? k_raster_bwd_bf16<true> : k_raster_bwd_bf16<false>, dim3((unsigned)cap),
-                         dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items, (const int2*)b.pairs,
-                         (const float4*)g.rec, (const uint4*)U, partials);
-    else
+    if (split) {
+      auto kern = g_depth != nullptr ? k_raster_bwd_bf16<true, 3>
+                                     : (v->no_depth_grad ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>);
+      hipLaunchKernelGGL(kern, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items,
+                         (const int2*)b.pairs, (const float4*)g.rec, (const uint4*)U, partials);
+    } else
       hipLaunchKernelGGL(k_raster_bwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
                          (const int*)b.num_items, (const int2*)b.pairs, (const float4*)g.rec, (const float*)U, partials,
                          g_depth != nullptr ? 1 : 0);
