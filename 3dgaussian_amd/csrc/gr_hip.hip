@@ -1049,8 +1049,13 @@ __device__ __forceinline__ f32x4 mfma16_split3(const s16x8 (&a)[3], const s16x8 
   c = mfma16(a[0], b[1], c);
   return mfma16(a[0], b[0], c);
 }
+// a in two round-to-nearest pieces, b in the first two pieces of a split (two RNE pieces, or the
+// truncated hi + mid of an exact three-piece split, whose lo then enters as a third product so that the
+// truncation leaves no one-signed error): the products of weight >= 2^-17.
+template <bool B3>
 __device__ __forceinline__ f32x4 mfma16_split2(const s16x8 (&a)[2], const s16x8 (&b)[3], f32x4 c) {
   c = mfma16(a[1], b[0], c);
+  if constexpr (B3) c = mfma16(a[0], b[2], c);
   c = mfma16(a[0], b[1], c);
   return mfma16(a[0], b[0], c);
 }
@@ -1117,9 +1122,9 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
         fb[0] = f2b[0];
         fb[1] = f2b[1];
         split2_frag(aW, f2);
-        cW = mfma16_split2(f2, fb, cW);
+        cW = mfma16_split2<false>(f2, fb, cW);
         split2_frag(aD, f2);
-        cD = mfma16_split2(f2, fb, cD);
+        cD = mfma16_split2<false>(f2, fb, cD);
       }
       if constexpr (!TAIL) {
 #ifdef GR_FWD_RGB3
@@ -1134,11 +1139,11 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
         {
         s16x8 f2[2];
         split2_frag(aR, f2);
-        cR = mfma16_split2(f2, fb, cR);
+        cR = mfma16_split2<PRECISE>(f2, fb, cR);
         split2_frag(aG, f2);
-        cG = mfma16_split2(f2, fb, cG);
+        cG = mfma16_split2<PRECISE>(f2, fb, cG);
         split2_frag(aB, f2);
-        cB = mfma16_split2(f2, fb, cB);
+        cB = mfma16_split2<PRECISE>(f2, fb, cB);
         }
       }
     }
