@@ -19,6 +19,7 @@ t = [x.requires_grad_(True) for x in t]
 g = torch.randn(R, R, 3, device=dev)
 gd = torch.randn(R, R, device=dev) if os.environ.get("AB_DEPTH") == "1" else None
 CORE = float(os.environ.get("AB_CORE", tr.DEFAULT_CORE_CUTOFF))  # 0: one zone
+DEPTH_GRAD = gd is not None or os.environ.get("AB_PRECISE") == "1"  # no depth loss -> no_depth_grad mode
 
 
 def loss_of(out, d):
@@ -27,12 +28,12 @@ def loss_of(out, d):
 
 
 for i in range(2):
-    out, a, d = tr.rasterize(*t, *views[i], R, R, core_cutoff=CORE)
+    out, a, d = tr.rasterize(*t, *views[i], R, R, core_cutoff=CORE, depth_grad=DEPTH_GRAD)
     loss_of(out, d).backward()
 torch.cuda.synchronize()
 pkg._native.profile_begin()
 for i in range(reps):
-    out, a, d = tr.rasterize(*t, *views[i % 10], R, R, core_cutoff=CORE)
+    out, a, d = tr.rasterize(*t, *views[i % 10], R, R, core_cutoff=CORE, depth_grad=DEPTH_GRAD)
     loss_of(out, d).backward()
 torch.cuda.synchronize()
 p = pkg._native.profile_end()
