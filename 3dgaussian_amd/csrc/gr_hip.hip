@@ -1770,21 +1770,32 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
         S[7] = fmaf(tdx, dx, S[7]);
       }
       }
-      // lanes r and r + 32 hold the two halves of Gaussian r's pixels: half 0 ends with the totals of
-      // S0, S2, S4, S6, S8, half 1 with S1, S3, S5, S7
-      const float P01 = pair32(S[0], S[1]), P23 = pair32(S[2], S[3]), P45 = pair32(S[4], S[5]);
-      const float P67 = pair32(S[6], S[7]), P8 = pair32(S[8], S[8]);
+      // lanes r and r + 32 hold the two halves of Gaussian r's pixels; pair32 leaves half 0 with the
+      // total of its first argument, half 1 with that of its second
+      if constexpr (!DEPTH) {
+        // S3 (the depth sum) is zero: 8-float rows ROW8 = [o S0, o S2, S4, S6 | o S1, S8, S5, S7], half h
+        // writes float4 h: one aligned, fully coalesced 16-byte store per lane (32 rows = 1 KiB)
+        const float Pa = pair32(S[0], S[1]), Pb = pair32(S[2], S[8]), Pc = pair32(S[4], S[5]);
+        const float Pd = pair32(S[6], S[7]);
 #ifdef GR_DIAG_NOSTORE
-      if (myslot == -12345) {
+        if (myslot == -12345)
 #else
-      if (myslot >= 0) {
+        if (myslot >= 0)
 #endif
-        float* dst = partials + (size_t)myslot * NPART + h;
-        dst[0] = b.x * P01;  // colour / depth sums carry the opacity
-        dst[2] = b.x * P23;
-        dst[4] = P45;
-        dst[6] = P67;
-        if (h == 0) dst[8] = P8;
+          reinterpret_cast<float4*>(partials)[2 * (size_t)myslot + h] =
+              h == 0 ? make_float4(b.x * Pa, b.x * Pb, Pc, Pd) : make_float4(b.x * Pa, Pb, Pc, Pd);
+      } else {
+        // half 0 ends with the totals of S0, S2, S4, S6, S8, half 1 with S1, S3, S5, S7 (9-float rows)
+        const float P01 = pair32(S[0], S[1]), P23 = pair32(S[2], S[3]), P45 = pair32(S[4], S[5]);
+        const float P67 = pair32(S[6], S[7]), P8 = pair32(S[8], S[8]);
+        if (myslot >= 0) {
+          float* dst = partials + (size_t)myslot * NPART + h;
+          dst[0] = b.x * P01;  // colour / depth sums carry the opacity
+          dst[2] = b.x * P23;
+          dst[4] = P45;
+          dst[6] = P67;
+          if (h == 0) dst[8] = P8;
+        }
       }
     }
   }
@@ -1854,7 +1865,8 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
 // (pos_of), where the backward splat wrote them with coalesced stores.  Lane q sums pairs q, q+4, ...
 // (core, then tail), the 4 sums are combined in a fixed order (deterministic, no atomics), and one
 // lane per Gaussian applies the chain rule.
-template <int CD>
+// ROW8: rows written by the no-depth split backward (8 floats, see bwd_item_bf16); else 9 floats.
+template <int CD, bool ROW8>
 __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const float* __restrict__ means,
                                                     const float* __restrict__ scales, const float* __restrict__ colors,
                                                     const float* __restrict__ opac, const Cnt2* __restrict__ counts,
@@ -1878,9 +1890,22 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
     // one contiguous run of the sorted array
     const int* pc = pos_of + (long long)of.c();
     for (int j = q4; j < (int)cn.c(); j += 4) {
-      const float* src = partials + (size_t)pc[j] * NPART;
+      if constexpr (ROW8) {
+        const float4* src = reinterpret_cast<const float4*>(partials) + 2 * (size_t)pc[j];
+        const float4 u = src[0], w = src[1];  // [o S0, o S2, S4, S6], [o S1, S8, S5, S7]
+        S[0] += (double)u.x;
+        S[2] += (double)u.y;
+        S[4] += (double)u.z;
+        S[6] += (double)u.w;
+        S[1] += (double)w.x;
+        S[8] += (double)w.y;
+        S[5] += (double)w.z;
+        S[7] += (double)w.w;
+      } else {
+        const float* src = partials + (size_t)pc[j] * NPART;
 #pragma unroll
-      for (int q = 0; q < NPART; ++q) S[q] += (double)src[q];
+        for (int q = 0; q < NPART; ++q) S[q] += (double)src[q];
+      }
     }
     if (depth) {
       const int* pt = pos_of + Kc + (long long)of.t();
@@ -2586,18 +2611,21 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
     prof_mark(PROF_RASTER_BWD, s);
   }
   prof_mark(PROF_REDUCE, s);
-  if (color_dim == 3)
-    hipLaunchKernelGGL(k_reduce_bwd<3>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
-                       (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const int*)b.pos_of, (const float*)partials, d_means, d_scales, d_colors,
-                       d_opacities, g_depth != nullptr ? 1 : 0);
-  else if (color_dim == 12)
-    hipLaunchKernelGGL(k_reduce_bwd<12>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
-                       (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const int*)b.pos_of, (const float*)partials, d_means, d_scales, d_colors,
-                       d_opacities, g_depth != nullptr ? 1 : 0);
-  else
-    hipLaunchKernelGGL(k_reduce_bwd<48>, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
-                       (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const int*)b.pos_of, (const float*)partials, d_means, d_scales, d_colors,
-                       d_opacities, g_depth != nullptr ? 1 : 0);
+  {
+    // the split backward without a depth gradient writes 8-float rows (bwd_item_bf16)
+    const bool row8 = bwd_split_precision() && g_depth == nullptr;
+    auto launch = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
+                         (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const int*)b.pos_of, (const float*)partials,
+                         d_means, d_scales, d_colors, d_opacities, g_depth != nullptr ? 1 : 0);
+    };
+    if (color_dim == 3)
+      row8 ? launch(k_reduce_bwd<3, true>) : launch(k_reduce_bwd<3, false>);
+    else if (color_dim == 12)
+      row8 ? launch(k_reduce_bwd<12, true>) : launch(k_reduce_bwd<12, false>);
+    else
+      row8 ? launch(k_reduce_bwd<48, true>) : launch(k_reduce_bwd<48, false>);
+  }
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_REDUCE, s);
   return GR_OK;
