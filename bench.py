@@ -14,7 +14,8 @@ density-matched scale 0.1061*(1200/N)^(1/3); targets are seed
 
 Also reported on rank 0:
   roofline      the dominant kernel (k_raster_bwd_bf16, the backward splat), timed live with HIP events
-                on its launch stream (gr_profile_begin/end): MFMA FLOP per launch (split-bf16
+                on its launch stream (gr_profile_begin/end) over one single-stream step after the timed
+                region (the timed steps overlap views on 3 streams): MFMA FLOP per launch (split-bf16
                 formulation) / average launch time, against the bf16 dense peak, with the
                 f32-equivalent rate beside it; plus its HBM traffic from rocprofv3 PMC counters when
                 profiles/pmc_traffic.json exists (tools/pmc_traffic.py).
@@ -51,13 +52,14 @@ F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 (f32-in MFMA) dense pe
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense peak
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak (spec)
 MFMA_32x32x16 = 2 * 32 * 32 * 16  # FLOP of one v_mfma_f32_32x32x16_bf16
-# Backward splat without an upstream depth gradient (the bench's loss: L1 + silhouette), per core pair
-# (DESIGN.md §5): two K = 16 contractions (over x and over y) of 4 upstream channels,
+# Backward splat without an upstream depth gradient (the bench's loss: L1 + silhouette; the fit driver
+# renders its views with depth_grad=False), per core pair: two K = 16 contractions (over
+# x and over y) of 4 upstream channels,
 #   f32-equivalent (algorithmic) FLOP = 2 sides x 4 channels x 16 x 16 x 2 = 4096,
-#   executed on the bf16 pipe as exact 3-piece splits: 2 sides x 2 channel pairs x 6 piece products
-#   of v_mfma_f32_32x32x16_bf16 per 32 pairs = 24,576 FLOP per pair.
+#   executed on the bf16 pipe as two-piece splits: 2 sides x 2 channel pairs x 3 piece products of
+#   v_mfma_f32_32x32x16_bf16 per 32 pairs = 12,288 FLOP per pair.
 F32_FLOP_PER_CORE_PAIR_BWD = 2 * 4 * 16 * 16 * 2
-BF16_FLOP_PER_CORE_PAIR_BWD = 2 * 2 * 6 * MFMA_32x32x16 / 32
+BF16_FLOP_PER_CORE_PAIR_BWD = 2 * 2 * 3 * MFMA_32x32x16 / 32
 # Forward splat, f32-equivalent: 5 channels (core) / 2 channels (tail) x 16 x 16 x 2 per pair.
 F32_FLOP_PER_CORE_PAIR_FWD = 5 * 16 * 16 * 2
 F32_FLOP_PER_TAIL_PAIR_FWD = 2 * 16 * 16 * 2
@@ -143,8 +145,19 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    prof = pkg._native.profile_end()
+    prof_concurrent = pkg._native.profile_end()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
+    # Roofline pass: the timed steps rotate views over several HIP streams, so a launch's duration
+    # there includes kernels of other views running beside it.  One more step on a single stream gives
+    # each launch its own duration (with GR_STREAMS=1 the whole run is single-stream and both agree).
+    streams_saved = fm.NUM_STREAMS
+    fm.NUM_STREAMS = 1
+    torch.cuda.synchronize()
+    pkg._native.profile_begin()
+    fitter.step()
+    torch.cuda.synchronize()
+    prof = pkg._native.profile_end()
+    fm.NUM_STREAMS = streams_saved
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
@@ -161,6 +174,7 @@ def main():
     if rank == 0:
         bwd_ms, bwd_n = prof["raster_bwd"]
         fwd_ms, fwd_n = prof["raster_fwd"]
+        bwd_conc_us = 1e3 * prof_concurrent["raster_bwd"][0] / max(prof_concurrent["raster_bwd"][1], 1)
         avg_pairs, avg_core = float(np.mean(pairs)), float(np.mean(core))
         bwd_avg_s = bwd_ms / max(bwd_n, 1) / 1e3
         fwd_avg_s = fwd_ms / max(fwd_n, 1) / 1e3
@@ -202,6 +216,8 @@ def main():
             "roofline": {"bound": "mfma", "kernel": BWD_KERNEL, "achieved": round(bf16_tflops, 1),
                          "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(bf16_tflops / BF16_MFMA_PEAK_TFLOPS, 4),
                          "traffic": traffic, "avg_launch_us": round(bwd_avg_s * 1e6, 1), "launches": bwd_n,
+                         "timing": "HIP events on the launch stream, one single-stream step after the timed region",
+                         "avg_launch_us_in_timed_region": round(bwd_conc_us, 1), "streams_in_timed_region": streams_saved,
                          "flop_per_pair_executed": BF16_FLOP_PER_CORE_PAIR_BWD, "pairs_per_launch": int(avg_core),
                          "f32_equivalent_tflops": round(f32eq_tflops, 1), "f32_peak": F32_MFMA_PEAK_TFLOPS,
                          "fwd_kernel_avg_us": round(fwd_avg_s * 1e6, 1),
