@@ -68,11 +68,13 @@ def build_params(n: int, device: torch.device, use_sh: bool, sh_degree: int = 1)
 
 
 def activations(params: dict):
-    """fit_multiview_stub.py:268-275."""
-    means = params["means"]
+    """fit_multiview_stub.py:268-275.  Leaf parameters used as they are (means, SH coefficients) pass
+    through a view, so the per-view gradients that arrive from the render streams meet in a node made on
+    this (the main) stream rather than in the leaf's accumulator."""
+    means = params["means"].view(params["means"].shape)
     scales = torch.nn.functional.softplus(params["scales_raw"]) + 1e-3
     opacities = torch.sigmoid(params["opacities_raw"])
-    colors = params["sh_raw"] if "sh_raw" in params else torch.sigmoid(params["colors_raw"])
+    colors = params["sh_raw"].view(params["sh_raw"].shape) if "sh_raw" in params else torch.sigmoid(params["colors_raw"])
     return means, scales, colors, opacities
 
 
