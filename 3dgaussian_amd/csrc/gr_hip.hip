@@ -262,13 +262,13 @@ __device__ __forceinline__ float qcoef(float s) { return (-0.5f * LOG2E) / (s * 
 // ------------------------------------------------------------------------------------------------
 // Geometry buffer layout.
 // ------------------------------------------------------------------------------------------------
-// Per-Gaussian raster record, 64 bytes = one aligned 64-byte segment, so the random per-pair gathers of
-// the raster kernels touch one memory segment per pair (instead of one per field array):
-//   rec[4i+0] = A: px, py, qx, qy  (q = -0.5*log2(e)/sigma^2)
-//   rec[4i+1] = B: o, r, g, b (clamped)
-//   rec[4i+2] = C: z_abs, 0, 0, 0
-//   rec[4i+3] = unused (zero)
-constexpr int REC4 = 4;  // float4 per record
+// Per-Gaussian raster record, 32 bytes = one aligned 32-byte sector, so the random per-pair gathers of
+// the raster kernels touch one sector per pair and two Morton neighbours share a 64-byte segment:
+//   rec[2i+0] = A: px, py, qx, qy  (q = -0.5*log2(e)/sigma^2)
+//   rec[2i+1] = B: o, r, g, b (clamped)
+// followed (same geom part) by the camera depths z_abs[n+1] (only the forward's D channel and the
+// depth-coupled backward read them): zrec_of().
+constexpr int REC4 = 2;  // float4 per record
 
 // Per-Gaussian pair counts of the two zones, packed core | tail << 32 into one u64; its exclusive
 // scan gives each Gaussian's first core pair (low word, in [0, Kc)) and first tail pair (high word,
@@ -283,7 +283,8 @@ struct Cnt2 {
 };
 
 struct Geom {
-  float4* rec;   // [n+1][4] raster records (record n: padding)
+  float4* rec;   // [n+1][REC4] raster records (record n: padding)
+  float* zr;     // [n+1] camera depth z_abs (entry n: padding), right after the records
   int4* rect;    // tile rectangle
   unsigned long long* counts;   // n+1, packed Cnt2
   unsigned long long* offsets;  // n+1, packed Cnt2
@@ -298,7 +299,7 @@ struct Geom {
 size_t geom_fixed(int n, size_t off[GR_GEOM_PARTS]) {
   size_t o = 0;
   const size_t nn = (size_t)(n > 0 ? n : 1);
-  off[0] = o; o = align_up(o + (nn + 1) * REC4 * sizeof(float4));  // + the pad record rec[n]
+  off[0] = o; o = align_up(o + (nn + 1) * (REC4 * sizeof(float4) + sizeof(float)));  // + pad record rec[n]; z[n+1]
   off[1] = o; o = align_up(o + nn * sizeof(int4));
   off[2] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
   off[3] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
@@ -322,6 +323,7 @@ Geom geom_view(void* base, int n) {
   Geom g;
   g.plan = (gr_plan*)(b + off[4]);
   g.rec = (float4*)(b + off[0]);
+  g.zr = (float*)(g.rec + (size_t)REC4 * ((size_t)n + 1));
   g.rect = (int4*)(b + off[1]);
   g.counts = (unsigned long long*)(b + off[2]);
   g.offsets = (unsigned long long*)(b + off[3]);
@@ -510,7 +512,8 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, int n, const float*
     g.counts[n] = 0ull;
     float4* pad = g.rec + (size_t)REC4 * n;  // padding record of the raster batches (rec_of)
     pad[0] = make_float4(1e30f, 1e30f, -1.0f, -1.0f);
-    pad[1] = pad[2] = pad[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+    pad[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    g.zr[n] = 0.0f;
   }
   unsigned long long kept = 0;
   if (i < n) kept = preprocess_one<CD>(v, i, means, scales, colors, opac, g);
@@ -550,8 +553,7 @@ __device__ __forceinline__ unsigned long long preprocess_one(const ViewK& v, int
   float4* rec = g.rec + (size_t)REC4 * i;
   rec[0] = make_float4(p.px, p.py, qx, qy);
   rec[1] = make_float4(op < 0.0f ? 0.0f : op, clamp01(c[0]), clamp01(c[1]), clamp01(c[2]));
-  rec[2] = make_float4(p.za, 0.0f, 0.0f, 0.0f);
-  rec[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+  g.zr[i] = p.za;
   g.rect[i] = r;
   g.counts[i] = (unsigned long long)core | ((unsigned long long)tail << 32);
   return (unsigned long long)(core + tail);
@@ -803,6 +805,10 @@ __device__ __forceinline__ void stage_wait() { asm volatile("s_waitcnt vmcnt(0)"
 // and px = +huge, so every weight it produces is exactly 0 (exp2(-inf) = 0) without a select.
 __device__ __forceinline__ const float4* rec_of(int g, int n, const float4* __restrict__ rec) {
   return rec + (size_t)REC4 * (g >= 0 ? g : n);
+}
+// camera depth of Gaussian g (n: padding), stored after the n+1 records
+__device__ __forceinline__ const float* zrec_of(int g, int n, const float4* __restrict__ rec) {
+  return reinterpret_cast<const float*>(rec + (size_t)REC4 * ((size_t)n + 1)) + (g >= 0 ? g : n);
 }
 
 // XCD-aware work-item order: the dispatcher deals workgroups round-robin over the 8 XCDs
@@ -1070,7 +1076,7 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
     float4* sA = reinterpret_cast<float4*>(smem) + b * BUF;
     glds16(p, sA + 64 * wave);
     glds16(p + 1, sA + TP + 64 * wave);
-    glds4(p + 2, reinterpret_cast<float*>(sA + 2 * TP) + 64 * wave);
+    glds4(zrec_of(g, n, rec), reinterpret_cast<float*>(sA + 2 * TP) + 64 * wave);
   };
   stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1).x, 0);
   int2 idn = stage_id(k0 + TP + tid, k1, pairs);
@@ -1165,7 +1171,7 @@ __device__ __forceinline__ void fwd_accumulate(float* smem, int n, int k0, int k
     float4* sA = reinterpret_cast<float4*>(smem) + b * BUF;
     glds16(p, sA + 64 * wave);
     glds16(p + 1, sA + TP + 64 * wave);
-    glds4(p + 2, reinterpret_cast<float*>(sA + 2 * TP) + 64 * wave);  // z = word C .x
+    glds4(zrec_of(g, n, rec), reinterpret_cast<float*>(sA + 2 * TP) + 64 * wave);
   };
   stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1).x, 0);
   int2 idn = stage_id(k0 + TP + tid, k1, pairs);  // raw: batch base + TP
@@ -1478,7 +1484,7 @@ __device__ __forceinline__ void bwd_item(int n, int tile, int k0, int k1, int ti
     const float4* p = rec_of(pr.x, n, rec);
     glds16(p, &sA[b][64 * wave]);
     glds16(p + 1, &sB[b][64 * wave]);
-    glds4(p + 2, &sZ[b][64 * wave]);
+    glds4(zrec_of(pr.x, n, rec), &sZ[b][64 * wave]);
   };
   stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1), 0);
   int2 idn = stage_id(k0 + TP + tid, k1, pairs);  // raw: batch base + TP
@@ -1667,7 +1673,7 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
 #endif
     glds16(p, &sA[b][64 * wave]);
     glds16(p + 1, &sB[b][64 * wave]);
-    if constexpr (DEPTH) glds4(p + 2, &sZ[b][64 * wave]);  // z enters only the depth-coupled terms
+    if constexpr (DEPTH) glds4(zrec_of(pr.x, n, rec), &sZ[b][64 * wave]);  // z enters only the depth-coupled terms
   };
   stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1), 0);
   int2 idn = stage_id(k0 + TP + tid, k1, pairs);  // raw: batch base + TP

@@ -169,8 +169,8 @@ gr_status gr_l1_loss_bwd(const float* a, const float* b, int64_t n1, const float
 /* ------------------------------------------------------------------------------------------ */
 
 /* Byte offsets of the sub-buffers inside geom / bins, for debugging and bit-exact tests.
- *   geom: [0] records float4[n+1][4], 64 bytes per Gaussian (record n: padding, o = 0):
- *             A = (px, py, qx, qy), B = (o, r, g, b), C = (z, 0, 0, 0), D = 0
+ *   geom: [0] records float4[n+1][2], 32 bytes per Gaussian (record n: padding, o = 0):
+ *             A = (px, py, qx, qy), B = (o, r, g, b); then float z_abs[n+1] (entry n: 0)
  *         [1] rect int4[n] (tx0,ty0,tx1,ty1) [2] counts u64[n+1] [3] offsets u64[n+1]
  *         [4] device copy of the plan (gr_plan) and the exact pair total [5] end of the fixed part
  *         (counts/offsets packed: core tiles / first core pair in the low word, tail tiles / first

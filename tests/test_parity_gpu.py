@@ -129,7 +129,7 @@ def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=CUTOFF)
     n = m.shape[0]
     g_off = nat.geom_layout(n)
     geom = st.geom.cpu().numpy()
-    rec = geom[g_off[0]: g_off[0] + 64 * (n + 1)].view(np.float32).reshape(n + 1, 16)  # 64-byte records A|B|C|D
+    rec = geom[g_off[0]: g_off[0] + 32 * (n + 1)].view(np.float32).reshape(n + 1, 8)  # 32-byte records A|B
     rect = geom[g_off[1]: g_off[1] + 16 * n].view(np.int32).reshape(n, 4)
     # packed u64 per Gaussian: core count | tail count << 32 (and their exclusive scan)
     c64 = geom[g_off[2]: g_off[2] + 8 * n].view(np.uint64)
