@@ -337,7 +337,7 @@ Geom geom_view(void* base, int n) {
 // Bins buffer layout.
 // ------------------------------------------------------------------------------------------------
 #ifndef GR_CH
-#define GR_CH 1024
+#define GR_CH 2048
 #endif
 constexpr int CH = GR_CH;  // Gaussians per raster work item (one chunk of one tile's list)
 constexpr int NPART = 9;  // backward partial sums per (Gaussian, tile) pair
