@@ -1730,6 +1730,34 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
       if (0)
 #endif
       {
+      if constexpr (!DEPTH && PIECES == 2) {
+        // Moments about the lane's first pixel centre: dy_q = d0 + o_q with o_q = kslot offset (a compile-
+        // time constant), so sum t dy = d0 S4 + sum t o_q and sum t dy^2 = d0^2 S4 + 2 d0 sum t o_q +
+        // sum t o_q^2: two constant-coefficient fmas per pixel instead of a subtraction, two products and
+        // two sums (the same for dx).  Cancellation is bounded by the tile's 16 px (two-piece mode only).
+        const float d0y = pyb - a.y, d0x = pxb - a.x;
+        float S6c = 0.f, S8c = 0.f, U0 = 0.f, S5c = 0.f, S7c = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float oq = (float)(q < 4 ? q : q + 4);
+          const float T0 = DT[0][q], T1 = DT[0][8 + q], T2 = DT[1][q], T3 = DT[1][8 + q];
+          S[0] = fmaf(ey[q], T0, S[0]);
+          S[1] = fmaf(ey[q], T1, S[1]);
+          S[2] = fmaf(ey[q], T2, S[2]);
+          const float t = ey[q] * fmaf(b.w, T2, fmaf(b.z, T1, fmaf(b.y, T0, T3)));
+          S[4] += t;
+          S6c = fmaf(t, oq, S6c);
+          S8c = fmaf(t, oq * oq, S8c);
+          const float u = ex[q] * fmaf(b.w, DR[1][q], fmaf(b.z, DR[0][8 + q], fmaf(b.y, DR[0][q], DR[1][8 + q])));
+          U0 += u;
+          S5c = fmaf(u, oq, S5c);
+          S7c = fmaf(u, oq * oq, S7c);
+        }
+        S[6] = fmaf(d0y, S[4], S6c);
+        S[8] = fmaf(d0y * d0y, S[4], fmaf(2.0f * d0y, S6c, S8c));
+        S[5] = fmaf(d0x, U0, S5c);
+        S[7] = fmaf(d0x * d0x, U0, fmaf(2.0f * d0x, S5c, S7c));
+      } else {
       // T: rows y = kslot_pixel(h, q) of channels pair_channel(pr, c) at register 8c + q
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -1774,6 +1802,7 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
         const float tdx = (ex[q] * GR) * dx;  // (0 * G) * dx: padding stays 0, never 0 * inf
         S[5] += tdx;
         S[7] = fmaf(tdx, dx, S[7]);
+      }
       }
       }
       // lanes r and r + 32 hold the two halves of Gaussian r's pixels; pair32 leaves half 0 with the
