@@ -46,6 +46,7 @@ RenderFn = Callable[..., tuple]
 DEVICE_DENSIFY_MIN = 100_000  # Gaussians from which densify/prune runs on the device (C5 scale)
 FUSED_LOSS = os.environ.get("GR_FUSED_LOSS", "1") != "0"  # losses.l1_loss for the L1 terms (A/B switch)
 NUM_STREAMS = max(1, int(os.environ.get("GR_STREAMS", "3")))  # HIP streams the views rotate over
+PREFETCH = max(1, int(os.environ.get("GR_PREFETCH", "3")))  # views prepared ahead of the one rendering
 
 
 # ------------------------------------------------------------------------------------------------
@@ -290,18 +291,22 @@ class ViewShardedFitter:
             s = streams[j % len(streams)]
             return torch.cuda.stream(s) if s is not None else contextlib.nullcontext()
 
-        nxt = None
-        if prefetch and views:
-            with on(0):
-                nxt = self._prepare(views[0], means, scales, colors, opacities)
+        # preparations run PREFETCH views ahead (each on its view's stream), so the host's wait for a
+        # view's pair count is for work enqueued well before
+        ahead = {}
+
+        def prepare(j):
+            if prefetch and j < len(views) and j not in ahead:
+                with on(j):
+                    ahead[j] = self._prepare(views[j], means, scales, colors, opacities)
+
+        for j in range(PREFETCH):
+            prepare(j)
         for j, i in enumerate(views):
-            cur = nxt
-            if prefetch and j + 1 < len(views):
-                with on(j + 1):
-                    nxt = self._prepare(views[j + 1], means, scales, colors, opacities)
+            prepare(j + PREFETCH)
             with on(j):
                 totals[j % len(streams)] = totals[j % len(streams)] + self.view_loss(i, means, scales, colors, opacities,
-                                                                                   prepared=cur)
+                                                                                   prepared=ahead.pop(j, None))
         for st in streams[1:]:
             streams[0].wait_stream(st)
         total = totals[0]
