@@ -1924,19 +1924,39 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
     // position pos_of[e]: the block's Gaussians are consecutive, so within each tile their rows are
     // one contiguous run of the sorted array
     const int* pc = pos_of + (long long)of.c();
-    for (int j = q4; j < (int)cn.c(); j += 4) {
-      if constexpr (ROW8) {
-        const float4* src = reinterpret_cast<const float4*>(partials) + 2 * (size_t)pc[j];
-        const float4 u = src[0], w = src[1];  // [o S0, o S2, S4, S6], [o S1, S8, S5, S7]
-        S[0] += (double)u.x;
-        S[2] += (double)u.y;
-        S[4] += (double)u.z;
-        S[6] += (double)u.w;
-        S[1] += (double)w.x;
-        S[8] += (double)w.y;
-        S[5] += (double)w.z;
-        S[7] += (double)w.w;
-      } else {
+    if constexpr (ROW8) {
+      // four rows per lane in flight at a time (their positions first, then the rows), summed in the
+      // same order as one row at a time
+      const float4* rows = reinterpret_cast<const float4*>(partials);
+      const int cc = (int)cn.c();
+      for (int j0 = q4; j0 < cc; j0 += 16) {
+        int pos[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pos[u] = j0 + 4 * u < cc ? pc[j0 + 4 * u] : -1;
+        float4 ru[4], rw[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const size_t r = pos[u] >= 0 ? (size_t)pos[u] : 0;
+          ru[u] = rows[2 * r];
+          rw[u] = rows[2 * r + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (pos[u] < 0) break;
+          const float4 a = ru[u], w = rw[u];  // [o S0, o S2, S4, S6], [o S1, S8, S5, S7]
+          S[0] += (double)a.x;
+          S[2] += (double)a.y;
+          S[4] += (double)a.z;
+          S[6] += (double)a.w;
+          S[1] += (double)w.x;
+          S[8] += (double)w.y;
+          S[5] += (double)w.z;
+          S[7] += (double)w.w;
+        }
+      }
+    }
+    for (int j = q4; !ROW8 && j < (int)cn.c(); j += 4) {
+      {
         const float* src = partials + (size_t)pc[j] * NPART;
 #pragma unroll
         for (int q = 0; q < NPART; ++q) S[q] += (double)src[q];
