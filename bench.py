@@ -13,7 +13,8 @@ Synthetic data (no network): means ~ U(-0.6,0.6)^3, opacity sigmoid(-2.2), colou
 density-matched scale 0.1061*(1200/N)^(1/3); targets are seeded random images.
 
 Also reported on rank 0:
-  roofline      the dominant kernel (k_raster_bwd_bf16, the backward splat), timed live with HIP events
+  roofline      the dominant kernel (the splat kernel with the longer launches, forward or backward; both
+                under "splats"), timed live with HIP events
                 on its launch stream (gr_profile_begin/end) over one single-stream step after the timed
                 region (the timed steps overlap views on 3 streams): MFMA FLOP per launch (split-bf16
                 formulation) / average launch time, against the bf16 dense peak, with the
@@ -60,9 +61,14 @@ MFMA_32x32x16 = 2 * 32 * 32 * 16  # FLOP of one v_mfma_f32_32x32x16_bf16
 #   v_mfma_f32_32x32x16_bf16 per 32 pairs = 12,288 FLOP per pair.
 F32_FLOP_PER_CORE_PAIR_BWD = 2 * 4 * 16 * 16 * 2
 BF16_FLOP_PER_CORE_PAIR_BWD = 2 * 2 * 3 * MFMA_32x32x16 / 32
-# Forward splat, f32-equivalent: 5 channels (core) / 2 channels (tail) x 16 x 16 x 2 per pair.
+# Forward splat, f32-equivalent: 5 channels (core) / 2 channels (tail) x 16 x 16 x 2 per pair; executed
+# (depth_grad=False: two pieces, 3 products of v_mfma_f32_16x16x32_bf16 per channel per 32 pairs).
 F32_FLOP_PER_CORE_PAIR_FWD = 5 * 16 * 16 * 2
 F32_FLOP_PER_TAIL_PAIR_FWD = 2 * 16 * 16 * 2
+MFMA_16x16x32 = 2 * 16 * 16 * 32
+BF16_FLOP_PER_CORE_PAIR_FWD = 5 * 3 * MFMA_16x16x32 / 32
+BF16_FLOP_PER_TAIL_PAIR_FWD = 2 * 3 * MFMA_16x16x32 / 32
+FWD_KERNEL = "k_raster_fwd_mfma"
 BWD_KERNEL = "k_raster_bwd_mfma" if os.environ.get("GR_BWD_F32") == "1" else "k_raster_bwd_bf16"
 # SURVEY.md §8(d) HBM model of the tile-binned algorithm (the north_star's "fraction of the HBM
 # roofline" framing): bytes per view = N (3 B_in + 2 x 36) + K (2 x 12 + 2 x 36 + 2 x 36) + 60 H W
@@ -178,14 +184,38 @@ def main():
         avg_pairs, avg_core = float(np.mean(pairs)), float(np.mean(core))
         bwd_avg_s = bwd_ms / max(bwd_n, 1) / 1e3
         fwd_avg_s = fwd_ms / max(fwd_n, 1) / 1e3
-        bf16_tflops = BF16_FLOP_PER_CORE_PAIR_BWD * avg_core / bwd_avg_s / 1e12
-        f32eq_tflops = F32_FLOP_PER_CORE_PAIR_BWD * avg_core / bwd_avg_s / 1e12
-        fwd_flop = F32_FLOP_PER_CORE_PAIR_FWD * avg_core + F32_FLOP_PER_TAIL_PAIR_FWD * (avg_pairs - avg_core)
-        traffic = None
+        fwd_conc_us = 1e3 * prof_concurrent["raster_fwd"][0] / max(prof_concurrent["raster_fwd"][1], 1)
+        pmc_tab = {}
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
-                traffic = json.load(f).get(BWD_KERNEL, {}).get("hbm_bytes_per_launch")
+                pmc_tab = json.load(f)
+        avg_tail = avg_pairs - avg_core
+        # the two splat kernels; the one with the longer launches is the bench's "roofline"
+        kernels = {
+            "bwd": dict(kernel=BWD_KERNEL, t=bwd_avg_s, n=bwd_n, conc_us=bwd_conc_us,
+                        flop=BF16_FLOP_PER_CORE_PAIR_BWD * avg_core, f32=F32_FLOP_PER_CORE_PAIR_BWD * avg_core,
+                        per_pair=f"{BF16_FLOP_PER_CORE_PAIR_BWD:.0f} per core pair (tail pairs skipped)"),
+            "fwd": dict(kernel=FWD_KERNEL, t=fwd_avg_s, n=fwd_n, conc_us=fwd_conc_us,
+                        flop=BF16_FLOP_PER_CORE_PAIR_FWD * avg_core + BF16_FLOP_PER_TAIL_PAIR_FWD * avg_tail,
+                        f32=F32_FLOP_PER_CORE_PAIR_FWD * avg_core + F32_FLOP_PER_TAIL_PAIR_FWD * avg_tail,
+                        per_pair=f"{BF16_FLOP_PER_CORE_PAIR_FWD:.0f} per core pair, {BF16_FLOP_PER_TAIL_PAIR_FWD:.0f} per tail pair"),
+        }
+
+        def roof(k):
+            e = kernels[k]
+            ach = e["flop"] / e["t"] / 1e12
+            return {"bound": "mfma", "kernel": e["kernel"], "achieved": round(ach, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4),
+                    "traffic": pmc_tab.get(e["kernel"], {}).get("hbm_bytes_per_launch"),
+                    "avg_launch_us": round(e["t"] * 1e6, 1), "launches": e["n"],
+                    "timing": "HIP events on the launch stream, one single-stream step after the timed region",
+                    "avg_launch_us_in_timed_region": round(e["conc_us"], 1), "streams_in_timed_region": streams_saved,
+                    "flop_executed": e["per_pair"], "core_pairs_per_launch": int(avg_core),
+                    "tail_pairs_per_launch": int(avg_tail),
+                    "f32_equivalent_tflops": round(e["f32"] / e["t"] / 1e12, 1), "f32_peak": F32_MFMA_PEAK_TFLOPS}
+
+        dominant = "fwd" if fwd_avg_s > bwd_avg_s else "bwd"
         hbm_bytes_view = n * (3 * B_IN_RGB + 2 * 36) + avg_pairs * (2 * 12 + 2 * 36 + 2 * 36) + 60 * R * R
         hbm_roof_mpx = HBM_PEAK_GBS * 1e9 / hbm_bytes_view * R * R / 1e6
         pixels = V * R * R * args.steps
@@ -210,18 +240,11 @@ def main():
                        "parallelism": f"view-sharded dp{world}", "pairs_per_view": int(avg_pairs),
                        "core_pairs_per_view": int(avg_core),
                        "gaussian_order": "random" if args.no_reorder else "morton (trainer layout, fit_multiview.spatial_order)"},
-            # achieved = the backward splat's MFMA FLOP/s as executed on the bf16 pipe (the split-precision
-            # algorithm's own FLOP: 6 piece products per contraction) against the bf16 dense peak; its
-            # f32-equivalent rate (the contraction's FLOP at f32) is reported beside it
-            "roofline": {"bound": "mfma", "kernel": BWD_KERNEL, "achieved": round(bf16_tflops, 1),
-                         "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(bf16_tflops / BF16_MFMA_PEAK_TFLOPS, 4),
-                         "traffic": traffic, "avg_launch_us": round(bwd_avg_s * 1e6, 1), "launches": bwd_n,
-                         "timing": "HIP events on the launch stream, one single-stream step after the timed region",
-                         "avg_launch_us_in_timed_region": round(bwd_conc_us, 1), "streams_in_timed_region": streams_saved,
-                         "flop_per_pair_executed": BF16_FLOP_PER_CORE_PAIR_BWD, "pairs_per_launch": int(avg_core),
-                         "f32_equivalent_tflops": round(f32eq_tflops, 1), "f32_peak": F32_MFMA_PEAK_TFLOPS,
-                         "fwd_kernel_avg_us": round(fwd_avg_s * 1e6, 1),
-                         "fwd_f32_equivalent_tflops": round(fwd_flop / fwd_avg_s / 1e12, 1)},
+            # achieved = the splat kernel's MFMA FLOP/s as executed on the bf16 pipe (the split-precision
+            # algorithm's own FLOP: 3 piece products per contraction) against the bf16 dense peak, for the
+            # splat kernel with the longer launches; both splats in "splats", f32-equivalent rates beside
+            "roofline": roof(dominant),
+            "splats": {"fwd": roof("fwd"), "bwd": roof("bwd")},
             "hbm_model": {"bytes_per_view": int(hbm_bytes_view), "roofline_mpx_per_s": round(hbm_roof_mpx, 1),
                           "frac": round(value / (hbm_roof_mpx * world), 4),
                           "source": "SURVEY.md 8(d) tile-binned byte model at the measured pairs/view, 8 TB/s"},
