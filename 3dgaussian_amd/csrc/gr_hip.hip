@@ -1,22 +1,26 @@
 // gr_hip.hip — MI355X (gfx950, CDNA4) differentiable Gaussian rasterizer: HIP kernels + C ABI.
 //
 // Replaces src/renderer.cu (4 CUDA kernels, forward only, uint8, static buffers) and the math of
-// python/torch_renderer.py:109-203 (+ its autograd backward) with a tile-binned forward/backward:
+// python/torch_renderer.py:109-203 (+ its autograd backward) with a tile-binned forward/backward
+// (DESIGN.md §5 has the costs; gr_fwd_prepare(_async) / gr_fwd_render / gr_bwd run them in order):
 //
-//   k_preprocess   per Gaussian: project (torch_renderer.py:57-78), colour (:81-106,:144),
-//                  sigma (:146-150), cutoff*sigma box -> 16x16 tile rectangle, pair count.
-//   hipcub scan    pair offsets (exclusive), K = total pairs.
-//   k_emit         (tile, gaussian) pairs in Gaussian-index order.
-//   hipcub sort    stable LSD radix sort by tile id -> per-tile lists in Gaussian-index order.
-//   k_ranges       per-tile [start, end) of the sorted list.
-//   k_raster_fwd   one workgroup per tile; Gaussian records staged through LDS in batches of 256;
-//                  one lane per pixel accumulates W, C, D (order-independent weighted average,
-//                  torch_renderer.py:184-203); writes out/alpha/depth + 5 floats of saved state.
-//   k_raster_bwd   one workgroup per tile; per-pixel upstream vector U = (dC, dW, dD) built in LDS
-//                  from the saved state, then one lane per Gaussian walks the tile's 256 pixels
-//                  (LDS broadcast reads) and writes 9 partial sums to the pair's slot.
-//   k_reduce_bwd   one lane per Gaussian sums its pair partials in a fixed order (deterministic,
-//                  no float atomics) and applies the chain rule back to means/scales/colours/opacity.
+//   k_preprocess     per Gaussian: project (torch_renderer.py:57-78), colour (:81-106,:144), sigma
+//                    (:146-150), 7-sigma tile rectangle, tile culling into core (5.5 sigma) and tail
+//                    tiles, pair counts, 32-byte raster record.
+//   hipcub scan      pair offsets (exclusive); k_plan: pair totals (overflow-checked) for the host.
+//   k_emit_zones     (tile, Gaussian) pairs in Gaussian order: core pairs, then tail pairs.
+//   k_tile_count / k_tile_colscan / k_tile_place
+//                    stable counting sort of each zone by tile (per-tile lists in Gaussian order) and
+//                    pos_of (sorted position of each pair, by emission index).
+//   k_work_items_zones  per-(virtual) tile ranges, work items of <= CH pairs.
+//   k_raster_fwd_mfma   per work item: records staged through LDS by LDS-DMA, the separable splat as
+//                    a contraction on bf16 MFMA with split operands (f32 MFMA behind GR_FWD_F32);
+//                    k_fwd_finalize combines tiles split over several items; out/alpha/depth + saved.
+//   k_pixel_grads    per pixel upstream vector U = (dC, dW, dD), pre-split into MFMA fragments.
+//   k_raster_bwd_bf16   per work item: the two K = 16 contractions (over x, over y) of U with the
+//                    Gaussians' exponentials; 8- or 9-float partial rows at the pairs' sorted positions.
+//   k_reduce_bwd     per Gaussian: its rows (through pos_of) summed in a fixed order (deterministic, no
+//                    float atomics), then the chain rule back to means/scales/colours/opacity.
 //
 // The legacy uint8 surface (gr_render_u8, renderer_cpu.cpp semantics) reuses the binning with a
 // 3-sigma box, and adds exact depth-sorted front-to-back compositing (enable_depth_sort=1).
