@@ -1070,91 +1070,139 @@ __device__ __forceinline__ f32x4 mfma16_split2(const s16x8 (&a)[2], const s16x8 
   return mfma16(a[0], b[0], c);
 }
 
+// two-piece split of 8 values held as 4 pairs (split2_frag)
+__device__ __forceinline__ void split2_frag2(const f32x2_t (&v)[4], s16x8 (&f)[2]) {
+  float u[8];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    u[2 * p] = v[p].x;
+    u[2 * p + 1] = v[p].y;
+  }
+  split2_frag(u, f);
+}
+__device__ __forceinline__ void split3_frag2(const f32x2_t (&v)[4], s16x8 (&f)[3]) {
+  float u[8];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    u[2 * p] = v[p].x;
+    u[2 * p + 1] = v[p].y;
+  }
+  split3_frag(u, f);
+}
+
+// Staged batch layout of the split-precision forward: nine planes of TP floats (px py qx qy o r g b z),
+// one LDS-DMA dword per lane and field.  A lane's eight Gaussians of a step are then consecutive in every
+// plane (two ds_read_b128 per field) and the operand arithmetic runs on packed f32 pairs of Gaussians
+// (v_pk_add_f32 / v_pk_mul_f32: two lanes' worth per issue, the same IEEE results as the scalar ops).
+constexpr int FWD_PLANES = 9;
+
+// The LDS-DMAs of one staged Gaussian: record fields f = 0..7 (0..4 for tail items, which need no
+// colour) to plane f, z to plane 8.  One asm block: m0 is saved once, and the fields share the record's
+// address register: the instruction offset (4f) is added to the LDS address too, so m0 is set to
+// plane f's base minus 4f.
+#define GR_GLDS_FIELD(F) "s_add_u32 m0, %3, " #F "*1020\n\ts_nop 0\n\tglobal_load_lds_dword %1, off offset:" #F "*4\n\t"
+template <bool TAIL>
+__device__ __forceinline__ void glds4_planes(const float4* rec, const float* z, float* wave_base) {
+  static_assert(TP == 256, "plane stride 1024 B is written into the asm below");
+  unsigned keep;
+  if constexpr (TAIL) {
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
+                 GR_GLDS_FIELD(1) GR_GLDS_FIELD(2) GR_GLDS_FIELD(3) GR_GLDS_FIELD(4)
+                 "s_add_u32 m0, %3, 8192\n\ts_nop 0\n\tglobal_load_lds_dword %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(rec), "v"(z), "s"(lds_addr(wave_base)) : "memory", "scc");
+  } else {
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
+                 GR_GLDS_FIELD(1) GR_GLDS_FIELD(2) GR_GLDS_FIELD(3) GR_GLDS_FIELD(4)
+                 GR_GLDS_FIELD(5) GR_GLDS_FIELD(6) GR_GLDS_FIELD(7)
+                 "s_add_u32 m0, %3, 8192\n\ts_nop 0\n\tglobal_load_lds_dword %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(rec), "v"(z), "s"(lds_addr(wave_base)) : "memory", "scc");
+  }
+}
+#undef GR_GLDS_FIELD
+
 template <bool TAIL, bool PRECISE>
 __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, int k1, int tid, int wave, float xc, float yc,
                                                     int gq, const int2* __restrict__ pairs, const float4* __restrict__ rec,
                                                     f32x4& cW, f32x4& cR, f32x4& cG, f32x4& cB, f32x4& cD) {
-  constexpr int BUF = 2 * TP + TP / 4;  // float4 units per buffer (fwd_accumulate's staging layout)
+  constexpr int BUF = FWD_PLANES * TP;  // floats per buffer
   auto stage = [&](int g, int b) {
-    const float4* p = rec_of(g, n, rec);
-    float4* sA = reinterpret_cast<float4*>(smem) + b * BUF;
-    glds16(p, sA + 64 * wave);
-    glds16(p + 1, sA + TP + 64 * wave);
-    glds4(zrec_of(g, n, rec), reinterpret_cast<float*>(sA + 2 * TP) + 64 * wave);
+    glds4_planes<TAIL>(rec_of(g, n, rec), zrec_of(g, n, rec), smem + b * BUF + 64 * wave);
   };
   stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1).x, 0);
   int2 idn = stage_id(k0 + TP + tid, k1, pairs);
   int buf = 0;
+  const f32x2_t X = {xc, xc}, Y = {yc, yc};
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
     stage_wait();
     __syncthreads();
     if (base + TP < k1) stage(stage_pair(idn, base + TP + tid, k1).x, buf ^ 1);
     idn = stage_id(base + 2 * TP + tid, k1, pairs);
-    const float4* sA = reinterpret_cast<const float4*>(smem) + buf * BUF;
-    const float4* sB = sA + TP;
-    const float* sZ = reinterpret_cast<const float*>(sB + TP);
     const int cnt = min(TP, k1 - base) - wave * 64;           // Gaussians of this batch for this wave
     const int nst = cnt <= 0 ? 0 : min(2, (cnt + 31) >> 5);  // steps of 32 (padding records are zero)
     for (int st = 0; st < nst; ++st) {
-      float aW[8], aR[8], aG[8], aB[8], aD[8], bv[8];
+      const float* s = smem + buf * BUF + wave * 64 + st * 32 + 8 * gq;
+      // the eight Gaussians of field f as four pairs
+      auto ld = [&](int f, f32x2_t (&v)[4]) {
+        const float4 u0 = *reinterpret_cast<const float4*>(s + f * TP);
+        const float4 u1 = *reinterpret_cast<const float4*>(s + f * TP + 4);
+        v[0] = f32x2_t{u0.x, u0.y};
+        v[1] = f32x2_t{u0.z, u0.w};
+        v[2] = f32x2_t{u1.x, u1.y};
+        v[3] = f32x2_t{u1.z, u1.w};
+      };
+      f32x2_t px[4], py[4], qx[4], qy[4], o[4], z[4];
+      ld(0, px);
+      ld(1, py);
+      ld(2, qx);
+      ld(3, qy);
+      ld(4, o);
+      ld(8, z);
+      f32x2_t aW[4], aD[4], bv[4], oe[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int g = wave * 64 + st * 32 + 8 * gq + j;
-        const float4 a = sA[g];
-        const float z = sZ[g];
-        const float dx = xc - a.x, dy = yc - a.y;
-        const float ex = __builtin_amdgcn_exp2f(dx * a.z * dx);
-        bv[j] = __builtin_amdgcn_exp2f(dy * a.w * dy);
-        if constexpr (TAIL) {
-          const float oe = sB[g].x * ex;
-          aW[j] = oe;
-          aD[j] = oe * z;
-        } else {
-          const float4 b = sB[g];
-          const float oe = b.x * ex;
-          aW[j] = oe;
-          aR[j] = oe * b.y;
-          aG[j] = oe * b.z;
-          aB[j] = oe * b.w;
-          aD[j] = oe * z;
-        }
+      for (int p = 0; p < 4; ++p) {
+        const f32x2_t dx = X - px[p], dy = Y - py[p];
+        const f32x2_t tx = (dx * qx[p]) * dx, ty = (dy * qy[p]) * dy;
+        const f32x2_t ex = {__builtin_amdgcn_exp2f(tx.x), __builtin_amdgcn_exp2f(tx.y)};
+        bv[p] = f32x2_t{__builtin_amdgcn_exp2f(ty.x), __builtin_amdgcn_exp2f(ty.y)};
+        oe[p] = o[p] * ex;
+        aW[p] = oe[p];
+        aD[p] = oe[p] * z[p];
       }
       s16x8 fb[3], f3[3];
       if constexpr (PRECISE) {
-        split3_frag(bv, fb);
-        split3_frag(aW, f3);
+        split3_frag2(bv, fb);
+        split3_frag2(aW, f3);
         cW = mfma16_split3(f3, fb, cW);
-        split3_frag(aD, f3);
+        split3_frag2(aD, f3);
         cD = mfma16_split3(f3, fb, cD);
       } else {  // no depth gradient will follow: W and D need only what the colours need
         s16x8 f2b[2], f2[2];
-        split2_frag(bv, f2b);
+        split2_frag2(bv, f2b);
         fb[0] = f2b[0];
         fb[1] = f2b[1];
-        split2_frag(aW, f2);
+        split2_frag2(aW, f2);
         cW = mfma16_split2<false>(f2, fb, cW);
-        split2_frag(aD, f2);
+        split2_frag2(aD, f2);
         cD = mfma16_split2<false>(f2, fb, cD);
       }
       if constexpr (!TAIL) {
-#ifdef GR_FWD_RGB3
-        split3_frag(aR, f3);
-        cR = mfma16_split3(f3, fb, cR);
-        split3_frag(aG, f3);
-        cG = mfma16_split3(f3, fb, cG);
-        split3_frag(aB, f3);
-        cB = mfma16_split3(f3, fb, cB);
-        if (false)
-#endif
-        {
+        f32x2_t c[4], a[4];
         s16x8 f2[2];
-        split2_frag(aR, f2);
+        ld(5, c);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) a[p] = oe[p] * c[p];
+        split2_frag2(a, f2);
         cR = mfma16_split2<PRECISE>(f2, fb, cR);
-        split2_frag(aG, f2);
+        ld(6, c);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) a[p] = oe[p] * c[p];
+        split2_frag2(a, f2);
         cG = mfma16_split2<PRECISE>(f2, fb, cG);
-        split2_frag(aB, f2);
+        ld(7, c);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) a[p] = oe[p] * c[p];
+        split2_frag2(a, f2);
         cB = mfma16_split2<PRECISE>(f2, fb, cB);
-        }
       }
     }
   }
