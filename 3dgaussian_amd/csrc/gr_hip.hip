@@ -842,6 +842,7 @@ __device__ __forceinline__ int xcd_item(int b, int nwg) {
 // Everything is walked in pair order, so the Gaussian ids inside each tile come out ascending:
 // exactly the oracle's stable sort (oracle/gr_oracle.c gro_bin), and deterministic.
 constexpr int TS_SEG = 32;  // 64-pair steps per register-resident segment (2048 pairs per wave)
+constexpr int TS_CQ = 8;    // tiles per thread per round of k_tile_place's cursor pass
 
 __global__ __launch_bounds__(256) void k_tile_count(int64_t K, int cw, int cols, int tiles,
                                                     const uint16_t* __restrict__ keys, int* __restrict__ M) {
@@ -940,7 +941,10 @@ __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int 
 }
 
 // ranges: per virtual tile; this region's pairs go to tile t's list 2t + zone.
-__global__ __launch_bounds__(256) void k_tile_place(int64_t K, int cw, int cols, int tiles, int bits,
+#ifndef GR_PLACE_WAVES
+#define GR_PLACE_WAVES 3
+#endif
+__global__ __launch_bounds__(256, GR_PLACE_WAVES) void k_tile_place(int64_t K, int cw, int cols, int tiles, int bits,
                                                     const uint16_t* __restrict__ keys, const int* __restrict__ ids_in,
                                                     const int* __restrict__ S, const int2* __restrict__ ranges,
                                                     int zone, int zbase, int2* __restrict__ pairs_out,
@@ -953,6 +957,19 @@ __global__ __launch_bounds__(256) void k_tile_place(int64_t K, int cw, int cols,
   const int64_t k0 = (int64_t)c * cw + (int64_t)w * pw, k1 = min(K, k0 + pw);
   int d[TS_SEG], id[TS_SEG];
   ts_load(k0, k1, K - 1, lane, keys, ids_in, d, id);  // in flight while the counters are cleared
+  // Tile bases (tile start + this column's start within the tile) of the cursor pass, TS_CQ tiles per
+  // thread per round, loaded together (one memory latency per round, not one per tile); the first
+  // round is issued here, under the count pass.
+  int rx[TS_CQ], sx[TS_CQ];
+  auto load_bases = [&](int t0) {
+#pragma unroll
+    for (int q = 0; q < TS_CQ; ++q) {
+      const int t = min(t0 + q * (int)blockDim.x, tiles - 1);
+      rx[q] = ranges[2 * t + zone].x;
+      sx[q] = S[(size_t)c * tiles + t];
+    }
+  };
+  load_bases((int)threadIdx.x);
   for (int t = lane; t < tiles; t += 64) my[t] = 0;
   __builtin_amdgcn_wave_barrier();
   for (int seg = 0; seg < nseg; ++seg) {  // this wave's count per tile
@@ -965,13 +982,18 @@ __global__ __launch_bounds__(256) void k_tile_place(int64_t K, int cw, int cols,
   }
   __syncthreads();
   // cursor of (tile, wave) = tile start + column start within the tile + lower waves' counts
-#pragma unroll 4
-  for (int t = threadIdx.x; t < tiles; t += blockDim.x) {
-    int run = ranges[2 * t + zone].x + S[(size_t)c * tiles + t];
-    for (int u = 0; u < waves; ++u) {
-      const int n = cur[(size_t)u * tiles + t];
-      cur[(size_t)u * tiles + t] = run;
-      run += n;
+  for (int t0 = threadIdx.x; t0 < tiles; t0 += TS_CQ * (int)blockDim.x) {
+    if (t0 != (int)threadIdx.x) load_bases(t0);
+#pragma unroll
+    for (int q = 0; q < TS_CQ; ++q) {
+      const int t = t0 + q * (int)blockDim.x;
+      if (t >= tiles) break;
+      int run = rx[q] + sx[q];
+      for (int u = 0; u < waves; ++u) {
+        const int n = cur[(size_t)u * tiles + t];
+        cur[(size_t)u * tiles + t] = run;
+        run += n;
+      }
     }
   }
   __syncthreads();
@@ -1297,8 +1319,11 @@ __device__ __forceinline__ void write_pixel(const ViewK& v, int p, const float* 
 
 // MODE 0: f32 MFMA (GR_FWD_F32=1); 1: split bf16, W and D f32-grade; 2: split bf16, W and D within
 // 2^-16 (views rendered with no_depth_grad).
+#ifndef GR_FWD_WAVES
+#define GR_FWD_WAVES 6
+#endif
 template <int MODE>
-__global__ __launch_bounds__(256) void k_raster_fwd_mfma(ViewK v, int n, const int4* __restrict__ items,
+__global__ __launch_bounds__(256, GR_FWD_WAVES) void k_raster_fwd_mfma(ViewK v, int n, const int4* __restrict__ items,
                                                          const int* __restrict__ num_items, const int2* __restrict__ ranges,
                                                          const int2* __restrict__ pairs, const float4* __restrict__ rec,
                                                          float* __restrict__ fwd_part, float* __restrict__ out_rgb,
