@@ -842,6 +842,7 @@ __device__ __forceinline__ int xcd_item(int b, int nwg) {
 // Everything is walked in pair order, so the Gaussian ids inside each tile come out ascending:
 // exactly the oracle's stable sort (oracle/gr_oracle.c gro_bin), and deterministic.
 constexpr int TS_SEG = 32;  // 64-pair steps per register-resident segment (2048 pairs per wave)
+constexpr int TS_RB = 9, TS_RH = 1 << (TS_RB - 1);  // relative tile keys in ts_place
 constexpr int TS_CQ = 8;    // tiles per thread per round of k_tile_place's cursor pass
 
 __global__ __launch_bounds__(256) void k_tile_count(int64_t K, int cw, int cols, int tiles,
@@ -923,13 +924,23 @@ __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int 
 #pragma unroll
   for (int j = 0; j < TS_SEG; ++j) {
     const bool ok = d[j] >= 0;
-    uint64_t m = __ballot(ok);
-    if (m == 0) break;  // wave-uniform: the rest of this wave's range is past its end
-    for (int b = 0; b < bits; ++b) {
-      const bool bit = (d[j] >> b) & 1;
-      const uint64_t v = __ballot(bit);
-      m &= bit ? v : ~v;
+    const uint64_t live = __ballot(ok);
+    if (live == 0) break;  // wave-uniform: the rest of this wave's range is past its end
+    // keep the lanes whose key bit b equals this lane's: m &= ~(ballot ^ bit mask), one v_bitop3 per half
+    // Usually the step's tiles lie within TS_RH of lane 0's (neighbouring Gaussians): then the keys
+    // relative to it take TS_RB bits instead of `bits` (lane 0 is live whenever any lane is).
+    const int rel = d[j] - __builtin_amdgcn_readfirstlane(d[j]) + TS_RH;
+    const bool near = __ballot(ok && (unsigned)rel >= 2u * TS_RH) == 0;
+    const int key = near ? rel : d[j];
+    const int nb = near && TS_RB < bits ? TS_RB : bits;
+    unsigned mlo = (unsigned)live, mhi = (unsigned)(live >> 32);
+    for (int b = 0; b < nb; ++b) {
+      const int bm = __builtin_amdgcn_sbfe(key, b, 1);  // 0 or -1
+      const uint64_t v = __ballot(bm != 0);
+      mlo &= ~((unsigned)v ^ (unsigned)bm);
+      mhi &= ~((unsigned)(v >> 32) ^ (unsigned)bm);
     }
+    const uint64_t m = ((uint64_t)mhi << 32) | mlo;
     if (ok) {
       const int pos = my[d[j]] + __popcll(m & below);
       pairs_out[pos] = make_int2(id[j], kseg + j * 64 + lane);
