@@ -864,9 +864,14 @@ __global__ __launch_bounds__(256) void k_tile_count(int64_t K, int cw, int cols,
   for (int t = threadIdx.x; t < tiles; t += 256) M[(size_t)c * tiles + t] = hist[t];
 }
 
-// Column scan of M: S[c][t] = sum of M[c'][t] over c' < c, T[t] = the tile's total.  A block takes 16
-// tiles x 64 column groups, so every wave reads 64-byte runs of 16 tiles and the whole chip is busy.
-constexpr int CS_T = 16, CS_G = 64;
+// Column scan of M: S[c][t] = sum of M[c'][t] over c' < c, T[t] = the tile's total.  A block takes
+// CS_T tiles x CS_G column groups; a thread's column run (up to CS_R of them) is loaded at once and kept
+// in registers for the second pass, so the kernel waits on memory about twice instead of once per 8
+// columns and never reads M again.
+#ifndef GR_CS_T
+#define GR_CS_T 16
+#endif
+constexpr int CS_T = GR_CS_T, CS_G = 1024 / GR_CS_T, CS_R = 24;
 
 __global__ __launch_bounds__(1024) void k_tile_colscan(int cols, int tiles, const int* __restrict__ M,
                                                        int* __restrict__ S, int* __restrict__ T) {
@@ -875,10 +880,19 @@ __global__ __launch_bounds__(1024) void k_tile_colscan(int cols, int tiles, cons
   const int t = (int)blockIdx.x * CS_T + tl;
   const int per = (cols + CS_G - 1) / CS_G;
   const int c0 = min(cols, g * per), c1 = min(cols, c0 + per);
+  const bool regs = per <= CS_R;  // uniform
+  int val[CS_R];
   int sum = 0;
   if (t < tiles) {
+    if (regs) {
+#pragma unroll
+      for (int q = 0; q < CS_R; ++q) val[q] = c0 + q < c1 ? M[(size_t)(c0 + q) * tiles + t] : 0;
+#pragma unroll
+      for (int q = 0; q < CS_R; ++q) sum += val[q];
+    } else {
 #pragma unroll 8
-    for (int c = c0; c < c1; ++c) sum += M[(size_t)c * tiles + t];
+      for (int c = c0; c < c1; ++c) sum += M[(size_t)c * tiles + t];
+    }
   }
   part[g][tl] = sum;
   __syncthreads();
@@ -894,11 +908,20 @@ __global__ __launch_bounds__(1024) void k_tile_colscan(int cols, int tiles, cons
   __syncthreads();
   if (t < tiles) {
     int run = part[g][tl];
+    if (regs) {
+#pragma unroll
+      for (int q = 0; q < CS_R; ++q)
+        if (c0 + q < c1) {
+          S[(size_t)(c0 + q) * tiles + t] = run;
+          run += val[q];
+        }
+    } else {
 #pragma unroll 8
-    for (int c = c0; c < c1; ++c) {
-      const int v = M[(size_t)c * tiles + t];
-      S[(size_t)c * tiles + t] = run;
-      run += v;
+      for (int c = c0; c < c1; ++c) {
+        const int v = M[(size_t)c * tiles + t];
+        S[(size_t)c * tiles + t] = run;
+        run += v;
+      }
     }
   }
 }
