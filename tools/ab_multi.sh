@@ -4,7 +4,7 @@
 set -e
 NAMES=$1; REPS=${2:-2}
 R=${GRAFT_REPO_ROOT:-$PWD}
-summ() { grep '^{' | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(d['value'], 'bwd_us', r['avg_launch_us'], 'fwd_us', r['fwd_kernel_avg_us'])"; }
+summ() { grep '^{' | python -c "import json,sys; d=json.loads(sys.stdin.read()); sp=d['splats']; print(d['value'], 'fwd_us', sp['fwd']['avg_launch_us'], 'bwd_us', sp['bwd']['avg_launch_us'])"; }
 for i in $(seq $REPS); do
   echo -n "tree: "; timeout -k 10 300 python $R/bench.py --no-cpu-baseline 2>/dev/null | summ
   for n in $NAMES; do
