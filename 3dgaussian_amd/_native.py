@@ -164,8 +164,8 @@ GEOM_PARTS = 6
 
 
 def geom_layout(n: int):
-    """[records ((n+1) x 64 B), rect, counts (core | tail << 32, u64), their exclusive scan, device plan,
-    end of the fixed part] (gr_hip.h gr_geom_layout)."""
+    """[records ((n+1) x 32 B, then z_abs[n+1]), rect, counts (core | tail << 32, u64), their exclusive
+    scan, device plan, end of the fixed part] (gr_hip.h gr_geom_layout)."""
     out = (ctypes.c_size_t * GEOM_PARTS)()
     lib().gr_geom_layout(int(n), out)
     return list(out)
