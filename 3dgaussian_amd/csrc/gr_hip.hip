@@ -418,17 +418,22 @@ struct TSortPlan {
   size_t cells;         // tiles * cols
 };
 
-// 2048 pairs per wave (k_tile_place's register-resident segment); more segments per wave only when
+// 64 * TS_SEG pairs per wave (k_tile_place's register-resident segment); more segments per wave only when
 // the count matrix would pass 2^28 cells.
 #ifndef GR_TSORT_NSEG
 #define GR_TSORT_NSEG 1
 #endif
+#ifndef GR_TS_SEG
+#define GR_TS_SEG 24
+#endif
+constexpr int TS_SEG = GR_TS_SEG;  // 64-pair steps per register-resident segment (1536 pairs per wave;
+                                   // 16 and 32 (2048) were slower, two segments per wave much slower)
 inline TSortPlan tsort_plan(int64_t K, int tiles) {
   TSortPlan p;
   p.waves = tsort_waves(tiles);
-  int64_t pw = 2048 * GR_TSORT_NSEG;
+  int64_t pw = 64 * TS_SEG * GR_TSORT_NSEG;
   const int64_t kk = K > 0 ? K : 1;
-  // Wider columns (more 2048-pair segments per wave) while the count matrix would outweigh half the
+  // Wider columns (more segments per wave) while the count matrix would outweigh half the
   // keys and there are columns to spare: at many tiles (1080p: 8160) and many pairs the matrices
   // (M and its scan, tiles x columns ints, each read and written) otherwise dominate the sort.
   auto cols_of = [&](int64_t w) { return (kk + w * p.waves - 1) / (w * p.waves); };
@@ -447,7 +452,7 @@ inline TSortPlan tsort_plan(int64_t K, int tiles) {
 // regions), per region its row scan S and tile totals T.  Every matrix is bounded by the cells of the
 // whole array at the smallest column width (a region's plan never has more).
 size_t tsort_cells_bound(int64_t K, int tiles) {
-  const int64_t cw = 2048ll * GR_TSORT_NSEG * tsort_waves(tiles), kk = K > 0 ? K : 1;
+  const int64_t cw = 64ll * TS_SEG * GR_TSORT_NSEG * tsort_waves(tiles), kk = K > 0 ? K : 1;
   return (size_t)tiles * (size_t)((kk + cw - 1) / cw);
 }
 size_t tile_sort_tmp_bytes(int64_t K, int tiles) {
@@ -841,7 +846,6 @@ __device__ __forceinline__ int xcd_item(int b, int nwg) {
 //                   every bit), and the highest lane of each group advances the tile's cursor.
 // Everything is walked in pair order, so the Gaussian ids inside each tile come out ascending:
 // exactly the oracle's stable sort (oracle/gr_oracle.c gro_bin), and deterministic.
-constexpr int TS_SEG = 32;  // 64-pair steps per register-resident segment (2048 pairs per wave)
 constexpr int TS_RB = 9, TS_RH = 1 << (TS_RB - 1);  // relative tile keys in ts_place
 constexpr int TS_CQ = 8;    // tiles per thread per round of k_tile_place's cursor pass
 
@@ -939,7 +943,7 @@ __device__ __forceinline__ void ts_load(int64_t kb, int64_t k1, int64_t klast, i
   }
 }
 
-// One register-resident segment of k_tile_place: 32 steps of 64 pairs, in pair order.
+// One register-resident segment of k_tile_place: TS_SEG steps of 64 pairs, in pair order.
 // kseg: emission index of the segment's first pair (the slot written next to the Gaussian id).
 __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int (&d)[TS_SEG], const int (&id)[TS_SEG],
                                          int kseg, int2* __restrict__ pairs_out, int* __restrict__ pos_of) {
