@@ -7,7 +7,7 @@
 //   k_preprocess     per Gaussian: project (torch_renderer.py:57-78), colour (:81-106,:144), sigma
 //                    (:146-150), 7-sigma tile rectangle, tile culling into core (5.5 sigma) and tail
 //                    tiles, pair counts, 32-byte raster record.
-//   hipcub scan      pair offsets (exclusive); k_plan: pair totals (overflow-checked) for the host.
+//   k_plan/k_offsets pair offsets (exclusive scan: blocks, then Gaussians); pair totals (overflow-checked) for the host.
 //   k_emit_zones     (tile, Gaussian) pairs in Gaussian order: core pairs, then tail pairs.
 //   k_tile_count / k_tile_colscan / k_tile_place
 //                    stable counting sort of each zone by tile (per-tile lists in Gaussian order) and
@@ -526,7 +526,8 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, int n, const float*
   }
   unsigned long long kept = 0;
   if (i < n) kept = preprocess_one<CD>(v, i, means, scales, colors, opac, g);
-  // exact 64-bit block total of kept pairs for the overflow check (k_plan sums the blocks)
+  // the block's packed pair counts (core | tail << 32; a block's counts cannot carry): k_plan scans the
+  // blocks, k_offsets the Gaussians inside each block
   __shared__ unsigned long long wsum[4];
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) kept += __shfl_xor(kept, m);
@@ -565,7 +566,7 @@ __device__ __forceinline__ unsigned long long preprocess_one(const ViewK& v, int
   g.zr[i] = p.za;
   g.rect[i] = r;
   g.counts[i] = (unsigned long long)core | ((unsigned long long)tail << 32);
-  return (unsigned long long)(core + tail);
+  return (unsigned long long)core | ((unsigned long long)tail << 32);
 }
 
 constexpr int EWIN = 4096;  // pairs staged in LDS per emit block
@@ -2553,23 +2554,75 @@ size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan) {
 
 // Decode the scanned totals (core, tail pairs) into the plan; a count that does not fit int32 is
 // flagged as num_pairs = -1 (gr_fwd_render then reports the overflow).
-__global__ __launch_bounds__(256) void k_plan(const Cnt2* __restrict__ scanned, const unsigned long long* __restrict__ total,
-                                              int blocks, gr_plan* plan) {
-  __shared__ unsigned long long red[256];
-  unsigned long long acc = 0;
-  for (int b = threadIdx.x; b < blocks; b += 256) acc += total[b];
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-    __syncthreads();
+// Exclusive scan of one value per thread over a block of NW waves (wave shuffles, then the wave totals
+// through LDS); `total` = the block's sum.
+extern "C++" {  // inside the C-ABI section
+template <int NW>
+__device__ __forceinline__ unsigned long long block_exclusive_scan(unsigned long long x, unsigned long long* sh,
+                                                                   unsigned long long& total) {
+  const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
+  unsigned long long inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
   }
-  if (threadIdx.x != 0) return;
-  const unsigned long long pairs = red[0];
-  const bool ok = pairs < (1ull << 31);  // then neither packed word of the scan carried
-  plan->num_pairs = ok ? (long long)pairs : -1;
-  plan->num_slots = ok ? (long long)pairs : -1;  // one partial-sum slot per pair
-  plan->num_core_pairs = ok ? (long long)scanned->c() : -1;
+  __syncthreads();  // sh may still be read by a previous call
+  if (lane == 63) sh[w] = inc;
+  __syncthreads();
+  unsigned long long base = 0, all = 0;
+#pragma unroll
+  for (int u = 0; u < NW; ++u) {
+    base += u < w ? sh[u] : 0ull;
+    all += sh[u];
+  }
+  total = all;
+  return base + inc - x;
+}
+}  // extern "C++"
+
+// Pair totals and the block level of the offsets scan (one workgroup): bsum[b] (k_preprocess's packed
+// block sums) is replaced by its exclusive scan, offsets[n] gets the packed grand total.  The packed
+// words cannot carry into each other as long as K < 2^31, which is checked against the exact total
+// (the sum of every block's two words) before the plan is trusted.
+__global__ __launch_bounds__(1024) void k_plan(unsigned long long* __restrict__ bsum, int blocks,
+                                               unsigned long long* __restrict__ off_end, gr_plan* plan) {
+  __shared__ unsigned long long sh[16];
+  const int tid = (int)threadIdx.x, per = (blocks + 1023) / 1024;
+  const int b0 = min(blocks, tid * per), b1 = min(blocks, b0 + per);
+  unsigned long long acc = 0, ex = 0;
+  for (int b = b0; b < b1; ++b) {
+    const unsigned long long t = bsum[b];
+    acc += t;
+    ex += (t & 0xffffffffull) + (t >> 32);
+  }
+  unsigned long long grand, exact;
+  const unsigned long long base = block_exclusive_scan<16>(acc, sh, grand);
+  (void)block_exclusive_scan<16>(ex, sh, exact);
+  unsigned long long run = base;
+  for (int b = b0; b < b1; ++b) {
+    const unsigned long long t = bsum[b];
+    bsum[b] = run;
+    run += t;
+  }
+  if (tid != 0) return;
+  const bool ok = exact < (1ull << 31);  // then neither packed word carried
+  *off_end = grand;
+  plan->num_pairs = ok ? (long long)exact : -1;
+  plan->num_slots = ok ? (long long)exact : -1;  // one partial-sum slot per pair
+  plan->num_core_pairs = ok ? (long long)(grand & 0xffffffffull) : -1;
+}
+
+// Gaussian level of the offsets scan: offsets[i] = its block's offset + the exclusive scan of the packed
+// counts inside the block (the blocks are k_preprocess's).
+__global__ __launch_bounds__(256) void k_offsets(int n, const unsigned long long* __restrict__ counts,
+                                                 const unsigned long long* __restrict__ boff,
+                                                 unsigned long long* __restrict__ offsets) {
+  __shared__ unsigned long long sh[4];
+  const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+  unsigned long long tot;
+  const unsigned long long e = block_exclusive_scan<4>(i < n ? counts[i] : 0ull, sh, tot);
+  if (i < n) offsets[i] = boff[blockIdx.x] + e;
 }
 
 gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, const float* scales, const float* colors,
@@ -2599,10 +2652,11 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
   else
     hipLaunchKernelGGL(k_preprocess<48>, dim3(blocks_for(n + 1)), dim3(256), 0, s, vk, n, means, scales, colors, opacities, g);
   GR_HIP_TRY(hipGetLastError());
-  size_t tmp = scan_tmp_bytes(n);
-  GR_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(g.scan_tmp, tmp, g.counts, g.offsets, n + 1, s));
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(256), 0, s, (const Cnt2*)(g.offsets + n), (const unsigned long long*)g.total,
-                     blocks_for(n + 1), g.plan);
+  // exclusive scan of the packed counts: blocks (k_plan), then Gaussians (k_offsets)
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, g.total, blocks_for(n + 1), g.offsets + n, g.plan);
+  GR_HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_offsets, dim3(blocks_for(n)), dim3(256), 0, s, n, (const unsigned long long*)g.counts,
+                     (const unsigned long long*)g.total, g.offsets);
   GR_HIP_TRY(hipGetLastError());
   GR_HIP_TRY(hipMemcpyAsync(plan, g.plan, sizeof(gr_plan), hipMemcpyDeviceToHost, s));
   return GR_OK;
