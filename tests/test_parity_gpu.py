@@ -147,9 +147,11 @@ def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=CUTOFF)
 
 
 @pytest.mark.parametrize("case", ["f1_n300_64x48", "f2_c1_view1", "c2_100k_512", "edge_big_sigma", "hd_1920x1080",
-                                  "xl_2304x2304"])
+                                  "xl_2304x2304", "n768_whole_blocks", "n300k_512"])
 def test_bins_bit_exact(pkg, cuda, case):
-    """hd: 8160 tiles (counting sort, 2 waves per column); xl: 20736 tiles (radix-sort fallback)."""
+    """hd: 8160 tiles (counting sort, 2 waves per column); xl: 20736 tiles (radix-sort fallback);
+    n768: N a multiple of the 256-Gaussian scan block (the padding entry opens a block of its own);
+    n300k: more scan blocks than k_plan's 1024 threads (several per thread)."""
     if case.startswith("f"):
         d = golden(case)
         scene = orc.Scene(d["means"], d["scales"], d["colors"], d["opacities"])
@@ -157,6 +159,14 @@ def test_bins_bit_exact(pkg, cuda, case):
     elif case == "c2_100k_512":
         scene = orc.synthetic_scene(100_000, seed=3)
         view, proj = orc.orbit_cameras(8, 512, 512)[5]
+        W = H = 512
+    elif case == "n768_whole_blocks":
+        scene = orc.synthetic_scene(768, seed=8)
+        view, proj = orc.orbit_cameras(4, 160, 96)[2]
+        W, H = 160, 96
+    elif case == "n300k_512":
+        scene = orc.synthetic_scene(300_000, seed=9)
+        view, proj = orc.orbit_cameras(8, 512, 512)[1]
         W = H = 512
     elif case in ("hd_1920x1080", "xl_2304x2304"):
         W, H = (1920, 1080) if case.startswith("hd") else (2304, 2304)
