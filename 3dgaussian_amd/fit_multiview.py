@@ -47,6 +47,9 @@ DEVICE_DENSIFY_MIN = 100_000  # Gaussians from which densify/prune runs on the d
 FUSED_LOSS = os.environ.get("GR_FUSED_LOSS", "1") != "0"  # losses.l1_loss for the L1 terms (A/B switch)
 NUM_STREAMS = max(1, int(os.environ.get("GR_STREAMS", "3")))  # HIP streams the views rotate over
 PREFETCH = max(1, int(os.environ.get("GR_PREFETCH", "3")))  # views prepared ahead of the one rendering
+# steps between re-establishing the Morton order of the moving Gaussians (ViewShardedFitter.respatialize;
+# 0 = only at construction and after densify/prune)
+RESORT_EVERY = max(0, int(os.environ.get("GR_RESORT", "4")))
 
 
 # ------------------------------------------------------------------------------------------------
@@ -199,6 +202,13 @@ class ViewShardedFitter:
         # order densify_and_prune and gaussians_fitted.npz see: top-k ties and jitter draws follow it)
         self.reorder = reorder
         self.perm = None
+        self.group = group
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            # data parallelism needs identical replicas: rank 0's initial parameters win (the Morton
+            # permutation below is then computed from identical means on every rank)
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            for k in sorted(params):
+                dist.broadcast(params[k].data, src, group=group)
         if reorder and params["means"].shape[0] >= 2:
             self.perm = morton_order(params["means"])
             params = {k: torch.nn.Parameter(v.detach()[self.perm].contiguous()) for k, v in params.items()}
@@ -215,6 +225,7 @@ class ViewShardedFitter:
         self.my_views = list(range(self.rank, len(targets), self.world))
         self.opt = torch.optim.Adam(list(self.params.values()), lr=lr)
         self.densify_seed = 1234
+        self.steps_done = 0
 
     def canonical_params(self) -> dict:
         """The parameters in the stub's order (undoes the trainer's Morton permutation)."""
@@ -226,6 +237,22 @@ class ViewShardedFitter:
             c[self.perm] = v.detach()
             out[k] = torch.nn.Parameter(c)
         return out
+
+    def respatialize(self) -> None:
+        """Re-establish the Morton order of the Gaussians as they move during the fit: parameters and
+        Adam moments are permuted in place (the optimizer keeps its state), self.perm follows."""
+        if not self.reorder or self.params["means"].shape[0] < 2:
+            return
+        with torch.no_grad():
+            p2 = morton_order(self.params["means"])
+            for p in self.params.values():
+                p.data.copy_(p.data[p2])
+                st = self.opt.state.get(p)
+                if st:
+                    for k in ("exp_avg", "exp_avg_sq"):
+                        if k in st:
+                            st[k].copy_(st[k][p2])
+            self.perm = p2 if self.perm is None else self.perm[p2]
 
     def reset_optimizer(self) -> None:
         self.opt = torch.optim.Adam(list(self.params.values()), lr=self.lr)
@@ -266,6 +293,9 @@ class ViewShardedFitter:
 
     def step(self) -> torch.Tensor:
         """One iteration; returns the full (all-rank) loss as a 0-d tensor on the device."""
+        if RESORT_EVERY and self.steps_done and self.steps_done % RESORT_EVERY == 0:
+            self.respatialize()
+        self.steps_done += 1
         self.opt.zero_grad(set_to_none=True)
         means, scales, colors, opacities = activations(self.params)
         device = means.device
@@ -284,7 +314,9 @@ class ViewShardedFitter:
             for st in side:
                 st.wait_stream(main)  # the activations are produced on the main stream
             streams = [main] + side
-        totals = [torch.zeros((), device=device) for _ in streams]
+        # per-stream accumulators start empty and are created by their stream's first view (a zeros
+        # tensor made here on the main stream would be read by a side stream with no ordering)
+        totals: list = [None for _ in streams]
         views = self.my_views
 
         def on(j):
@@ -305,13 +337,19 @@ class ViewShardedFitter:
         for j, i in enumerate(views):
             prepare(j + PREFETCH)
             with on(j):
-                totals[j % len(streams)] = totals[j % len(streams)] + self.view_loss(i, means, scales, colors, opacities,
-                                                                                   prepared=ahead.pop(j, None))
+                k = j % len(streams)
+                lv = self.view_loss(i, means, scales, colors, opacities, prepared=ahead.pop(j, None))
+                totals[k] = lv if totals[k] is None else totals[k] + lv
         for st in streams[1:]:
             streams[0].wait_stream(st)
-        total = totals[0]
-        for t in totals[1:]:
-            total = total + t
+        total = None
+        for t in totals:
+            if t is not None:
+                total = t if total is None else total + t
+        if total is None:
+            # a rank with no views (world size > number of views): a zero loss that still reaches every
+            # parameter, so backward() runs and the rank joins the all-reduce with zero gradients
+            total = sum(p.sum() for p in self.params.values()) * 0.0
         loss = total / len(self.targets)
         if self.rank == 0:
             loss = loss + self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean()
@@ -429,15 +467,18 @@ def main(argv=None) -> None:
     ap.add_argument("--reg_opacity", type=float, default=0.001)
     ap.add_argument("--reg_scale", type=float, default=0.001)
     ap.add_argument("--seed", type=int, default=None, help="torch.manual_seed before initialisation")
+    ap.add_argument("--device", default="", help="cpu: host tensors (cpu_renderer, gloo); default: the HIP device")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    on_host = args.device == "cpu" or not torch.cuda.is_available()
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        if not on_host:
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group("gloo" if on_host else "nccl")
     rank = dist.get_rank() if world > 1 else 0
-    device = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    device = torch.device("cpu") if on_host else torch.device("cuda", local_rank)
     if args.seed is not None:
         torch.manual_seed(args.seed)
     if rank == 0:

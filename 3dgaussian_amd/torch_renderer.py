@@ -14,11 +14,14 @@ libgr_hip.so through a ``torch.autograd.Function`` — not by torch ops.  Differ
   dense reference to <=5e-6 relative L2 on its own fixtures, with and without depth gradients;
 * ``chunk_size`` is accepted and ignored (no chunk loop);
 * gradients flow to means, scales, colours/SH, opacities and background; not to the camera matrices;
-* tensors must live on a HIP device: CPU tensors raise ``RuntimeError`` (there is no CPU fallback).
+* the op dispatches on the tensors' device like the reference: HIP tensors always run the HIP kernels
+  (a missing libgr_hip.so raises ImportError; nothing falls back), CPU tensors run ``cpu_renderer``'s
+  dense torch op (config C1, the reference's own CPU plumbing case; no tile cutoff there).
 """
 from __future__ import annotations
 
 import ctypes
+import weakref
 from dataclasses import dataclass
 from typing import Optional
 
@@ -26,9 +29,10 @@ import numpy as np
 import torch
 
 try:  # package import (3dgaussian_amd.torch_renderer) or flat import (drop-in on sys.path)
-    from . import _native
+    from . import _native, cpu_renderer
 except ImportError:  # pragma: no cover
     import _native  # type: ignore
+    import cpu_renderer  # type: ignore
 
 DEFAULT_CUTOFF = 7.0
 DEFAULT_CORE_CUTOFF = 5.5
@@ -96,13 +100,26 @@ def _host_copy(t: torch.Tensor, shape) -> np.ndarray:
     read them twice."""
     key = (id(t), t.data_ptr(), t._version, str(t.device))
     hit = _MAT_CACHE.get(key)
-    if hit is not None and hit[0] is t:
+    if hit is not None and hit[0]() is t:
         return hit[1]
     m = t.detach().to(device="cpu", dtype=torch.float32).reshape(shape).numpy().copy()
     if len(_MAT_CACHE) > 4096:
         _MAT_CACHE.clear()
-    _MAT_CACHE[key] = (t, m)
+    # a weak reference: the cache never keeps a caller's tensor alive (a dead entry can only miss)
+    _MAT_CACHE[key] = (weakref.ref(t), m)
     return m
+
+
+_ZERO_BG: dict = {}
+
+
+def _default_background(device: torch.device) -> torch.Tensor:
+    """The background=None value (zeros), one persistent tensor per device: its host copy is cached,
+    so a caller that passes no background costs no device-to-host read per view."""
+    t = _ZERO_BG.get(str(device))
+    if t is None:
+        t = _ZERO_BG[str(device)] = torch.zeros(3, dtype=torch.float32, device=device)
+    return t
 
 
 def _host_matrix(t: torch.Tensor) -> np.ndarray:
@@ -319,9 +336,15 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
     ``prepared`` (from ``prepare_view`` with the same inputs) skips the preparation step;
     ``depth_grad=False``: see ``make_view``."""
     dev = means.device
+    if dev.type != "cuda":
+        # tensors on the host: the dense CPU op (config C1; cpu_renderer.py).  HIP tensors never take it.
+        if background is None:
+            background = torch.zeros(3, dtype=torch.float32, device=dev)
+        return cpu_renderer.render(means, scales, colors, opacities, view, proj, width, height,
+                                   background.to(dtype=torch.float32, device=dev))
     m, s, c, o = _device_inputs(means, scales, colors, opacities)
     if background is None:
-        background = torch.zeros(3, dtype=torch.float32, device=dev)
+        background = _default_background(dev)
     background = background.to(dtype=torch.float32, device=dev)
     gv = make_view(view, proj, width, height, background, cutoff, core_cutoff, depth_grad)
     return _RasterizeGaussians.apply(m, s, c, o, background, gv, prepared)
@@ -352,7 +375,7 @@ def render_gaussians_torch(
     extensions; the reference has none.
     """
     if background is None:
-        background = torch.tensor([0.0, 0.0, 0.0], dtype=torch.float32, device=means.device)
+        background = _default_background(means.device)
     background = background.to(dtype=torch.float32, device=means.device)
 
     if means.ndim != 2 or means.shape[1] != 3:

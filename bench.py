@@ -14,19 +14,25 @@ density-matched scale 0.1061*(1200/N)^(1/3); targets are seed
 
 Also reported on rank 0:
   roofline      the dominant kernel (the splat kernel with the longer launches, forward or backward; both
-                under "splats"), timed live with HIP events
-                on its launch stream (gr_profile_begin/end) over one single-stream step after the timed
-                region (the timed steps overlap views on 3 streams): MFMA FLOP per launch (split-bf16
-                formulation) / average launch time, against the bf16 dense peak, with the
-                f32-equivalent rate beside it; plus its HBM traffic from rocprofv3 PMC counters when
-                profiles/pmc_traffic.json exists (tools/pmc_traffic.py).
-  hbm_model     the north_star's framing: SURVEY.md §8(d)'s byte model of the tile-binned path at the
-                measured pairs per view, and the bench value as a fraction of its 8 TB/s roofline.
+                under "splats") against the HBM roofline: SURVEY.md 8(d)'s algorithmic bytes per unit
+                (48 B per pair forward, 84 B per core pair backward, + 40 B per pixel) x the units of one
+                launch / its average launch time (HIP events on its launch stream, gr_profile_begin/end,
+                over one single-stream step after the timed region: the timed steps overlap views on 3
+                streams), vs 8 TB/s; its PMC HBM traffic from profiles/pmc_traffic.json
+                (tools/pmc_traffic.py); the executed bf16 MFMA rate beside it
+  hbm_model     the north_star's framing: SURVEY.md 8(d)'s byte model of the tile-binned path per view at
+                the survey's fixed 5-sigma footprint and at this build's 7-sigma pair count, and the bench
+                value as a fraction of each 8 TB/s roofline
+  default_precision_mode
+                a few more timed steps with a depth term in the loss (the f32-grade mode a depth-loss
+                caller gets; the headline runs the fit's own loss, which has no depth term)
+  sclk_mhz      the shader clock before and after (rocm-smi)
   cpu_baseline  the CPU oracle (oracle/gr_oracle.c, OpenMP) on one view of the same workload.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--device cpu]
 N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
      --master-port P bench.py --gpus N --steps K --warmup W
+     (or plain `python bench.py --gpus N`: it starts that launcher itself as a child process)
 """
 from __future__ import annotations
 
@@ -85,9 +91,43 @@ def parse():
     ap.add_argument("--views", type=int, default=50)
     ap.add_argument("--res", type=int, default=800)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra-modes", action="store_true",
+                    help="skip the extra timed steps of the default (depth-loss) precision mode")
+    ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
+                    help="cpu: a dry run of the launcher and sharding on host tensors (gloo; cpu_renderer), "
+                         "not a measurement")
     ap.add_argument("--no-reorder", action="store_true",
                     help="keep the synthetic Gaussians in their random order (A/B of the trainer's Morton order)")
     return ap.parse_args()
+
+
+def launch(args) -> int:
+    """``--gpus N`` without a torch.distributed environment: start N local ranks with
+    torch.distributed.run (one process per GPU) as a child process, before this process touches the GPU,
+    and return its exit status.  The driver's own command (torch.distributed.run ... bench.py --gpus N)
+    sets WORLD_SIZE and never comes here."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def sclk_mhz():
+    """Current shader clock of the visible GPU (rocm-smi), or None."""
+    import subprocess
+
+    try:
+        r = subprocess.run(["rocm-smi", "--showclocks", "--json"], capture_output=True, text=True, timeout=20)
+        card = next(iter(json.loads(r.stdout).values()))
+        v = card.get("sclk clock speed:", "")
+        return int(v.strip("()Mhz")) if v else None
+    except Exception:  # noqa: BLE001 - diagnostics only
+        return None
 
 
 def synthetic_params(n: int, device) -> dict:
@@ -119,16 +159,42 @@ def cpu_baseline(n: int, res: int, views: int) -> dict:
                       f"OpenMP {cores} threads, {dt:.1f} s"}
 
 
+def pairs_per_view(fitter, cams, R, cutoff, core_cutoff):
+    """Mean (pairs, core pairs) per view of this rank's views at the given footprint (the same
+    binning kernels as the render; no splat)."""
+    pairs, core = [], []
+    with torch.no_grad():
+        means, scales, colors, opac = fm.activations(fitter.params)
+        m, s, c, o = (t.contiguous() for t in (means, scales, colors, opac))
+        for i in fitter.my_views:
+            gv = tr.make_view(cams[i].view, cams[i].proj, R, R, None, cutoff, core_cutoff)
+            plan = tr.prepare_native(m, s, c, o, gv).plan()
+            pairs.append(int(plan.num_pairs))
+            core.append(int(plan.num_core_pairs))
+    return float(np.mean(pairs)), float(np.mean(core))
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    on_gpu = args.device == "cuda"
+    if on_gpu:
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+    else:
+        device = torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if on_gpu:
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
+    sync = torch.cuda.synchronize if on_gpu else (lambda: None)
     n, V, R = args.gaussians, args.views, args.res
+    clk0 = sclk_mhz() if (on_gpu and rank == 0) else None
 
     params = synthetic_params(n, device)
     cams = fm.orbit_cameras(V, R, R, device)
@@ -136,90 +202,128 @@ def main():
     targets = [torch.rand((R, R, 3), generator=g, device=device) for _ in range(V)]
     masks = [(t.mean(dim=2) > 0.5).to(torch.float32) for t in targets]
     fitter = fm.ViewShardedFitter(params, cams, targets, R, R, lr=0.02, masks=masks, reorder=not args.no_reorder)
+    views_per_rank = [len(range(r, V, world)) for r in range(world)]
+
+    def timed(steps):
+        sync()
+        if world > 1:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        loss = None
+        for _ in range(steps):
+            loss = fitter.step()
+        sync()
+        if world > 1:
+            dist.barrier()
+        dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        return float(dt.item()), loss
 
     for _ in range(args.warmup):
         fitter.step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    pkg._native.profile_begin()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = fitter.step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    prof_concurrent = pkg._native.profile_end()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
+    if on_gpu:
+        pkg._native.profile_begin()
+    elapsed, loss = timed(args.steps)
+    prof_concurrent = pkg._native.profile_end() if on_gpu else None
+    pixels = V * R * R * args.steps
+    value = pixels / elapsed / 1e6
+
+    if not on_gpu:  # dry run of the launcher / sharding: no measurement keys
+        if rank == 0:
+            print(json.dumps({"metric": "Mpixels/sec fwd+bwd @1M Gaussians 800x800 (dry run on host tensors)",
+                              "value": round(value, 4), "unit": "Mpixels/sec", "n_gpus": world, "steps": args.steps,
+                              "warmup": args.warmup, "device": "cpu", "views_per_rank": views_per_rank,
+                              "loss": float(loss)}), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
     # Roofline pass: the timed steps rotate views over several HIP streams, so a launch's duration
     # there includes kernels of other views running beside it.  One more step on a single stream gives
     # each launch its own duration (with GR_STREAMS=1 the whole run is single-stream and both agree).
     streams_saved = fm.NUM_STREAMS
     fm.NUM_STREAMS = 1
-    torch.cuda.synchronize()
+    sync()
     pkg._native.profile_begin()
     fitter.step()
-    torch.cuda.synchronize()
+    sync()
     prof = pkg._native.profile_end()
     fm.NUM_STREAMS = streams_saved
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    avg_pairs, avg_core = pairs_per_view(fitter, cams, R, tr.DEFAULT_CUTOFF, tr.DEFAULT_CORE_CUTOFF)
+    k5_pairs, _ = pairs_per_view(fitter, cams, R, 5.0, 5.0)
 
-    # pairs per view for the algorithmic FLOP count (same binning as the kernels)
-    pairs, core = [], []
-    with torch.no_grad():
-        means, scales, colors, opac = fm.activations(fitter.params)
-        for i in fitter.my_views:
-            gv = tr.make_view(cams[i].view, cams[i].proj, R, R, None, tr.DEFAULT_CUTOFF)
-            _, _, _, st = tr.forward_native(means.contiguous(), scales.contiguous(), colors.contiguous(), opac.contiguous(), gv)
-            pairs.append(st.num_pairs)
-            core.append(int(st.plan.num_core_pairs))
+    # the default precision mode: what a caller with a depth loss gets (f32-grade W / D, three-piece
+    # backward with the tail pairs): the same fit with a depth term in the loss (C3's losses)
+    extra = {}
+    if not args.no_extra_modes:
+        gd = torch.Generator(device=device).manual_seed(2)
+        fitter.depths = [torch.rand((R, R), generator=gd, device=device) for _ in range(V)]
+        fitter.step()
+        k = max(1, min(args.steps, 5))
+        dt, _ = timed(k)
+        fitter.depths = None
+        extra = {"value": round(V * R * R * k / dt / 1e6, 2), "steps": k, "ms_per_step": round(1e3 * dt / k, 3),
+                 "mode": "depth_grad=True: forward W/D f32-grade (3-piece bf16 split), backward 3-piece with tail "
+                         "pairs; loss L1 + silhouette + 0.05 depth L1 (fit_multiview_stub.py:299-305)"}
+    clk1 = sclk_mhz() if rank == 0 else None
+
     if rank == 0:
         bwd_ms, bwd_n = prof["raster_bwd"]
         fwd_ms, fwd_n = prof["raster_fwd"]
         bwd_conc_us = 1e3 * prof_concurrent["raster_bwd"][0] / max(prof_concurrent["raster_bwd"][1], 1)
-        avg_pairs, avg_core = float(np.mean(pairs)), float(np.mean(core))
+        fwd_conc_us = 1e3 * prof_concurrent["raster_fwd"][0] / max(prof_concurrent["raster_fwd"][1], 1)
         bwd_avg_s = bwd_ms / max(bwd_n, 1) / 1e3
         fwd_avg_s = fwd_ms / max(fwd_n, 1) / 1e3
-        fwd_conc_us = 1e3 * prof_concurrent["raster_fwd"][0] / max(prof_concurrent["raster_fwd"][1], 1)
         pmc_tab = {}
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
                 pmc_tab = json.load(f)
         avg_tail = avg_pairs - avg_core
-        # the two splat kernels; the one with the longer launches is the bench's "roofline"
+        px = R * R
+        # SURVEY.md 8(d) per-unit bytes: a pair = 12 B key/value + 36 B projected record read once per
+        # splat pass; the backward also writes its 36 B of gradient partials; per pixel 20 B of outputs
+        # + 20 B of saved state written (forward) / 20 B of upstream grads + 20 B saved read (backward)
         kernels = {
-            "bwd": dict(kernel=BWD_KERNEL, t=bwd_avg_s, n=bwd_n, conc_us=bwd_conc_us,
-                        flop=BF16_FLOP_PER_CORE_PAIR_BWD * avg_core, f32=F32_FLOP_PER_CORE_PAIR_BWD * avg_core,
-                        per_pair=f"{BF16_FLOP_PER_CORE_PAIR_BWD:.0f} per core pair (tail pairs skipped)"),
-            "fwd": dict(kernel=FWD_KERNEL, t=fwd_avg_s, n=fwd_n, conc_us=fwd_conc_us,
+            "fwd": dict(kernel=FWD_KERNEL, t=fwd_avg_s, n=fwd_n, conc_us=fwd_conc_us, units=avg_pairs,
+                        unit_bytes=12 + 36, px_bytes=40,
+                        units_desc="pairs (core + tail) per launch",
                         flop=BF16_FLOP_PER_CORE_PAIR_FWD * avg_core + BF16_FLOP_PER_TAIL_PAIR_FWD * avg_tail,
-                        f32=F32_FLOP_PER_CORE_PAIR_FWD * avg_core + F32_FLOP_PER_TAIL_PAIR_FWD * avg_tail,
-                        per_pair=f"{BF16_FLOP_PER_CORE_PAIR_FWD:.0f} per core pair, {BF16_FLOP_PER_TAIL_PAIR_FWD:.0f} per tail pair"),
+                        f32=F32_FLOP_PER_CORE_PAIR_FWD * avg_core + F32_FLOP_PER_TAIL_PAIR_FWD * avg_tail),
+            "bwd": dict(kernel=BWD_KERNEL, t=bwd_avg_s, n=bwd_n, conc_us=bwd_conc_us, units=avg_core,
+                        unit_bytes=12 + 36 + 36, px_bytes=40,
+                        units_desc="core pairs per launch (no upstream depth gradient: tail pairs skipped)",
+                        flop=BF16_FLOP_PER_CORE_PAIR_BWD * avg_core, f32=F32_FLOP_PER_CORE_PAIR_BWD * avg_core),
         }
 
         def roof(k):
             e = kernels[k]
-            ach = e["flop"] / e["t"] / 1e12
-            return {"bound": "mfma", "kernel": e["kernel"], "achieved": round(ach, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4),
+            nbytes = e["unit_bytes"] * e["units"] + e["px_bytes"] * px
+            ach = nbytes / e["t"] / 1e9
+            mf = e["flop"] / e["t"] / 1e12
+            return {"bound": "hbm", "kernel": e["kernel"], "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": pmc_tab.get(e["kernel"], {}).get("hbm_bytes_per_launch"),
+                    "algorithmic_bytes_per_launch": int(nbytes),
+                    "bytes_model": f"{e['unit_bytes']} B x {e['units_desc']} ({int(e['units'])}) + {e['px_bytes']} B x {px} px",
                     "avg_launch_us": round(e["t"] * 1e6, 1), "launches": e["n"],
                     "timing": "HIP events on the launch stream, one single-stream step after the timed region",
                     "avg_launch_us_in_timed_region": round(e["conc_us"], 1), "streams_in_timed_region": streams_saved,
-                    "flop_executed": e["per_pair"], "core_pairs_per_launch": int(avg_core),
-                    "tail_pairs_per_launch": int(avg_tail),
-                    "f32_equivalent_tflops": round(e["f32"] / e["t"] / 1e12, 1), "f32_peak": F32_MFMA_PEAK_TFLOPS}
+                    "mfma": {"executed_bf16_tflops": round(mf, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
+                             "frac": round(mf / BF16_MFMA_PEAK_TFLOPS, 4),
+                             "f32_equivalent_tflops": round(e["f32"] / e["t"] / 1e12, 1), "f32_peak": F32_MFMA_PEAK_TFLOPS}}
 
         dominant = "fwd" if fwd_avg_s > bwd_avg_s else "bwd"
-        hbm_bytes_view = n * (3 * B_IN_RGB + 2 * 36) + avg_pairs * (2 * 12 + 2 * 36 + 2 * 36) + 60 * R * R
-        hbm_roof_mpx = HBM_PEAK_GBS * 1e9 / hbm_bytes_view * R * R / 1e6
-        pixels = V * R * R * args.steps
-        value = pixels / elapsed / 1e6
+
+        def hbm_model(k):
+            b = n * (3 * B_IN_RGB + 2 * 36) + k * (2 * 12 + 2 * 36 + 2 * 36) + 60 * px
+            roof_mpx = HBM_PEAK_GBS * 1e9 / b * px / 1e6
+            return {"pairs_per_view": int(k), "bytes_per_view": int(b), "roofline_mpx_per_s": round(roof_mpx, 1),
+                    "frac": round(value / (roof_mpx * world), 4)}
+
         out = {
             "metric": "Mpixels/sec fwd+bwd @1M Gaussians 800x800",
             "value": round(value, 2),
@@ -231,23 +335,26 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32 (splat contractions on bf16 MFMA with two-piece operand splits, ~2^-16 per product; "
+                     "depth_grad=False mode)",
             "data": "synthetic (seeded Gaussians per SURVEY.md 8(d), random targets)",
             "config": {"workload": f"C4: {n} Gaussians, {V} orbit views {R}x{R}, fwd+bwd+grad all-reduce+Adam per step",
                        "gaussians": n, "views": V, "width": R, "height": R, "cutoff_sigma": tr.DEFAULT_CUTOFF,
                        "core_cutoff_sigma": tr.DEFAULT_CORE_CUTOFF,
                        "scale": round(0.1061 * (1200.0 / n) ** (1.0 / 3.0), 5), "seed": 0,
-                       "parallelism": f"view-sharded dp{world}", "pairs_per_view": int(avg_pairs),
-                       "core_pairs_per_view": int(avg_core),
-                       "gaussian_order": "random" if args.no_reorder else "morton (trainer layout, fit_multiview.spatial_order)"},
-            # achieved = the splat kernel's MFMA FLOP/s as executed on the bf16 pipe (the split-precision
-            # algorithm's own FLOP: 3 piece products per contraction) against the bf16 dense peak, for the
-            # splat kernel with the longer launches; both splats in "splats", f32-equivalent rates beside
+                       "parallelism": f"view-sharded dp{world}", "views_per_rank": views_per_rank,
+                       "pairs_per_view": int(avg_pairs), "core_pairs_per_view": int(avg_core),
+                       "gaussian_order": "random" if args.no_reorder else
+                       f"morton (trainer layout, re-established every {fm.RESORT_EVERY} steps)"},
+            # the dominant splat kernel against the HBM roofline (SURVEY.md 8(d) bytes per pair); both
+            # splats in "splats", with their MFMA rates beside
             "roofline": roof(dominant),
             "splats": {"fwd": roof("fwd"), "bwd": roof("bwd")},
-            "hbm_model": {"bytes_per_view": int(hbm_bytes_view), "roofline_mpx_per_s": round(hbm_roof_mpx, 1),
-                          "frac": round(value / (hbm_roof_mpx * world), 4),
-                          "source": "SURVEY.md 8(d) tile-binned byte model at the measured pairs/view, 8 TB/s"},
+            "hbm_model": {"survey_5sigma": hbm_model(k5_pairs), "build_7sigma": hbm_model(avg_pairs),
+                          "source": "SURVEY.md 8(d) tile-binned byte model, 8 TB/s: at its fixed 5-sigma footprint "
+                                    "(the survey's 2,830 Mpx/s roof) and at this build's 7-sigma pair count"},
+            "default_precision_mode": extra or None,
+            "sclk_mhz": {"before": clk0, "after": clk1},
             "loss": float(loss),
         }
         if not args.no_cpu_baseline and world == 1:

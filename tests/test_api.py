@@ -55,11 +55,11 @@ def test_zero_gaussians_returns_single_zero_image(pkg):
     assert isinstance(out, torch.Tensor) and out.shape == (5, 7, 3) and not out.any()
 
 
-def test_cpu_tensors_fail_loudly(pkg):
-    """There is no CPU fallback in the product path."""
+def test_hip_inputs_refuse_cpu_tensors(pkg):
+    """The HIP entry points never take host tensors (no silent fallback); render_gaussians_torch
+    dispatches host tensors to cpu_renderer instead (tests/test_cpu_path.py)."""
     with pytest.raises(RuntimeError, match="HIP device"):
-        pkg.torch_renderer.render_gaussians_torch(torch.zeros(3, 3), torch.ones(3, 3), torch.zeros(3, 3), torch.ones(3),
-                                                  _cam(pkg), 8, 8)
+        pkg.torch_renderer._device_inputs(torch.zeros(3, 3), torch.ones(3, 3), torch.zeros(3, 3), torch.ones(3))
 
 
 def test_device_policy_prefers_hip(pkg):

@@ -45,8 +45,6 @@ def test_morton_order_is_spatially_coherent():
 
 
 def test_fit_loss_independent_of_order():
-    import dense_torch
-
     torch.manual_seed(7)
     params = fm.build_params(30, torch.device("cpu"), use_sh=False)
     with torch.no_grad():
@@ -56,9 +54,9 @@ def test_fit_loss_independent_of_order():
     g = torch.Generator().manual_seed(3)
     targets = [torch.rand((H, W, 3), generator=g) for _ in range(3)]
     a = fm.ViewShardedFitter({k: torch.nn.Parameter(v.detach().clone()) for k, v in params.items()}, cams, targets, W,
-                             H, render_fn=dense_torch.render, reorder=False)
+                             H, reorder=False)
     b = fm.ViewShardedFitter({k: torch.nn.Parameter(v.detach().clone()) for k, v in params.items()}, cams, targets, W,
-                             H, render_fn=dense_torch.render, reorder=True)
+                             H, reorder=True)
     perm = fm.morton_order(params["means"])
     la, lb = float(a.step()), float(b.step())
     assert abs(la - lb) <= 1e-6 * max(1.0, abs(la))
@@ -90,3 +88,42 @@ def test_densify_sees_the_stub_order():
     for k in ref:
         assert torch.equal(got[k].detach(), ref[k].detach()), k
     assert torch.equal(torch.sort(f.perm).values, torch.arange(ref["means"].shape[0]))
+
+
+def test_respatialize_keeps_the_fit():
+    """Re-establishing the Morton order mid-fit (ViewShardedFitter.respatialize, every RESORT_EVERY steps)
+    permutes parameters and Adam moments together: the fit continues exactly as without it, and the
+    canonical (stub-order) parameters are unchanged by the permutation."""
+    torch.manual_seed(7)
+    params = fm.build_params(60, torch.device("cpu"), use_sh=False)
+    with torch.no_grad():
+        params["scales_raw"].fill_(-1.0)
+    W, H = 16, 12
+    cams = fm.orbit_cameras(3, W, H, torch.device("cpu"))
+    g = torch.Generator().manual_seed(3)
+    targets = [torch.rand((H, W, 3), generator=g) for _ in range(3)]
+    saved = fm.RESORT_EVERY
+    try:
+        fm.RESORT_EVERY = 0
+        a = fm.ViewShardedFitter({k: torch.nn.Parameter(v.detach().clone()) for k, v in params.items()}, cams, targets, W, H)
+        b = fm.ViewShardedFitter({k: torch.nn.Parameter(v.detach().clone()) for k, v in params.items()}, cams, targets, W, H)
+        for _ in range(3):
+            a.step()
+            b.step()
+        with torch.no_grad():  # move b's Gaussians out of order, as a long fit does
+            for f in (a, b):
+                f.params["means"].mul_(-1.0)
+        before = {k: v.detach().clone() for k, v in b.canonical_params().items()}
+        b.respatialize()
+        after = b.canonical_params()
+        for k in before:
+            assert torch.equal(before[k], after[k].detach()), k
+        assert torch.equal(b.perm.sort().values, torch.arange(60))
+        for _ in range(2):
+            la, lb = float(a.step()), float(b.step())
+            assert abs(la - lb) <= 1e-6 * max(1.0, abs(la))
+        ca, cb = a.canonical_params(), b.canonical_params()
+        for k in ca:
+            torch.testing.assert_close(ca[k].detach(), cb[k].detach(), rtol=1e-5, atol=1e-6)
+    finally:
+        fm.RESORT_EVERY = saved
