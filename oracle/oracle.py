@@ -78,6 +78,9 @@ def lib() -> ctypes.CDLL:
         _LIB.gro_forward.argtypes = [ctypes.POINTER(GrView), ctypes.c_int, f, f, f, ctypes.c_int, f, ctypes.c_int] + [f] * 4
         _LIB.gro_backward.argtypes = [ctypes.POINTER(GrView), ctypes.c_int, f, f, f, ctypes.c_int, f, ctypes.c_int] + [f] * 7
         _LIB.gro_render_u8.argtypes = [ctypes.POINTER(GrRenderParams), ctypes.c_int] + [f] * 5
+        _LIB.gro_dense_pixels.argtypes = [ctypes.POINTER(GrView), ctypes.c_int, f, f, f, ctypes.c_int, f, ctypes.c_int] + [f] * 4
+        _LIB.gro_dense_grads_sel.argtypes = ([ctypes.POINTER(GrView), ctypes.c_int, f, f, f, ctypes.c_int, f] + [f] * 3
+                                             + [ctypes.c_int] + [f] * 5)
     return _LIB
 
 
@@ -180,6 +183,37 @@ def backward(v: GrView, scene: Scene, g_rgb, g_alpha=None, g_depth=None, binned:
     dc = np.zeros_like(c)
     do = np.zeros_like(o)
     lib().gro_backward(ctypes.byref(v), n, _p(m), _p(s), _p(c), color_dim(c), _p(o), int(binned), _p(g_rgb), _p(g_alpha), _p(g_depth), _p(dm), _p(ds), _p(dc), _p(do))
+    return dm, ds, dc, do
+
+
+def dense_pixels(v: GrView, scene: Scene, pix: np.ndarray):
+    """Dense (no cutoff, every Gaussian) float64 out (P,3), alpha (P,), depth (P,) at pixel indices y*W+x."""
+    m, s, c, o = scene.arrays()
+    pix = np.ascontiguousarray(pix, np.int32)
+    P = pix.shape[0]
+    out = np.zeros((P, 3), np.float32)
+    alpha = np.zeros((P,), np.float32)
+    depth = np.zeros((P,), np.float32)
+    lib().gro_dense_pixels(ctypes.byref(v), m.shape[0], _p(m), _p(s), _p(c), color_dim(c), _p(o), P, _p(pix),
+                           _p(out), _p(alpha), _p(depth))
+    return out, alpha, depth
+
+
+def dense_grads_sel(v: GrView, scene: Scene, sel: np.ndarray, g_rgb, g_alpha=None, g_depth=None):
+    """Exact gradients of the selected Gaussians over the whole image (no cutoff), per-pixel sums from the
+    binned forward: (d_means, d_scales, d_colors, d_opac) rows in sel order."""
+    m, s, c, o = scene.arrays()
+    sel = np.ascontiguousarray(sel, np.int32)
+    k = sel.shape[0]
+    g_rgb = _f32(g_rgb)
+    g_alpha = None if g_alpha is None else _f32(g_alpha)
+    g_depth = None if g_depth is None else _f32(g_depth)
+    dm = np.zeros((k, 3), np.float32)
+    ds = np.zeros((k, 3), np.float32)
+    dc = np.zeros((k,) + c.shape[1:], np.float32)
+    do = np.zeros((k,), np.float32)
+    lib().gro_dense_grads_sel(ctypes.byref(v), m.shape[0], _p(m), _p(s), _p(c), color_dim(c), _p(o), _p(g_rgb),
+                              _p(g_alpha), _p(g_depth), k, _p(sel), _p(dm), _p(ds), _p(dc), _p(do))
     return dm, ds, dc, do
 
 

@@ -1,0 +1,88 @@
+"""GPU parity at the bench's own scale: one full view of config C4 (1M Gaussians, 800x800) and of C5
+(3M Gaussians, 1920x1080), in the bench's precision mode (depth_grad=False: no upstream depth gradient,
+two-piece splits) and in the default mode (depth_grad=True, upstream depth gradient), against
+
+* the float64 binned oracle (the product's footprint) on every pixel and every Gaussian:
+  relL2 <= 2e-5 on out/alpha/depth, <= 1e-4 on all four gradients, PSNR >= 60 dB;
+* the float64 DENSE reference semantics (torch_renderer.py:164-203: every Gaussian at every pixel, no
+  cutoff) on a sample: out/alpha/depth at 1000 random pixels summed over all N Gaussians, and the exact
+  gradients of 1000 random Gaussians each summed over the whole image (SURVEY.md §7 "oracle reach");
+  relL2 <= 1e-4 over the sample.  This ties the tile footprint (7 sigma / 5.5 sigma core) to the dense
+  math at the sizes the headline runs.
+
+Scenes: SURVEY.md §8(d)'s synthetic recipe (density-matched scale), Gaussians in the trainer's Morton
+order (bench.py's layout), orbit view 0.  Upstream gradients: seeded standard normal."""
+from __future__ import annotations
+
+import importlib
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = {"C4": (1_000_000, 800, 800, 50), "C5": (3_000_000, 1920, 1080, 100)}
+GRADS = ("d_means", "d_scales", "d_colors", "d_opac")
+
+
+def _scene(n):
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    sc = orc.synthetic_scene(n, seed=0)
+    perm = fm.morton_order(torch.from_numpy(sc.means)).numpy()
+    return orc.Scene(sc.means[perm].copy(), sc.scales[perm].copy(), sc.colors[perm].copy(), sc.opacities[perm].copy())
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("depth_grad", [False, True])
+@pytest.mark.parametrize("cfg", ["C4", "C5"])
+def test_full_view_vs_oracle(pkg, cuda, cfg, depth_grad):
+    tr = pkg.torch_renderer
+    n, W, H, V = CONFIGS[cfg]
+    sc = _scene(n)
+    view, proj = orc.orbit_cameras(V, W, H)[0]
+    rng = np.random.default_rng(7)
+    g_rgb = rng.standard_normal((H, W, 3)).astype(np.float32)
+    g_a = rng.standard_normal((H, W)).astype(np.float32)
+    g_d = rng.standard_normal((H, W)).astype(np.float32) if depth_grad else None
+
+    t = [torch.from_numpy(a).to(cuda).requires_grad_(True) for a in sc.arrays()]
+    out, alpha, depth = tr.rasterize(*t, view, proj, W, H, depth_grad=depth_grad)
+    loss = (out * torch.from_numpy(g_rgb).to(cuda)).sum() + (alpha * torch.from_numpy(g_a).to(cuda)).sum()
+    if depth_grad:
+        loss = loss + (depth * torch.from_numpy(g_d).to(cuda)).sum()
+    loss.backward()
+    torch.cuda.synchronize()
+    hip = {"out": out.detach().cpu().numpy(), "alpha": alpha.detach().cpu().numpy(), "depth": depth.detach().cpu().numpy()}
+    for k, x in zip(GRADS, t):
+        hip[k] = x.grad.cpu().numpy()
+
+    t0 = time.perf_counter()
+    v = orc.make_view(view, proj, W, H, None, cutoff=tr.DEFAULT_CUTOFF, core_cutoff=tr.DEFAULT_CORE_CUTOFF)
+    ora = dict(zip(("out", "alpha", "depth"), orc.forward(v, sc, binned=True)))
+    ora.update(zip(GRADS, orc.backward(v, sc, g_rgb, g_a, g_d, binned=True)))
+    errs = {k: orc.rel_l2(hip[k], ora[k]) for k in ora}
+    t1 = time.perf_counter()
+
+    pix = rng.choice(W * H, 1000, replace=False).astype(np.int32)
+    d_out, d_a, d_d = orc.dense_pixels(v, sc, pix)
+    sel = np.sort(rng.choice(n, 1000, replace=False)).astype(np.int32)
+    dense_g = orc.dense_grads_sel(v, sc, sel, g_rgb, g_a, g_d)
+    dense = {"out": orc.rel_l2(hip["out"].reshape(-1, 3)[pix], d_out),
+             "alpha": orc.rel_l2(hip["alpha"].reshape(-1)[pix], d_a),
+             "depth": orc.rel_l2(hip["depth"].reshape(-1)[pix], d_d)}
+    for k, gd in zip(GRADS, dense_g):
+        dense[k] = orc.rel_l2(hip[k][sel], gd)
+    print(f"{cfg} depth_grad={depth_grad}: vs binned oracle", {k: f"{e:.2e}" for k, e in errs.items()},
+          f"({t1 - t0:.1f} s); vs dense sample", {k: f"{e:.2e}" for k, e in dense.items()},
+          f"({time.perf_counter() - t1:.1f} s)")
+    for k in ("out", "alpha", "depth"):
+        assert errs[k] <= 2e-5, (k, errs[k])
+    for k in GRADS:
+        assert errs[k] <= 1e-4, (k, errs[k])
+    assert orc.psnr(hip["out"], ora["out"]) >= 60.0
+    for k, e in dense.items():
+        assert e <= 1e-4, (k, e)
