@@ -119,11 +119,13 @@ def densify_and_prune(params: dict, max_gaussians: int, densify_ratio: float, pr
 
 
 def densify_and_prune_device(params: dict, max_gaussians: int, densify_ratio: float, prune_opacity: float,
-                             generator: torch.Generator) -> dict:
+                             generator: Optional[torch.Generator] = None, noise: Optional[torch.Tensor] = None) -> dict:
     """The same rule as densify_and_prune (fit_multiview_stub.py:140-197) evaluated on the device, for
     fits at scale (config C5: millions of Gaussians), with the jitter drawn from a device generator:
     no host round trip of the parameters.  Same keep / top-k / jitter / -0.1 opacity / colour
-    duplication; only the random stream differs from the stub's CPU one."""
+    duplication; only the random stream differs from the stub's CPU one.  ``noise`` (>= added rows x 3,
+    standard normal) replaces the generator's draw: with the stub's own draw the result is the host
+    rule's (tests/test_densify.py)."""
     with torch.no_grad():
         means, scales_raw, op_raw = params["means"].detach(), params["scales_raw"].detach(), params["opacities_raw"].detach()
         key = "sh_raw" if "sh_raw" in params else "colors_raw"
@@ -141,8 +143,11 @@ def densify_and_prune_device(params: dict, max_gaussians: int, densify_ratio: fl
         if add_n > 0 and n > 0:
             idx = torch.topk(torch.sigmoid(op_raw), k=min(n, add_n), largest=True).indices
             scales = torch.nn.functional.softplus(scales_raw[idx]) + 1e-3
-            jitter = 0.25 * scales * torch.randn(means[idx].shape, generator=generator, device=means.device,
-                                                 dtype=means.dtype)
+            if noise is not None:
+                z = noise[:idx.shape[0]].to(device=means.device, dtype=means.dtype)
+            else:
+                z = torch.randn(means[idx].shape, generator=generator, device=means.device, dtype=means.dtype)
+            jitter = 0.25 * scales * z
             means = torch.cat([means, means[idx] + jitter], dim=0)
             scales_raw = torch.cat([scales_raw, scales_raw[idx]], dim=0)
             col = torch.cat([col, col[idx]], dim=0)
@@ -263,10 +268,15 @@ class ViewShardedFitter:
             self._bg = torch.zeros(3, device=device)
         return self._bg
 
+    def _depth_grad(self) -> bool:
+        """The loss differentiates the depth output (a depth term): the views render in the default
+        precision mode with the depth-gradient cutoff; otherwise depth_grad=False (gr_view.no_depth_grad)."""
+        return self.depths is not None and self.w_depth > 0.0
+
     def _prepare(self, i: int, means, scales, colors, opacities):
         cam = self.cams[i]
         return tr.prepare_view(means, scales, colors, opacities, cam.view, cam.proj, self.width, self.height,
-                               self._background(means.device))
+                               self._background(means.device), depth_grad=self._depth_grad())
 
     def view_loss(self, i: int, means, scales, colors, opacities, prepared=None) -> torch.Tensor:
         device = means.device
@@ -274,7 +284,7 @@ class ViewShardedFitter:
         if self.render_fn is hip_render:
             # without a depth loss the depth output gets no gradient: the forward may accumulate W and D
             # at the colours' precision (gr_view.no_depth_grad)
-            kw["depth_grad"] = self.depths is not None and self.w_depth > 0.0
+            kw["depth_grad"] = self._depth_grad()
         pred, alpha, depth = self.render_fn(means, scales, colors, opacities, self.cams[i], self.width, self.height,
                                             self._background(device), **kw)
         use_sil = self.masks is not None and self.w_sil > 0.0

@@ -8,10 +8,12 @@ libgr_hip.so through a ``torch.autograd.Function`` — not by torch ops.  Differ
 (DESIGN.md §Semantics):
 
 * a Gaussian is evaluated on the 16x16 tiles where its largest weight is >= o*exp(-cutoff^2/2)
-  (default cutoff 7); tiles where it stays below o*exp(-core_cutoff^2/2) (default 5.5) are "tail"
+  (cutoff 8 when the depth output may be differentiated, 7 with ``depth_grad=False``;
+  ``default_cutoff``); tiles where it stays below o*exp(-core_cutoff^2/2) (default 5.5) are "tail"
   tiles that carry only the weight and depth sums forward and the depth-coupled gradient terms
   backward (only when an upstream depth gradient is given): outputs and gradients agree with the
-  dense reference to <=5e-6 relative L2 on its own fixtures, with and without depth gradients;
+  dense reference to <=5e-6 relative L2 on its own fixtures, with and without depth gradients, and to
+  <=1e-4 on sampled dense checks at configs C4 and C5 (tests/test_scale_gpu.py);
 * ``chunk_size`` is accepted and ignored (no chunk loop);
 * gradients flow to means, scales, colours/SH, opacities and background; not to the camera matrices;
 * the op dispatches on the tensors' device like the reference: HIP tensors always run the HIP kernels
@@ -34,8 +36,18 @@ except ImportError:  # pragma: no cover
     import _native  # type: ignore
     import cpu_renderer  # type: ignore
 
-DEFAULT_CUTOFF = 7.0
+DEFAULT_CUTOFF = 7.0  # tail zone (W and D) when no depth gradient will follow (depth_grad=False)
+DEPTH_GRAD_CUTOFF = 8.0  # tail zone when the depth output may be differentiated (the default mode)
 DEFAULT_CORE_CUTOFF = 5.5
+
+
+def default_cutoff(depth_grad: bool = True) -> float:
+    """Tail cutoff (in sigma) of a view rendered with/without a depth gradient to follow.  With one, the
+    depth-coupled gradient d depth / d w = (z - depth) / (W + 1e-6) amplifies far tails by up to 1e6 on
+    near-empty pixels: at config C5 (1080p, empty image sides) 7 sigma leaves the dense reference's
+    position/scale gradients 4e-5..4e-4 relL2 away, 8 sigma 2.5e-6 (tests/test_scale_gpu.py,
+    tools/probe_cutoff.py).  Without one the tail only feeds the alpha/depth outputs: 7 sigma."""
+    return DEPTH_GRAD_CUTOFF if depth_grad else DEFAULT_CUTOFF
 
 
 @dataclass
@@ -126,11 +138,14 @@ def _host_matrix(t: torch.Tensor) -> np.ndarray:
     return _host_copy(t, (4, 4))
 
 
-def make_view(view, proj, width: int, height: int, background=None, cutoff: float = DEFAULT_CUTOFF,
+def make_view(view, proj, width: int, height: int, background=None, cutoff: Optional[float] = None,
               core_cutoff: float = DEFAULT_CORE_CUTOFF, depth_grad: bool = True) -> _native.GrView:
     """Build a gr_view from host (numpy / tensor) matrices.  ``depth_grad=False`` promises that the
     depth output will get no gradient (gr_view.no_depth_grad): W and D are then accumulated within
-    2^-16 relative instead of f32-grade, and a depth gradient raises in the backward."""
+    2^-16 relative instead of f32-grade, and a depth gradient raises in the backward.
+    ``cutoff=None``: ``default_cutoff(depth_grad)``."""
+    if cutoff is None:
+        cutoff = default_cutoff(depth_grad)
     V = view if isinstance(view, np.ndarray) else _host_matrix(view)
     P = proj if isinstance(proj, np.ndarray) else _host_matrix(proj)
     V = np.asarray(V, dtype=np.float32).reshape(4, 4)
@@ -235,8 +250,9 @@ def forward_native(means, scales, colors, opacities, gv: _native.GrView, prepare
     s = _stream(dev)
     if prepared is None:
         prepared = prepare_native(means, scales, colors, opacities, gv)
-    elif prepared.n != n or prepared.gv.width != W or prepared.gv.height != H:
-        raise ValueError("prepared view does not match this render (Gaussian count or image size)")
+    elif (prepared.n != n or prepared.gv.width != W or prepared.gv.height != H or prepared.gv.cutoff != gv.cutoff
+          or prepared.gv.core_cutoff != gv.core_cutoff):
+        raise ValueError("prepared view does not match this render (Gaussian count, image size or cutoffs)")
     geom = prepared.geom
     plan = prepared.plan()
     bins = torch.empty((_ws_round(L.gr_bins_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8,
@@ -322,14 +338,14 @@ def _device_inputs(means, scales, colors, opacities):
 
 
 def prepare_view(means, scales, colors, opacities, view, proj, width, height, background=None,
-                 cutoff=DEFAULT_CUTOFF, core_cutoff=DEFAULT_CORE_CUTOFF) -> Prepared:
+                 cutoff=None, core_cutoff=DEFAULT_CORE_CUTOFF, depth_grad: bool = True) -> Prepared:
     """Enqueue the preparation of one view (see ``Prepared``); pass it to ``rasterize(prepared=...)``
-    with the same tensors.  The tensors' values must not change in between."""
-    gv = make_view(view, proj, width, height, background, cutoff, core_cutoff)
+    with the same tensors, cutoffs and ``depth_grad``.  The tensors' values must not change in between."""
+    gv = make_view(view, proj, width, height, background, cutoff, core_cutoff, depth_grad)
     return prepare_native(*_device_inputs(means, scales, colors, opacities), gv)
 
 
-def rasterize(means, scales, colors, opacities, view, proj, width, height, background=None, cutoff=DEFAULT_CUTOFF,
+def rasterize(means, scales, colors, opacities, view, proj, width, height, background=None, cutoff=None,
               prepared: Optional[Prepared] = None, core_cutoff=DEFAULT_CORE_CUTOFF, depth_grad: bool = True):
     """Differentiable render of one view on the HIP device: returns (rgb (H,W,3), alpha (H,W), depth (H,W)).
 
@@ -362,7 +378,7 @@ def render_gaussians_torch(
     max_gaussians: int = 10000,
     chunk_size: int = 256,
     return_aux: bool = False,
-    cutoff: float = DEFAULT_CUTOFF,
+    cutoff: Optional[float] = None,
     prepared: Optional[Prepared] = None,
     core_cutoff: float = DEFAULT_CORE_CUTOFF,
     depth_grad: bool = True,
@@ -398,4 +414,4 @@ def render_gaussians_torch(
 
 __all__ = ["Camera", "get_default_device", "perspective", "look_at", "render_gaussians_torch", "rasterize",
            "make_view", "prepare_view", "prepare_native", "Prepared", "forward_native", "backward_native",
-           "DEFAULT_CUTOFF", "DEFAULT_CORE_CUTOFF"]
+           "DEFAULT_CUTOFF", "DEPTH_GRAD_CUTOFF", "DEFAULT_CORE_CUTOFF", "default_cutoff"]

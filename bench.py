@@ -148,7 +148,7 @@ def cpu_baseline(n: int, res: int, views: int) -> dict:
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     scene = orc.synthetic_scene(n, seed=0)
     view, proj = orc.orbit_cameras(views, res, res)[0]
-    v = orc.make_view(view, proj, res, res, cutoff=tr.DEFAULT_CUTOFF, core_cutoff=tr.DEFAULT_CORE_CUTOFF)
+    v = orc.make_view(view, proj, res, res, cutoff=tr.default_cutoff(False), core_cutoff=tr.DEFAULT_CORE_CUTOFF)
     g = np.random.default_rng(0).standard_normal((res, res, 3)).astype(np.float32)
     t0 = time.perf_counter()
     orc.forward(v, scene, binned=True)
@@ -252,7 +252,7 @@ def main():
     sync()
     prof = pkg._native.profile_end()
     fm.NUM_STREAMS = streams_saved
-    avg_pairs, avg_core = pairs_per_view(fitter, cams, R, tr.DEFAULT_CUTOFF, tr.DEFAULT_CORE_CUTOFF)
+    avg_pairs, avg_core = pairs_per_view(fitter, cams, R, tr.default_cutoff(False), tr.DEFAULT_CORE_CUTOFF)
     k5_pairs, _ = pairs_per_view(fitter, cams, R, 5.0, 5.0)
 
     # the default precision mode: what a caller with a depth loss gets (f32-grade W / D, three-piece
@@ -339,7 +339,7 @@ def main():
                      "depth_grad=False mode)",
             "data": "synthetic (seeded Gaussians per SURVEY.md 8(d), random targets)",
             "config": {"workload": f"C4: {n} Gaussians, {V} orbit views {R}x{R}, fwd+bwd+grad all-reduce+Adam per step",
-                       "gaussians": n, "views": V, "width": R, "height": R, "cutoff_sigma": tr.DEFAULT_CUTOFF,
+                       "gaussians": n, "views": V, "width": R, "height": R, "cutoff_sigma": tr.default_cutoff(False),
                        "core_cutoff_sigma": tr.DEFAULT_CORE_CUTOFF,
                        "scale": round(0.1061 * (1200.0 / n) ** (1.0 / 3.0), 5), "seed": 0,
                        "parallelism": f"view-sharded dp{world}", "views_per_rank": views_per_rank,

@@ -44,3 +44,28 @@ def test_device_densify_at_c5_scale(cuda):
     kept = int((op > 0.05).sum())
     assert out["means"].shape[0] == min(3_000_000, kept + int(kept * 0.15))
     assert all(v.is_cuda and v.shape[0] == out["means"].shape[0] for v in out.values())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sh", [False, True])
+def test_device_rule_on_device_equals_host_rule(cuda, sh):
+    """On device tensors, given the host rule's own jitter draw, the device rule gives the host rule's
+    parameters (same keep set, same top-k, same jitter, same duplication order)."""
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    p = _params(200_000, 5, sh)
+    with torch.no_grad():  # distinct opacities, well apart in float32: no top-k ties (whose order the
+        # CPU and GPU top-k may break differently) and no ulp-level sigmoid difference at the threshold
+        g = torch.Generator().manual_seed(6)
+        p["opacities_raw"].copy_(torch.linspace(-4.0, 4.0, 200_000)[torch.randperm(200_000, generator=g)])
+    n_keep = int((torch.sigmoid(p["opacities_raw"].detach()) > 0.05).sum())
+    add_n = min(max(0, 300_000 - n_keep), int(n_keep * 0.15))
+    torch.manual_seed(21)
+    host = fm.densify_and_prune(p, 300_000, 0.15, 0.05)
+    torch.manual_seed(21)
+    noise = torch.randn((add_n, 3))  # the draw torch.randn_like(means[idx]) makes in the host rule
+    pd = {k: torch.nn.Parameter(v.detach().to(cuda)) for k, v in p.items()}
+    dev = fm.densify_and_prune_device(pd, 300_000, 0.15, 0.05, noise=noise.to(cuda))
+    assert set(host) == set(dev)
+    for k in host:
+        assert dev[k].is_cuda and dev[k].shape == host[k].shape, k
+        torch.testing.assert_close(dev[k].detach().cpu(), host[k].detach(), rtol=1e-6, atol=1e-7)

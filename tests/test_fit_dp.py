@@ -35,7 +35,7 @@ def _setup(n_views=4, n=40, W=16, H=12):
     return fm, params, cams, targets, masks, W, H
 
 
-def _worker(rank, world, port, out_q):
+def _worker(rank, world, port, out_q, on_device=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     fm, params, cams, targets, masks, W, H = _setup()
@@ -44,7 +44,7 @@ def _worker(rank, world, port, out_q):
     grads = {k: v.grad.clone() for k, v in fit.params.items()}
     before = {k: v.detach().numpy().copy() for k, v in fit.params.items()}
     torch.manual_seed(11)  # only rank 0's RNG decides the densify jitter
-    fit.densify_and_prune(max_gaussians=60, densify_ratio=0.5, prune_opacity=0.05)
+    fit.densify_and_prune(max_gaussians=60, densify_ratio=0.5, prune_opacity=0.05, on_device=on_device)
     losses.append(float(fit.step()))
     # numpy, not tensors: tensor shared-memory handles die with the worker process
     out_q.put((rank, losses, before, {k: v.detach().numpy().copy() for k, v in fit.params.items()},
@@ -62,7 +62,10 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gloo_matches_single_process():
+@pytest.mark.parametrize("on_device", [False, True])
+def test_two_rank_gloo_matches_single_process(on_device):
+    """on_device: the device-side densify rule (the C5 path: generator on the parameters' device),
+    decided on rank 0 and broadcast, as the host rule."""
     fm, params, cams, targets, masks, W, H = _setup()
     ref = fm.ViewShardedFitter(params, cams, targets, W, H, masks=masks)
     ref_losses = [float(ref.step()) for _ in range(2)]
@@ -72,7 +75,7 @@ def test_two_rank_gloo_matches_single_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, on_device)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict((r, (l, before, after, g)) for r, l, before, after, g in (q.get(timeout=240) for _ in procs))

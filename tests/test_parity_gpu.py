@@ -21,7 +21,8 @@ from oracle import oracle as orc
 pytestmark = pytest.mark.gpu
 
 GRAD_KEYS = ("d_means", "d_scales", "d_colors", "d_opacities")
-CUTOFF = 7.0  # product defaults (3dgaussian_amd/torch_renderer.py DEFAULT_CUTOFF, DEFAULT_CORE_CUTOFF)
+CUTOFF = 7.0  # product defaults (3dgaussian_amd/torch_renderer.py DEFAULT_CUTOFF, DEFAULT_CORE_CUTOFF);
+DEPTH_CUTOFF = 8.0  # the tail cutoff of views rendered with depth_grad=True (DEPTH_GRAD_CUTOFF)
 CORE = 5.5
 
 
@@ -50,8 +51,10 @@ def _run_hip(pkg, d, device, cutoff=None, with_depth=True, depth_grad=True):
     return r
 
 
-def _oracle(d, binned, with_depth=True):
-    v = orc.make_view(d["view"], d["proj"], int(d["width"]), int(d["height"]), d["background"], cutoff=CUTOFF,
+def _oracle(d, binned, with_depth=True, depth_grad=True):
+    """depth_grad: the precision mode the HIP view was rendered in (its tail cutoff)."""
+    v = orc.make_view(d["view"], d["proj"], int(d["width"]), int(d["height"]), d["background"],
+                      cutoff=DEPTH_CUTOFF if depth_grad else CUTOFF,
                       core_cutoff=CORE)
     sc = orc.Scene(d["means"], d["scales"], d["colors"], d["opacities"])
     out, alpha, depth = orc.forward(v, sc, binned=binned)
@@ -101,7 +104,7 @@ def test_no_depth_gradient(pkg, cuda, name, depth_grad):
     outputs and gradients still meet the bar against the reference's own outputs."""
     d = golden(name)
     hip = _run_hip(pkg, d, cuda, with_depth=False, depth_grad=depth_grad)
-    ora = _oracle(d, binned=True, with_depth=False)
+    ora = _oracle(d, binned=True, with_depth=False, depth_grad=depth_grad)
     exact = _oracle(d, binned=False, with_depth=False)
     for k in ("out_rgb", "out_alpha", "out_depth"):
         assert orc.rel_l2(hip[k], d[k]) <= 1e-4, k
@@ -235,7 +238,7 @@ def test_c2_scale_vs_binned_oracle(pkg, cuda, depth_grad):
              g_alpha=rng.standard_normal((512, 512)).astype(np.float32),
              g_depth=rng.standard_normal((512, 512)).astype(np.float32))
     hip = _run_hip(pkg, d, cuda, with_depth=depth_grad, depth_grad=depth_grad)
-    ora = _oracle(d, binned=True, with_depth=depth_grad)
+    ora = _oracle(d, binned=True, with_depth=depth_grad, depth_grad=depth_grad)
     errs = {k: orc.rel_l2(hip[k], ora[k]) for k in ("out_rgb", "out_alpha", "out_depth") + GRAD_KEYS}
     print(f"C2 depth_grad={depth_grad} relL2 vs float64 oracle:", {k: f"{e:.2e}" for k, e in errs.items()})
     for k in ("out_rgb", "out_alpha", "out_depth"):

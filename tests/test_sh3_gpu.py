@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from oracle import oracle as orc
-from test_parity_gpu import CORE, CUTOFF, GRAD_KEYS
+from test_parity_gpu import CORE, DEPTH_CUTOFF, GRAD_KEYS
 
 pytestmark = pytest.mark.gpu
 
@@ -35,7 +35,7 @@ def test_sh3_vs_binned_oracle(pkg, cuda, n, res, scale):
     out, alpha, depth = tr.rasterize(*t, view, proj, res, res)
     ((out * torch.from_numpy(g_rgb).to(cuda)).sum() + (alpha * torch.from_numpy(g_a).to(cuda)).sum()
      + (depth * torch.from_numpy(g_d).to(cuda)).sum()).backward()
-    v = orc.make_view(view, proj, res, res, cutoff=CUTOFF, core_cutoff=CORE)
+    v = orc.make_view(view, proj, res, res, cutoff=DEPTH_CUTOFF, core_cutoff=CORE)
     o_out, o_a, o_d = orc.forward(v, sc, binned=True)
     grads = orc.backward(v, sc, g_rgb, g_a, g_d, binned=True)
     for got, ref in ((out, o_out), (alpha, o_a), (depth, o_d)):
