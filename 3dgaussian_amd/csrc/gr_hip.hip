@@ -14,7 +14,7 @@
 //                    pos_of (sorted position of each pair, by emission index).
 //   k_work_items_zones  per-(virtual) tile ranges, work items of <= CH pairs.
 //   k_raster_fwd_mfma   per work item: records staged through LDS by LDS-DMA, the separable splat as
-//                    a contraction on bf16 MFMA with split operands (f32 MFMA behind GR_FWD_F32);
+//                    a contraction on bf16 MFMA with split operands;
 //                    k_fwd_finalize combines tiles split over several items; out/alpha/depth + saved.
 //   k_pixel_grads    per pixel upstream vector U = (dC, dW, dD), pre-split into MFMA fragments.
 //   k_raster_bwd_bf16   per work item: the two K = 16 contractions (over x, over y) of U with the
@@ -693,14 +693,9 @@ __global__ __launch_bounds__(256) void k_ranges(int64_t K, const KeyT* __restric
 // so the per-tile splat is a dense contraction over the tile's Gaussians g:
 //   forward   C_k[x][y] = sum_g (o_g v_gk ex_g(x)) * ey_g(y),  v = (1, r, g, b, z)
 //   backward  D_k,f[y][g] = sum_x U_k[x][y] * (f(x) ex_g(x)),  f in {1, dx, dx^2}
-// evaluated with v_mfma_f32_16x16x4_f32 (exact f32 fma chain, K = 4).  Lane l supplies
-// A[l&15][l>>4] and B[l>>4][l&15]; it receives C[4(l>>4)+r][l&15], r = 0..3.
+// evaluated on bf16 MFMA with exactly split operands (k_raster_fwd_mfma, k_raster_bwd_bf16).
 // ------------------------------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
 
 // Work items: each non-empty (virtual) tile's pair list is cut into chunks of CH Gaussians, so every
 // workgroup gets about the same amount of work however unevenly Gaussians fall on tiles.
@@ -810,6 +805,14 @@ __device__ __forceinline__ void glds4(const void* gsrc, void* wave_base) {
 }
 // This wave's LDS-DMAs (and every other vector memory op) have completed; follow with a barrier.
 __device__ __forceinline__ void stage_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// In the splat kernels every wave stages (LDS-DMA) and reads only its own 64-Gaussian slice of a batch,
+// so the wave's own vmcnt orders its reads (MI355X_MICROARCH.md item 7) and no barrier is needed
+// between batches: a wave never waits for another wave's copy.
+#ifdef GR_STAGE_BARRIER
+#define GR_STAGE_SYNC() __syncthreads()
+#else
+#define GR_STAGE_SYNC() ((void)0)
+#endif
 
 // Record of Gaussian g; g < 0 (padding) reads the pad record rec[n] written by k_preprocess: o = 0
 // and px = +huge, so every weight it produces is exactly 0 (exp2(-inf) = 0) without a select.
@@ -1195,7 +1198,7 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
   const f32x2_t X = {xc, xc}, Y = {yc, yc};
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
     stage_wait();
-    __syncthreads();
+    GR_STAGE_SYNC();
     if (base + TP < k1) stage(stage_pair(idn, base + TP + tid, k1).x, buf ^ 1);
     idn = stage_id(base + 2 * TP + tid, k1, pairs);
     const int cnt = min(TP, k1 - base) - wave * 64;           // Gaussians of this batch for this wave
@@ -1269,74 +1272,6 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
   }
 }
 
-// Forward: one workgroup (4 waves) per work item.  Batches of 256 Gaussians go through a double-
-// buffered LDS stage; wave w takes Gaussians [64w, 64w+64) of each batch in blocks of 4 steps of 4
-// (the MFMA K dimension).  Padding entries are exact zeros, so whole blocks are processed.
-// TAIL items (tail pairs of the two-zone footprint) accumulate W and D only: 2 MFMA per step.
-template <bool TAIL>
-__device__ __forceinline__ void fwd_accumulate(float* smem, int n, int k0, int k1, int tid, int wave, float xc, float yc,
-                                               int gs, const int2* __restrict__ pairs, const float4* __restrict__ rec,
-                                               f32x4& cW, f32x4& cR, f32x4& cG, f32x4& cB, f32x4& cD) {
-  // buffer b: float4 A[TP], float4 B[TP], float Z[TP] (lane-linear per wave, as LDS-DMA writes them)
-  constexpr int BUF = 2 * TP + TP / 4;  // float4 units per buffer
-  auto stage = [&](int g, int b) {
-    const float4* p = rec_of(g, n, rec);
-    float4* sA = reinterpret_cast<float4*>(smem) + b * BUF;
-    glds16(p, sA + 64 * wave);
-    glds16(p + 1, sA + TP + 64 * wave);
-    glds4(zrec_of(g, n, rec), reinterpret_cast<float*>(sA + 2 * TP) + 64 * wave);
-  };
-  stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1).x, 0);
-  int2 idn = stage_id(k0 + TP + tid, k1, pairs);  // raw: batch base + TP
-  int buf = 0;
-  for (int base = k0; base < k1; base += TP, buf ^= 1) {
-    stage_wait();
-    __syncthreads();  // batch `buf` has landed; the other buffer's readers (previous batch) are done
-    if (base + TP < k1) stage(stage_pair(idn, base + TP + tid, k1).x, buf ^ 1);
-    idn = stage_id(base + 2 * TP + tid, k1, pairs);
-    const float4* sA = reinterpret_cast<const float4*>(smem) + buf * BUF;
-    const float4* sB = sA + TP;
-    const float* sZ = reinterpret_cast<const float*>(sB + TP);
-    const int cnt = min(TP, k1 - base) - wave * 64;           // Gaussians of this batch for this wave
-    const int nblk = cnt <= 0 ? 0 : min(4, (cnt + 15) >> 4);  // blocks of 4 steps (16 Gaussians)
-    for (int blk = 0; blk < nblk; ++blk) {
-      float A0[4], A1[4], A2[4], A3[4], A4[4], Bv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = wave * 64 + blk * 16 + 4 * u + gs;
-        const float4 a = sA[j];
-        const float z = sZ[j];
-        const float dx = xc - a.x, dy = yc - a.y;
-        const float ex = __builtin_amdgcn_exp2f(dx * a.z * dx);
-        Bv[u] = __builtin_amdgcn_exp2f(dy * a.w * dy);
-        if constexpr (TAIL) {
-          const float oe = sB[j].x * ex;
-          A0[u] = oe;
-          A4[u] = oe * z;
-        } else {
-          const float4 b = sB[j];
-          const float oe = b.x * ex;
-          A0[u] = oe;
-          A1[u] = oe * b.y;
-          A2[u] = oe * b.z;
-          A3[u] = oe * b.w;
-          A4[u] = oe * z;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        cW = mfma4(A0[u], Bv[u], cW);
-        if constexpr (!TAIL) {
-          cR = mfma4(A1[u], Bv[u], cR);
-          cG = mfma4(A2[u], Bv[u], cG);
-          cB = mfma4(A3[u], Bv[u], cB);
-        }
-        cD = mfma4(A4[u], Bv[u], cD);
-      }
-    }
-  }
-}
-
 // Items of a tile (virtual tiles 2t: core, 2t+1: tail; contiguous in the item list).
 __device__ __forceinline__ int tile_chunks(int2 r) { return (r.y - r.x + CH - 1) / CH; }
 
@@ -1356,8 +1291,8 @@ __device__ __forceinline__ void write_pixel(const ViewK& v, int p, const float* 
   savedD[p] = acc[4];
 }
 
-// MODE 0: f32 MFMA (GR_FWD_F32=1); 1: split bf16, W and D f32-grade; 2: split bf16, W and D within
-// 2^-16 (views rendered with no_depth_grad).
+// MODE 1: split bf16, W and D f32-grade; 2: split bf16, W and D within 2^-16 (views rendered with
+// no_depth_grad).
 #ifndef GR_FWD_WAVES
 #define GR_FWD_WAVES 6
 #endif
@@ -1381,17 +1316,10 @@ __global__ __launch_bounds__(256, GR_FWD_WAVES) void k_raster_fwd_mfma(ViewK v, 
   const float xc = (float)(tx * T + li) + 0.5f;  // A row = x
   const float yc = (float)(ty * T + li) + 0.5f;  // B col = y
   f32x4 cW = {0.f, 0.f, 0.f, 0.f}, cR = cW, cG = cW, cB = cW, cD = cW;
-  if constexpr (MODE > 0) {
-    if (it.x & 1)
-      fwd_accumulate_bf16<true, MODE == 1>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
-    else
-      fwd_accumulate_bf16<false, MODE == 1>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
-  } else {
-    if (it.x & 1)
-      fwd_accumulate<true>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
-    else
-      fwd_accumulate<false>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
-  }
+  if (it.x & 1)
+    fwd_accumulate_bf16<true, MODE == 1>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
+  else
+    fwd_accumulate_bf16<false, MODE == 1>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
   __syncthreads();
   {  // lane holds C[x = 4*gs + r][y = li]: pixel index y*16 + x, 4 consecutive x
     float* rw = smem + wave * 5 * TP + li * T + 4 * gs;
@@ -1440,7 +1368,6 @@ __global__ __launch_bounds__(256) void k_fwd_finalize(ViewK v, const int2* __res
   write_pixel(v, y * v.W + x, acc, out_rgb, out_alpha, out_depth, saved4, savedD);
 }
 
-constexpr int UL = 5 * 2 * TP;  // floats of backward operands per tile (k_pixel_grads, f32 kernel)
 // bf16 split-precision backward (k_raster_bwd_bf16): per tile, A fragments of v_mfma_f32_32x32x16_bf16
 // for 2 sides (T: contraction over x, R: over y) x 3 channel pairs x 3 bf16 pieces x 64 lanes, 16 B each.
 constexpr int UF_FRAGS = 2 * 3 * 3 * 64;  // uint4 per tile
@@ -1463,7 +1390,7 @@ __device__ __forceinline__ int kslot_pixel(int h, int j) { return (j < 4) ? 4 * 
 __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __restrict__ saved4,
                                                      const float* __restrict__ savedD, const float* __restrict__ g_rgb,
                                                      const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
-                                                     float* __restrict__ U, uint4* __restrict__ UF, int pieces) {
+                                                     uint4* __restrict__ UF, int pieces) {
   const int tile = blockIdx.x, tid = threadIdx.x;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
@@ -1496,9 +1423,7 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
     }
     u[3] = gW;
   }
-  // operand layout of k_raster_bwd_mfma (UL floats per tile): per channel k, AT[l][s] = U_k(x = 4xs+s,
-  // y = li) and then AR[l][s] = U_k(x = li, y = 4xs+s), l = li + 16 xs: lane l reads one float4 each
-  if (UF) {  // bf16 fragments: stage u in LDS, then 384 (side, pair, lane) fragment triples
+  {  // bf16 fragments: stage u in LDS, then 384 (side, pair, lane) fragment triples
     __shared__ float sU[5][TP];
 #pragma unroll
     for (int k = 0; k < 5; ++k) sU[k][tid] = u[k];
@@ -1535,35 +1460,8 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
                          pack_bf16(mid[6], mid[7]));
       o[128] = make_uint4(pack_bf16(lo[0], lo[1]), pack_bf16(lo[2], lo[3]), pack_bf16(lo[4], lo[5]), pack_bf16(lo[6], lo[7]));
     }
-    return;
-  }
-  float* dst = U + (size_t)tile * UL;
-  const int px = tid & (T - 1), py = tid >> 4;
-  const int at = (py + 16 * (px >> 2)) * 4 + (px & 3), ar = TP + (px + 16 * (py >> 2)) * 4 + (py & 3);
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    dst[k * 2 * TP + at] = u[k];
-    dst[k * 2 * TP + ar] = u[k];
   }
 }
-
-// Backward: one workgroup (4 waves) per work item; wave w takes groups [4w, 4w+4) of 16 Gaussians of
-// each staged batch of 256.  Per group two sets of five K = 16 contractions (one per upstream
-// channel k, U = (dC_r, dC_g, dC_b, dW, dD)):
-//   T_k[y][g] = sum_x U_k[x][y] ex_g(x)     (over x; the VALU then weights rows y by ey, dy, dy^2)
-//   R_k[x][g] = sum_y U_k[x][y] ey_g(y)     (over y; rows x weighted by ex, dx, dx^2)
-// which give every moment the 9 pair partials need:
-//   S0..2 = sum_y ey T_{rgb}, S3 = sum_y ey T_D (times o), and with the colour/depth fold
-//   G = sum_k vv_k (.)_k, vv = (r, g, b, 1, z):  S4 = sum_y ey G_T, S6 = sum_y ey dy G_T,
-//   S8 = sum_y ey dy^2 G_T, S5 = sum_x ex dx G_R, S7 = sum_x ex dx^2 G_R.
-// 40 MFMA 16x16x4 per 16 pairs (the dx-weighted x contractions of a single-axis form need 60).
-// K step s of lane row xs covers pixel 4 xs + s on the contracted axis, so the ex (ey) a lane feeds
-// to the T (R) MFMA are exactly the weights its R (T) output rows need: 8 exponentials per lane.
-// Partials per pair (9 floats) go to the pair's slot (Gaussian's first slot + index of the tile
-// inside its rectangle), so k_reduce_bwd reads each Gaussian's partials contiguously and in order.
-#ifndef GR_BWD_WAVES
-#define GR_BWD_WAVES 4
-#endif
 
 // Sum over the 4 lane rows (lanes l, l+16, l+32, l+48) of a pair of values with one
 // v_permlane16_swap: returns rows {a01, b01, a23, b23} (row r of the result holds the named sum).
@@ -1577,138 +1475,8 @@ __device__ __forceinline__ float pair32(float ab, float cd) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// One staged batch loop of a backward work item.  TAIL items (tail pairs of the two-zone
-// footprint) carry only the depth-coupled terms: channels dW and dD (16 MFMA per 16 pairs), colour
-// sums 0, gw = dW + z dD.
-template <bool TAIL>
-__device__ __forceinline__ void bwd_item(int n, int tile, int k0, int k1, int tid, int wave, int li, int xs, int tx, int ty,
-                                         const float* __restrict__ U, const int2* __restrict__ pairs,
-                                         const float4* __restrict__ rec, float* __restrict__ partials,
-                                         float4 (*sA)[TP], float4 (*sB)[TP], float (*sZ)[TP],
-                                         float4* sU) {
-  constexpr int KLO = TAIL ? 3 : 0;  // first upstream channel contracted
-  const int lane = tid & 63;
-  // A operands (tile-constant) staged in LDS in lane order: sU[k][0][l] = AT_k, sU[k][1][l] = AR_k,
-  // AT_k[s] = U_k(x = 4xs+s, y = li), AR_k[s] = U_k(x = li, y = 4xs+s)
-  {
-    const float4* Ug = reinterpret_cast<const float4*>(U + (size_t)tile * UL);
-    for (int c = wave; c < UL / 256; c += 4) glds16(Ug + 64 * c + lane, sU + 64 * c);
-  }
-  const float x0 = (float)(tx * T + 4 * xs) + 0.5f, y0 = (float)(ty * T + 4 * xs) + 0.5f;
-  // records by LDS-DMA; the pair's partial-sum slot (its emission index) by a plain LDS store
-  auto stage = [&](int2 pr, int b) {
-    const float4* p = rec_of(pr.x, n, rec);
-    glds16(p, &sA[b][64 * wave]);
-    glds16(p + 1, &sB[b][64 * wave]);
-    glds4(zrec_of(pr.x, n, rec), &sZ[b][64 * wave]);
-  };
-  stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1), 0);
-  int2 idn = stage_id(k0 + TP + tid, k1, pairs);  // raw: batch base + TP
-  int buf = 0;
-  for (int base = k0; base < k1; base += TP, buf ^= 1) {
-    stage_wait();
-    __syncthreads();  // batch `buf` has landed; the other buffer's readers (previous batch) are done
-    if (base + TP < k1) stage(stage_pair(idn, base + TP + tid, k1), buf ^ 1);
-    idn = stage_id(base + 2 * TP + tid, k1, pairs);
-    const int nb = min(TP, k1 - base);  // Gaussians of this batch
-    const int cnt = nb - wave * 64;
-    const int ngr = cnt <= 0 ? 0 : min(4, (cnt + 15) >> 4);
-    for (int gi = 0; gi < ngr; ++gi) {
-      const int j = wave * 64 + gi * 16 + li;
-      const float4 a = sA[buf][j];
-      const float4 b = sB[buf][j];
-      const float z = sZ[buf][j];
-      const int myslot = j < nb ? base + j : -1;  // the pair's sorted position = its partial-sum row
-      float ex[4], ey[4], dx[4], dy[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        dx[s] = (x0 + (float)s) - a.x;
-        dy[s] = (y0 + (float)s) - a.y;
-        ex[s] = __builtin_amdgcn_exp2f(dx[s] * a.z * dx[s]);  // exactly 0 for padding
-        ey[s] = __builtin_amdgcn_exp2f(dy[s] * a.w * dy[s]);
-      }
-      f32x4 DT[5], DR[5];
-#pragma unroll
-      for (int k = KLO; k < 5; ++k) {
-        DT[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-        DR[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int k = KLO; k < 5; ++k) {
-        const float4 at = sU[(2 * k) * 64 + lane], ar = sU[(2 * k + 1) * 64 + lane];
-        DT[k] = mfma4(at.x, ex[0], DT[k]);
-        DR[k] = mfma4(ar.x, ey[0], DR[k]);
-        DT[k] = mfma4(at.y, ex[1], DT[k]);
-        DR[k] = mfma4(ar.y, ey[1], DR[k]);
-        DT[k] = mfma4(at.z, ex[2], DT[k]);
-        DR[k] = mfma4(ar.z, ey[2], DR[k]);
-        DT[k] = mfma4(at.w, ex[3], DT[k]);
-        DR[k] = mfma4(ar.w, ey[3], DR[k]);
-      }
-      // lane holds T[y = 4xs + r][g = li] and R[x = 4xs + r][g = li]
-      float S[NPART] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if constexpr (!TAIL) {
-          S[0] = fmaf(ey[r], DT[0][r], S[0]);
-          S[1] = fmaf(ey[r], DT[1][r], S[1]);
-          S[2] = fmaf(ey[r], DT[2][r], S[2]);
-        }
-        S[3] = fmaf(ey[r], DT[4][r], S[3]);
-        const float GT = TAIL ? fmaf(z, DT[4][r], DT[3][r])
-                              : fmaf(z, DT[4][r], fmaf(b.w, DT[2][r], fmaf(b.z, DT[1][r], fmaf(b.y, DT[0][r], DT[3][r]))));
-        const float t = ey[r] * GT;
-        S[4] += t;
-        const float tdy = t * dy[r];
-        S[6] += tdy;
-        S[8] = fmaf(tdy, dy[r], S[8]);
-        const float GR = TAIL ? fmaf(z, DR[4][r], DR[3][r])
-                              : fmaf(z, DR[4][r], fmaf(b.w, DR[2][r], fmaf(b.z, DR[1][r], fmaf(b.y, DR[0][r], DR[3][r]))));
-        const float tdx = (ex[r] * GR) * dx[r];  // (0 * G) * dx: padding stays 0, never 0 * inf
-        S[5] += tdx;
-        S[7] = fmaf(tdx, dx[r], S[7]);
-      }
-      // row r of R03 holds the total of S_r, of R47 the total of S_{4+r}; rows 0 and 1 of R8 hold S8
-      const float R03 = pair32(pair16(S[0], S[1]), pair16(S[2], S[3]));
-      const float R47 = pair32(pair16(S[4], S[5]), pair16(S[6], S[7]));
-      const float R8 = pair32(pair16(S[8], S[8]), 0.0f);
-      if (myslot >= 0) {
-        float* dst = partials + (size_t)myslot * NPART;
-        dst[xs] = b.x * R03;  // colour / depth sums carry the opacity
-        dst[4 + xs] = R47;
-        if (xs == 0) dst[8] = R8;
-      }
-    }
-  }
-}
-
-// depth = 0 (no upstream depth gradient): tail items have nothing to add and return at once; their
-// slots are never read (k_reduce_bwd skips tail tiles in that mode).
-__global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
-    ViewK v, int n, const int4* __restrict__ items, const int* __restrict__ num_items, const int2* __restrict__ pairs,
-    const float4* __restrict__ rec, const float* __restrict__ U, float* __restrict__ partials, int depth) {
-  __shared__ __attribute__((aligned(16))) float4 sA[2][TP];
-  __shared__ __attribute__((aligned(16))) float4 sB[2][TP];
-  __shared__ float sZ[2][TP];
-  __shared__ __attribute__((aligned(16))) float4 sU[UL / 4];
-  const int nitems = *num_items;
-  if ((int)blockIdx.x >= nitems) return;
-  const int item = xcd_item(blockIdx.x, nitems);
-  const int4 it = items[item];
-  const bool tail = it.x & 1;
-  if (tail && !depth) return;
-  const int tile = it.x >> 1, k0 = it.y, k1 = it.z;
-  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int li = lane & 15, xs = lane >> 4;
-  if (tail)
-    bwd_item<true>(n, tile, k0, k1, tid, wave, li, xs, tx, ty, U, pairs, rec, partials, sA, sB, sZ, sU);
-  else
-    bwd_item<false>(n, tile, k0, k1, tid, wave, li, xs, tx, ty, U, pairs, rec, partials, sA, sB, sZ, sU);
-}
-
 // ------------------------------------------------------------------------------------------------
-// Backward, split-precision form.  The same two contractions as k_raster_bwd_mfma,
+// Backward splat, split-precision form: per work item the two contractions
 //   T_k[y][g] = sum_x U_k[x][y] ex_g(x),   R_k[x][g] = sum_y U_k[x][y] ey_g(y),
 // on v_mfma_f32_32x32x16_bf16 (K = the 16 pixels of a tile row / column, N = 32 Gaussians, M = two
 // channels x 16 pixels) with both operands split exactly into three bf16 pieces, x = x0 + x1 + x2,
@@ -1727,15 +1495,6 @@ __global__ __launch_bounds__(256, GR_BWD_WAVES) void k_raster_bwd_mfma(
 // that keeps the kernel at 4 waves per SIMD.
 __device__ __forceinline__ f32x16 mfma_split(const uint4* __restrict__ A, int lane, const s16x8 (&B)[3]) {
   f32x16 c = {};
-#ifdef GR_DIAG_NOMFMA
-  {
-    const uint4 u = A[lane];
-    const float f = __uint_as_float(u.x) + __uint_as_float((unsigned)B[0][0] << 16);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) c[i] = f;
-    return c;
-  }
-#endif
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(A[128 + lane]), B[0], c, 0, 0, 0);
   const s16x8 a1 = as_frag(A[64 + lane]);
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, B[1], c, 0, 0, 0);
@@ -1782,11 +1541,7 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
 #define PX0(q) (pxb + (float)((q) < 4 ? (q) : (q) + 4))
 #define PY0(q) (pyb + (float)((q) < 4 ? (q) : (q) + 4))
   auto stage = [&](int2 pr, int b) {
-#ifdef GR_DIAG_SAMEREC
-    const float4* p = rec_of(pr.x < 0 ? -1 : (pr.x & 63), n, rec);
-#else
     const float4* p = rec_of(pr.x, n, rec);
-#endif
     glds16(p, &sA[b][64 * wave]);
     glds16(p + 1, &sB[b][64 * wave]);
     if constexpr (DEPTH) glds4(zrec_of(pr.x, n, rec), &sZ[b][64 * wave]);  // z enters only the depth-coupled terms
@@ -1796,7 +1551,7 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
   int buf = 0;
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
     stage_wait();
-    __syncthreads();  // batch `buf` has landed; the other buffer's readers (previous batch) are done
+    GR_STAGE_SYNC();
     if (base + TP < k1) stage(stage_pair(idn, base + TP + tid, k1), buf ^ 1);
     idn = stage_id(base + 2 * TP + tid, k1, pairs);
     const int nb = min(TP, k1 - base);
@@ -1812,13 +1567,8 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const float dx = PX0(q) - a.x, dy = PY0(q) - a.y;
-#ifdef GR_DIAG_NOEXP
-        ex[q] = dx * a.z * dx;
-        ey[q] = dy * a.w * dy;
-#else
         ex[q] = __builtin_amdgcn_exp2f(dx * a.z * dx);  // exactly 0 for padding
         ey[q] = __builtin_amdgcn_exp2f(dy * a.w * dy);
-#endif
       }
       // both contractions are issued before either epilogue, so the T epilogue's VALU work runs while
       // the R MFMAs execute
@@ -1841,10 +1591,6 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
         for (int pr = P0; pr < P1; ++pr) DR[pr] = mfma_split2(sUF + (1 * 3 + pr) * 3 * 64, lane, BR);
       }
       float S[NPART] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#ifdef GR_DIAG_NOEPI
-      S[0] = DT[0][0] + DR[0][1]; S[4] = DT[1][3] + DR[1][5]; S[5] = DT[0][9];
-      if (0)
-#endif
       {
       if constexpr (!DEPTH && PIECES == 2) {
         // Moments about the lane's first pixel centre: dy_q = d0 + o_q with o_q = kslot offset (a compile-
@@ -1928,11 +1674,7 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
         // writes float4 h: one aligned, fully coalesced 16-byte store per lane (32 rows = 1 KiB)
         const float Pa = pair32(S[0], S[1]), Pb = pair32(S[2], S[8]), Pc = pair32(S[4], S[5]);
         const float Pd = pair32(S[6], S[7]);
-#ifdef GR_DIAG_NOSTORE
-        if (myslot == -12345)
-#else
         if (myslot >= 0)
-#endif
           reinterpret_cast<float4*>(partials)[2 * (size_t)myslot + h] =
               h == 0 ? make_float4(b.x * Pa, b.x * Pb, Pc, Pd) : make_float4(b.x * Pa, Pb, Pc, Pd);
       } else {
@@ -2448,26 +2190,6 @@ void prof_mark(int which, hipStream_t s) {
 
 inline int blocks_for(int64_t n, int bs = 256) { return (int)((n + bs - 1) / bs); }
 
-// Backward splat kernel: the bf16 split-precision one (default) or the f32 one (GR_BWD_F32=1, kept
-// as the reference form and for A/B timing).  Both meet the same tests.
-bool bwd_split_precision() {
-  static const bool f32 = [] {
-    const char* e = std::getenv("GR_BWD_F32");
-    return e && e[0] == '1';
-  }();
-  return !f32;
-}
-
-// Forward splat kernel: the split bf16 one (default) or the f32 one (GR_FWD_F32=1, kept as the
-// reference form and for A/B timing).  Both meet the same tests.
-bool fwd_split_precision() {
-  static const bool f32 = [] {
-    const char* e = std::getenv("GR_FWD_F32");
-    return e && e[0] == '1';
-  }();
-  return !f32;
-}
-
 gr_status check_view(const gr_view* v) {
   if (!v) return set_error(GR_ERR_INVALID_ARGUMENT, "view is null");
   if (v->width <= 0 || v->height <= 0) return set_error(GR_ERR_INVALID_ARGUMENT, "width/height must be positive");
@@ -2548,7 +2270,7 @@ size_t gr_fwd_scratch_bytes(const gr_view* v, int n, const gr_plan* plan) {
 size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
   const size_t tiles = (size_t)tiles_x_of(v->width) * tiles_y_of(v->height);
-  const size_t per_tile = UL * sizeof(float) > UF_FRAGS * sizeof(uint4) ? UL * sizeof(float) : UF_FRAGS * sizeof(uint4);
+  const size_t per_tile = UF_FRAGS * sizeof(uint4);
   return align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)) + align_up(tiles * per_tile);
 }
 
@@ -2776,7 +2498,7 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
   const int64_t cap = item_cap(vtiles, num_pairs);
   if (num_pairs > 0) {
     prof_mark(PROF_RASTER_FWD, s);
-    hipLaunchKernelGGL(!fwd_split_precision() ? k_raster_fwd_mfma<0> : (v->no_depth_grad ? k_raster_fwd_mfma<2> : k_raster_fwd_mfma<1>),
+    hipLaunchKernelGGL(v->no_depth_grad ? k_raster_fwd_mfma<2> : k_raster_fwd_mfma<1>,
                        dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
                        (const int*)b.num_items, (const int2*)b.ranges, (const int2*)b.pairs, (const float4*)g.rec,
                        sc.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
@@ -2815,29 +2537,23 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
   const size_t HW = (size_t)v->width * v->height;
   float* partials = (float*)ws;
   if (num_pairs > 0) {
-    float* U = (float*)((char*)ws + align_up((size_t)plan->num_slots * NPART * sizeof(float)));
-    const bool split = bwd_split_precision();
+    uint4* UF = (uint4*)((char*)ws + align_up((size_t)plan->num_slots * NPART * sizeof(float)));
     hipLaunchKernelGGL(k_pixel_grads, dim3(tiles), dim3(256), 0, s, vk, (const float4*)saved, saved + 4 * HW, g_rgb,
-                       g_alpha, g_depth, U, split ? (uint4*)U : (uint4*)nullptr, v->no_depth_grad ? 2 : 3);
+                       g_alpha, g_depth, UF, v->no_depth_grad ? 2 : 3);
     GR_HIP_TRY(hipGetLastError());
     const int64_t cap = item_cap(2 * tiles, num_pairs);
     prof_mark(PROF_RASTER_BWD, s);
-    if (split) {
-      auto kern = g_depth != nullptr ? k_raster_bwd_bf16<true, 3>
-                                     : (v->no_depth_grad ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>);
-      hipLaunchKernelGGL(kern, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items,
-                         (const int2*)b.pairs, (const float4*)g.rec, (const uint4*)U, partials);
-    } else
-      hipLaunchKernelGGL(k_raster_bwd_mfma, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
-                         (const int*)b.num_items, (const int2*)b.pairs, (const float4*)g.rec, (const float*)U, partials,
-                         g_depth != nullptr ? 1 : 0);
+    auto kern = g_depth != nullptr ? k_raster_bwd_bf16<true, 3>
+                                   : (v->no_depth_grad ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items,
+                       (const int2*)b.pairs, (const float4*)g.rec, (const uint4*)UF, partials);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_BWD, s);
   }
   prof_mark(PROF_REDUCE, s);
   {
-    // the split backward without a depth gradient writes 8-float rows (bwd_item_bf16)
-    const bool row8 = bwd_split_precision() && g_depth == nullptr;
+    // the backward without a depth gradient writes 8-float rows (bwd_item_bf16)
+    const bool row8 = g_depth == nullptr;
     auto launch = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
                          (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const int*)b.pos_of, (const float*)partials,

@@ -75,7 +75,7 @@ MFMA_16x16x32 = 2 * 16 * 16 * 32
 BF16_FLOP_PER_CORE_PAIR_FWD = 5 * 3 * MFMA_16x16x32 / 32
 BF16_FLOP_PER_TAIL_PAIR_FWD = 2 * 3 * MFMA_16x16x32 / 32
 FWD_KERNEL = "k_raster_fwd_mfma"
-BWD_KERNEL = "k_raster_bwd_mfma" if os.environ.get("GR_BWD_F32") == "1" else "k_raster_bwd_bf16"
+BWD_KERNEL = "k_raster_bwd_bf16"
 # SURVEY.md §8(d) HBM model of the tile-binned algorithm (the north_star's "fraction of the HBM
 # roofline" framing): bytes per view = N (3 B_in + 2 x 36) + K (2 x 12 + 2 x 36 + 2 x 36) + 60 H W
 # with B_in = 40 (RGB), K = pairs per view as binned here.
