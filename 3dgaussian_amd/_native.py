@@ -86,6 +86,9 @@ _SIG = {
     "gr_bwd_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
     "gr_bwd": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, _P, _P, _P, ctypes.c_size_t, _P]),
+    "gr_bwd_l1": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P,
+                                 ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t,
+                                 _P]),
     "gr_render_u8": (ctypes.c_int, [ctypes.POINTER(GrRenderParams), ctypes.c_int, _P, _P, _P, _P, _P]),
     "gr_geom_layout": (None, [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
     "gr_bins_layout": (None, [_VP, ctypes.c_int, _PP, ctypes.POINTER(ctypes.c_size_t)]),

@@ -37,6 +37,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -1387,14 +1388,28 @@ __device__ __forceinline__ int kslot_pixel(int h, int j) { return (j < 4) ? 4 * 
 
 // Per-pixel upstream vector U = (dC_r, dC_g, dC_b, dW, dD) of the OIT finalize
 // (torch_renderer.py:192-203), laid out [tile][channel][256] for the backward work items.
+// Fused fit loss (L1 != nullptr, gr_bwd_l1): the upstream gradients are those of the fit loop's
+// view loss mean|out - t| + w_sil mean|alpha - m| (fit_multiview_stub.py:292-299) scaled by g_scale,
+// evaluated here from the outputs recomputed bit-exactly from the saved sums (as write_pixel made them),
+// with torch's abs' = sign (sign(0) = 0); per-tile sums of |out - t| and |alpha - m| go to tile_loss.
+struct L1Args {
+  const float* t_rgb;   // (H,W,3) target image
+  const float* t_mask;  // (H,W) silhouette target or nullptr
+  float w_sil, g_scale;
+  float* tile_loss;     // [tiles][2]
+};
+
+__device__ __forceinline__ float sign0(float t) { return t > 0.0f ? 1.0f : (t < 0.0f ? -1.0f : 0.0f); }
+
 __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __restrict__ saved4,
                                                      const float* __restrict__ savedD, const float* __restrict__ g_rgb,
                                                      const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
-                                                     uint4* __restrict__ UF, int pieces) {
+                                                     uint4* __restrict__ UF, int pieces, L1Args l1) {
   const int tile = blockIdx.x, tid = threadIdx.x;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
   float u[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  float l_rgb = 0.f, l_sil = 0.f;
   if (x < v.W && y < v.H) {
     const int p = y * v.W + x;
     const float4 s = saved4[p];
@@ -1402,17 +1417,34 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
     const float den = 1.0f + s.x, dden = s.x + 1e-6f;
     float gW = 0.f;
     const float C[3] = {s.y, s.z, s.w};
+    const float HWf = (float)v.W * (float)v.H;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const float r = (v.bg[k] + C[k]) / den;
-      const float go = (r >= 0.0f && r <= 1.0f) ? g_rgb[3 * p + k] : 0.0f;
+      float gk;
+      if (l1.t_rgb) {
+        const float t = clamp01(r) - l1.t_rgb[3 * p + k];
+        l_rgb += fabsf(t);
+        gk = sign0(t) * (l1.g_scale / (3.0f * HWf));
+      } else {
+        gk = g_rgb[3 * p + k];
+      }
+      const float go = (r >= 0.0f && r <= 1.0f) ? gk : 0.0f;
       u[k] = go / den;
       gW -= go * r / den;
     }
-    if (g_alpha) {
-      const float al = s.x / den;
-      if (al >= 0.0f && al <= 1.0f) gW += g_alpha[p] / (den * den);
+    const float al = s.x / den;
+    float ga = 0.0f;
+    bool has_a = g_alpha != nullptr;
+    if (l1.t_rgb && l1.t_mask) {
+      const float t = clamp01(al) - l1.t_mask[p];
+      l_sil = fabsf(t);
+      ga = sign0(t) * ((l1.w_sil * l1.g_scale) / HWf);
+      has_a = true;
+    } else if (g_alpha) {
+      ga = g_alpha[p];
     }
+    if (has_a && al >= 0.0f && al <= 1.0f) gW += ga / (den * den);
     if (g_depth) {
       const float d = Dp / dden;
       if (d >= 0.0f) {
@@ -1422,6 +1454,23 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
       }
     }
     u[3] = gW;
+  }
+  if (l1.tile_loss) {  // per-tile loss sums: waves, then the 4 wave sums in a fixed order
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      l_rgb += __shfl_xor(l_rgb, o);
+      l_sil += __shfl_xor(l_sil, o);
+    }
+    __shared__ float sL[2][4];
+    if ((tid & 63) == 0) {
+      sL[0][tid >> 6] = l_rgb;
+      sL[1][tid >> 6] = l_sil;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      l1.tile_loss[2 * tile] = ((sL[0][0] + sL[0][1]) + sL[0][2]) + sL[0][3];
+      l1.tile_loss[2 * tile + 1] = ((sL[1][0] + sL[1][1]) + sL[1][2]) + sL[1][3];
+    }
   }
   {  // bf16 fragments: stage u in LDS, then 384 (side, pair, lane) fragment triples
     __shared__ float sU[5][TP];
@@ -1750,7 +1799,7 @@ template <int CD, typename F>
 __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, const float* __restrict__ means,
                            const float* __restrict__ scales, const float* __restrict__ colors,
                            const float* __restrict__ opac, float* __restrict__ d_means, float* __restrict__ d_scales,
-                           float* __restrict__ d_colors, float* __restrict__ d_opac);
+                           float* __restrict__ d_colors, float* __restrict__ d_opac, bool acc);
 
 // Block of RG Gaussians, 4 lanes each.  A Gaussian's pairs are its emission indices: core pairs
 // [c_i, c_i + core_i) and (only with an upstream depth gradient; otherwise the backward skipped them)
@@ -1766,7 +1815,7 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
                                                     const Cnt2* __restrict__ offsets, const int* __restrict__ pos_of,
                                                     const float* __restrict__ partials, float* __restrict__ d_means,
                                                     float* __restrict__ d_scales, float* __restrict__ d_colors,
-                                                    float* __restrict__ d_opac, int depth) {
+                                                    float* __restrict__ d_opac, int depth, int acc) {
   const int g0 = blockIdx.x * RG;
   const int tid = threadIdx.x, q4 = tid & 3;
   const int i = g0 + (tid >> 2);
@@ -1848,14 +1897,17 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
 #pragma unroll
   for (int q = 0; q < NPART; ++q) Sf[q] = sS[tid][q];
   chain_rule<CD, float>(v, g0 + tid, Sf, sS[tid][NPART] != 0.0f ? 1u : 0u, means, scales, colors, opac, d_means, d_scales,
-                        d_colors, d_opac);
+                        d_colors, d_opac, acc != 0);
 }
 
 template <int CD, typename F>
 __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, const float* __restrict__ means,
                            const float* __restrict__ scales, const float* __restrict__ colors,
                            const float* __restrict__ opac, float* __restrict__ d_means, float* __restrict__ d_scales,
-                           float* __restrict__ d_colors, float* __restrict__ d_opac) {
+                           float* __restrict__ d_colors, float* __restrict__ d_opac, bool acc) {
+  // acc: add this view's gradient to the buffers (a fit's per-stream gradient accumulators, summed
+  // over its views in view order: deterministic) instead of writing it
+  auto put = [acc](float* dst, float val) { *dst = acc ? *dst + val : val; };
   const float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
   const float s0 = scales[3 * i], s1 = scales[3 * i + 1];
   const float op = opac[i];
@@ -1864,12 +1916,12 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
   if (cnt == 0) {
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      d_means[3 * i + q] = 0.f;
-      d_scales[3 * i + q] = 0.f;
+      put(&d_means[3 * i + q], 0.f);
+      put(&d_scales[3 * i + q], 0.f);
     }
 #pragma unroll
-    for (int q = 0; q < CD; ++q) dc[q] = 0.f;
-    d_opac[i] = 0.f;
+    for (int q = 0; q < CD; ++q) put(&dc[q], 0.f);
+    put(&d_opac[i], 0.f);
     return;
   }
   Proj p;
@@ -1885,9 +1937,9 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
   const F kx = F(0.5) * v.W * fx / p.za, ky = F(0.5) * v.H * fy / p.za;
   const F sgx = s0 > 0.f ? F(1) : (s0 < 0.f ? F(-1) : F(0));
   const F sgy = s1 > 0.f ? F(1) : (s1 < 0.f ? F(-1) : F(0));
-  d_scales[3 * i + 0] = (float)(dsx * kx * sgx);
-  d_scales[3 * i + 1] = (float)(dsy * ky * sgy);
-  d_scales[3 * i + 2] = 0.f;
+  put(&d_scales[3 * i + 0], (float)(dsx * kx * sgx));
+  put(&d_scales[3 * i + 1], (float)(dsy * ky * sgy));
+  put(&d_scales[3 * i + 2], 0.f);
   const F dza = S[3] - dsx * p.sxr / p.za - dsy * p.syr / p.za;
   F dpc[4] = {F(0), F(0), F(0), F(0)};
   if (fabsf(p.pc[2]) >= 1e-6f) dpc[2] += dza * (p.pc[2] > 0.f ? F(1) : (p.pc[2] < 0.f ? F(-1) : F(0)));
@@ -1909,7 +1961,7 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
 #pragma unroll
     for (int r = 0; r < 4; ++r) dm[j] += (F)v.V[r * 4 + j] * dpc[r];
   }
-  d_opac[i] = (float)((op >= 0.0f) ? S[4] : F(0));
+  put(&d_opac[i], (float)((op >= 0.0f) ? S[4] : F(0)));
   float cpre[3];
   eval_color<CD>(v, mx, my, mz, col, cpre);
   F dcol[3];
@@ -1917,7 +1969,7 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
   for (int k = 0; k < 3; ++k) dcol[k] = (cpre[k] >= 0.0f && cpre[k] <= 1.0f) ? S[k] : F(0);
   if constexpr (CD == 3) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) dc[k] = (float)dcol[k];
+    for (int k = 0; k < 3; ++k) put(&dc[k], (float)dcol[k]);
   } else {
     const F vv[3] = {(F)v.cam[0] - mx, (F)v.cam[1] - my, (F)v.cam[2] - mz};
     const F nn = std::sqrt(vv[0] * vv[0] + vv[1] * vv[1] + vv[2] * vv[2]);
@@ -1927,10 +1979,10 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
     if constexpr (CD == 12) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        dc[k] = (float)dcol[k];
+        put(&dc[k], (float)dcol[k]);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          dc[(1 + j) * 3 + k] = (float)(dcol[k] * d[j]);
+          put(&dc[(1 + j) * 3 + k], (float)(dcol[k] * d[j]));
           gd[j] += dcol[k] * (F)col[(1 + j) * 3 + k];
         }
       }
@@ -1941,7 +1993,7 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
       for (int i = 0; i < 16; ++i)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          dc[3 * i + k] = (float)(dcol[k] * Y[i]);
+          put(&dc[3 * i + k], (float)(dcol[k] * Y[i]));
           const F t = dcol[k] * (F)col[3 * i + k];
 #pragma unroll
           for (int j = 0; j < 3; ++j) gd[j] += t * G[i][j];
@@ -1954,7 +2006,7 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
     }
   }
 #pragma unroll
-  for (int j = 0; j < 3; ++j) d_means[3 * i + j] = (float)dm[j];
+  for (int j = 0; j < 3; ++j) put(&d_means[3 * i + j], (float)dm[j]);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2148,6 +2200,32 @@ __global__ __launch_bounds__(256) void k_l1_final(const float* __restrict__ part
   *loss = n2 > 0 ? m1 + w2 * (float)(r2[0] / (double)n2) : m1;
 }
 
+// The view loss of gr_bwd_l1 from its per-tile sums (double, fixed order): mean|out - t| +
+// w_sil mean|alpha - m|, the value k_l1_final gives for the same images.
+__global__ __launch_bounds__(256) void k_tile_loss_final(const float* __restrict__ tile_loss, int tiles, int64_t n1,
+                                                         int64_t n2, float w_sil, float* __restrict__ loss) {
+  __shared__ double r1[256], r2[256];
+  const int t = threadIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = t; i < tiles; i += 256) {
+    s1 += (double)tile_loss[2 * i];
+    s2 += (double)tile_loss[2 * i + 1];
+  }
+  r1[t] = s1;
+  r2[t] = s2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) {
+      r1[t] += r1[t + w];
+      r2[t] += r2[t + w];
+    }
+    __syncthreads();
+  }
+  if (t != 0) return;
+  const float m1 = (float)(r1[0] / (double)n1);
+  *loss = n2 > 0 ? m1 + w_sil * (float)(r2[0] / (double)n2) : m1;
+}
+
 // d/da = g sign(a - b) / n1, d/dc = (w2 g) sign(c - d) / n2 (torch: abs' = sign, sign(0) = 0).
 __global__ __launch_bounds__(256) void k_l1_grad(const float* __restrict__ a, const float* __restrict__ b, int64_t n1,
                                                  const float* __restrict__ c, const float* __restrict__ d, int64_t n2,
@@ -2173,12 +2251,14 @@ struct ProfSlot {
   size_t used = 0;
 };
 std::mutex g_prof_mu;
-bool g_prof_on = false;
+std::atomic<bool> g_prof_on{false};
 ProfSlot g_prof[PROF_SLOTS];
 
+// Off (the default): one relaxed atomic load per mark, no lock on the launch path.
 void prof_mark(int which, hipStream_t s) {
+  if (!g_prof_on.load(std::memory_order_relaxed)) return;
   std::lock_guard<std::mutex> lk(g_prof_mu);
-  if (!g_prof_on) return;
+  if (!g_prof_on.load(std::memory_order_relaxed)) return;
   ProfSlot& sl = g_prof[which];
   if (sl.used == sl.ev.size()) {
     hipEvent_t e;
@@ -2208,13 +2288,13 @@ const char* gr_last_error(void) { return g_last_error.c_str(); }
 
 void gr_profile_begin(void) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
-  g_prof_on = true;
   for (auto& sl : g_prof) sl.used = 0;
+  g_prof_on.store(true, std::memory_order_relaxed);
 }
 
 gr_status gr_profile_end(double total_ms[4], int launches[4]) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
-  g_prof_on = false;
+  g_prof_on.store(false, std::memory_order_relaxed);
   for (int k = 0; k < PROF_SLOTS; ++k) {
     ProfSlot& sl = g_prof[k];
     double tot = 0.0;
@@ -2271,7 +2351,8 @@ size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
   const size_t tiles = (size_t)tiles_x_of(v->width) * tiles_y_of(v->height);
   const size_t per_tile = UF_FRAGS * sizeof(uint4);
-  return align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)) + align_up(tiles * per_tile);
+  return align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)) + align_up(tiles * per_tile) +
+         align_up(tiles * 2 * sizeof(float));  // per-tile loss sums (gr_bwd_l1)
 }
 
 // Decode the scanned totals (core, tail pairs) into the plan; a count that does not fit int32 is
@@ -2511,10 +2592,14 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
   return GR_OK;
 }
 
-gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
-                 const float* colors, int color_dim, const float* opacities, const void* geom, const void* bins,
-                 const float* saved, const float* g_rgb, const float* g_alpha, const float* g_depth, float* d_means,
-                 float* d_scales, float* d_colors, float* d_opacities, void* ws, size_t ws_bytes, void* stream) {
+}  // extern "C" (bwd_impl is internal)
+
+static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
+                          const float* colors, int color_dim, const float* opacities, const void* geom, const void* bins,
+                          const float* saved, const float* g_rgb, const float* g_alpha, const float* g_depth,
+                          const float* t_rgb, const float* t_mask, float w_sil, float g_scale, float* loss_out,
+                          float* d_means, float* d_scales, float* d_colors, float* d_opacities, int accumulate, void* ws,
+                          size_t ws_bytes, void* stream) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
   if (g_depth && v->no_depth_grad)
@@ -2524,10 +2609,11 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
   if (color_dim != 3 && color_dim != 12 && color_dim != 48)
     return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");
   if (n == 0) return GR_OK;
-  if (!g_rgb || !saved || !geom || !bins || !d_means || !d_scales || !d_colors || !d_opacities)
+  if ((!g_rgb && !t_rgb) || !saved || !geom || !bins || !d_means || !d_scales || !d_colors || !d_opacities)
     return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+  if (t_rgb && (!loss_out || !ws)) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_l1: null loss or workspace");
   const int64_t num_pairs = plan->num_pairs;
-  if (num_pairs > 0 && (!ws || ws_bytes < gr_bwd_bytes(v, n, plan)))
+  if ((num_pairs > 0 || t_rgb) && (!ws || ws_bytes < gr_bwd_bytes(v, n, plan)))
     return set_error(GR_ERR_WORKSPACE, "backward workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const ViewK vk = make_viewk(v);
@@ -2536,11 +2622,20 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
   Bins b = bins_view((void*)bins, 2 * tiles, num_pairs);
   const size_t HW = (size_t)v->width * v->height;
   float* partials = (float*)ws;
-  if (num_pairs > 0) {
-    uint4* UF = (uint4*)((char*)ws + align_up((size_t)plan->num_slots * NPART * sizeof(float)));
+  uint4* UF = (uint4*)((char*)ws + align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)));
+  float* tile_loss = (float*)((char*)UF + align_up((size_t)tiles * UF_FRAGS * sizeof(uint4)));
+  const L1Args l1{t_rgb, t_mask, w_sil, g_scale, t_rgb ? tile_loss : nullptr};
+  if (num_pairs > 0 || t_rgb) {
     hipLaunchKernelGGL(k_pixel_grads, dim3(tiles), dim3(256), 0, s, vk, (const float4*)saved, saved + 4 * HW, g_rgb,
-                       g_alpha, g_depth, UF, v->no_depth_grad ? 2 : 3);
+                       g_alpha, g_depth, UF, v->no_depth_grad ? 2 : 3, l1);
     GR_HIP_TRY(hipGetLastError());
+  }
+  if (t_rgb) {
+    hipLaunchKernelGGL(k_tile_loss_final, dim3(1), dim3(256), 0, s, (const float*)tile_loss, tiles, (int64_t)(3 * HW),
+                       (int64_t)(t_mask ? HW : 0), w_sil, loss_out);
+    GR_HIP_TRY(hipGetLastError());
+  }
+  if (num_pairs > 0) {
     const int64_t cap = item_cap(2 * tiles, num_pairs);
     prof_mark(PROF_RASTER_BWD, s);
     auto kern = g_depth != nullptr ? k_raster_bwd_bf16<true, 3>
@@ -2557,7 +2652,7 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
     auto launch = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
                          (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const int*)b.pos_of, (const float*)partials,
-                         d_means, d_scales, d_colors, d_opacities, g_depth != nullptr ? 1 : 0);
+                         d_means, d_scales, d_colors, d_opacities, g_depth != nullptr ? 1 : 0, accumulate);
     };
     if (color_dim == 3)
       row8 ? launch(k_reduce_bwd<3, true>) : launch(k_reduce_bwd<3, false>);
@@ -2569,6 +2664,27 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_REDUCE, s);
   return GR_OK;
+}
+
+extern "C" {
+
+gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
+                 const float* colors, int color_dim, const float* opacities, const void* geom, const void* bins,
+                 const float* saved, const float* g_rgb, const float* g_alpha, const float* g_depth, float* d_means,
+                 float* d_scales, float* d_colors, float* d_opacities, void* ws, size_t ws_bytes, void* stream) {
+  return bwd_impl(v, n, plan, means, scales, colors, color_dim, opacities, geom, bins, saved, g_rgb, g_alpha, g_depth,
+                  nullptr, nullptr, 0.0f, 0.0f, nullptr, d_means, d_scales, d_colors, d_opacities, 0, ws, ws_bytes, stream);
+}
+
+gr_status gr_bwd_l1(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
+                    const float* colors, int color_dim, const float* opacities, const void* geom, const void* bins,
+                    const float* saved, const float* target_rgb, const float* target_mask, float w_sil, float g_scale,
+                    float* loss_out, float* d_means, float* d_scales, float* d_colors, float* d_opacities,
+                    int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  if (!target_rgb) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_l1: target_rgb is null");
+  return bwd_impl(v, n, plan, means, scales, colors, color_dim, opacities, geom, bins, saved, nullptr, nullptr, nullptr,
+                  target_rgb, target_mask, w_sil, g_scale, loss_out, d_means, d_scales, d_colors, d_opacities,
+                  accumulate, ws, ws_bytes, stream);
 }
 
 gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, const float* scales, const float* colors,

@@ -50,6 +50,9 @@ PREFETCH = max(1, int(os.environ.get("GR_PREFETCH", "3")))  # views prepared ahe
 # steps between re-establishing the Morton order of the moving Gaussians (ViewShardedFitter.respatialize;
 # 0 = only at construction and after densify/prune)
 RESORT_EVERY = max(0, int(os.environ.get("GR_RESORT", "4")))
+# the fit step without a depth loss renders through the fused path (ViewShardedFitter._views_direct:
+# gr_bwd_l1 + per-stream gradient accumulators, no autograd per view); 0 = the autograd path
+DIRECT_BACKWARD = os.environ.get("GR_DIRECT", "1") != "0"
 
 
 # ------------------------------------------------------------------------------------------------
@@ -301,6 +304,11 @@ class ViewShardedFitter:
             loss = loss + self.w_depth * torch.mean(torch.abs(d_pred - self.depths[i]))
         return loss
 
+    def _direct(self, device) -> bool:
+        """The fused path (step_views_direct): HIP render op, fused L1 losses, no depth term."""
+        return (self.render_fn is hip_render and device.type == "cuda" and FUSED_LOSS and DIRECT_BACKWARD
+                and not self._depth_grad())
+
     def step(self) -> torch.Tensor:
         """One iteration; returns the full (all-rank) loss as a 0-d tensor on the device."""
         if RESORT_EVERY and self.steps_done and self.steps_done % RESORT_EVERY == 0:
@@ -309,6 +317,17 @@ class ViewShardedFitter:
         self.opt.zero_grad(set_to_none=True)
         means, scales, colors, opacities = activations(self.params)
         device = means.device
+        if self._direct(device) and means.shape[0] > 0:
+            total = self._views_direct(means, scales, colors, opacities)
+            loss = total / len(self.targets)
+            if self.rank == 0:
+                reg = self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean()
+                loss = loss + reg.detach()
+                torch.autograd.backward([means, scales, colors, opacities, reg], list(self._acc) + [None])
+            else:
+                torch.autograd.backward([means, scales, colors, opacities], list(self._acc))
+            self._acc = None
+            return self._finish_step(loss)
         # HIP renderer: the next view's preparation is enqueued before this view renders, so the
         # host reads each view's pair count while the device is still busy (no idle gap per view);
         # views rotate over NUM_STREAMS HIP streams, so one view's latency-bound binning kernels run
@@ -364,6 +383,63 @@ class ViewShardedFitter:
         if self.rank == 0:
             loss = loss + self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean()
         loss.backward()
+        return self._finish_step(loss)
+
+    def _views_direct(self, means, scales, colors, opacities) -> torch.Tensor:
+        """This rank's views without autograd: per view, the HIP forward, then gr_bwd_l1 (the view's
+        L1 + silhouette loss and its backward fused, fit_multiview_stub.py:292-310) adding the gradient
+        w.r.t. the activated parameters into one accumulator set per HIP stream (in view order:
+        deterministic).  The accumulators are summed in stream order and leave in self._acc for one
+        autograd pass through the activations; returns the sum of the view losses (device, 0-d)."""
+        device = means.device
+        m, s, c, o = (t.detach().contiguous() for t in (means, scales, colors, opacities))
+        views = self.my_views
+        main = torch.cuda.current_stream(device)
+        ns = max(1, min(NUM_STREAMS, len(views)))
+        side = getattr(self, "_side", None)
+        if ns > 1 and (side is None or len(side) != ns - 1 or side[0].device != device):
+            self._side = side = [torch.cuda.Stream(device) for _ in range(ns - 1)]
+        streams = [main] + (side[:ns - 1] if ns > 1 else [])
+        # made on the main stream before the side streams wait for it: every stream's use is ordered
+        # after its allocation, and main waits for every stream before they are read or freed
+        losses_v = torch.empty(max(1, len(views)), dtype=torch.float32, device=device)
+        acc = [tuple(torch.empty_like(t) for t in (m, s, c, o)) for _ in streams]
+        for st in streams[1:]:
+            st.wait_stream(main)
+        bg = self._background(device)
+        w_sil = self.w_sil if (self.masks is not None and self.w_sil > 0.0) else 0.0
+        g_scale = 1.0 / len(self.targets)
+        ahead = {}
+
+        def prepare(j):
+            if j < len(views) and j not in ahead:
+                with torch.cuda.stream(streams[j % ns]):
+                    ahead[j] = self._prepare(views[j], m, s, c, o)
+
+        for j in range(PREFETCH):
+            prepare(j)
+        for j, i in enumerate(views):
+            prepare(j + PREFETCH)
+            k = j % ns
+            with torch.cuda.stream(streams[k]):
+                cam = self.cams[i]
+                gv = tr.make_view(cam.view, cam.proj, self.width, self.height, bg, depth_grad=False)
+                _, _, _, rs = tr.forward_native(m, s, c, o, gv, ahead.pop(j))
+                tr.backward_l1_native(m, s, c, o, rs, self.targets[i], self.masks[i] if w_sil > 0.0 else None, w_sil,
+                                      g_scale, losses_v[j:j + 1], acc[k], accumulate=j >= ns)
+        for st in streams[1:]:
+            main.wait_stream(st)
+        used = min(ns, len(views))
+        out = []
+        for q in range(4):
+            t = acc[0][q]
+            for k in range(1, used):
+                t = t + acc[k][q]
+            out.append(t if used > 0 else torch.zeros_like(acc[0][q]))
+        self._acc = tuple(out)
+        return losses_v[:len(views)].sum() if views else torch.zeros((), device=device)
+
+    def _finish_step(self, loss) -> torch.Tensor:
         plist = list(self.params.values())
         for p in plist:
             if p.grad is None:

@@ -290,6 +290,25 @@ def backward_native(means, scales, colors, opacities, st: RenderState, g_out, g_
     return dm, ds, dc, do
 
 
+def backward_l1_native(means, scales, colors, opacities, st: RenderState, target, mask, w_sil: float, g_scale: float,
+                       loss_out, grads, accumulate: bool) -> None:
+    """gr_bwd_l1 on the current stream: the backward of the fit loop's view loss
+    ``mean|out - target| + w_sil mean|alpha - mask|`` (mask may be None) scaled by ``g_scale``, written
+    (accumulate=False) or added (accumulate=True) into ``grads`` = (d_means, d_scales, d_colors,
+    d_opacities); the unscaled view loss goes to the 0-d / 1-element device tensor ``loss_out``."""
+    L = _native.lib()
+    dev = means.device
+    ws = torch.empty((_ws_round(L.gr_bwd_bytes(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan))),), dtype=torch.uint8,
+                     device=dev)
+    dm, ds, dc, do = grads
+    _native.check(L.gr_bwd_l1(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan), _native.ptr(means), _native.ptr(scales),
+                              _native.ptr(colors), _color_dim(colors), _native.ptr(opacities), _native.ptr(st.geom),
+                              _native.ptr(st.bins), _native.ptr(st.saved), _native.ptr(target), _native.ptr(mask),
+                              ctypes.c_float(w_sil), ctypes.c_float(g_scale), _native.ptr(loss_out), _native.ptr(dm),
+                              _native.ptr(ds), _native.ptr(dc), _native.ptr(do), 1 if accumulate else 0,
+                              _native.ptr(ws), ws.numel(), _stream(dev)), "gr_bwd_l1")
+
+
 def _grad_background(st: RenderState, background: torch.Tensor, g_out: torch.Tensor) -> torch.Tensor:
     """d(out)/d(bg) = sum_p g_out * [0<=out_r<=1] / (1+W)  (torch_renderer.py:194-196)."""
     HW = st.gv.width * st.gv.height
@@ -414,4 +433,5 @@ def render_gaussians_torch(
 
 __all__ = ["Camera", "get_default_device", "perspective", "look_at", "render_gaussians_torch", "rasterize",
            "make_view", "prepare_view", "prepare_native", "Prepared", "forward_native", "backward_native",
+           "backward_l1_native",
            "DEFAULT_CUTOFF", "DEPTH_GRAD_CUTOFF", "DEFAULT_CORE_CUTOFF", "default_cutoff"]

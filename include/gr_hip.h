@@ -18,8 +18,10 @@
  *   - Plain C: no C++ or torch types in any signature.  All matrices are 4x4 row-major float32,
  *     exactly as RenderParams::view/proj (gaussian_types.h:28-30).
  *   - The differentiable entry points (gr_fwd_*, gr_bwd) take DEVICE pointers owned by the caller
- *     and a hipStream_t passed as void*.  They allocate nothing and keep no global state, so they
- *     are reentrant and stream-ordered (unlike renderer.cu:349's function-static buffers).
+ *     and a hipStream_t passed as void*.  They allocate nothing and keep no render state between
+ *     calls, so they are reentrant and stream-ordered (unlike renderer.cu:349's function-static
+ *     buffers).  The only process-global state is the optional diagnostic profiler
+ *     (gr_profile_begin/end, off by default: one atomic load per launch when off).
  *     Workspace sizes come from the *_bytes() queries.
  *   - gr_fwd_prepare is the one call that synchronises its stream: it returns the number of
  *     (Gaussian, tile) pairs, which sizes the binning workspace.  gr_fwd_prepare_async enqueues
@@ -141,6 +143,21 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
                  const void* geom, const void* bins, const float* saved, const float* g_rgb,
                  const float* g_alpha, const float* g_depth, float* d_means, float* d_scales,
                  float* d_colors, float* d_opacities, void* ws, size_t ws_bytes, void* stream);
+
+/* Backward of gr_fwd_render fused with the fit loop's view loss (fit_multiview_stub.py:292-299):
+ *   loss = mean|out - target_rgb| + w_sil * mean|alpha - target_mask|   (target_mask may be NULL)
+ * The upstream gradients are those of g_scale * loss (torch's abs' = sign, sign(0) = 0), computed
+ * per pixel from the saved sums (the outputs recomputed bit-exactly); *loss_out (device float)
+ * receives the unscaled view loss.  accumulate != 0 adds the gradients to d_* (a fit's gradient
+ * accumulators, one per stream: deterministic in view order) instead of writing them.
+ * Replaces, for the fit loop, the autograd chain L1 loss -> gr_bwd -> gradient accumulation across
+ * views (fit_multiview_stub.py:299-310).  Same workspace as gr_bwd.  n == 0: no-op. */
+gr_status gr_bwd_l1(const gr_view* v, int n, const gr_plan* plan, const float* means,
+                    const float* scales, const float* colors, int color_dim, const float* opacities,
+                    const void* geom, const void* bins, const float* saved, const float* target_rgb,
+                    const float* target_mask, float w_sil, float g_scale, float* loss_out,
+                    float* d_means, float* d_scales, float* d_colors, float* d_opacities,
+                    int accumulate, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Legacy uint8 surface (host pointers), replaces gr::render_gaussians (renderer.h:33-39).    */
