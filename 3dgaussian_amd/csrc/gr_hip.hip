@@ -1166,11 +1166,23 @@ constexpr int FWD_PLANES = 9;
 // address register: the instruction offset (4f) is added to the LDS address too, so m0 is set to
 // plane f's base minus 4f.
 #define GR_GLDS_FIELD(F) "s_add_u32 m0, %3, " #F "*1020\n\ts_nop 0\n\tglobal_load_lds_dword %1, off offset:" #F "*4\n\t"
-template <bool TAIL>
+#define GR_GLDS_FIELD2(F) "s_add_u32 m0, %2, " #F "*1020\n\ts_nop 0\n\tglobal_load_lds_dword %1, off offset:" #F "*4\n\t"
+template <bool TAIL, bool ZCH = true>
 __device__ __forceinline__ void glds4_planes(const float4* rec, const float* z, float* wave_base) {
   static_assert(TP == 256, "plane stride 1024 B is written into the asm below");
   unsigned keep;
-  if constexpr (TAIL) {
+  if constexpr (!ZCH) {  // no depth channel: px py qx qy o (tail: W only) or all eight record fields
+    if constexpr (TAIL)
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
+                   GR_GLDS_FIELD2(1) GR_GLDS_FIELD2(2) GR_GLDS_FIELD2(3) GR_GLDS_FIELD2(4) "s_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(rec), "s"(lds_addr(wave_base)) : "memory", "scc");
+    else
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
+                   GR_GLDS_FIELD2(1) GR_GLDS_FIELD2(2) GR_GLDS_FIELD2(3) GR_GLDS_FIELD2(4)
+                   GR_GLDS_FIELD2(5) GR_GLDS_FIELD2(6) GR_GLDS_FIELD2(7) "s_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(rec), "s"(lds_addr(wave_base)) : "memory", "scc");
+    (void)z;
+  } else if constexpr (TAIL) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
                  GR_GLDS_FIELD(1) GR_GLDS_FIELD(2) GR_GLDS_FIELD(3) GR_GLDS_FIELD(4)
                  "s_add_u32 m0, %3, 8192\n\ts_nop 0\n\tglobal_load_lds_dword %2, off\n\ts_mov_b32 m0, %0"
@@ -1184,14 +1196,17 @@ __device__ __forceinline__ void glds4_planes(const float4* rec, const float* z, 
   }
 }
 #undef GR_GLDS_FIELD
+#undef GR_GLDS_FIELD2
 
-template <bool TAIL, bool PRECISE>
+// ZCH = false (views rendered for the fused fit path: no depth output, no depth gradient): the depth
+// channel is not accumulated (no z staging, no D products).
+template <bool TAIL, bool PRECISE, bool ZCH = true>
 __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, int k1, int tid, int wave, float xc, float yc,
                                                     int gq, const int2* __restrict__ pairs, const float4* __restrict__ rec,
                                                     f32x4& cW, f32x4& cR, f32x4& cG, f32x4& cB, f32x4& cD) {
   constexpr int BUF = FWD_PLANES * TP;  // floats per buffer
   auto stage = [&](int g, int b) {
-    glds4_planes<TAIL>(rec_of(g, n, rec), zrec_of(g, n, rec), smem + b * BUF + 64 * wave);
+    glds4_planes<TAIL, ZCH>(rec_of(g, n, rec), zrec_of(g, n, rec), smem + b * BUF + 64 * wave);
   };
   stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1).x, 0);
   int2 idn = stage_id(k0 + TP + tid, k1, pairs);
@@ -1221,7 +1236,7 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
       ld(2, qx);
       ld(3, qy);
       ld(4, o);
-      ld(8, z);
+      if constexpr (ZCH) ld(8, z);
       f32x2_t aW[4], aD[4], bv[4], oe[4];
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
@@ -1231,7 +1246,7 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
         bv[p] = f32x2_t{__builtin_amdgcn_exp2f(ty.x), __builtin_amdgcn_exp2f(ty.y)};
         oe[p] = o[p] * ex;
         aW[p] = oe[p];
-        aD[p] = oe[p] * z[p];
+        if constexpr (ZCH) aD[p] = oe[p] * z[p];
       }
       s16x8 fb[3], f3[3];
       if constexpr (PRECISE) {
@@ -1247,8 +1262,10 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
         fb[1] = f2b[1];
         split2_frag2(aW, f2);
         cW = mfma16_split2<false>(f2, fb, cW);
-        split2_frag2(aD, f2);
-        cD = mfma16_split2<false>(f2, fb, cD);
+        if constexpr (ZCH) {
+          split2_frag2(aD, f2);
+          cD = mfma16_split2<false>(f2, fb, cD);
+        }
       }
       if constexpr (!TAIL) {
         f32x2_t c[4], a[4];
@@ -1293,7 +1310,8 @@ __device__ __forceinline__ void write_pixel(const ViewK& v, int p, const float* 
 }
 
 // MODE 1: split bf16, W and D f32-grade; 2: split bf16, W and D within 2^-16 (views rendered with
-// no_depth_grad).
+// no_depth_grad); 3: as 2 without the depth channel (no_depth_grad views rendered with no depth output:
+// the fused fit path; the saved depth sums are then 0 and unused).
 #ifndef GR_FWD_WAVES
 #define GR_FWD_WAVES 6
 #endif
@@ -1318,9 +1336,9 @@ __global__ __launch_bounds__(256, GR_FWD_WAVES) void k_raster_fwd_mfma(ViewK v, 
   const float yc = (float)(ty * T + li) + 0.5f;  // B col = y
   f32x4 cW = {0.f, 0.f, 0.f, 0.f}, cR = cW, cG = cW, cB = cW, cD = cW;
   if (it.x & 1)
-    fwd_accumulate_bf16<true, MODE == 1>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
+    fwd_accumulate_bf16<true, MODE == 1, MODE != 3>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
   else
-    fwd_accumulate_bf16<false, MODE == 1>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
+    fwd_accumulate_bf16<false, MODE == 1, MODE != 3>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
   __syncthreads();
   {  // lane holds C[x = 4*gs + r][y = li]: pixel index y*16 + x, 4 consecutive x
     float* rw = smem + wave * 5 * TP + li * T + 4 * gs;
@@ -2579,7 +2597,7 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
   const int64_t cap = item_cap(vtiles, num_pairs);
   if (num_pairs > 0) {
     prof_mark(PROF_RASTER_FWD, s);
-    hipLaunchKernelGGL(v->no_depth_grad ? k_raster_fwd_mfma<2> : k_raster_fwd_mfma<1>,
+    hipLaunchKernelGGL(!v->no_depth_grad ? k_raster_fwd_mfma<1> : (out_depth ? k_raster_fwd_mfma<2> : k_raster_fwd_mfma<3>),
                        dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
                        (const int*)b.num_items, (const int2*)b.ranges, (const int2*)b.pairs, (const float4*)g.rec,
                        sc.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);

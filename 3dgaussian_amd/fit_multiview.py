@@ -276,10 +276,14 @@ class ViewShardedFitter:
         precision mode with the depth-gradient cutoff; otherwise depth_grad=False (gr_view.no_depth_grad)."""
         return self.depths is not None and self.w_depth > 0.0
 
-    def _prepare(self, i: int, means, scales, colors, opacities):
+    def _prepare(self, i: int, means, scales, colors, opacities, fit_view: bool = False):
+        """fit_view: a view of the fused path (_views_direct): one zone at tr.FIT_CUTOFF."""
         cam = self.cams[i]
+        cut = tr.FIT_CUTOFF if fit_view else None
         return tr.prepare_view(means, scales, colors, opacities, cam.view, cam.proj, self.width, self.height,
-                               self._background(means.device), depth_grad=self._depth_grad())
+                               self._background(means.device), cutoff=cut,
+                               core_cutoff=tr.FIT_CUTOFF if fit_view else tr.DEFAULT_CORE_CUTOFF,
+                               depth_grad=self._depth_grad())
 
     def view_loss(self, i: int, means, scales, colors, opacities, prepared=None) -> torch.Tensor:
         device = means.device
@@ -414,7 +418,7 @@ class ViewShardedFitter:
         def prepare(j):
             if j < len(views) and j not in ahead:
                 with torch.cuda.stream(streams[j % ns]):
-                    ahead[j] = self._prepare(views[j], m, s, c, o)
+                    ahead[j] = self._prepare(views[j], m, s, c, o, fit_view=True)
 
         for j in range(PREFETCH):
             prepare(j)
@@ -423,8 +427,11 @@ class ViewShardedFitter:
             k = j % ns
             with torch.cuda.stream(streams[k]):
                 cam = self.cams[i]
-                gv = tr.make_view(cam.view, cam.proj, self.width, self.height, bg, depth_grad=False)
-                _, _, _, rs = tr.forward_native(m, s, c, o, gv, ahead.pop(j))
+                # one zone at the core cutoff and no depth channel: the loss reads neither depth nor the
+                # tail-only part of W's footprint (torch_renderer.FIT_CUTOFF)
+                gv = tr.make_view(cam.view, cam.proj, self.width, self.height, bg, cutoff=tr.FIT_CUTOFF,
+                                  core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
+                _, _, _, rs = tr.forward_native(m, s, c, o, gv, ahead.pop(j), want_depth=False)
                 tr.backward_l1_native(m, s, c, o, rs, self.targets[i], self.masks[i] if w_sil > 0.0 else None, w_sil,
                                       g_scale, losses_v[j:j + 1], acc[k], accumulate=j >= ns)
         for st in streams[1:]:

@@ -39,6 +39,10 @@ except ImportError:  # pragma: no cover
 DEFAULT_CUTOFF = 7.0  # tail zone (W and D) when no depth gradient will follow (depth_grad=False)
 DEPTH_GRAD_CUTOFF = 8.0  # tail zone when the depth output may be differentiated (the default mode)
 DEFAULT_CORE_CUTOFF = 5.5
+# Views of the fused fit path (no depth output, no depth gradient: fit_multiview._views_direct) are
+# binned with one zone at the core cutoff: the tail zone carries only W and D, and W's tail beyond
+# 5.5 sigma (<= o e^-15.1 per Gaussian) is below the colours' own cutoff error
+FIT_CUTOFF = DEFAULT_CORE_CUTOFF
 
 
 def default_cutoff(depth_grad: bool = True) -> float:
@@ -241,8 +245,11 @@ def prepare_native(means, scales, colors, opacities, gv: _native.GrView) -> Prep
     return Prepared(gv, n, geom, plan_host, ev)
 
 
-def forward_native(means, scales, colors, opacities, gv: _native.GrView, prepared: Optional[Prepared] = None):
-    """Run gr_fwd_prepare(_async) + gr_fwd_render.  Returns (out, alpha, depth, RenderState)."""
+def forward_native(means, scales, colors, opacities, gv: _native.GrView, prepared: Optional[Prepared] = None,
+                   want_depth: bool = True):
+    """Run gr_fwd_prepare(_async) + gr_fwd_render.  Returns (out, alpha, depth, RenderState).
+    ``want_depth=False`` on a no_depth_grad view: no depth output (None) and no depth sums (gr_fwd_render
+    with out_depth = NULL: the forward skips its depth channel)."""
     L = _native.lib()
     dev = means.device
     n = int(means.shape[0])
@@ -259,7 +266,7 @@ def forward_native(means, scales, colors, opacities, gv: _native.GrView, prepare
                        device=dev)
     out = torch.empty((H, W, 3), dtype=torch.float32, device=dev)
     alpha = torch.empty((H, W), dtype=torch.float32, device=dev)
-    depth = torch.empty((H, W), dtype=torch.float32, device=dev)
+    depth = torch.empty((H, W), dtype=torch.float32, device=dev) if (want_depth or not gv.no_depth_grad) else None
     saved = torch.empty((int(L.gr_saved_floats(ctypes.byref(gv))),), dtype=torch.float32, device=dev)
     # scratch is released when this function returns; the caching allocator keeps it stream-ordered
     scratch = torch.empty((_ws_round(L.gr_fwd_scratch_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),),
@@ -434,4 +441,4 @@ def render_gaussians_torch(
 __all__ = ["Camera", "get_default_device", "perspective", "look_at", "render_gaussians_torch", "rasterize",
            "make_view", "prepare_view", "prepare_native", "Prepared", "forward_native", "backward_native",
            "backward_l1_native",
-           "DEFAULT_CUTOFF", "DEPTH_GRAD_CUTOFF", "DEFAULT_CORE_CUTOFF", "default_cutoff"]
+           "DEFAULT_CUTOFF", "DEPTH_GRAD_CUTOFF", "DEFAULT_CORE_CUTOFF", "FIT_CUTOFF", "default_cutoff"]

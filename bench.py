@@ -60,20 +60,21 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense peak
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak (spec)
 MFMA_32x32x16 = 2 * 32 * 32 * 16  # FLOP of one v_mfma_f32_32x32x16_bf16
 # Backward splat without an upstream depth gradient (the bench's loss: L1 + silhouette; the fit driver
-# renders its views with depth_grad=False), per core pair: two K = 16 contractions (over
+# renders its views without a depth gradient), per core pair: two K = 16 contractions (over
 # x and over y) of 4 upstream channels,
 #   f32-equivalent (algorithmic) FLOP = 2 sides x 4 channels x 16 x 16 x 2 = 4096,
 #   executed on the bf16 pipe as two-piece splits: 2 sides x 2 channel pairs x 3 piece products of
 #   v_mfma_f32_32x32x16_bf16 per 32 pairs = 12,288 FLOP per pair.
 F32_FLOP_PER_CORE_PAIR_BWD = 2 * 4 * 16 * 16 * 2
 BF16_FLOP_PER_CORE_PAIR_BWD = 2 * 2 * 3 * MFMA_32x32x16 / 32
-# Forward splat, f32-equivalent: 5 channels (core) / 2 channels (tail) x 16 x 16 x 2 per pair; executed
-# (depth_grad=False: two pieces, 3 products of v_mfma_f32_16x16x32_bf16 per channel per 32 pairs).
-F32_FLOP_PER_CORE_PAIR_FWD = 5 * 16 * 16 * 2
-F32_FLOP_PER_TAIL_PAIR_FWD = 2 * 16 * 16 * 2
+# Forward splat of the fused fit path (no depth channel, one zone), f32-equivalent: 4 channels (W, R, G, B)
+# x 16 x 16 x 2 per pair; executed as two pieces, 3 products of v_mfma_f32_16x16x32_bf16 per channel per
+# 32 pairs.  (The fit path has no tail pairs.)
+F32_FLOP_PER_CORE_PAIR_FWD = 4 * 16 * 16 * 2
+F32_FLOP_PER_TAIL_PAIR_FWD = 1 * 16 * 16 * 2
 MFMA_16x16x32 = 2 * 16 * 16 * 32
-BF16_FLOP_PER_CORE_PAIR_FWD = 5 * 3 * MFMA_16x16x32 / 32
-BF16_FLOP_PER_TAIL_PAIR_FWD = 2 * 3 * MFMA_16x16x32 / 32
+BF16_FLOP_PER_CORE_PAIR_FWD = 4 * 3 * MFMA_16x16x32 / 32
+BF16_FLOP_PER_TAIL_PAIR_FWD = 1 * 3 * MFMA_16x16x32 / 32
 FWD_KERNEL = "k_raster_fwd_mfma"
 BWD_KERNEL = "k_raster_bwd_bf16"
 # SURVEY.md §8(d) HBM model of the tile-binned algorithm (the north_star's "fraction of the HBM
@@ -252,7 +253,8 @@ def main():
     sync()
     prof = pkg._native.profile_end()
     fm.NUM_STREAMS = streams_saved
-    avg_pairs, avg_core = pairs_per_view(fitter, cams, R, tr.default_cutoff(False), tr.DEFAULT_CORE_CUTOFF)
+    # the fit step renders its views through the fused path: one zone at FIT_CUTOFF (fit_multiview._views_direct)
+    avg_pairs, avg_core = pairs_per_view(fitter, cams, R, tr.FIT_CUTOFF, tr.FIT_CUTOFF)
     k5_pairs, _ = pairs_per_view(fitter, cams, R, 5.0, 5.0)
 
     # the default precision mode: what a caller with a depth loss gets (f32-grade W / D, three-piece
@@ -290,7 +292,7 @@ def main():
         kernels = {
             "fwd": dict(kernel=FWD_KERNEL, t=fwd_avg_s, n=fwd_n, conc_us=fwd_conc_us, units=avg_pairs,
                         unit_bytes=12 + 36, px_bytes=40,
-                        units_desc="pairs (core + tail) per launch",
+                        units_desc="pairs per launch",
                         flop=BF16_FLOP_PER_CORE_PAIR_FWD * avg_core + BF16_FLOP_PER_TAIL_PAIR_FWD * avg_tail,
                         f32=F32_FLOP_PER_CORE_PAIR_FWD * avg_core + F32_FLOP_PER_TAIL_PAIR_FWD * avg_tail),
             "bwd": dict(kernel=BWD_KERNEL, t=bwd_avg_s, n=bwd_n, conc_us=bwd_conc_us, units=avg_core,
@@ -336,11 +338,12 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32 (splat contractions on bf16 MFMA with two-piece operand splits, ~2^-16 per product; "
-                     "depth_grad=False mode)",
+                     "no-depth-gradient mode)",
             "data": "synthetic (seeded Gaussians per SURVEY.md 8(d), random targets)",
             "config": {"workload": f"C4: {n} Gaussians, {V} orbit views {R}x{R}, fwd+bwd+grad all-reduce+Adam per step",
-                       "gaussians": n, "views": V, "width": R, "height": R, "cutoff_sigma": tr.default_cutoff(False),
-                       "core_cutoff_sigma": tr.DEFAULT_CORE_CUTOFF,
+                       "gaussians": n, "views": V, "width": R, "height": R, "cutoff_sigma": tr.FIT_CUTOFF, "core_cutoff_sigma": tr.FIT_CUTOFF,
+                       "render_path": "fused fit path (gr_fwd_render without depth channel + gr_bwd_l1, per-stream "
+                                      "gradient accumulators; fit_multiview._views_direct)",
                        "scale": round(0.1061 * (1200.0 / n) ** (1.0 / 3.0), 5), "seed": 0,
                        "parallelism": f"view-sharded dp{world}", "views_per_rank": views_per_rank,
                        "pairs_per_view": int(avg_pairs), "core_pairs_per_view": int(avg_core),

@@ -37,11 +37,25 @@ def _scene(n):
     return orc.Scene(sc.means[perm].copy(), sc.scales[perm].copy(), sc.colors[perm].copy(), sc.opacities[perm].copy())
 
 
+def _fit_mode(tr, t, view, proj, W, H, g_rgb, g_a, cuda):
+    """The fused fit path's render settings (fit_multiview._views_direct): one zone at FIT_CUTOFF, no
+    depth channel, forward_native(want_depth=False) + gr_bwd (generic upstream gradients)."""
+    gv = tr.make_view(view, proj, W, H, None, cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
+    m, s, c, o = (x.detach() for x in t)
+    out, alpha, depth, st = tr.forward_native(m, s, c, o, gv, want_depth=False)
+    assert depth is None
+    grads = tr.backward_native(m, s, c, o, st, torch.from_numpy(g_rgb).to(cuda), torch.from_numpy(g_a).to(cuda), None)
+    return out, alpha, grads
+
+
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("depth_grad", [False, True])
+@pytest.mark.parametrize("mode", ["no_depth_grad", "depth_grad", "fit"])
 @pytest.mark.parametrize("cfg", ["C4", "C5"])
-def test_full_view_vs_oracle(pkg, cuda, cfg, depth_grad):
+def test_full_view_vs_oracle(pkg, cuda, cfg, mode):
+    """mode: the bench's drop-in mode (depth_grad=False), the default mode (depth_grad=True, with an
+    upstream depth gradient), or the fused fit path's settings (one 5.5-sigma zone, no depth)."""
     tr = pkg.torch_renderer
+    depth_grad = mode == "depth_grad"
     n, W, H, V = CONFIGS[cfg]
     sc = _scene(n)
     view, proj = orc.orbit_cameras(V, W, H)[0]
@@ -51,19 +65,30 @@ def test_full_view_vs_oracle(pkg, cuda, cfg, depth_grad):
     g_d = rng.standard_normal((H, W)).astype(np.float32) if depth_grad else None
 
     t = [torch.from_numpy(a).to(cuda).requires_grad_(True) for a in sc.arrays()]
-    out, alpha, depth = tr.rasterize(*t, view, proj, W, H, depth_grad=depth_grad)
-    loss = (out * torch.from_numpy(g_rgb).to(cuda)).sum() + (alpha * torch.from_numpy(g_a).to(cuda)).sum()
-    if depth_grad:
-        loss = loss + (depth * torch.from_numpy(g_d).to(cuda)).sum()
-    loss.backward()
+    if mode == "fit":
+        out, alpha, grads = _fit_mode(tr, t, view, proj, W, H, g_rgb, g_a, cuda)
+        depth = None
+    else:
+        out, alpha, depth = tr.rasterize(*t, view, proj, W, H, depth_grad=depth_grad)
+        loss = (out * torch.from_numpy(g_rgb).to(cuda)).sum() + (alpha * torch.from_numpy(g_a).to(cuda)).sum()
+        if depth_grad:
+            loss = loss + (depth * torch.from_numpy(g_d).to(cuda)).sum()
+        loss.backward()
+        grads = [x.grad for x in t]
     torch.cuda.synchronize()
-    hip = {"out": out.detach().cpu().numpy(), "alpha": alpha.detach().cpu().numpy(), "depth": depth.detach().cpu().numpy()}
-    for k, x in zip(GRADS, t):
-        hip[k] = x.grad.cpu().numpy()
+    hip = {"out": out.detach().cpu().numpy(), "alpha": alpha.detach().cpu().numpy()}
+    if depth is not None:
+        hip["depth"] = depth.detach().cpu().numpy()
+    for k, x in zip(GRADS, grads):
+        hip[k] = x.cpu().numpy()
 
     t0 = time.perf_counter()
-    v = orc.make_view(view, proj, W, H, None, cutoff=tr.default_cutoff(depth_grad), core_cutoff=tr.DEFAULT_CORE_CUTOFF)
+    cut = tr.FIT_CUTOFF if mode == "fit" else tr.default_cutoff(depth_grad)
+    core = tr.FIT_CUTOFF if mode == "fit" else tr.DEFAULT_CORE_CUTOFF
+    v = orc.make_view(view, proj, W, H, None, cutoff=cut, core_cutoff=core)
     ora = dict(zip(("out", "alpha", "depth"), orc.forward(v, sc, binned=True)))
+    if depth is None:
+        del ora["depth"]
     ora.update(zip(GRADS, orc.backward(v, sc, g_rgb, g_a, g_d, binned=True)))
     errs = {k: orc.rel_l2(hip[k], ora[k]) for k in ora}
     t1 = time.perf_counter()
@@ -73,15 +98,17 @@ def test_full_view_vs_oracle(pkg, cuda, cfg, depth_grad):
     sel = np.sort(rng.choice(n, 1000, replace=False)).astype(np.int32)
     dense_g = orc.dense_grads_sel(v, sc, sel, g_rgb, g_a, g_d)
     dense = {"out": orc.rel_l2(hip["out"].reshape(-1, 3)[pix], d_out),
-             "alpha": orc.rel_l2(hip["alpha"].reshape(-1)[pix], d_a),
-             "depth": orc.rel_l2(hip["depth"].reshape(-1)[pix], d_d)}
+             "alpha": orc.rel_l2(hip["alpha"].reshape(-1)[pix], d_a)}
+    if depth is not None:
+        dense["depth"] = orc.rel_l2(hip["depth"].reshape(-1)[pix], d_d)
     for k, gd in zip(GRADS, dense_g):
         dense[k] = orc.rel_l2(hip[k][sel], gd)
-    print(f"{cfg} depth_grad={depth_grad}: vs binned oracle", {k: f"{e:.2e}" for k, e in errs.items()},
+    print(f"{cfg} {mode}: vs binned oracle", {k: f"{e:.2e}" for k, e in errs.items()},
           f"({t1 - t0:.1f} s); vs dense sample", {k: f"{e:.2e}" for k, e in dense.items()},
           f"({time.perf_counter() - t1:.1f} s)")
     for k in ("out", "alpha", "depth"):
-        assert errs[k] <= 2e-5, (k, errs[k])
+        if k in errs:
+            assert errs[k] <= 2e-5, (k, errs[k])
     for k in GRADS:
         assert errs[k] <= 1e-4, (k, errs[k])
     assert orc.psnr(hip["out"], ora["out"]) >= 60.0
