@@ -1145,6 +1145,7 @@ __device__ __forceinline__ void split2_frag2(const f32x2_t (&v)[4], s16x8 (&f)[2
   }
   split2_frag(u, f);
 }
+
 __device__ __forceinline__ void split3_frag2(const f32x2_t (&v)[4], s16x8 (&f)[3]) {
   float u[8];
 #pragma unroll
@@ -1315,8 +1316,11 @@ __device__ __forceinline__ void write_pixel(const ViewK& v, int p, const float* 
 #ifndef GR_FWD_WAVES
 #define GR_FWD_WAVES 6
 #endif
+#ifndef GR_FWD_WAVES3
+#define GR_FWD_WAVES3 6
+#endif
 template <int MODE>
-__global__ __launch_bounds__(256, GR_FWD_WAVES) void k_raster_fwd_mfma(ViewK v, int n, const int4* __restrict__ items,
+__global__ __launch_bounds__(256, MODE == 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void k_raster_fwd_mfma(ViewK v, int n, const int4* __restrict__ items,
                                                          const int* __restrict__ num_items, const int2* __restrict__ ranges,
                                                          const int2* __restrict__ pairs, const float4* __restrict__ rec,
                                                          float* __restrict__ fwd_part, float* __restrict__ out_rgb,

@@ -23,6 +23,7 @@ libgr_hip.so through a ``torch.autograd.Function`` — not by torch ops.  Differ
 from __future__ import annotations
 
 import ctypes
+import os
 import weakref
 from dataclasses import dataclass
 from typing import Optional
@@ -40,9 +41,11 @@ DEFAULT_CUTOFF = 7.0  # tail zone (W and D) when no depth gradient will follow (
 DEPTH_GRAD_CUTOFF = 8.0  # tail zone when the depth output may be differentiated (the default mode)
 DEFAULT_CORE_CUTOFF = 5.5
 # Views of the fused fit path (no depth output, no depth gradient: fit_multiview._views_direct) are
-# binned with one zone at the core cutoff: the tail zone carries only W and D, and W's tail beyond
-# 5.5 sigma (<= o e^-15.1 per Gaussian) is below the colours' own cutoff error
-FIT_CUTOFF = DEFAULT_CORE_CUTOFF
+# binned with one zone at 5 sigma (SURVEY.md 8(d)'s footprint; elliptical tile culling): no tail zone
+# (it only carries W and D), and the dropped weight (<= o e^-12.5 per Gaussian and tile) keeps the
+# outputs and gradients within 5e-5 relL2 of the dense reference at configs C4 and C5, also on the
+# bench's fit state after several Adam steps (tests/test_scale_gpu.py; 5.5 sigma: 2.5e-5, 10% slower)
+FIT_CUTOFF = float(os.environ.get("GR_FIT_CUTOFF", "5.0"))
 
 
 def default_cutoff(depth_grad: bool = True) -> float:

@@ -114,3 +114,44 @@ def test_full_view_vs_oracle(pkg, cuda, cfg, mode):
     assert orc.psnr(hip["out"], ora["out"]) >= 60.0
     for k, e in dense.items():
         assert e <= 1e-4, (k, e)
+
+
+@pytest.mark.timeout(400)
+def test_fit_path_on_fitted_state_vs_dense(pkg, cuda):
+    """The bench's own workload after several fit steps (Gaussians moved, scales and opacities changed by
+    Adam): the fused fit path's render settings (one FIT_CUTOFF zone, no depth) against the dense
+    float64 reference on a sample (1000 pixels, 1000 Gaussians), relL2 <= 1e-4."""
+    import importlib
+
+    tr = pkg.torch_renderer
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    bench = importlib.import_module("bench")
+    n, W, H, V = CONFIGS["C4"]
+    params = bench.synthetic_params(n, cuda)
+    cams = fm.orbit_cameras(V, W, H, cuda)
+    g = torch.Generator(device=cuda).manual_seed(1)
+    targets = [torch.rand((H, W, 3), generator=g, device=cuda) for _ in range(V)]
+    masks = [(t.mean(dim=2) > 0.5).float() for t in targets]
+    fit = fm.ViewShardedFitter(params, cams, targets, W, H, lr=0.02, masks=masks)
+    for _ in range(8):
+        fit.step()
+    with torch.no_grad():
+        acts = [a.detach().contiguous() for a in fm.activations(fit.params)]
+    sc = orc.Scene(*(a.cpu().numpy() for a in acts))
+    view, proj = orc.orbit_cameras(V, W, H)[3]
+    rng = np.random.default_rng(9)
+    g_rgb = rng.standard_normal((H, W, 3)).astype(np.float32)
+    g_a = rng.standard_normal((H, W)).astype(np.float32)
+    out, alpha, grads = _fit_mode(tr, acts, view, proj, W, H, g_rgb, g_a, cuda)
+    v = orc.make_view(view, proj, W, H, None, cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF)
+    pix = rng.choice(W * H, 1000, replace=False).astype(np.int32)
+    d_out, d_a, _ = orc.dense_pixels(v, sc, pix)
+    sel = np.sort(rng.choice(n, 1000, replace=False)).astype(np.int32)
+    dense_g = orc.dense_grads_sel(v, sc, sel, g_rgb, g_a, None)
+    errs = {"out": orc.rel_l2(out.cpu().numpy().reshape(-1, 3)[pix], d_out),
+            "alpha": orc.rel_l2(alpha.cpu().numpy().reshape(-1)[pix], d_a)}
+    for k, x, gd in zip(GRADS, grads, dense_g):
+        errs[k] = orc.rel_l2(x.cpu().numpy()[sel], gd)
+    print("fitted C4 state, fit path vs dense sample:", {k: f"{e:.2e}" for k, e in errs.items()})
+    for k, e in errs.items():
+        assert e <= 1e-4, (k, e)
