@@ -413,29 +413,32 @@ class ViewShardedFitter:
         bg = self._background(device)
         w_sil = self.w_sil if (self.masks is not None and self.w_sil > 0.0) else 0.0
         g_scale = 1.0 / len(self.targets)
-        ahead = {}
-
-        def prepare(j):
-            if j < len(views) and j not in ahead:
-                with torch.cuda.stream(streams[j % ns]):
-                    ahead[j] = self._prepare(views[j], m, s, c, o, fit_view=True)
-
-        for j in range(PREFETCH):
-            prepare(j)
+        # every view's preparation (projection, culling, pair counts) is enqueued at once on a stream of
+        # its own: the host's read of a view's pair count never waits behind other views' renders, and
+        # the preparations run beside the splat kernels (their workspaces: ~70 B per Gaussian per view)
+        prep = getattr(self, "_prep", None)
+        if prep is None or prep.device != device:
+            self._prep = prep = torch.cuda.Stream(device)
+        prep.wait_stream(main)
+        with torch.cuda.stream(prep):
+            ahead = [self._prepare(i, m, s, c, o, fit_view=True) for i in views]
         for j, i in enumerate(views):
-            prepare(j + PREFETCH)
             k = j % ns
+            streams[k].wait_event(ahead[j].event)
+            ahead[j].geom.record_stream(streams[k])
             with torch.cuda.stream(streams[k]):
                 cam = self.cams[i]
                 # one zone at the core cutoff and no depth channel: the loss reads neither depth nor the
                 # tail-only part of W's footprint (torch_renderer.FIT_CUTOFF)
                 gv = tr.make_view(cam.view, cam.proj, self.width, self.height, bg, cutoff=tr.FIT_CUTOFF,
                                   core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
-                _, _, _, rs = tr.forward_native(m, s, c, o, gv, ahead.pop(j), want_depth=False)
+                _, _, _, rs = tr.forward_native(m, s, c, o, gv, ahead[j], want_depth=False)
+                ahead[j] = None
                 tr.backward_l1_native(m, s, c, o, rs, self.targets[i], self.masks[i] if w_sil > 0.0 else None, w_sil,
                                       g_scale, losses_v[j:j + 1], acc[k], accumulate=j >= ns)
         for st in streams[1:]:
             main.wait_stream(st)
+        main.wait_stream(prep)
         used = min(ns, len(views))
         out = []
         for q in range(4):
