@@ -66,6 +66,16 @@ class GrPlan(ctypes.Structure):
     _fields_ = [("num_pairs", ctypes.c_int64), ("num_slots", ctypes.c_int64), ("num_core_pairs", ctypes.c_int64)]
 
 
+REDUCE_MAX_VIEWS = 16  # GR_REDUCE_MAX_VIEWS
+
+
+class GrReduceView(ctypes.Structure):
+    """gr_reduce_view (include/gr_hip.h): one view of a gr_reduce_views batch."""
+
+    _fields_ = [("view", GrView), ("plan", GrPlan), ("geom", ctypes.c_void_p), ("bins", ctypes.c_void_p),
+                ("ws", ctypes.c_void_p)]
+
+
 class NativeLibraryError(ImportError):
     pass
 
@@ -89,6 +99,10 @@ _SIG = {
     "gr_bwd_l1": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P,
                                  ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t,
                                  _P]),
+    "gr_bwd_l1_splat": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P,
+                                       ctypes.c_float, ctypes.c_float, _P, _P, ctypes.c_size_t, _P]),
+    "gr_reduce_views": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(GrReduceView), ctypes.c_int, _P, _P, _P, ctypes.c_int,
+                                       _P, _P, _P, _P, _P, ctypes.c_int, _P]),
     "gr_render_u8": (ctypes.c_int, [ctypes.POINTER(GrRenderParams), ctypes.c_int, _P, _P, _P, _P, _P]),
     "gr_geom_layout": (None, [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
     "gr_bins_layout": (None, [_VP, ctypes.c_int, _PP, ctypes.POINTER(ctypes.c_size_t)]),

@@ -1817,11 +1817,42 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
 #endif
 constexpr int RG = GR_RG;        // Gaussians per reduce block (4 lanes each; one wave runs the chain rule)
 
-template <int CD, typename F>
+// Where the chain rule puts one view's gradient of Gaussian i: GradOut writes (or adds, acc) it to the
+// gradient buffers; GradRegs adds it to registers (k_reduce_views: several views, one write).
+struct GradOut {
+  float *dm, *ds, *dc, *dop;  // Gaussian i's entries
+  bool acc;
+  __device__ void put(float* d, float x) const { *d = acc ? *d + x : x; }
+  __device__ void mean(int j, float x) const { put(dm + j, x); }
+  __device__ void scale(int j, float x) const { put(ds + j, x); }
+  __device__ void opac(float x) const { put(dop, x); }
+  __device__ void color(int q, float x) const { put(dc + q, x); }
+  __device__ void none(int cd) const {  // a Gaussian on no tile: zero gradient
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      mean(q, 0.f);
+      scale(q, 0.f);
+    }
+    for (int q = 0; q < cd; ++q) color(q, 0.f);
+    opac(0.f);
+  }
+  __device__ void scale_z() const { put(ds + 2, 0.f); }
+};
+template <int CD>
+struct GradRegs {
+  float m[3] = {0.f, 0.f, 0.f}, s[2] = {0.f, 0.f}, o = 0.f, c[CD] = {};
+  __device__ void mean(int j, float x) { m[j] += x; }
+  __device__ void scale(int j, float x) { s[j] += x; }
+  __device__ void opac(float x) { o += x; }
+  __device__ void color(int q, float x) { c[q] += x; }
+  __device__ void none(int) {}
+  __device__ void scale_z() {}
+};
+
+template <int CD, typename F, typename Out>
 __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, const float* __restrict__ means,
                            const float* __restrict__ scales, const float* __restrict__ colors,
-                           const float* __restrict__ opac, float* __restrict__ d_means, float* __restrict__ d_scales,
-                           float* __restrict__ d_colors, float* __restrict__ d_opac, bool acc);
+                           const float* __restrict__ opac, Out& out);
 
 // Block of RG Gaussians, 4 lanes each.  A Gaussian's pairs are its emission indices: core pairs
 // [c_i, c_i + core_i) and (only with an upstream depth gradient; otherwise the backward skipped them)
@@ -1918,32 +1949,160 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
   float Sf[NPART];
 #pragma unroll
   for (int q = 0; q < NPART; ++q) Sf[q] = sS[tid][q];
-  chain_rule<CD, float>(v, g0 + tid, Sf, sS[tid][NPART] != 0.0f ? 1u : 0u, means, scales, colors, opac, d_means, d_scales,
-                        d_colors, d_opac, acc != 0);
+  const int gi = g0 + tid;
+  GradOut out{d_means + 3 * (size_t)gi, d_scales + 3 * (size_t)gi, d_colors + (size_t)CD * gi, d_opac + gi, acc != 0};
+  chain_rule<CD, float>(v, gi, Sf, sS[tid][NPART] != 0.0f ? 1u : 0u, means, scales, colors, opac, out);
 }
 
-template <int CD, typename F>
+// Batched reduction (gr_reduce_views): the 8-float rows of up to GR_REDUCE_MAX_VIEWS views rendered
+// without a depth gradient, one pass over the Gaussians.  Per view a Gaussian's rows are gathered as in
+// k_reduce_bwd (4 lanes, fixed order, double sums); the chain rules then run one lane per Gaussian,
+// wave w taking views w, w + 4 (CRW = 4 waves; SH degree 3: wave 0 alone), their gradients summed in
+// registers and the wave sums combined in wave order: the parameters are read and the gradient written
+// (or added to, acc) once per batch instead of once per view.  Deterministic.
+struct RViewK {
+  ViewK v;
+  const Cnt2* offsets;  // the view's packed pair offsets (offsets[n] = totals)
+  const int* pos_of;    // sorted position of each pair, by emission index
+  const float4* rows;   // 8-float partial rows at sorted positions (bwd_item_bf16, no depth gradient)
+};
+struct RBatch {
+  int nv;
+  RViewK r[GR_REDUCE_MAX_VIEWS];
+};
+
+template <int CD>
+__global__ __launch_bounds__(4 * RG) void k_reduce_views(RBatch B, int n, const float* __restrict__ means,
+                                                      const float* __restrict__ scales, const float* __restrict__ colors,
+                                                      const float* __restrict__ opac, float* __restrict__ d_means,
+                                                      float* __restrict__ d_scales, float* __restrict__ d_colors,
+                                                      float* __restrict__ d_opac, int acc) {
+  constexpr int CRW = CD == 48 ? 1 : 4;  // waves running chain rules
+  constexpr int NG = 6 + CD;             // gradient floats per Gaussian (means 3, scales 2, opacity, colours)
+  constexpr int VG = 8;                  // views staged in LDS at a time
+  // per view and Gaussian: the 9 sums; S3 (the depth sum) is 0 without a depth gradient, so its slot
+  // carries the "on any tile" flag
+  __shared__ float sS[VG][RG][NPART];
+  __shared__ float sG[CRW > 1 ? CRW : 1][RG][NG + 1];
+  const int g0 = blockIdx.x * RG;
+  const int tid = threadIdx.x, q4 = tid & 3;
+  const int i = g0 + (tid >> 2);
+  const int w = tid >> 6, lane = tid & 63, gi = g0 + lane;
+  GradRegs<CD> gr;
+  for (int vg = 0; vg < B.nv; vg += VG) {
+  const int nvg = min(VG, B.nv - vg);
+  if (vg > 0) __syncthreads();  // the previous group's sums have been read
+  for (int vi = 0; vi < nvg; ++vi) {
+    const RViewK& rv = B.r[vg + vi];
+    double S[NPART];
+#pragma unroll
+    for (int q = 0; q < NPART; ++q) S[q] = 0.0;
+    unsigned cnt = 0;
+    if (i < n) {
+      const Cnt2 a = rv.offsets[i], b = rv.offsets[i + 1];
+      const int cc = (int)(b.c() - a.c());
+      cnt = (cc != 0 || b.t() != a.t()) ? 1u : 0u;
+      const int* pc = rv.pos_of + (long long)a.c();
+      for (int j0 = q4; j0 < cc; j0 += 16) {
+        int pos[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pos[u] = j0 + 4 * u < cc ? pc[j0 + 4 * u] : -1;
+        float4 ru[4], rw[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const size_t r = pos[u] >= 0 ? (size_t)pos[u] : 0;
+          ru[u] = rv.rows[2 * r];
+          rw[u] = rv.rows[2 * r + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (pos[u] < 0) break;
+          const float4 x = ru[u], w = rw[u];  // [o S0, o S2, S4, S6], [o S1, S8, S5, S7]
+          S[0] += (double)x.x;
+          S[2] += (double)x.y;
+          S[4] += (double)x.z;
+          S[6] += (double)x.w;
+          S[1] += (double)w.x;
+          S[8] += (double)w.y;
+          S[5] += (double)w.z;
+          S[7] += (double)w.w;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NPART; ++q) {
+      S[q] += __shfl_xor(S[q], 1);
+      S[q] += __shfl_xor(S[q], 2);
+    }
+    if (q4 == 0) {
+#pragma unroll
+      for (int q = 0; q < NPART; ++q) sS[vi][tid >> 2][q] = (float)S[q];
+      sS[vi][tid >> 2][3] = cnt ? 1.0f : 0.0f;
+    }
+  }
+  __syncthreads();
+  if (w < CRW && gi < n) {
+    for (int vi = w; vi < nvg; vi += CRW) {
+      float Sf[NPART];
+#pragma unroll
+      for (int q = 0; q < NPART; ++q) Sf[q] = sS[vi][lane][q];
+      const unsigned on = Sf[3] != 0.0f ? 1u : 0u;
+      Sf[3] = 0.0f;
+      chain_rule<CD, float>(B.r[vg + vi].v, gi, Sf, on, means, scales, colors, opac, gr);
+    }
+  }
+  }
+  if constexpr (CRW > 1) {
+    if (w < CRW) {
+      float* mine = sG[w][lane];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) mine[q] = gr.m[q];
+      mine[3] = gr.s[0];
+      mine[4] = gr.s[1];
+      mine[5] = gr.o;
+#pragma unroll
+      for (int q = 0; q < CD; ++q) mine[6 + q] = gr.c[q];
+    }
+    __syncthreads();
+    if (w != 0 || gi >= n) return;
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      float t = sG[0][lane][q];
+#pragma unroll
+      for (int u = 1; u < CRW; ++u) t += sG[u][lane][q];
+      sG[0][lane][q] = t;
+    }
+    const float* tot = sG[0][lane];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) gr.m[q] = tot[q];
+    gr.s[0] = tot[3];
+    gr.s[1] = tot[4];
+    gr.o = tot[5];
+#pragma unroll
+    for (int q = 0; q < CD; ++q) gr.c[q] = tot[6 + q];
+  }
+  if (w != 0 || gi >= n) return;
+  GradOut out{d_means + 3 * (size_t)gi, d_scales + 3 * (size_t)gi, d_colors + (size_t)CD * gi, d_opac + gi, acc != 0};
+#pragma unroll
+  for (int q = 0; q < 3; ++q) out.mean(q, gr.m[q]);
+  out.scale(0, gr.s[0]);
+  out.scale(1, gr.s[1]);
+  out.scale_z();
+  out.opac(gr.o);
+#pragma unroll
+  for (int q = 0; q < CD; ++q) out.color(q, gr.c[q]);
+}
+
+template <int CD, typename F, typename Out>
 __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, const float* __restrict__ means,
                            const float* __restrict__ scales, const float* __restrict__ colors,
-                           const float* __restrict__ opac, float* __restrict__ d_means, float* __restrict__ d_scales,
-                           float* __restrict__ d_colors, float* __restrict__ d_opac, bool acc) {
-  // acc: add this view's gradient to the buffers (a fit's per-stream gradient accumulators, summed
-  // over its views in view order: deterministic) instead of writing it
-  auto put = [acc](float* dst, float val) { *dst = acc ? *dst + val : val; };
+                           const float* __restrict__ opac, Out& out) {
   const float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
   const float s0 = scales[3 * i], s1 = scales[3 * i + 1];
   const float op = opac[i];
   const float* col = colors + (size_t)CD * i;
-  float* dc = d_colors + (size_t)CD * i;
   if (cnt == 0) {
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      put(&d_means[3 * i + q], 0.f);
-      put(&d_scales[3 * i + q], 0.f);
-    }
-#pragma unroll
-    for (int q = 0; q < CD; ++q) put(&dc[q], 0.f);
-    put(&d_opac[i], 0.f);
+    out.none(CD);
     return;
   }
   Proj p;
@@ -1959,9 +2118,9 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
   const F kx = F(0.5) * v.W * fx / p.za, ky = F(0.5) * v.H * fy / p.za;
   const F sgx = s0 > 0.f ? F(1) : (s0 < 0.f ? F(-1) : F(0));
   const F sgy = s1 > 0.f ? F(1) : (s1 < 0.f ? F(-1) : F(0));
-  put(&d_scales[3 * i + 0], (float)(dsx * kx * sgx));
-  put(&d_scales[3 * i + 1], (float)(dsy * ky * sgy));
-  put(&d_scales[3 * i + 2], 0.f);
+  out.scale(0, (float)(dsx * kx * sgx));
+  out.scale(1, (float)(dsy * ky * sgy));
+  out.scale_z();
   const F dza = S[3] - dsx * p.sxr / p.za - dsy * p.syr / p.za;
   F dpc[4] = {F(0), F(0), F(0), F(0)};
   if (fabsf(p.pc[2]) >= 1e-6f) dpc[2] += dza * (p.pc[2] > 0.f ? F(1) : (p.pc[2] < 0.f ? F(-1) : F(0)));
@@ -1983,7 +2142,7 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
 #pragma unroll
     for (int r = 0; r < 4; ++r) dm[j] += (F)v.V[r * 4 + j] * dpc[r];
   }
-  put(&d_opac[i], (float)((op >= 0.0f) ? S[4] : F(0)));
+  out.opac((float)((op >= 0.0f) ? S[4] : F(0)));
   float cpre[3];
   eval_color<CD>(v, mx, my, mz, col, cpre);
   F dcol[3];
@@ -1991,7 +2150,7 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
   for (int k = 0; k < 3; ++k) dcol[k] = (cpre[k] >= 0.0f && cpre[k] <= 1.0f) ? S[k] : F(0);
   if constexpr (CD == 3) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) put(&dc[k], (float)dcol[k]);
+    for (int k = 0; k < 3; ++k) out.color(k, (float)dcol[k]);
   } else {
     const F vv[3] = {(F)v.cam[0] - mx, (F)v.cam[1] - my, (F)v.cam[2] - mz};
     const F nn = std::sqrt(vv[0] * vv[0] + vv[1] * vv[1] + vv[2] * vv[2]);
@@ -2001,10 +2160,10 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
     if constexpr (CD == 12) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        put(&dc[k], (float)dcol[k]);
+        out.color(k, (float)dcol[k]);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          put(&dc[(1 + j) * 3 + k], (float)(dcol[k] * d[j]));
+          out.color((1 + j) * 3 + k, (float)(dcol[k] * d[j]));
           gd[j] += dcol[k] * (F)col[(1 + j) * 3 + k];
         }
       }
@@ -2012,10 +2171,11 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
       F Y[16], G[16][3];
       sh3_basis(d[0], d[1], d[2], Y);
       sh3_basis_grad(d[0], d[1], d[2], G);
+#pragma unroll
       for (int i = 0; i < 16; ++i)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          put(&dc[3 * i + k], (float)(dcol[k] * Y[i]));
+          out.color(3 * i + k, (float)(dcol[k] * Y[i]));
           const F t = dcol[k] * (F)col[3 * i + k];
 #pragma unroll
           for (int j = 0; j < 3; ++j) gd[j] += t * G[i][j];
@@ -2028,7 +2188,7 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
     }
   }
 #pragma unroll
-  for (int j = 0; j < 3; ++j) put(&d_means[3 * i + j], (float)dm[j]);
+  for (int j = 0; j < 3; ++j) out.mean(j, (float)dm[j]);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2621,7 +2781,7 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
                           const float* saved, const float* g_rgb, const float* g_alpha, const float* g_depth,
                           const float* t_rgb, const float* t_mask, float w_sil, float g_scale, float* loss_out,
                           float* d_means, float* d_scales, float* d_colors, float* d_opacities, int accumulate, void* ws,
-                          size_t ws_bytes, void* stream) {
+                          size_t ws_bytes, void* stream, bool reduce = true) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
   if (g_depth && v->no_depth_grad)
@@ -2631,7 +2791,8 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
   if (color_dim != 3 && color_dim != 12 && color_dim != 48)
     return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");
   if (n == 0) return GR_OK;
-  if ((!g_rgb && !t_rgb) || !saved || !geom || !bins || !d_means || !d_scales || !d_colors || !d_opacities)
+  if ((!g_rgb && !t_rgb) || !saved || !geom || !bins ||
+      (reduce && (!d_means || !d_scales || !d_colors || !d_opacities)))
     return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
   if (t_rgb && (!loss_out || !ws)) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_l1: null loss or workspace");
   const int64_t num_pairs = plan->num_pairs;
@@ -2667,6 +2828,7 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_BWD, s);
   }
+  if (!reduce) return GR_OK;  // gr_bwd_l1_splat: the partials stay in ws for gr_reduce_views
   prof_mark(PROF_REDUCE, s);
   {
     // the backward without a depth gradient writes 8-float rows (bwd_item_bf16)
@@ -2707,6 +2869,66 @@ gr_status gr_bwd_l1(const gr_view* v, int n, const gr_plan* plan, const float* m
   return bwd_impl(v, n, plan, means, scales, colors, color_dim, opacities, geom, bins, saved, nullptr, nullptr, nullptr,
                   target_rgb, target_mask, w_sil, g_scale, loss_out, d_means, d_scales, d_colors, d_opacities,
                   accumulate, ws, ws_bytes, stream);
+}
+
+gr_status gr_bwd_l1_splat(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
+                          const float* colors, int color_dim, const float* opacities, const void* geom, const void* bins,
+                          const float* saved, const float* target_rgb, const float* target_mask, float w_sil,
+                          float g_scale, float* loss_out, void* ws, size_t ws_bytes, void* stream) {
+  if (!target_rgb) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_l1_splat: target_rgb is null");
+  if (!v || !v->no_depth_grad)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_l1_splat: the view must be rendered with no_depth_grad = 1");
+  return bwd_impl(v, n, plan, means, scales, colors, color_dim, opacities, geom, bins, saved, nullptr, nullptr, nullptr,
+                  target_rgb, target_mask, w_sil, g_scale, loss_out, nullptr, nullptr, nullptr, nullptr, 0, ws, ws_bytes,
+                  stream, false);
+}
+
+gr_status gr_reduce_views(int num_views, const gr_reduce_view* views, int n, const float* means, const float* scales,
+                          const float* colors, int color_dim, const float* opacities, float* d_means, float* d_scales,
+                          float* d_colors, float* d_opacities, int accumulate, void* stream) {
+  if (num_views < 0 || num_views > GR_REDUCE_MAX_VIEWS)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_reduce_views: num_views must be in [0, GR_REDUCE_MAX_VIEWS]");
+  if (color_dim != 3 && color_dim != 12 && color_dim != 48)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");
+  if (n < 0) return set_error(GR_ERR_INVALID_ARGUMENT, "n must be >= 0");
+  if (n == 0) return GR_OK;
+  if (!means || !scales || !colors || !opacities || !d_means || !d_scales || !d_colors || !d_opacities ||
+      (num_views > 0 && !views))
+    return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+  RBatch B;
+  B.nv = num_views;
+  for (int k = 0; k < num_views; ++k) {
+    const gr_reduce_view& rv = views[k];
+    gr_status st = check_view(&rv.view);
+    if (st != GR_OK) return st;
+    if (!rv.view.no_depth_grad)
+      return set_error(GR_ERR_INVALID_ARGUMENT, "gr_reduce_views: views must be rendered with no_depth_grad = 1");
+    if (rv.plan.num_pairs < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
+    if (!rv.geom || (rv.plan.num_pairs > 0 && (!rv.bins || !rv.ws)))
+      return set_error(GR_ERR_INVALID_ARGUMENT, "gr_reduce_views: null workspace");
+    const ViewK vk = make_viewk(&rv.view);
+    const Geom g = geom_view((void*)rv.geom, n);
+    const Bins b = bins_view((void*)rv.bins, 2 * vk.tiles_x * vk.tiles_y, rv.plan.num_pairs);
+    B.r[k].v = vk;
+    B.r[k].offsets = (const Cnt2*)g.offsets;
+    B.r[k].pos_of = rv.plan.num_pairs > 0 ? (const int*)b.pos_of : nullptr;
+    B.r[k].rows = (const float4*)rv.ws;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  prof_mark(PROF_REDUCE, s);
+  const dim3 grid((n + RG - 1) / RG), block(4 * RG);
+  if (color_dim == 3)
+    hipLaunchKernelGGL(k_reduce_views<3>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
+                       d_colors, d_opacities, accumulate);
+  else if (color_dim == 12)
+    hipLaunchKernelGGL(k_reduce_views<12>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
+                       d_colors, d_opacities, accumulate);
+  else
+    hipLaunchKernelGGL(k_reduce_views<48>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
+                       d_colors, d_opacities, accumulate);
+  GR_HIP_TRY(hipGetLastError());
+  prof_mark(PROF_REDUCE, s);
+  return GR_OK;
 }
 
 gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, const float* scales, const float* colors,

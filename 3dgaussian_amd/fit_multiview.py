@@ -53,6 +53,10 @@ RESORT_EVERY = max(0, int(os.environ.get("GR_RESORT", "4")))
 # the fit step without a depth loss renders through the fused path (ViewShardedFitter._views_direct:
 # gr_bwd_l1 + per-stream gradient accumulators, no autograd per view); 0 = the autograd path
 DIRECT_BACKWARD = os.environ.get("GR_DIRECT", "1") != "0"
+# views of one stream whose gradient partials are reduced together (gr_reduce_views): the parameters are
+# read and the stream's gradient accumulator read and written once per batch instead of once per view
+# (at most REDUCE_BATCH views per batch, a stream's views split into equal batches)
+REDUCE_BATCH = max(1, min(16, int(os.environ.get("GR_REDUCE_BATCH", "16"))))
 
 
 # ------------------------------------------------------------------------------------------------
@@ -390,11 +394,12 @@ class ViewShardedFitter:
         return self._finish_step(loss)
 
     def _views_direct(self, means, scales, colors, opacities) -> torch.Tensor:
-        """This rank's views without autograd: per view, the HIP forward, then gr_bwd_l1 (the view's
-        L1 + silhouette loss and its backward fused, fit_multiview_stub.py:292-310) adding the gradient
-        w.r.t. the activated parameters into one accumulator set per HIP stream (in view order:
-        deterministic).  The accumulators are summed in stream order and leave in self._acc for one
-        autograd pass through the activations; returns the sum of the view losses (device, 0-d)."""
+        """This rank's views without autograd: per view, the HIP forward, then gr_bwd_l1_splat (the
+        view's L1 + silhouette loss gradients and its backward splat, fit_multiview_stub.py:292-310);
+        every REDUCE_BATCH views of a HIP stream, gr_reduce_views adds their gradient w.r.t. the
+        activated parameters into that stream's accumulator set (in view order: deterministic).  The
+        accumulators are summed in stream order and leave in self._acc for one autograd pass through the
+        activations; returns the sum of the view losses (device, 0-d)."""
         device = means.device
         m, s, c, o = (t.detach().contiguous() for t in (means, scales, colors, opacities))
         views = self.my_views
@@ -422,6 +427,22 @@ class ViewShardedFitter:
         prep.wait_stream(main)
         with torch.cuda.stream(prep):
             ahead = [self._prepare(i, m, s, c, o, fit_view=True) for i in views]
+        pending: list = [[] for _ in streams]  # per stream: (render state, partials) awaiting their reduction
+        started = [False] * ns
+        # stream k's views in nb near-equal batches of at most REDUCE_BATCH (sizes in the order they fill)
+        sizes = []
+        for k in range(ns):
+            p = len(range(k, len(views), ns))
+            nb = max(1, -(-p // REDUCE_BATCH))
+            sizes.append([p // nb + (1 if b < p % nb else 0) for b in range(nb)])
+
+        def reduce_pending(k):
+            if pending[k]:
+                with torch.cuda.stream(streams[k]):
+                    tr.reduce_views_native(m, s, c, o, pending[k], acc[k], accumulate=started[k])
+                started[k] = True
+                pending[k] = []
+
         for j, i in enumerate(views):
             k = j % ns
             streams[k].wait_event(ahead[j].event)
@@ -434,8 +455,15 @@ class ViewShardedFitter:
                                   core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
                 _, _, _, rs = tr.forward_native(m, s, c, o, gv, ahead[j], want_depth=False)
                 ahead[j] = None
-                tr.backward_l1_native(m, s, c, o, rs, self.targets[i], self.masks[i] if w_sil > 0.0 else None, w_sil,
-                                      g_scale, losses_v[j:j + 1], acc[k], accumulate=j >= ns)
+                ws = tr.backward_l1_splat_native(m, s, c, o, rs, self.targets[i], self.masks[i] if w_sil > 0.0 else None,
+                                                 w_sil, g_scale, losses_v[j:j + 1])
+            pending[k].append((rs, ws))
+            if len(pending[k]) >= sizes[k][0]:
+                reduce_pending(k)
+                if len(sizes[k]) > 1:
+                    sizes[k].pop(0)
+        for k in range(ns):
+            reduce_pending(k)
         for st in streams[1:]:
             main.wait_stream(st)
         main.wait_stream(prep)

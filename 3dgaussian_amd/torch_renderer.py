@@ -319,6 +319,44 @@ def backward_l1_native(means, scales, colors, opacities, st: RenderState, target
                               _native.ptr(ws), ws.numel(), _stream(dev)), "gr_bwd_l1")
 
 
+def backward_l1_splat_native(means, scales, colors, opacities, st: RenderState, target, mask, w_sil: float,
+                             g_scale: float, loss_out) -> torch.Tensor:
+    """gr_bwd_l1_splat on the current stream: the first half of ``backward_l1_native`` (loss gradients and
+    backward splat of one no_depth_grad view).  Returns the workspace holding the view's pair partials;
+    pass it with ``st`` to ``reduce_views_native`` (and keep both alive until then)."""
+    L = _native.lib()
+    dev = means.device
+    ws = torch.empty((_ws_round(L.gr_bwd_bytes(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan))),), dtype=torch.uint8,
+                     device=dev)
+    _native.check(L.gr_bwd_l1_splat(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan), _native.ptr(means),
+                                    _native.ptr(scales), _native.ptr(colors), _color_dim(colors), _native.ptr(opacities),
+                                    _native.ptr(st.geom), _native.ptr(st.bins), _native.ptr(st.saved), _native.ptr(target),
+                                    _native.ptr(mask), ctypes.c_float(w_sil), ctypes.c_float(g_scale),
+                                    _native.ptr(loss_out), _native.ptr(ws), ws.numel(), _stream(dev)), "gr_bwd_l1_splat")
+    return ws
+
+
+def reduce_views_native(means, scales, colors, opacities, batch, grads, accumulate: bool) -> None:
+    """gr_reduce_views on the current stream: ``batch`` = [(RenderState, workspace from
+    backward_l1_splat_native), ...] (at most _native.REDUCE_MAX_VIEWS); their summed gradient is written
+    (accumulate=False) or added (accumulate=True) to ``grads`` = (d_means, d_scales, d_colors, d_opacities)."""
+    L = _native.lib()
+    if len(batch) > _native.REDUCE_MAX_VIEWS:
+        raise ValueError(f"at most {_native.REDUCE_MAX_VIEWS} views per gr_reduce_views batch")
+    arr = (_native.GrReduceView * max(1, len(batch)))()
+    for k, (st, ws) in enumerate(batch):
+        arr[k].view = st.gv
+        arr[k].plan = st.plan
+        arr[k].geom = st.geom.data_ptr()
+        arr[k].bins = st.bins.data_ptr()
+        arr[k].ws = ws.data_ptr()
+    dm, ds, dc, do = grads
+    _native.check(L.gr_reduce_views(len(batch), arr, int(means.shape[0]), _native.ptr(means), _native.ptr(scales),
+                                    _native.ptr(colors), _color_dim(colors), _native.ptr(opacities), _native.ptr(dm),
+                                    _native.ptr(ds), _native.ptr(dc), _native.ptr(do), 1 if accumulate else 0,
+                                    _stream(means.device)), "gr_reduce_views")
+
+
 def _grad_background(st: RenderState, background: torch.Tensor, g_out: torch.Tensor) -> torch.Tensor:
     """d(out)/d(bg) = sum_p g_out * [0<=out_r<=1] / (1+W)  (torch_renderer.py:194-196)."""
     HW = st.gv.width * st.gv.height
@@ -443,5 +481,5 @@ def render_gaussians_torch(
 
 __all__ = ["Camera", "get_default_device", "perspective", "look_at", "render_gaussians_torch", "rasterize",
            "make_view", "prepare_view", "prepare_native", "Prepared", "forward_native", "backward_native",
-           "backward_l1_native",
+           "backward_l1_native", "backward_l1_splat_native", "reduce_views_native",
            "DEFAULT_CUTOFF", "DEPTH_GRAD_CUTOFF", "DEFAULT_CORE_CUTOFF", "FIT_CUTOFF", "default_cutoff"]

@@ -160,6 +160,36 @@ gr_status gr_bwd_l1(const gr_view* v, int n, const gr_plan* plan, const float* m
                     float* d_means, float* d_scales, float* d_colors, float* d_opacities,
                     int accumulate, void* ws, size_t ws_bytes, void* stream);
 
+/* gr_bwd_l1 in two halves, for a fit that reduces several views at once (fit_multiview.py's fused
+ * path; the views are rendered with no_depth_grad = 1).  gr_bwd_l1_splat runs the loss gradients and
+ * the backward splat of one view and leaves the view's per-pair gradient partials in ws (same
+ * workspace as gr_bwd); gr_reduce_views then sums the partials of up to GR_REDUCE_MAX_VIEWS such
+ * views per Gaussian, applies each view's chain rule and writes (accumulate = 0) or adds
+ * (accumulate != 0) the summed gradient once: the parameters are read and the gradient buffers
+ * written once per batch instead of once per view (gr_bwd_l1 = gr_bwd_l1_splat + a one-view
+ * gr_reduce_views).  Each view's geom, bins and ws must stay untouched until gr_reduce_views has
+ * run on the stream.  Deterministic for a given batch composition. */
+#define GR_REDUCE_MAX_VIEWS 16
+typedef struct gr_reduce_view {
+  gr_view view;     /* the view as rendered (same camera, size and cutoffs)     */
+  gr_plan plan;     /* its plan                                                */
+  const void* geom; /* its gr_fwd_prepare(_async) workspace                    */
+  const void* bins; /* its gr_fwd_render bins                                  */
+  const void* ws;   /* its gr_bwd_l1_splat workspace (the pair partials)       */
+} gr_reduce_view;
+
+gr_status gr_bwd_l1_splat(const gr_view* v, int n, const gr_plan* plan, const float* means,
+                          const float* scales, const float* colors, int color_dim,
+                          const float* opacities, const void* geom, const void* bins,
+                          const float* saved, const float* target_rgb, const float* target_mask,
+                          float w_sil, float g_scale, float* loss_out, void* ws, size_t ws_bytes,
+                          void* stream);
+
+gr_status gr_reduce_views(int num_views, const gr_reduce_view* views, int n, const float* means,
+                          const float* scales, const float* colors, int color_dim,
+                          const float* opacities, float* d_means, float* d_scales, float* d_colors,
+                          float* d_opacities, int accumulate, void* stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Legacy uint8 surface (host pointers), replaces gr::render_gaussians (renderer.h:33-39).    */
 /* Semantics of renderer_cpu.cpp: 3-sigma box, w < 1e-5 skip, uint8 round-half-up, A = 255.  */

@@ -106,3 +106,63 @@ def test_direct_path_matches_autograd_path(cuda, sh):
         # 7 / 5.5 sigma): each is within the parity bar of the dense reference, so of each other
         err = float((gd[k] - ga[k]).norm() / ga[k].norm())
         assert err <= 1e-4, (k, err)
+
+
+def test_batched_reduce_matches_per_view_reduce(cuda):
+    """gr_reduce_views over a batch of views gives the sum of the per-view reductions (gr_bwd_l1 of each
+    view alone) within float summation order; a one-view batch is the per-view reduction exactly; the
+    fit step is the same for every REDUCE_BATCH and deterministic for each."""
+    import torch
+
+    tr = importlib.import_module("3dgaussian_amd.torch_renderer")
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    bench = importlib.import_module("bench")
+    W, H = 144, 112
+    n = 25_000
+    cams = fm.orbit_cameras(5, W, H, cuda)
+    g = torch.Generator(device=cuda).manual_seed(6)
+    targets = [torch.rand((H, W, 3), generator=g, device=cuda) for _ in cams]
+    masks = [(t.mean(dim=2) > 0.5).float() for t in targets]
+    p = bench.synthetic_params(n, cuda)
+    m, s, c, o = (t.detach().contiguous() for t in fm.activations(p))
+    per_view, batch = [], []
+    loss = torch.zeros(len(cams), device=cuda)
+    for i, cam in enumerate(cams):
+        gv = tr.make_view(cam.view, cam.proj, W, H, None, cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
+        _, _, _, st = tr.forward_native(m, s, c, o, gv, want_depth=False)
+        grads = tuple(torch.empty_like(t) for t in (m, s, c, o))
+        tr.backward_l1_native(m, s, c, o, st, targets[i], masks[i], 0.2, 0.25, loss[i:i + 1], grads, accumulate=False)
+        per_view.append(grads)
+        ws = tr.backward_l1_splat_native(m, s, c, o, st, targets[i], masks[i], 0.2, 0.25, loss[i:i + 1])
+        batch.append((st, ws))
+    one = tuple(torch.empty_like(t) for t in (m, s, c, o))
+    tr.reduce_views_native(m, s, c, o, batch[:1], one, accumulate=False)
+    for a, b in zip(one, per_view[0]):
+        assert torch.equal(a, b)
+    tot = tuple(torch.empty_like(t) for t in (m, s, c, o))
+    tr.reduce_views_native(m, s, c, o, batch, tot, accumulate=False)
+    tr.reduce_views_native(m, s, c, o, batch[:2], tot, accumulate=True)  # accumulate adds
+    for q in range(4):
+        ref = sum(pv[q] for pv in per_view) + per_view[0][q] + per_view[1][q]
+        torch.testing.assert_close(tot[q], ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
+
+    def one_step(rb):
+        saved = fm.REDUCE_BATCH
+        fm.REDUCE_BATCH = rb
+        try:
+            f = fm.ViewShardedFitter(bench.synthetic_params(n, cuda), cams, targets, W, H, masks=masks)
+            lv = float(f.step())
+            return lv, {k: v.grad.detach().clone() for k, v in f.params.items()}
+        finally:
+            fm.REDUCE_BATCH = saved
+
+    l1, g1 = one_step(1)
+    for rb in (2, 8, 8):
+        lb, gb = one_step(rb)
+        assert lb == l1
+        for k in g1:
+            torch.testing.assert_close(gb[k], g1[k], rtol=1e-5, atol=1e-6 * float(g1[k].abs().max())), k
+    _, g8 = one_step(8)
+    _, g8b = one_step(8)
+    for k in g8:
+        assert torch.equal(g8[k], g8b[k]), k
