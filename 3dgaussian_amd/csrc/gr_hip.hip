@@ -741,7 +741,7 @@ __global__ __launch_bounds__(1024) void k_work_items_zones(int tiles, int tiles_
   __syncthreads();
   for (int base = 0; base < tiles; base += 1024) {
     const int t = base + (int)threadIdx.x;
-    const int nc = t < tiles ? Tc[t] : 0, nt = t < tiles ? Tt[t] : 0;
+    const int nc = (t < tiles && Tc) ? Tc[t] : 0, nt = (t < tiles && Tt) ? Tt[t] : 0;  // null: an empty zone
     int sc, totc, st, tott;
     Scan(tmp).ExclusiveSum(nc, sc, totc);
     __syncthreads();
@@ -1298,21 +1298,198 @@ __device__ __forceinline__ void write_pixel(const ViewK& v, int p, const float* 
                                             float* __restrict__ out_alpha, float* __restrict__ out_depth,
                                             float4* __restrict__ saved4, float* __restrict__ savedD) {
   const float aW = acc[0], den = 1.0f + aW;
-  out_rgb[3 * p + 0] = clamp01((v.bg[0] + acc[1]) / den);
-  out_rgb[3 * p + 1] = clamp01((v.bg[1] + acc[2]) / den);
-  out_rgb[3 * p + 2] = clamp01((v.bg[2] + acc[3]) / den);
+  if (out_rgb) {  // (gr_fwd_render_l1 may render no image: its loss gradients come from the sums)
+    out_rgb[3 * p + 0] = clamp01((v.bg[0] + acc[1]) / den);
+    out_rgb[3 * p + 1] = clamp01((v.bg[1] + acc[2]) / den);
+    out_rgb[3 * p + 2] = clamp01((v.bg[2] + acc[3]) / den);
+  }
   if (out_alpha) out_alpha[p] = clamp01(aW / den);
   if (out_depth) {
     const float d = acc[4] / (aW + 1e-6f);
     out_depth[p] = d < 0.0f ? 0.0f : d;
   }
-  saved4[p] = make_float4(aW, acc[1], acc[2], acc[3]);
-  savedD[p] = acc[4];
+  if (saved4) {
+    saved4[p] = make_float4(aW, acc[1], acc[2], acc[3]);
+    savedD[p] = acc[4];
+  }
+}
+
+// bf16 split-precision backward (k_raster_bwd_bf16): per tile, A fragments of v_mfma_f32_32x32x16_bf16
+// for 2 sides (T: contraction over x, R: over y) x 3 channel pairs x 3 bf16 pieces x 64 lanes, 16 B each.
+constexpr int UF_FRAGS = 2 * 3 * 3 * 64;  // uint4 per tile
+// channel pairs on the 32 MFMA rows (16 per channel): (dC_r, dC_g), (dC_b, -), (dW, dD); tail items
+// (depth-coupled terms only) need just the last pair
+// Without an upstream depth gradient dD is identically zero, so the four live channels fill two pairs:
+// (dC_r, dC_g), (dC_b, dW) and the third pair is never contracted (two thirds of the MFMA work).
+__device__ __forceinline__ int pair_channel(int pr, int c, bool depth) {
+  if (!depth) return pr == 0 ? c : (pr == 1 ? 2 + c : -1);
+  return pr == 0 ? c : (pr == 1 ? (c == 0 ? 2 : -1) : 3 + c);
+}
+// contracted coordinate of k-slot 8h + j of the 32x32x16 operands: the 8 pixels a lane half h owns,
+// {4h..4h+3, 8+4h..8+4h+3}, which are also the output rows that lane half holds (C map, row =
+// (reg&3) + 8 (reg>>2) + 4h): one set of exponentials per lane serves both contractions.
+__device__ __forceinline__ int kslot_pixel(int h, int j) { return (j < 4) ? 4 * h + j : 8 + 4 * h + (j - 4); }
+
+// Per-pixel upstream vector U = (dC_r, dC_g, dC_b, dW, dD) of the OIT finalize
+// (torch_renderer.py:192-203), laid out as pre-split MFMA fragments [tile][UF_FRAGS] for the backward
+// work items.  Fused fit loss (L1Args.t_rgb != nullptr, gr_bwd_l1 / gr_fwd_render_l1): the upstream
+// gradients are those of the fit loop's view loss mean|out - t| + w_sil mean|alpha - m|
+// (fit_multiview_stub.py:292-299) scaled by g_scale, evaluated from the pixel's sums exactly as
+// write_pixel turns them into outputs, with torch's abs' = sign (sign(0) = 0); per-tile sums of
+// |out - t| and |alpha - m| go to tile_loss.
+struct L1Args {
+  const float* t_rgb;   // (H,W,3) target image
+  const float* t_mask;  // (H,W) silhouette target or nullptr
+  float w_sil, g_scale;
+  float* tile_loss;     // [tiles][2]
+};
+
+__device__ __forceinline__ float sign0(float t) { return t > 0.0f ? 1.0f : (t < 0.0f ? -1.0f : 0.0f); }
+
+// U of pixel p from its sums s = (W, C_r, C_g, C_b) and D; l_rgb / l_sil get the pixel's L1 terms.
+__device__ __forceinline__ void pixel_upstream(const ViewK& v, int p, float4 s, float Dp, const float* __restrict__ g_rgb,
+                                               const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
+                                               const L1Args& l1, float (&u)[5], float& l_rgb, float& l_sil) {
+  const float den = 1.0f + s.x, dden = s.x + 1e-6f;
+  float gW = 0.f;
+  const float C[3] = {s.y, s.z, s.w};
+  const float HWf = (float)v.W * (float)v.H;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float r = (v.bg[k] + C[k]) / den;
+    float gk;
+    if (l1.t_rgb) {
+      const float t = clamp01(r) - l1.t_rgb[3 * p + k];
+      l_rgb += fabsf(t);
+      gk = sign0(t) * (l1.g_scale / (3.0f * HWf));
+    } else {
+      gk = g_rgb[3 * p + k];
+    }
+    const float go = (r >= 0.0f && r <= 1.0f) ? gk : 0.0f;
+    u[k] = go / den;
+    gW -= go * r / den;
+  }
+  const float al = s.x / den;
+  float ga = 0.0f;
+  bool has_a = g_alpha != nullptr;
+  if (l1.t_rgb && l1.t_mask) {
+    const float t = clamp01(al) - l1.t_mask[p];
+    l_sil = fabsf(t);
+    ga = sign0(t) * ((l1.w_sil * l1.g_scale) / HWf);
+    has_a = true;
+  } else if (g_alpha) {
+    ga = g_alpha[p];
+  }
+  if (has_a && al >= 0.0f && al <= 1.0f) gW += ga / (den * den);
+  if (g_depth) {
+    const float d = Dp / dden;
+    if (d >= 0.0f) {
+      const float gd = g_depth[p];
+      gW -= gd * Dp / (dden * dden);
+      u[4] = gd / dden;
+    }
+  }
+  u[3] = gW;
+}
+
+// The tile's L1 sums (block of 256 threads, one pixel each): waves, then the 4 wave sums in a fixed order.
+__device__ __forceinline__ void tile_loss_sums(int tile, int tid, float l_rgb, float l_sil, float* tile_loss) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    l_rgb += __shfl_xor(l_rgb, o);
+    l_sil += __shfl_xor(l_sil, o);
+  }
+  __shared__ float sL[2][4];
+  if ((tid & 63) == 0) {
+    sL[0][tid >> 6] = l_rgb;
+    sL[1][tid >> 6] = l_sil;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    tile_loss[2 * tile] = ((sL[0][0] + sL[0][1]) + sL[0][2]) + sL[0][3];
+    tile_loss[2 * tile + 1] = ((sL[1][0] + sL[1][1]) + sL[1][2]) + sL[1][3];
+  }
+}
+
+// The tile's U (sU[5][256] in LDS, published by a barrier) -> its bf16 fragments in UF: 384 (side,
+// pair, lane) fragment sets over the block's 256 threads; pair 2 (dW, dD) only with a depth gradient.
+__device__ __forceinline__ void tile_fragments(const float (*sU)[TP], uint4* __restrict__ fr, int tid, int pieces, bool depth) {
+  for (int cmb = tid; cmb < 2 * 3 * 64; cmb += 256) {
+    const int side = cmb / 192, pr = (cmb / 64) % 3, l = cmb & 63;
+    if (!depth && pr == 2) continue;  // never read
+    const int r = l & 31, h = l >> 5, ch = pair_channel(pr, r >> 4, depth), i = r & 15;
+    uint4* o = fr + ((side * 3 + pr) * 3) * 64 + l;
+    if (pieces == 2) {  // no_depth_grad views: two round-to-nearest pieces (split2_frag)
+      float val[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kk = kslot_pixel(h, j);
+        val[j] = ch < 0 ? 0.0f : (side == 0 ? sU[ch][i * T + kk] : sU[ch][kk * T + i]);
+      }
+      s16x8 f2[2];
+      split2_frag(val, f2);
+      __builtin_memcpy(&o[0], &f2[0], 16);
+      __builtin_memcpy(&o[64], &f2[1], 16);
+      continue;
+    }
+    float hi[8], mid[8], lo[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kk = kslot_pixel(h, j);
+      const float val = ch < 0 ? 0.0f : (side == 0 ? sU[ch][i * T + kk] : sU[ch][kk * T + i]);
+      split3(val, hi[j], mid[j], lo[j]);
+    }
+    o[0] = make_uint4(pack_bf16(hi[0], hi[1]), pack_bf16(hi[2], hi[3]), pack_bf16(hi[4], hi[5]), pack_bf16(hi[6], hi[7]));
+    o[64] = make_uint4(pack_bf16(mid[0], mid[1]), pack_bf16(mid[2], mid[3]), pack_bf16(mid[4], mid[5]),
+                       pack_bf16(mid[6], mid[7]));
+    o[128] = make_uint4(pack_bf16(lo[0], lo[1]), pack_bf16(lo[2], lo[3]), pack_bf16(lo[4], lo[5]), pack_bf16(lo[6], lo[7]));
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __restrict__ saved4,
+                                                     const float* __restrict__ savedD, const float* __restrict__ g_rgb,
+                                                     const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
+                                                     uint4* __restrict__ UF, int pieces, L1Args l1) {
+  const int tile = blockIdx.x, tid = threadIdx.x;
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
+  float u[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  float l_rgb = 0.f, l_sil = 0.f;
+  if (x < v.W && y < v.H) {
+    const int p = y * v.W + x;
+    pixel_upstream(v, p, saved4[p], savedD[p], g_rgb, g_alpha, g_depth, l1, u, l_rgb, l_sil);
+  }
+  if (l1.tile_loss) tile_loss_sums(tile, tid, l_rgb, l_sil, l1.tile_loss);
+  __shared__ float sU[5][TP];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) sU[k][tid] = u[k];
+  __syncthreads();
+  tile_fragments(sU, reinterpret_cast<uint4*>(UF) + (size_t)tile * UF_FRAGS, tid, pieces, g_depth != nullptr);
+}
+
+// gr_fwd_render_l1: a finished tile's pixel sums -> the fit loss's upstream fragments (the backward's
+// A operands, two pieces, no depth gradient) and the tile's L1 sums, in the forward's epilogue instead
+// of a k_pixel_grads pass over saved sums.  `lds` holds >= 4 x TP free floats; every thread of the block
+// calls this (two barriers).
+__device__ __forceinline__ void l1_tile_epilogue(const ViewK& v, int tile, int tid, const float (&acc)[5], bool inside,
+                                                 int p, const L1Args& l1, uint4* __restrict__ UF, float* lds) {
+  float u[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  float l_rgb = 0.f, l_sil = 0.f;
+  if (inside)
+    pixel_upstream(v, p, make_float4(acc[0], acc[1], acc[2], acc[3]), acc[4], nullptr, nullptr, nullptr, l1, u, l_rgb,
+                   l_sil);
+  tile_loss_sums(tile, tid, l_rgb, l_sil, l1.tile_loss);  // its barrier also ends every read of lds
+  float (*sU)[TP] = reinterpret_cast<float (*)[TP]>(lds);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) sU[k][tid] = u[k];
+  __syncthreads();
+  tile_fragments(sU, UF + (size_t)tile * UF_FRAGS, tid, 2, false);
 }
 
 // MODE 1: split bf16, W and D f32-grade; 2: split bf16, W and D within 2^-16 (views rendered with
-// no_depth_grad); 3: as 2 without the depth channel (no_depth_grad views rendered with no depth output:
-// the fused fit path; the saved depth sums are then 0 and unused).
+// no_depth_grad); 3: as 2 without the depth channel (no_depth_grad views rendered with no depth output;
+// the saved depth sums are then 0 and unused); 4: as 3, with the fit loss's upstream fragments and tile
+// L1 sums made in the epilogue (gr_fwd_render_l1, the fused fit path).
 #ifndef GR_FWD_WAVES
 #define GR_FWD_WAVES 6
 #endif
@@ -1320,12 +1497,13 @@ __device__ __forceinline__ void write_pixel(const ViewK& v, int p, const float* 
 #define GR_FWD_WAVES3 6
 #endif
 template <int MODE>
-__global__ __launch_bounds__(256, MODE == 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void k_raster_fwd_mfma(ViewK v, int n, const int4* __restrict__ items,
+__global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void k_raster_fwd_mfma(ViewK v, int n, const int4* __restrict__ items,
                                                          const int* __restrict__ num_items, const int2* __restrict__ ranges,
                                                          const int2* __restrict__ pairs, const float4* __restrict__ rec,
                                                          float* __restrict__ fwd_part, float* __restrict__ out_rgb,
                                                          float* __restrict__ out_alpha, float* __restrict__ out_depth,
-                                                         float4* __restrict__ saved4, float* __restrict__ savedD) {
+                                                         float4* __restrict__ saved4, float* __restrict__ savedD,
+                                                         L1Args l1, uint4* __restrict__ UF) {
   // LDS: two staged record buffers (2 x 9 KiB) during the loop, then the 4-wave reduction (20 KiB).
   __shared__ __attribute__((aligned(16))) float smem[4 * 5 * TP];
   const int nitems = *num_items;
@@ -1340,9 +1518,9 @@ __global__ __launch_bounds__(256, MODE == 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
   const float yc = (float)(ty * T + li) + 0.5f;  // B col = y
   f32x4 cW = {0.f, 0.f, 0.f, 0.f}, cR = cW, cG = cW, cB = cW, cD = cW;
   if (it.x & 1)
-    fwd_accumulate_bf16<true, MODE == 1, MODE != 3>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
+    fwd_accumulate_bf16<true, MODE == 1, MODE < 3>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
   else
-    fwd_accumulate_bf16<false, MODE == 1, MODE != 3>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
+    fwd_accumulate_bf16<false, MODE == 1, MODE < 3>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
   __syncthreads();
   {  // lane holds C[x = 4*gs + r][y = li]: pixel index y*16 + x, 4 consecutive x
     float* rw = smem + wave * 5 * TP + li * T + 4 * gs;
@@ -1366,17 +1544,20 @@ __global__ __launch_bounds__(256, MODE == 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
     return;
   }
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
-  if (x >= v.W || y >= v.H) return;
-  write_pixel(v, y * v.W + x, acc, out_rgb, out_alpha, out_depth, saved4, savedD);
+  const bool inside = x < v.W && y < v.H;
+  if (inside) write_pixel(v, y * v.W + x, acc, out_rgb, out_alpha, out_depth, saved4, savedD);
+  if constexpr (MODE == 4) l1_tile_epilogue(v, tile, tid, acc, inside, y * v.W + x, l1, UF, smem);
 }
 
 // Tiles with no Gaussians (background) or split over several work items: sum the items' partial
-// accumulators in item order (core chunks, then tail chunks: deterministic) and write the outputs.
+// accumulators in item order (core chunks, then tail chunks: deterministic) and write the outputs
+// (and with l1.t_rgb the fit loss's upstream fragments, as k_raster_fwd_mfma<4>).
 __global__ __launch_bounds__(256) void k_fwd_finalize(ViewK v, const int2* __restrict__ ranges,
                                                       const int* __restrict__ tile_item0, const float* __restrict__ fwd_part,
                                                       float* __restrict__ out_rgb, float* __restrict__ out_alpha,
                                                       float* __restrict__ out_depth, float4* __restrict__ saved4,
-                                                      float* __restrict__ savedD) {
+                                                      float* __restrict__ savedD, L1Args l1, uint4* __restrict__ UF) {
+  __shared__ float lds[4 * TP];
   const int tile = blockIdx.x, tid = threadIdx.x;
   const int nch = tile_chunks(ranges[2 * tile]) + tile_chunks(ranges[2 * tile + 1]);
   if (nch == 1) return;  // written by k_raster_fwd_mfma
@@ -1387,151 +1568,9 @@ __global__ __launch_bounds__(256) void k_fwd_finalize(ViewK v, const int2* __res
     for (int q = 0; q < 5; ++q) acc[q] += src[(size_t)c * 5 * TP + q * TP + tid];
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
-  if (x >= v.W || y >= v.H) return;
-  write_pixel(v, y * v.W + x, acc, out_rgb, out_alpha, out_depth, saved4, savedD);
-}
-
-// bf16 split-precision backward (k_raster_bwd_bf16): per tile, A fragments of v_mfma_f32_32x32x16_bf16
-// for 2 sides (T: contraction over x, R: over y) x 3 channel pairs x 3 bf16 pieces x 64 lanes, 16 B each.
-constexpr int UF_FRAGS = 2 * 3 * 3 * 64;  // uint4 per tile
-// channel pairs on the 32 MFMA rows (16 per channel): (dC_r, dC_g), (dC_b, -), (dW, dD); tail items
-// (depth-coupled terms only) need just the last pair
-// Without an upstream depth gradient dD is identically zero, so the four live channels fill two pairs:
-// (dC_r, dC_g), (dC_b, dW) and the third pair is never contracted (two thirds of the MFMA work).
-__device__ __forceinline__ int pair_channel(int pr, int c, bool depth) {
-  if (!depth) return pr == 0 ? c : (pr == 1 ? 2 + c : -1);
-  return pr == 0 ? c : (pr == 1 ? (c == 0 ? 2 : -1) : 3 + c);
-}
-// contracted coordinate of k-slot 8h + j of the 32x32x16 operands: the 8 pixels a lane half h owns,
-// {4h..4h+3, 8+4h..8+4h+3}, which are also the output rows that lane half holds (C map, row =
-// (reg&3) + 8 (reg>>2) + 4h): one set of exponentials per lane serves both contractions.
-__device__ __forceinline__ int kslot_pixel(int h, int j) { return (j < 4) ? 4 * h + j : 8 + 4 * h + (j - 4); }
-
-
-// Per-pixel upstream vector U = (dC_r, dC_g, dC_b, dW, dD) of the OIT finalize
-// (torch_renderer.py:192-203), laid out [tile][channel][256] for the backward work items.
-// Fused fit loss (L1 != nullptr, gr_bwd_l1): the upstream gradients are those of the fit loop's
-// view loss mean|out - t| + w_sil mean|alpha - m| (fit_multiview_stub.py:292-299) scaled by g_scale,
-// evaluated here from the outputs recomputed bit-exactly from the saved sums (as write_pixel made them),
-// with torch's abs' = sign (sign(0) = 0); per-tile sums of |out - t| and |alpha - m| go to tile_loss.
-struct L1Args {
-  const float* t_rgb;   // (H,W,3) target image
-  const float* t_mask;  // (H,W) silhouette target or nullptr
-  float w_sil, g_scale;
-  float* tile_loss;     // [tiles][2]
-};
-
-__device__ __forceinline__ float sign0(float t) { return t > 0.0f ? 1.0f : (t < 0.0f ? -1.0f : 0.0f); }
-
-__global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __restrict__ saved4,
-                                                     const float* __restrict__ savedD, const float* __restrict__ g_rgb,
-                                                     const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
-                                                     uint4* __restrict__ UF, int pieces, L1Args l1) {
-  const int tile = blockIdx.x, tid = threadIdx.x;
-  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
-  const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
-  float u[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  float l_rgb = 0.f, l_sil = 0.f;
-  if (x < v.W && y < v.H) {
-    const int p = y * v.W + x;
-    const float4 s = saved4[p];
-    const float Dp = savedD[p];
-    const float den = 1.0f + s.x, dden = s.x + 1e-6f;
-    float gW = 0.f;
-    const float C[3] = {s.y, s.z, s.w};
-    const float HWf = (float)v.W * (float)v.H;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const float r = (v.bg[k] + C[k]) / den;
-      float gk;
-      if (l1.t_rgb) {
-        const float t = clamp01(r) - l1.t_rgb[3 * p + k];
-        l_rgb += fabsf(t);
-        gk = sign0(t) * (l1.g_scale / (3.0f * HWf));
-      } else {
-        gk = g_rgb[3 * p + k];
-      }
-      const float go = (r >= 0.0f && r <= 1.0f) ? gk : 0.0f;
-      u[k] = go / den;
-      gW -= go * r / den;
-    }
-    const float al = s.x / den;
-    float ga = 0.0f;
-    bool has_a = g_alpha != nullptr;
-    if (l1.t_rgb && l1.t_mask) {
-      const float t = clamp01(al) - l1.t_mask[p];
-      l_sil = fabsf(t);
-      ga = sign0(t) * ((l1.w_sil * l1.g_scale) / HWf);
-      has_a = true;
-    } else if (g_alpha) {
-      ga = g_alpha[p];
-    }
-    if (has_a && al >= 0.0f && al <= 1.0f) gW += ga / (den * den);
-    if (g_depth) {
-      const float d = Dp / dden;
-      if (d >= 0.0f) {
-        const float gd = g_depth[p];
-        gW -= gd * Dp / (dden * dden);
-        u[4] = gd / dden;
-      }
-    }
-    u[3] = gW;
-  }
-  if (l1.tile_loss) {  // per-tile loss sums: waves, then the 4 wave sums in a fixed order
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      l_rgb += __shfl_xor(l_rgb, o);
-      l_sil += __shfl_xor(l_sil, o);
-    }
-    __shared__ float sL[2][4];
-    if ((tid & 63) == 0) {
-      sL[0][tid >> 6] = l_rgb;
-      sL[1][tid >> 6] = l_sil;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      l1.tile_loss[2 * tile] = ((sL[0][0] + sL[0][1]) + sL[0][2]) + sL[0][3];
-      l1.tile_loss[2 * tile + 1] = ((sL[1][0] + sL[1][1]) + sL[1][2]) + sL[1][3];
-    }
-  }
-  {  // bf16 fragments: stage u in LDS, then 384 (side, pair, lane) fragment triples
-    __shared__ float sU[5][TP];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) sU[k][tid] = u[k];
-    __syncthreads();
-    uint4* fr = reinterpret_cast<uint4*>(UF) + (size_t)tile * UF_FRAGS;
-    const bool depth = g_depth != nullptr;
-    for (int cmb = tid; cmb < 2 * 3 * 64; cmb += 256) {
-      const int side = cmb / 192, pr = (cmb / 64) % 3, l = cmb & 63;
-      if (!depth && pr == 2) continue;  // never read
-      const int r = l & 31, h = l >> 5, ch = pair_channel(pr, r >> 4, depth), i = r & 15;
-      uint4* o = fr + ((side * 3 + pr) * 3) * 64 + l;
-      if (pieces == 2) {  // no_depth_grad views: two round-to-nearest pieces (split2_frag)
-        float val[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int kk = kslot_pixel(h, j);
-          val[j] = ch < 0 ? 0.0f : (side == 0 ? sU[ch][i * T + kk] : sU[ch][kk * T + i]);
-        }
-        s16x8 f2[2];
-        split2_frag(val, f2);
-        __builtin_memcpy(&o[0], &f2[0], 16);
-        __builtin_memcpy(&o[64], &f2[1], 16);
-        continue;
-      }
-      float hi[8], mid[8], lo[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int kk = kslot_pixel(h, j);
-        const float val = ch < 0 ? 0.0f : (side == 0 ? sU[ch][i * T + kk] : sU[ch][kk * T + i]);
-        split3(val, hi[j], mid[j], lo[j]);
-      }
-      o[0] = make_uint4(pack_bf16(hi[0], hi[1]), pack_bf16(hi[2], hi[3]), pack_bf16(hi[4], hi[5]), pack_bf16(hi[6], hi[7]));
-      o[64] = make_uint4(pack_bf16(mid[0], mid[1]), pack_bf16(mid[2], mid[3]), pack_bf16(mid[4], mid[5]),
-                         pack_bf16(mid[6], mid[7]));
-      o[128] = make_uint4(pack_bf16(lo[0], lo[1]), pack_bf16(lo[2], lo[3]), pack_bf16(lo[4], lo[5]), pack_bf16(lo[6], lo[7]));
-    }
-  }
+  const bool inside = x < v.W && y < v.H;
+  if (inside) write_pixel(v, y * v.W + x, acc, out_rgb, out_alpha, out_depth, saved4, savedD);
+  if (l1.t_rgb) l1_tile_epilogue(v, tile, tid, acc, inside, y * v.W + x, l1, UF, lds);
 }
 
 // Sum over the 4 lane rows (lanes l, l+16, l+32, l+48) of a pair of values with one
@@ -1795,9 +1834,13 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
   const int tile = it.x >> 1, k0 = it.y, k1 = it.z;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  {  // the tile's A fragments -> LDS (DMA), then this lane's into registers
+  {  // the tile's A fragments this item contracts -> LDS (DMA): chunk (side * 3 + pair) * 3 + piece
     const uint4* src = UF + (size_t)tile * UF_FRAGS;
-    for (int c = wave; c < UF_FRAGS / 64; c += 4) glds16(src + 64 * c + lane, sUF + 64 * c);
+    const int p0 = tail ? 2 : 0, p1 = DEPTH ? 3 : 2;
+    for (int c = wave; c < UF_FRAGS / 64; c += 4) {
+      const int pr = (c / 3) % 3, piece = c % 3;
+      if (piece < PIECES && pr >= p0 && pr < p1) glds16(src + 64 * c + lane, sUF + 64 * c);
+    }
     stage_wait();
     __syncthreads();
   }
@@ -2662,14 +2705,36 @@ gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const floa
   return GR_OK;
 }
 
-gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins, size_t bins_bytes,
-                        void* scratch, size_t scratch_bytes, float* out_rgb, float* out_alpha, float* out_depth,
-                        float* saved, void* stream) {
+}  // extern "C" (fwd_impl and the backward workspace layout are internal)
+
+// The backward workspace (gr_bwd_bytes): pair partials, then the per-tile upstream fragments, then the
+// per-tile loss sums.
+struct BwdWs {
+  float* partials;
+  uint4* UF;
+  float* tile_loss;
+};
+static BwdWs bwd_ws(const gr_view* v, const gr_plan* plan, void* ws) {
+  const size_t tiles = (size_t)tiles_x_of(v->width) * tiles_y_of(v->height);
+  BwdWs w;
+  w.partials = (float*)ws;
+  w.UF = (uint4*)((char*)ws + align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)));
+  w.tile_loss = (float*)((char*)w.UF + align_up(tiles * UF_FRAGS * sizeof(uint4)));
+  return w;
+}
+
+// l1 != nullptr (gr_fwd_render_l1): no_depth_grad view without depth output; the fit loss's upstream
+// fragments and tile sums go to the backward workspace `ws`, the view loss to l1_loss_out.
+static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins, size_t bins_bytes,
+                          void* scratch, size_t scratch_bytes, float* out_rgb, float* out_alpha, float* out_depth,
+                          float* saved, void* stream, const L1Args* l1, float* l1_loss_out, void* ws, size_t ws_bytes) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
   if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
   if (plan->num_pairs < 0 || plan->num_slots < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
-  if (!out_rgb || !saved) return set_error(GR_ERR_INVALID_ARGUMENT, "out_rgb and saved are required");
+  if (!l1 && (!out_rgb || !saved)) return set_error(GR_ERR_INVALID_ARGUMENT, "out_rgb and saved are required");
+  if (l1 && (!ws || ws_bytes < gr_bwd_bytes(v, n, plan) || !l1_loss_out))
+    return set_error(GR_ERR_WORKSPACE, "gr_fwd_render_l1: backward workspace too small (or null loss)");
   if (n > 0 && (!geom || !bins)) return set_error(GR_ERR_INVALID_ARGUMENT, "null workspace");
   const int64_t num_pairs = plan->num_pairs;
   if (bins_bytes < gr_bins_bytes(v, n, plan)) return set_error(GR_ERR_WORKSPACE, "bins workspace too small");
@@ -2714,13 +2779,12 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
           GR_HIP_TRY(hipGetLastError());
           hipLaunchKernelGGL(k_tile_colscan, dim3((tiles + CS_T - 1) / CS_T), dim3(CS_T * CS_G), 0, s, tp[z].cols, tiles,
                              (const int*)M, Sz[z], Tz[z]);
-        } else {
-          GR_HIP_TRY(hipMemsetAsync(Tz[z], 0, (size_t)tiles * sizeof(int), s));
         }
         GR_HIP_TRY(hipGetLastError());
       }
-      hipLaunchKernelGGL(k_work_items_zones, dim3(1), dim3(1024), 0, s, tiles, vk.tiles_x, (int)Kc, (const int*)Tz[0],
-                         (const int*)Tz[1], b.ranges, b.items, b.num_items, b.tile_item0);
+      hipLaunchKernelGGL(k_work_items_zones, dim3(1), dim3(1024), 0, s, tiles, vk.tiles_x, (int)Kc,
+                         Kr[0] > 0 ? (const int*)Tz[0] : nullptr, Kr[1] > 0 ? (const int*)Tz[1] : nullptr, b.ranges,
+                         b.items, b.num_items, b.tile_item0);
       GR_HIP_TRY(hipGetLastError());
       for (int z = 0; z < 2; ++z) {
         if (Kr[z] == 0) continue;
@@ -2759,19 +2823,57 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
   Geom g = geom_view((void*)geom, n > 0 ? n : 1);
   const size_t HW = (size_t)v->width * v->height;
   const int64_t cap = item_cap(vtiles, num_pairs);
+  L1Args la{nullptr, nullptr, 0.f, 0.f, nullptr};
+  uint4* UF = nullptr;
+  if (l1) {
+    const BwdWs w = bwd_ws(v, plan, ws);
+    la = *l1;
+    la.tile_loss = w.tile_loss;
+    UF = w.UF;
+  }
+  float4* saved4 = saved ? (float4*)saved : nullptr;
+  float* savedD = saved ? saved + 4 * HW : nullptr;
   if (num_pairs > 0) {
     prof_mark(PROF_RASTER_FWD, s);
-    hipLaunchKernelGGL(!v->no_depth_grad ? k_raster_fwd_mfma<1> : (out_depth ? k_raster_fwd_mfma<2> : k_raster_fwd_mfma<3>),
+    hipLaunchKernelGGL(l1 ? k_raster_fwd_mfma<4>
+                          : (!v->no_depth_grad ? k_raster_fwd_mfma<1>
+                                               : (out_depth ? k_raster_fwd_mfma<2> : k_raster_fwd_mfma<3>)),
                        dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
                        (const int*)b.num_items, (const int2*)b.ranges, (const int2*)b.pairs, (const float4*)g.rec,
-                       sc.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
+                       sc.fwd_part, out_rgb, out_alpha, out_depth, saved4, savedD, la, UF);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_FWD, s);
   }
   hipLaunchKernelGGL(k_fwd_finalize, dim3(tiles), dim3(256), 0, s, vk, (const int2*)b.ranges, (const int*)b.tile_item0,
-                     (const float*)sc.fwd_part, out_rgb, out_alpha, out_depth, (float4*)saved, saved + 4 * HW);
+                     (const float*)sc.fwd_part, out_rgb, out_alpha, out_depth, saved4, savedD, la, UF);
   GR_HIP_TRY(hipGetLastError());
+  if (l1) {
+    hipLaunchKernelGGL(k_tile_loss_final, dim3(1), dim3(256), 0, s, (const float*)la.tile_loss, tiles, (int64_t)(3 * HW),
+                       (int64_t)(l1->t_mask ? HW : 0), l1->w_sil, l1_loss_out);
+    GR_HIP_TRY(hipGetLastError());
+  }
   return GR_OK;
+}
+
+extern "C" {
+
+gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins, size_t bins_bytes,
+                        void* scratch, size_t scratch_bytes, float* out_rgb, float* out_alpha, float* out_depth,
+                        float* saved, void* stream) {
+  return fwd_impl(v, n, plan, geom, bins, bins_bytes, scratch, scratch_bytes, out_rgb, out_alpha, out_depth, saved, stream,
+                  nullptr, nullptr, nullptr, 0);
+}
+
+gr_status gr_fwd_render_l1(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins, size_t bins_bytes,
+                           void* scratch, size_t scratch_bytes, const float* target_rgb, const float* target_mask,
+                           float w_sil, float g_scale, float* loss_out, float* out_rgb, float* out_alpha, void* ws,
+                           size_t ws_bytes, void* stream) {
+  if (!v || !v->no_depth_grad)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fwd_render_l1: the view must have no_depth_grad = 1");
+  if (!target_rgb) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fwd_render_l1: target_rgb is null");
+  const L1Args l1{target_rgb, target_mask, w_sil, g_scale, nullptr};
+  return fwd_impl(v, n, plan, geom, bins, bins_bytes, scratch, scratch_bytes, out_rgb, out_alpha, nullptr, nullptr, stream,
+                  &l1, loss_out, ws, ws_bytes);
 }
 
 }  // extern "C" (bwd_impl is internal)
@@ -2781,7 +2883,7 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
                           const float* saved, const float* g_rgb, const float* g_alpha, const float* g_depth,
                           const float* t_rgb, const float* t_mask, float w_sil, float g_scale, float* loss_out,
                           float* d_means, float* d_scales, float* d_colors, float* d_opacities, int accumulate, void* ws,
-                          size_t ws_bytes, void* stream, bool reduce = true) {
+                          size_t ws_bytes, void* stream) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
   if (g_depth && v->no_depth_grad)
@@ -2791,8 +2893,7 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
   if (color_dim != 3 && color_dim != 12 && color_dim != 48)
     return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");
   if (n == 0) return GR_OK;
-  if ((!g_rgb && !t_rgb) || !saved || !geom || !bins ||
-      (reduce && (!d_means || !d_scales || !d_colors || !d_opacities)))
+  if ((!g_rgb && !t_rgb) || !saved || !geom || !bins || !d_means || !d_scales || !d_colors || !d_opacities)
     return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
   if (t_rgb && (!loss_out || !ws)) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_l1: null loss or workspace");
   const int64_t num_pairs = plan->num_pairs;
@@ -2804,9 +2905,10 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
   Geom g = geom_view((void*)geom, n);
   Bins b = bins_view((void*)bins, 2 * tiles, num_pairs);
   const size_t HW = (size_t)v->width * v->height;
-  float* partials = (float*)ws;
-  uint4* UF = (uint4*)((char*)ws + align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)));
-  float* tile_loss = (float*)((char*)UF + align_up((size_t)tiles * UF_FRAGS * sizeof(uint4)));
+  const BwdWs w = bwd_ws(v, plan, ws);
+  float* partials = w.partials;
+  uint4* UF = w.UF;
+  float* tile_loss = w.tile_loss;
   const L1Args l1{t_rgb, t_mask, w_sil, g_scale, t_rgb ? tile_loss : nullptr};
   if (num_pairs > 0 || t_rgb) {
     hipLaunchKernelGGL(k_pixel_grads, dim3(tiles), dim3(256), 0, s, vk, (const float4*)saved, saved + 4 * HW, g_rgb,
@@ -2828,7 +2930,6 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_BWD, s);
   }
-  if (!reduce) return GR_OK;  // gr_bwd_l1_splat: the partials stay in ws for gr_reduce_views
   prof_mark(PROF_REDUCE, s);
   {
     // the backward without a depth gradient writes 8-float rows (bwd_item_bf16)
@@ -2871,16 +2972,29 @@ gr_status gr_bwd_l1(const gr_view* v, int n, const gr_plan* plan, const float* m
                   accumulate, ws, ws_bytes, stream);
 }
 
-gr_status gr_bwd_l1_splat(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
-                          const float* colors, int color_dim, const float* opacities, const void* geom, const void* bins,
-                          const float* saved, const float* target_rgb, const float* target_mask, float w_sil,
-                          float g_scale, float* loss_out, void* ws, size_t ws_bytes, void* stream) {
-  if (!target_rgb) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_l1_splat: target_rgb is null");
-  if (!v || !v->no_depth_grad)
-    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_l1_splat: the view must be rendered with no_depth_grad = 1");
-  return bwd_impl(v, n, plan, means, scales, colors, color_dim, opacities, geom, bins, saved, nullptr, nullptr, nullptr,
-                  target_rgb, target_mask, w_sil, g_scale, loss_out, nullptr, nullptr, nullptr, nullptr, 0, ws, ws_bytes,
-                  stream, false);
+gr_status gr_bwd_splat(const gr_view* v, int n, const gr_plan* plan, const void* geom, const void* bins, void* ws,
+                       size_t ws_bytes, void* stream) {
+  gr_status st = check_view(v);
+  if (st != GR_OK) return st;
+  if (!v->no_depth_grad) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_splat: the view must have no_depth_grad = 1");
+  if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
+  if (plan->num_pairs < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
+  if (n <= 0 || plan->num_pairs == 0) return GR_OK;
+  if (!geom || !bins) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+  if (!ws || ws_bytes < gr_bwd_bytes(v, n, plan)) return set_error(GR_ERR_WORKSPACE, "backward workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const ViewK vk = make_viewk(v);
+  const int tiles = vk.tiles_x * vk.tiles_y;
+  const Geom g = geom_view((void*)geom, n);
+  const Bins b = bins_view((void*)bins, 2 * tiles, plan->num_pairs);
+  const BwdWs w = bwd_ws(v, plan, ws);
+  const int64_t cap = item_cap(2 * tiles, plan->num_pairs);
+  prof_mark(PROF_RASTER_BWD, s);
+  hipLaunchKernelGGL((k_raster_bwd_bf16<false, 2>), dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
+                     (const int*)b.num_items, (const int2*)b.pairs, (const float4*)g.rec, (const uint4*)w.UF, w.partials);
+  GR_HIP_TRY(hipGetLastError());
+  prof_mark(PROF_RASTER_BWD, s);
+  return GR_OK;
 }
 
 gr_status gr_reduce_views(int num_views, const gr_reduce_view* views, int n, const float* means, const float* scales,

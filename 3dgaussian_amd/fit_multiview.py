@@ -394,9 +394,10 @@ class ViewShardedFitter:
         return self._finish_step(loss)
 
     def _views_direct(self, means, scales, colors, opacities) -> torch.Tensor:
-        """This rank's views without autograd: per view, the HIP forward, then gr_bwd_l1_splat (the
-        view's L1 + silhouette loss gradients and its backward splat, fit_multiview_stub.py:292-310);
-        every REDUCE_BATCH views of a HIP stream, gr_reduce_views adds their gradient w.r.t. the
+        """This rank's views without autograd: per view, gr_fwd_render_l1 (the HIP forward whose epilogue
+        evaluates the view's L1 + silhouette loss and its upstream gradients, fit_multiview_stub.py:292-299)
+        and gr_bwd_splat (the backward splat, :310); every REDUCE_BATCH views of a HIP stream,
+        gr_reduce_views adds their gradient w.r.t. the
         activated parameters into that stream's accumulator set (in view order: deterministic).  The
         accumulators are summed in stream order and leave in self._acc for one autograd pass through the
         activations; returns the sum of the view losses (device, 0-d)."""
@@ -453,10 +454,10 @@ class ViewShardedFitter:
                 # tail-only part of W's footprint (torch_renderer.FIT_CUTOFF)
                 gv = tr.make_view(cam.view, cam.proj, self.width, self.height, bg, cutoff=tr.FIT_CUTOFF,
                                   core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
-                _, _, _, rs = tr.forward_native(m, s, c, o, gv, ahead[j], want_depth=False)
+                rs, ws = tr.forward_l1_native(m, s, c, o, gv, ahead[j], self.targets[i],
+                                              self.masks[i] if w_sil > 0.0 else None, w_sil, g_scale, losses_v[j:j + 1])
                 ahead[j] = None
-                ws = tr.backward_l1_splat_native(m, s, c, o, rs, self.targets[i], self.masks[i] if w_sil > 0.0 else None,
-                                                 w_sil, g_scale, losses_v[j:j + 1])
+                tr.backward_splat_native(rs, ws)
             pending[k].append((rs, ws))
             if len(pending[k]) >= sizes[k][0]:
                 reduce_pending(k)

@@ -319,26 +319,45 @@ def backward_l1_native(means, scales, colors, opacities, st: RenderState, target
                               _native.ptr(ws), ws.numel(), _stream(dev)), "gr_bwd_l1")
 
 
-def backward_l1_splat_native(means, scales, colors, opacities, st: RenderState, target, mask, w_sil: float,
-                             g_scale: float, loss_out) -> torch.Tensor:
-    """gr_bwd_l1_splat on the current stream: the first half of ``backward_l1_native`` (loss gradients and
-    backward splat of one no_depth_grad view).  Returns the workspace holding the view's pair partials;
-    pass it with ``st`` to ``reduce_views_native`` (and keep both alive until then)."""
+def forward_l1_native(means, scales, colors, opacities, gv: _native.GrView, prepared: Prepared, target, mask,
+                      w_sil: float, g_scale: float, loss_out):
+    """gr_fwd_render_l1 on the current stream (the fused fit path; gv with no_depth_grad, no depth output):
+    the forward of one view whose epilogue evaluates the fit loss ``mean|out - target| + w_sil
+    mean|alpha - mask|`` (mask may be None) into ``loss_out`` and its upstream gradients (scaled by
+    ``g_scale``) into the backward workspace.  No image is written.  Returns (RenderState, workspace):
+    pass them to ``backward_splat_native`` and then ``reduce_views_native``."""
     L = _native.lib()
     dev = means.device
-    ws = torch.empty((_ws_round(L.gr_bwd_bytes(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan))),), dtype=torch.uint8,
-                     device=dev)
-    _native.check(L.gr_bwd_l1_splat(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan), _native.ptr(means),
-                                    _native.ptr(scales), _native.ptr(colors), _color_dim(colors), _native.ptr(opacities),
-                                    _native.ptr(st.geom), _native.ptr(st.bins), _native.ptr(st.saved), _native.ptr(target),
-                                    _native.ptr(mask), ctypes.c_float(w_sil), ctypes.c_float(g_scale),
-                                    _native.ptr(loss_out), _native.ptr(ws), ws.numel(), _stream(dev)), "gr_bwd_l1_splat")
-    return ws
+    n = int(means.shape[0])
+    if (prepared.n != n or prepared.gv.width != gv.width or prepared.gv.height != gv.height
+            or prepared.gv.cutoff != gv.cutoff or prepared.gv.core_cutoff != gv.core_cutoff):
+        raise ValueError("prepared view does not match this render (Gaussian count, image size or cutoffs)")
+    plan = prepared.plan()
+    bins = torch.empty((_ws_round(L.gr_bins_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8,
+                       device=dev)
+    ws = torch.empty((_ws_round(L.gr_bwd_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8, device=dev)
+    scratch = torch.empty((_ws_round(L.gr_fwd_scratch_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),),
+                          dtype=torch.uint8, device=dev)
+    _native.check(L.gr_fwd_render_l1(ctypes.byref(gv), n, ctypes.byref(plan), _native.ptr(prepared.geom),
+                                     _native.ptr(bins), bins.numel(), _native.ptr(scratch), scratch.numel(),
+                                     _native.ptr(target), _native.ptr(mask), ctypes.c_float(w_sil), ctypes.c_float(g_scale),
+                                     _native.ptr(loss_out), None, None, _native.ptr(ws), ws.numel(), _stream(dev)),
+                  "gr_fwd_render_l1")
+    del scratch
+    return RenderState(gv, n, plan, prepared.geom, bins, None), ws
+
+
+def backward_splat_native(st: RenderState, ws) -> None:
+    """gr_bwd_splat on the current stream: the backward splat of a view rendered by forward_l1_native;
+    its per-pair gradient partials stay in ``ws`` for reduce_views_native."""
+    L = _native.lib()
+    _native.check(L.gr_bwd_splat(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan), _native.ptr(st.geom),
+                                 _native.ptr(st.bins), _native.ptr(ws), ws.numel(), _stream(ws.device)), "gr_bwd_splat")
 
 
 def reduce_views_native(means, scales, colors, opacities, batch, grads, accumulate: bool) -> None:
-    """gr_reduce_views on the current stream: ``batch`` = [(RenderState, workspace from
-    backward_l1_splat_native), ...] (at most _native.REDUCE_MAX_VIEWS); their summed gradient is written
+    """gr_reduce_views on the current stream: ``batch`` = [(RenderState, workspace) of views through
+    forward_l1_native + backward_splat_native, ...] (at most _native.REDUCE_MAX_VIEWS); their summed gradient is written
     (accumulate=False) or added (accumulate=True) to ``grads`` = (d_means, d_scales, d_colors, d_opacities)."""
     L = _native.lib()
     if len(batch) > _native.REDUCE_MAX_VIEWS:
@@ -481,5 +500,5 @@ def render_gaussians_torch(
 
 __all__ = ["Camera", "get_default_device", "perspective", "look_at", "render_gaussians_torch", "rasterize",
            "make_view", "prepare_view", "prepare_native", "Prepared", "forward_native", "backward_native",
-           "backward_l1_native", "backward_l1_splat_native", "reduce_views_native",
+           "backward_l1_native", "forward_l1_native", "backward_splat_native", "reduce_views_native",
            "DEFAULT_CUTOFF", "DEPTH_GRAD_CUTOFF", "DEFAULT_CORE_CUTOFF", "FIT_CUTOFF", "default_cutoff"]

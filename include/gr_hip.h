@@ -160,30 +160,38 @@ gr_status gr_bwd_l1(const gr_view* v, int n, const gr_plan* plan, const float* m
                     float* d_means, float* d_scales, float* d_colors, float* d_opacities,
                     int accumulate, void* ws, size_t ws_bytes, void* stream);
 
-/* gr_bwd_l1 in two halves, for a fit that reduces several views at once (fit_multiview.py's fused
- * path; the views are rendered with no_depth_grad = 1).  gr_bwd_l1_splat runs the loss gradients and
- * the backward splat of one view and leaves the view's per-pair gradient partials in ws (same
- * workspace as gr_bwd); gr_reduce_views then sums the partials of up to GR_REDUCE_MAX_VIEWS such
- * views per Gaussian, applies each view's chain rule and writes (accumulate = 0) or adds
- * (accumulate != 0) the summed gradient once: the parameters are read and the gradient buffers
- * written once per batch instead of once per view (gr_bwd_l1 = gr_bwd_l1_splat + a one-view
- * gr_reduce_views).  Each view's geom, bins and ws must stay untouched until gr_reduce_views has
- * run on the stream.  Deterministic for a given batch composition. */
+/* The fused fit path in three calls (fit_multiview.py; views rendered with no_depth_grad = 1):
+ *   gr_fwd_render_l1  gr_fwd_render without depth output, whose epilogue also evaluates the fit
+ *                     loop's view loss (as gr_bwd_l1) from the pixel sums: the view loss goes to
+ *                     *loss_out, its upstream gradients (pre-split backward operands) to ws (the
+ *                     gr_bwd_bytes workspace).  out_rgb / out_alpha may be NULL (no image written);
+ *                     no saved sums are kept.
+ *   gr_bwd_splat      the backward splat of that view: per-pair gradient partials into ws.
+ *   gr_reduce_views   sums the partials of up to GR_REDUCE_MAX_VIEWS such views per Gaussian, applies
+ *                     each view's chain rule and writes (accumulate = 0) or adds (accumulate != 0)
+ *                     the summed gradient once: the parameters are read and the gradient buffers
+ *                     written once per batch instead of once per view.
+ * Together: gr_fwd_render + gr_bwd_l1 per view, up to float summation order.  Each view's geom,
+ * bins and ws must stay untouched until gr_reduce_views has run on the stream.  Deterministic for a
+ * given batch composition.  Replaces, for the fit loop, fit_multiview_stub.py:277-310 (render,
+ * L1 + silhouette loss, autograd backward and its gradient sums over the views). */
 #define GR_REDUCE_MAX_VIEWS 16
 typedef struct gr_reduce_view {
   gr_view view;     /* the view as rendered (same camera, size and cutoffs)     */
   gr_plan plan;     /* its plan                                                */
   const void* geom; /* its gr_fwd_prepare(_async) workspace                    */
-  const void* bins; /* its gr_fwd_render bins                                  */
-  const void* ws;   /* its gr_bwd_l1_splat workspace (the pair partials)       */
+  const void* bins; /* its gr_fwd_render_l1 bins                               */
+  const void* ws;   /* its gr_fwd_render_l1 / gr_bwd_splat workspace           */
 } gr_reduce_view;
 
-gr_status gr_bwd_l1_splat(const gr_view* v, int n, const gr_plan* plan, const float* means,
-                          const float* scales, const float* colors, int color_dim,
-                          const float* opacities, const void* geom, const void* bins,
-                          const float* saved, const float* target_rgb, const float* target_mask,
-                          float w_sil, float g_scale, float* loss_out, void* ws, size_t ws_bytes,
-                          void* stream);
+gr_status gr_fwd_render_l1(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins,
+                           size_t bins_bytes, void* scratch, size_t scratch_bytes,
+                           const float* target_rgb, const float* target_mask, float w_sil,
+                           float g_scale, float* loss_out, float* out_rgb, float* out_alpha,
+                           void* ws, size_t ws_bytes, void* stream);
+
+gr_status gr_bwd_splat(const gr_view* v, int n, const gr_plan* plan, const void* geom,
+                       const void* bins, void* ws, size_t ws_bytes, void* stream);
 
 gr_status gr_reduce_views(int num_views, const gr_reduce_view* views, int n, const float* means,
                           const float* scales, const float* colors, int color_dim,

@@ -109,9 +109,10 @@ def test_direct_path_matches_autograd_path(cuda, sh):
 
 
 def test_batched_reduce_matches_per_view_reduce(cuda):
-    """gr_reduce_views over a batch of views gives the sum of the per-view reductions (gr_bwd_l1 of each
-    view alone) within float summation order; a one-view batch is the per-view reduction exactly; the
-    fit step is the same for every REDUCE_BATCH and deterministic for each."""
+    """The fused fit path's three calls (gr_fwd_render_l1, gr_bwd_splat, gr_reduce_views) against
+    gr_fwd_render + gr_bwd_l1 per view: the same view losses bit for bit, a one-view batch the per-view
+    gradient exactly, a batch the sum of the per-view gradients within float summation order; the fit
+    step is the same for every REDUCE_BATCH and deterministic for each."""
     import torch
 
     tr = importlib.import_module("3dgaussian_amd.torch_renderer")
@@ -127,14 +128,18 @@ def test_batched_reduce_matches_per_view_reduce(cuda):
     m, s, c, o = (t.detach().contiguous() for t in fm.activations(p))
     per_view, batch = [], []
     loss = torch.zeros(len(cams), device=cuda)
+    loss2 = torch.zeros(len(cams), device=cuda)
     for i, cam in enumerate(cams):
         gv = tr.make_view(cam.view, cam.proj, W, H, None, cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
         _, _, _, st = tr.forward_native(m, s, c, o, gv, want_depth=False)
         grads = tuple(torch.empty_like(t) for t in (m, s, c, o))
         tr.backward_l1_native(m, s, c, o, st, targets[i], masks[i], 0.2, 0.25, loss[i:i + 1], grads, accumulate=False)
         per_view.append(grads)
-        ws = tr.backward_l1_splat_native(m, s, c, o, st, targets[i], masks[i], 0.2, 0.25, loss[i:i + 1])
-        batch.append((st, ws))
+        prep = tr.prepare_native(m, s, c, o, gv)
+        st2, ws = tr.forward_l1_native(m, s, c, o, gv, prep, targets[i], masks[i], 0.2, 0.25, loss2[i:i + 1])
+        tr.backward_splat_native(st2, ws)
+        batch.append((st2, ws))
+    assert torch.equal(loss, loss2)  # the forward-epilogue loss is the backward's (same per-tile sums)
     one = tuple(torch.empty_like(t) for t in (m, s, c, o))
     tr.reduce_views_native(m, s, c, o, batch[:1], one, accumulate=False)
     for a, b in zip(one, per_view[0]):
