@@ -2035,43 +2035,69 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_views(RBatch B, int n, const 
   for (int vg = 0; vg < B.nv; vg += VG) {
   const int nvg = min(VG, B.nv - vg);
   if (vg > 0) __syncthreads();  // the previous group's sums have been read
+  // Three-stage pipeline over the group's views: the offsets of view vi + 2, the positions of view vi + 1
+  // and the rows of view vi are in flight together (three independent loads instead of a chain of three
+  // per view).  A Gaussian's first 16 pairs go through the pipeline; more are read after (rare).
+  auto load_off = [&](int vi, Cnt2& a, Cnt2& b) {
+    if (vi < nvg && i < n) {
+      a = B.r[vg + vi].offsets[i];
+      b = B.r[vg + vi].offsets[i + 1];
+    } else {
+      a.v = b.v = 0ull;
+    }
+  };
+  auto load_pos = [&](int vi, Cnt2 a, Cnt2 b, int (&pos)[4]) {
+    const int cc = (int)(b.c() - a.c());
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pos[u] = q4 + 4 * u < cc ? B.r[vg + vi].pos_of[(size_t)a.c() + q4 + 4 * u] : -1;
+  };
+  Cnt2 a0, b0, a1, b1;
+  int p0[4], p1[4];
+  load_off(0, a0, b0);
+  load_off(1, a1, b1);
+  load_pos(0, a0, b0, p0);
   for (int vi = 0; vi < nvg; ++vi) {
     const RViewK& rv = B.r[vg + vi];
+    Cnt2 a2, b2;
+    load_off(vi + 2, a2, b2);
+    if (vi + 1 < nvg) load_pos(vi + 1, a1, b1, p1);
+    float4 ru[4], rw[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t r = p0[u] >= 0 ? (size_t)p0[u] : 0;
+      ru[u] = rv.rows[2 * r];
+      rw[u] = rv.rows[2 * r + 1];
+    }
     double S[NPART];
 #pragma unroll
     for (int q = 0; q < NPART; ++q) S[q] = 0.0;
-    unsigned cnt = 0;
-    if (i < n) {
-      const Cnt2 a = rv.offsets[i], b = rv.offsets[i + 1];
-      const int cc = (int)(b.c() - a.c());
-      cnt = (cc != 0 || b.t() != a.t()) ? 1u : 0u;
-      const int* pc = rv.pos_of + (long long)a.c();
-      for (int j0 = q4; j0 < cc; j0 += 16) {
-        int pos[4];
+    const int cc = (int)(b0.c() - a0.c());
+    const unsigned cnt = (cc != 0 || b0.t() != a0.t()) ? 1u : 0u;
+    auto add_row = [&](float4 x, float4 w) {  // [o S0, o S2, S4, S6], [o S1, S8, S5, S7]
+      S[0] += (double)x.x;
+      S[2] += (double)x.y;
+      S[4] += (double)x.z;
+      S[6] += (double)x.w;
+      S[1] += (double)w.x;
+      S[8] += (double)w.y;
+      S[5] += (double)w.z;
+      S[7] += (double)w.w;
+    };
 #pragma unroll
-        for (int u = 0; u < 4; ++u) pos[u] = j0 + 4 * u < cc ? pc[j0 + 4 * u] : -1;
-        float4 ru[4], rw[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const size_t r = pos[u] >= 0 ? (size_t)pos[u] : 0;
-          ru[u] = rv.rows[2 * r];
-          rw[u] = rv.rows[2 * r + 1];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (pos[u] < 0) break;
-          const float4 x = ru[u], w = rw[u];  // [o S0, o S2, S4, S6], [o S1, S8, S5, S7]
-          S[0] += (double)x.x;
-          S[2] += (double)x.y;
-          S[4] += (double)x.z;
-          S[6] += (double)x.w;
-          S[1] += (double)w.x;
-          S[8] += (double)w.y;
-          S[5] += (double)w.z;
-          S[7] += (double)w.w;
-        }
-      }
+    for (int u = 0; u < 4; ++u) {
+      if (p0[u] < 0) break;
+      add_row(ru[u], rw[u]);
     }
+    for (int j = q4 + 16; j < cc; j += 4) {  // pairs past the first 16, in the same lane order
+      const size_t r = (size_t)rv.pos_of[(size_t)a0.c() + j];
+      add_row(rv.rows[2 * r], rv.rows[2 * r + 1]);
+    }
+    a0 = a1;
+    b0 = b1;
+    a1 = a2;
+    b1 = b2;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) p0[u] = p1[u];
 #pragma unroll
     for (int q = 0; q < NPART; ++q) {
       S[q] += __shfl_xor(S[q], 1);

@@ -353,6 +353,9 @@ def main():
             # splats in "splats", with their MFMA rates beside
             "roofline": roof(dominant),
             "splats": {"fwd": roof("fwd"), "bwd": roof("bwd")},
+            # the batched per-Gaussian reduction (gr_reduce_views), HIP events, per view of the single-stream step
+            "reduce_us_per_view": round(1e3 * prof["reduce_bwd"][0] / max(len(fitter.my_views), 1), 1),
+            "binning_us_per_view": round(1e3 * prof["binning"][0] / max(len(fitter.my_views), 1), 1),
             "hbm_model": {"survey_5sigma": hbm_model(k5_pairs), "build_7sigma": hbm_model(avg_pairs),
                           "source": "SURVEY.md 8(d) tile-binned byte model, 8 TB/s: at its fixed 5-sigma footprint "
                                     "(the survey's 2,830 Mpx/s roof) and at this build's 7-sigma pair count"},
