@@ -57,6 +57,8 @@ DIRECT_BACKWARD = os.environ.get("GR_DIRECT", "1") != "0"
 # read and the stream's gradient accumulator read and written once per batch instead of once per view
 # (at most REDUCE_BATCH views per batch, a stream's views split into equal batches)
 REDUCE_BATCH = max(1, min(16, int(os.environ.get("GR_REDUCE_BATCH", "16"))))
+# fused path: views prepared ahead of the one being rendered (on the preparation stream)
+PREP_AHEAD = max(1, int(os.environ.get("GR_PREP_AHEAD", "6")))
 
 
 # ------------------------------------------------------------------------------------------------
@@ -179,8 +181,9 @@ def morton_order(means: torch.Tensor) -> torch.Tensor:
     pairs) and a tile's records are gathered from few cache lines."""
     with torch.no_grad():
         m = means.detach()
-        lo = m.amin(0)
-        ext = (m.amax(0) - lo).clamp_min(1e-20)
+        mt = m.t().contiguous()  # (3, N): row reductions (a dim-0 reduction of (N,3) is a slow strided kernel)
+        lo = mt.amin(1)
+        ext = (mt.amax(1) - lo).clamp_min(1e-20)
         q = ((m - lo) / ext * 1023.0).round().to(torch.int64).clamp_(0, 1023)
         key = _spread3(q[:, 0]) | (_spread3(q[:, 1]) << 1) | (_spread3(q[:, 2]) << 2)
         return torch.argsort(key, stable=True)
@@ -280,14 +283,22 @@ class ViewShardedFitter:
         precision mode with the depth-gradient cutoff; otherwise depth_grad=False (gr_view.no_depth_grad)."""
         return self.depths is not None and self.w_depth > 0.0
 
-    def _prepare(self, i: int, means, scales, colors, opacities, fit_view: bool = False):
+    def _prepare(self, i: int, means, scales, colors, opacities, fit_view: bool = False, plan_host=None):
         """fit_view: a view of the fused path (_views_direct): one zone at tr.FIT_CUTOFF."""
         cam = self.cams[i]
         cut = tr.FIT_CUTOFF if fit_view else None
         return tr.prepare_view(means, scales, colors, opacities, cam.view, cam.proj, self.width, self.height,
                                self._background(means.device), cutoff=cut,
                                core_cutoff=tr.FIT_CUTOFF if fit_view else tr.DEFAULT_CORE_CUTOFF,
-                               depth_grad=self._depth_grad())
+                               depth_grad=self._depth_grad(), plan_host=plan_host)
+
+    def _plan_pins(self, count: int) -> torch.Tensor:
+        """One pinned (count, 3) int64 buffer for the views' plans, kept across steps (a pinned allocation
+        per view and step costs host time on the render path)."""
+        pins = getattr(self, "_pins", None)
+        if pins is None or pins.shape[0] < count:
+            self._pins = pins = torch.zeros((max(count, 1), 3), dtype=torch.int64, pin_memory=True)
+        return pins
 
     def view_loss(self, i: int, means, scales, colors, opacities, prepared=None) -> torch.Tensor:
         device = means.device
@@ -419,15 +430,24 @@ class ViewShardedFitter:
         bg = self._background(device)
         w_sil = self.w_sil if (self.masks is not None and self.w_sil > 0.0) else 0.0
         g_scale = 1.0 / len(self.targets)
-        # every view's preparation (projection, culling, pair counts) is enqueued at once on a stream of
-        # its own: the host's read of a view's pair count never waits behind other views' renders, and
-        # the preparations run beside the splat kernels (their workspaces: ~70 B per Gaussian per view)
+        # the views' preparations (projection, culling, pair counts) run on a stream of their own,
+        # PREP_AHEAD views ahead of the view being rendered: the host's read of a view's pair count never
+        # waits behind other views' renders, the preparations run beside the splat kernels, and the host
+        # starts the first render after enqueueing a few preparations (not all of them)
         prep = getattr(self, "_prep", None)
         if prep is None or prep.device != device:
             self._prep = prep = torch.cuda.Stream(device)
         prep.wait_stream(main)
-        with torch.cuda.stream(prep):
-            ahead = [self._prepare(i, m, s, c, o, fit_view=True) for i in views]
+        pins = self._plan_pins(len(views))
+        ahead: dict = {}
+
+        def prepare(j):
+            if j < len(views) and j not in ahead:
+                with torch.cuda.stream(prep):
+                    ahead[j] = self._prepare(views[j], m, s, c, o, fit_view=True, plan_host=pins[j])
+
+        for j in range(PREP_AHEAD):
+            prepare(j)
         pending: list = [[] for _ in streams]  # per stream: (render state, partials) awaiting their reduction
         started = [False] * ns
         # stream k's views in nb near-equal batches of at most REDUCE_BATCH (sizes in the order they fill)
@@ -446,17 +466,19 @@ class ViewShardedFitter:
 
         for j, i in enumerate(views):
             k = j % ns
-            streams[k].wait_event(ahead[j].event)
-            ahead[j].geom.record_stream(streams[k])
+            prepare(j + PREP_AHEAD)
+            pv = ahead.pop(j)
+            streams[k].wait_event(pv.event)
+            pv.geom.record_stream(streams[k])
             with torch.cuda.stream(streams[k]):
                 cam = self.cams[i]
                 # one zone at the core cutoff and no depth channel: the loss reads neither depth nor the
                 # tail-only part of W's footprint (torch_renderer.FIT_CUTOFF)
                 gv = tr.make_view(cam.view, cam.proj, self.width, self.height, bg, cutoff=tr.FIT_CUTOFF,
                                   core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
-                rs, ws = tr.forward_l1_native(m, s, c, o, gv, ahead[j], self.targets[i],
+                rs, ws = tr.forward_l1_native(m, s, c, o, gv, pv, self.targets[i],
                                               self.masks[i] if w_sil > 0.0 else None, w_sil, g_scale, losses_v[j:j + 1])
-                ahead[j] = None
+                pv = None
                 tr.backward_splat_native(rs, ws)
             pending[k].append((rs, ws))
             if len(pending[k]) >= sizes[k][0]:

@@ -231,14 +231,16 @@ class Prepared:
         return _native.GrPlan(pairs, slots, core)
 
 
-def prepare_native(means, scales, colors, opacities, gv: _native.GrView) -> Prepared:
-    """Enqueue gr_fwd_prepare_async for one view on the current stream (no host wait)."""
+def prepare_native(means, scales, colors, opacities, gv: _native.GrView, plan_host=None) -> Prepared:
+    """Enqueue gr_fwd_prepare_async for one view on the current stream (no host wait).  ``plan_host``: a
+    pinned int64 tensor of 3 elements to receive the plan (a fit passes slices of one buffer it keeps)."""
     L = _native.lib()
     dev = means.device
     n = int(means.shape[0])
     cd = _color_dim(colors)
     geom = torch.empty((int(L.gr_geom_bytes(n)),), dtype=torch.uint8, device=dev)
-    plan_host = torch.zeros(3, dtype=torch.int64, pin_memory=True)  # gr_plan {num_pairs, num_slots, num_core_pairs}
+    if plan_host is None:
+        plan_host = torch.zeros(3, dtype=torch.int64, pin_memory=True)  # gr_plan {num_pairs, num_slots, num_core_pairs}
     _native.check(L.gr_fwd_prepare_async(ctypes.byref(gv), n, _native.ptr(means), _native.ptr(scales),
                                          _native.ptr(colors), cd, _native.ptr(opacities), _native.ptr(geom),
                                          geom.numel(), ctypes.c_void_p(plan_host.data_ptr()), _stream(dev)),
@@ -424,11 +426,11 @@ def _device_inputs(means, scales, colors, opacities):
 
 
 def prepare_view(means, scales, colors, opacities, view, proj, width, height, background=None,
-                 cutoff=None, core_cutoff=DEFAULT_CORE_CUTOFF, depth_grad: bool = True) -> Prepared:
+                 cutoff=None, core_cutoff=DEFAULT_CORE_CUTOFF, depth_grad: bool = True, plan_host=None) -> Prepared:
     """Enqueue the preparation of one view (see ``Prepared``); pass it to ``rasterize(prepared=...)``
     with the same tensors, cutoffs and ``depth_grad``.  The tensors' values must not change in between."""
     gv = make_view(view, proj, width, height, background, cutoff, core_cutoff, depth_grad)
-    return prepare_native(*_device_inputs(means, scales, colors, opacities), gv)
+    return prepare_native(*_device_inputs(means, scales, colors, opacities), gv, plan_host)
 
 
 def rasterize(means, scales, colors, opacities, view, proj, width, height, background=None, cutoff=None,
