@@ -190,7 +190,8 @@ def geom_layout(n: int):
 
 
 def bins_layout(gv: GrView, n: int, num_pairs: int):
-    out = (ctypes.c_size_t * 3)()
+    """[keys (radix path), sorted Gaussian ids int[K], ranges int2[2 tiles], pos_of int[K]]."""
+    out = (ctypes.c_size_t * 4)()
     plan = GrPlan(int(num_pairs), 0, 0)
     lib().gr_bins_layout(ctypes.byref(gv), int(n), ctypes.byref(plan), out)
     return list(out)

@@ -356,7 +356,7 @@ inline bool short_keys(int tiles) { return tiles <= TSORT_MAX_TILES; }
 // Persistent binning state (kept from forward to backward).
 struct Bins {
   uint32_t* keys;      // [K] sorted tile keys (radix-sort path only; the counting sort needs none)
-  int2* pairs;         // [K] sorted pairs: (gaussian id, emission index = partial-sum slot)
+  int* pairs;          // [K] Gaussian id of each sorted pair (its emission index: pos_of's inverse)
   int2* ranges;        // [vtiles] pair range of each virtual tile
   int4* items;         // [cap] work items (tile, k0, k1, chunk)
   int* num_items;      // [1]
@@ -370,6 +370,7 @@ struct Scratch {
   int* ids_in;         // [K]
   float* fwd_part;     // [cap][5][256] partial accumulators of tiles split over several items
   int2* pairs_in;      // [K] (radix path) unsorted (id, emission index) pairs
+  int2* pairs_sorted;  // [K] (radix path) the same, sorted by virtual tile
   void* sort_tmp;
 };
 
@@ -382,7 +383,7 @@ size_t bins_fixed(int vtiles, int64_t K, size_t off[7]) {
   const size_t cap = (size_t)item_cap(tiles, K);
   size_t o = 0;
   off[0] = o; o = align_up(o + (short_keys(tiles) ? 1 : kk) * sizeof(uint32_t));
-  off[1] = o; o = align_up(o + kk * sizeof(int2));
+  off[1] = o; o = align_up(o + kk * sizeof(int));
   off[2] = o; o = align_up(o + (size_t)tiles * sizeof(int2));
   off[3] = o; o = align_up(o + cap * sizeof(int4));
   off[4] = o; o = align_up(o + sizeof(int));
@@ -391,8 +392,9 @@ size_t bins_fixed(int vtiles, int64_t K, size_t off[7]) {
   return o;
 }
 
-// off: [0] emitted keys, [1] emitted ids, [2] split-tile partials, [3] (radix path) unsorted pairs
-size_t scratch_fixed(int vtiles, int64_t K, size_t off[4]) {
+// off: [0] emitted keys, [1] emitted ids, [2] split-tile partials, [3] / [4] (radix path) unsorted /
+// sorted pairs
+size_t scratch_fixed(int vtiles, int64_t K, size_t off[5]) {
   const int tiles = vtiles;
   const size_t kk = (size_t)(K > 0 ? K : 1);
   const size_t cap = (size_t)item_cap(tiles, K);
@@ -401,6 +403,7 @@ size_t scratch_fixed(int vtiles, int64_t K, size_t off[4]) {
   off[1] = o; o = align_up(o + kk * sizeof(int));
   off[2] = o; o = align_up(o + cap * 5 * TP * sizeof(float));
   off[3] = o; o = align_up(o + (short_keys(tiles) ? 1 : kk) * sizeof(int2));
+  off[4] = o; o = align_up(o + (short_keys(tiles) ? 1 : kk) * sizeof(int2));
   return o;
 }
 
@@ -482,7 +485,7 @@ Bins bins_view(void* base, int tiles, int64_t K) {
   char* b = (char*)base;
   Bins r;
   r.keys = (uint32_t*)(b + off[0]);
-  r.pairs = (int2*)(b + off[1]);
+  r.pairs = (int*)(b + off[1]);
   r.ranges = (int2*)(b + off[2]);
   r.items = (int4*)(b + off[3]);
   r.num_items = (int*)(b + off[4]);
@@ -492,7 +495,7 @@ Bins bins_view(void* base, int tiles, int64_t K) {
 }
 
 Scratch scratch_view(void* base, int tiles, int64_t K) {
-  size_t off[4];
+  size_t off[5];
   const size_t fixed = scratch_fixed(tiles, K, off);
   char* b = (char*)base;
   Scratch r;
@@ -500,6 +503,7 @@ Scratch scratch_view(void* base, int tiles, int64_t K) {
   r.ids_in = (int*)(b + off[1]);
   r.fwd_part = (float*)(b + off[2]);
   r.pairs_in = (int2*)(b + off[3]);
+  r.pairs_sorted = (int2*)(b + off[4]);
   r.sort_tmp = b + fixed;
   return r;
 }
@@ -665,11 +669,15 @@ __global__ __launch_bounds__(256) void k_emit_zones(ViewK v, int n, const int4* 
   }
 }
 
-// Radix-sort path: sorted position of each pair by emission index (the counting sort writes it in
-// k_tile_place).
-__global__ __launch_bounds__(256) void k_pos_of(int64_t K, const int2* __restrict__ pairs, int* __restrict__ pos_of) {
+// Radix-sort path: the sorted (id, emission index) values -> the Gaussian ids and the sorted position of
+// each pair by emission index (the counting sort writes both in k_tile_place).
+__global__ __launch_bounds__(256) void k_pos_of(int64_t K, const int2* __restrict__ sorted, int* __restrict__ ids,
+                                                int* __restrict__ pos_of) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < K) pos_of[pairs[k].y] = (int)k;
+  if (k >= K) return;
+  const int2 p = sorted[k];
+  ids[k] = p.x;
+  pos_of[p.y] = (int)k;
 }
 
 // Radix-sort path: the sort's values, (gaussian id, emission index).
@@ -782,8 +790,8 @@ __global__ __launch_bounds__(1024) void k_work_items_zones(int tiles, int tiles_
 // only when the pair is consumed, a batch later (stage_pair): selecting here lets the compiler turn
 // the load into a predicated one, and the join after it waits for every outstanding memory
 // operation, the in-flight DMA included.
-__device__ __forceinline__ int2 stage_id(int k, int k1, const int2* __restrict__ pairs) { return pairs[min(k, k1 - 1)]; }
-__device__ __forceinline__ int2 stage_pair(int2 raw, int k, int k1) { return k < k1 ? raw : make_int2(-1, -1); }
+__device__ __forceinline__ int stage_id(int k, int k1, const int* __restrict__ pairs) { return pairs[min(k, k1 - 1)]; }
+__device__ __forceinline__ int stage_pair(int raw, int k, int k1) { return k < k1 ? raw : -1; }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -951,7 +959,7 @@ __device__ __forceinline__ void ts_load(int64_t kb, int64_t k1, int64_t klast, i
 // One register-resident segment of k_tile_place: TS_SEG steps of 64 pairs, in pair order.
 // kseg: emission index of the segment's first pair (the slot written next to the Gaussian id).
 __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int (&d)[TS_SEG], const int (&id)[TS_SEG],
-                                         int kseg, int2* __restrict__ pairs_out, int* __restrict__ pos_of) {
+                                         int kseg, int* __restrict__ pairs_out, int* __restrict__ pos_of) {
   const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
   for (int j = 0; j < TS_SEG; ++j) {
@@ -975,7 +983,7 @@ __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int 
     const uint64_t m = ((uint64_t)mhi << 32) | mlo;
     if (ok) {
       const int pos = my[d[j]] + __popcll(m & below);
-      pairs_out[pos] = make_int2(id[j], kseg + j * 64 + lane);
+      pairs_out[pos] = id[j];
       pos_of[kseg + j * 64 + lane] = pos;  // emission order: coalesced
       __builtin_amdgcn_wave_barrier();  // every lane has read the cursor before it moves
       if ((m >> lane) == 1ull) my[d[j]] = pos + 1;  // highest lane of its group
@@ -990,7 +998,7 @@ __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int 
 __global__ __launch_bounds__(256, GR_PLACE_WAVES) void k_tile_place(int64_t K, int cw, int cols, int tiles, int bits,
                                                     const uint16_t* __restrict__ keys, const int* __restrict__ ids_in,
                                                     const int* __restrict__ S, const int2* __restrict__ ranges,
-                                                    int zone, int zbase, int2* __restrict__ pairs_out,
+                                                    int zone, int zbase, int* __restrict__ pairs_out,
                                                     int* __restrict__ pos_of) {
   extern __shared__ int cur[];  // [waves][tiles]
   const int c = xcd_item(blockIdx.x, cols);
@@ -1203,20 +1211,20 @@ __device__ __forceinline__ void glds4_planes(const float4* rec, const float* z, 
 // channel is not accumulated (no z staging, no D products).
 template <bool TAIL, bool PRECISE, bool ZCH = true>
 __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, int k1, int tid, int wave, float xc, float yc,
-                                                    int gq, const int2* __restrict__ pairs, const float4* __restrict__ rec,
+                                                    int gq, const int* __restrict__ pairs, const float4* __restrict__ rec,
                                                     f32x4& cW, f32x4& cR, f32x4& cG, f32x4& cB, f32x4& cD) {
   constexpr int BUF = FWD_PLANES * TP;  // floats per buffer
   auto stage = [&](int g, int b) {
     glds4_planes<TAIL, ZCH>(rec_of(g, n, rec), zrec_of(g, n, rec), smem + b * BUF + 64 * wave);
   };
-  stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1).x, 0);
-  int2 idn = stage_id(k0 + TP + tid, k1, pairs);
+  stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1), 0);
+  int idn = stage_id(k0 + TP + tid, k1, pairs);
   int buf = 0;
   const f32x2_t X = {xc, xc}, Y = {yc, yc};
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
     stage_wait();
     GR_STAGE_SYNC();
-    if (base + TP < k1) stage(stage_pair(idn, base + TP + tid, k1).x, buf ^ 1);
+    if (base + TP < k1) stage(stage_pair(idn, base + TP + tid, k1), buf ^ 1);
     idn = stage_id(base + 2 * TP + tid, k1, pairs);
     const int cnt = min(TP, k1 - base) - wave * 64;           // Gaussians of this batch for this wave
     const int nst = cnt <= 0 ? 0 : min(2, (cnt + 31) >> 5);  // steps of 32 (padding records are zero)
@@ -1499,7 +1507,7 @@ __device__ __forceinline__ void l1_tile_epilogue(const ViewK& v, int tile, int t
 template <int MODE>
 __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void k_raster_fwd_mfma(ViewK v, int n, const int4* __restrict__ items,
                                                          const int* __restrict__ num_items, const int2* __restrict__ ranges,
-                                                         const int2* __restrict__ pairs, const float4* __restrict__ rec,
+                                                         const int* __restrict__ pairs, const float4* __restrict__ rec,
                                                          float* __restrict__ fwd_part, float* __restrict__ out_rgb,
                                                          float* __restrict__ out_alpha, float* __restrict__ out_depth,
                                                          float4* __restrict__ saved4, float* __restrict__ savedD,
@@ -1639,7 +1647,7 @@ __device__ __forceinline__ void split_frag(const float (&v)[8], s16x8 (&f)[3]) {
 
 template <bool TAIL, bool DEPTH, int PIECES>
 __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, int wave, int tx, int ty,
-                                              const int2* __restrict__ pairs, const float4* __restrict__ rec,
+                                              const int* __restrict__ pairs, const float4* __restrict__ rec,
                                               float* __restrict__ partials, float4 (*sA)[TP], float4 (*sB)[TP],
                                               float (*sZ)[TP], const uint4* sUF) {
   static_assert(DEPTH || !TAIL, "tail items carry only depth-coupled terms");
@@ -1650,14 +1658,14 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
   const float pxb = (float)(tx * T + 4 * h) + 0.5f, pyb = (float)(ty * T + 4 * h) + 0.5f;
 #define PX0(q) (pxb + (float)((q) < 4 ? (q) : (q) + 4))
 #define PY0(q) (pyb + (float)((q) < 4 ? (q) : (q) + 4))
-  auto stage = [&](int2 pr, int b) {
-    const float4* p = rec_of(pr.x, n, rec);
+  auto stage = [&](int gid, int b) {
+    const float4* p = rec_of(gid, n, rec);
     glds16(p, &sA[b][64 * wave]);
     glds16(p + 1, &sB[b][64 * wave]);
-    if constexpr (DEPTH) glds4(zrec_of(pr.x, n, rec), &sZ[b][64 * wave]);  // z enters only the depth-coupled terms
+    if constexpr (DEPTH) glds4(zrec_of(gid, n, rec), &sZ[b][64 * wave]);  // z enters only the depth-coupled terms
   };
   stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1), 0);
-  int2 idn = stage_id(k0 + TP + tid, k1, pairs);  // raw: batch base + TP
+  int idn = stage_id(k0 + TP + tid, k1, pairs);  // raw: batch base + TP
   int buf = 0;
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
     stage_wait();
@@ -1818,7 +1826,7 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
 // PIECES = 2: no_depth_grad views (two round-to-nearest pieces per operand, three products).
 template <bool DEPTH, int PIECES>
 __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void k_raster_bwd_bf16(ViewK v, int n, const int4* __restrict__ items,
-                                                           const int* __restrict__ num_items, const int2* __restrict__ pairs,
+                                                           const int* __restrict__ num_items, const int* __restrict__ pairs,
                                                            const float4* __restrict__ rec, const uint4* __restrict__ UF,
                                                            float* __restrict__ partials) {
   __shared__ __attribute__((aligned(16))) float4 sA[2][TP];
@@ -2567,13 +2575,14 @@ const char* gr_version(void) { return GR_VERSION_STR; }
 
 void gr_geom_layout(int n, size_t offsets_out[GR_GEOM_PARTS]) { geom_fixed(n, offsets_out); }
 
-void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[3]) {
+void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[4]) {
   (void)n;
   size_t off[7];
   bins_fixed(vtiles_of(v), plan ? plan->num_pairs : 0, off);
   offsets_out[0] = off[0];
   offsets_out[1] = off[1];
   offsets_out[2] = off[2];
+  offsets_out[3] = off[6];
 }
 
 size_t gr_geom_bytes(int n) {
@@ -2592,7 +2601,7 @@ size_t gr_bins_bytes(const gr_view* v, int n, const gr_plan* plan) {
 size_t gr_fwd_scratch_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
   const int vtiles = vtiles_of(v);
-  size_t off[4];
+  size_t off[5];
   return scratch_fixed(vtiles, plan->num_pairs, off) + align_up(tile_sort_tmp_bytes(plan->num_pairs, vtiles));
 }
 
@@ -2830,11 +2839,12 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
       GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * vtiles, s));
       const int bits = bits_for((uint32_t)vtiles);
       size_t tmp = tile_sort_tmp_bytes(num_pairs, vtiles);
-      GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp, tmp, sc.keys_in, b.keys, sc.pairs_in, b.pairs,
+      GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp, tmp, sc.keys_in, b.keys, sc.pairs_in, sc.pairs_sorted,
                                                     (int)num_pairs, 0, bits, s));
       hipLaunchKernelGGL(k_ranges<uint32_t>, dim3(blocks_for(num_pairs)), dim3(256), 0, s, num_pairs, b.keys, b.ranges);
       GR_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_pos_of, dim3(blocks_for(num_pairs)), dim3(256), 0, s, num_pairs, (const int2*)b.pairs, b.pos_of);
+      hipLaunchKernelGGL(k_pos_of, dim3(blocks_for(num_pairs)), dim3(256), 0, s, num_pairs, (const int2*)sc.pairs_sorted,
+                         b.pairs, b.pos_of);
       GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
                          b.tile_item0);
@@ -2865,7 +2875,7 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
                           : (!v->no_depth_grad ? k_raster_fwd_mfma<1>
                                                : (out_depth ? k_raster_fwd_mfma<2> : k_raster_fwd_mfma<3>)),
                        dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
-                       (const int*)b.num_items, (const int2*)b.ranges, (const int2*)b.pairs, (const float4*)g.rec,
+                       (const int*)b.num_items, (const int2*)b.ranges, (const int*)b.pairs, (const float4*)g.rec,
                        sc.fwd_part, out_rgb, out_alpha, out_depth, saved4, savedD, la, UF);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_FWD, s);
@@ -2952,7 +2962,7 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
     auto kern = g_depth != nullptr ? k_raster_bwd_bf16<true, 3>
                                    : (v->no_depth_grad ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>);
     hipLaunchKernelGGL(kern, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items,
-                       (const int2*)b.pairs, (const float4*)g.rec, (const uint4*)UF, partials);
+                       (const int*)b.pairs, (const float4*)g.rec, (const uint4*)UF, partials);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_BWD, s);
   }
@@ -3017,7 +3027,7 @@ gr_status gr_bwd_splat(const gr_view* v, int n, const gr_plan* plan, const void*
   const int64_t cap = item_cap(2 * tiles, plan->num_pairs);
   prof_mark(PROF_RASTER_BWD, s);
   hipLaunchKernelGGL((k_raster_bwd_bf16<false, 2>), dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
-                     (const int*)b.num_items, (const int2*)b.pairs, (const float4*)g.rec, (const uint4*)w.UF, w.partials);
+                     (const int*)b.num_items, (const int*)b.pairs, (const float4*)g.rec, (const uint4*)w.UF, w.partials);
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_RASTER_BWD, s);
   return GR_OK;

@@ -21,8 +21,8 @@ Also reported on rank 0:
                 streams), vs 8 TB/s; its PMC HBM traffic from profiles/pmc_traffic.json
                 (tools/pmc_traffic.py); the executed bf16 MFMA rate beside it
   hbm_model     the north_star's framing: SURVEY.md 8(d)'s byte model of the tile-binned path per view at
-                the survey's fixed 5-sigma footprint and at this build's 7-sigma pair count, and the bench
-                value as a fraction of each 8 TB/s roofline
+                this run's pair count (the fit path bins the survey's 5-sigma footprint), the bench value
+                as a fraction of that 8 TB/s roofline and of the survey table's C4 roof (2,830 Mpx/s)
   default_precision_mode
                 a few more timed steps with a depth term in the loss (the f32-grade mode a depth-loss
                 caller gets; the headline runs the fit's own loss, which has no depth term)
@@ -81,6 +81,7 @@ BWD_KERNEL = "k_raster_bwd_bf16"
 # roofline" framing): bytes per view = N (3 B_in + 2 x 36) + K (2 x 12 + 2 x 36 + 2 x 36) + 60 H W
 # with B_in = 40 (RGB), K = pairs per view as binned here.
 B_IN_RGB = 40
+SURVEY_C4_ROOF_MPX = 2830.0  # the north_star target is >= 50% of it
 
 
 def parse():
@@ -255,7 +256,6 @@ def main():
     fm.NUM_STREAMS = streams_saved
     # the fit step renders its views through the fused path: one zone at FIT_CUTOFF (fit_multiview._views_direct)
     avg_pairs, avg_core = pairs_per_view(fitter, cams, R, tr.FIT_CUTOFF, tr.FIT_CUTOFF)
-    k5_pairs, _ = pairs_per_view(fitter, cams, R, 5.0, 5.0)
 
     # the default precision mode: what a caller with a depth loss gets (f32-grade W / D, three-piece
     # backward with the tail pairs): the same fit with a depth term in the loss (C3's losses)
@@ -356,9 +356,12 @@ def main():
             # the batched per-Gaussian reduction (gr_reduce_views), HIP events, per view of the single-stream step
             "reduce_us_per_view": round(1e3 * prof["reduce_bwd"][0] / max(len(fitter.my_views), 1), 1),
             "binning_us_per_view": round(1e3 * prof["binning"][0] / max(len(fitter.my_views), 1), 1),
-            "hbm_model": {"survey_5sigma": hbm_model(k5_pairs), "build_7sigma": hbm_model(avg_pairs),
-                          "source": "SURVEY.md 8(d) tile-binned byte model, 8 TB/s: at its fixed 5-sigma footprint "
-                                    "(the survey's 2,830 Mpx/s roof) and at this build's 7-sigma pair count"},
+            "hbm_model": dict(hbm_model(avg_pairs),
+                              survey_table_roofline_mpx_per_s=SURVEY_C4_ROOF_MPX,
+                              frac_of_survey_table=round(value / (SURVEY_C4_ROOF_MPX * world), 4),
+                              source=f"SURVEY.md 8(d) tile-binned byte model at 8 TB/s with this run's pair count (the "
+                                     f"fit path bins one {tr.FIT_CUTOFF:g}-sigma zone, the survey's footprint), and "
+                                     f"the survey table's C4 roof (K = 9.41e6 pairs per view at view 0)"),
             "default_precision_mode": extra or None,
             "sclk_mhz": {"before": clk0, "after": clk1},
             "loss": float(loss),

@@ -231,12 +231,13 @@ gr_status gr_l1_loss_bwd(const float* a, const float* b, int64_t n1, const float
  *         [4] device copy of the plan (gr_plan) and the exact pair total [5] end of the fixed part
  *         (counts/offsets packed: core tiles / first core pair in the low word, tail tiles / first
  *         tail pair after the num_core_pairs core pairs in the high word)
- *   bins: [0] keys (radix-sort fallback only, > 8192 tiles) [1] pairs int2[K] (gaussian id,
- *         emission index = backward partial-sum slot)
- *         [2] ranges int2[2 * tiles]: per virtual tile (2t: core list of tile t, 2t+1: its tail list) */
+ *   bins: [0] keys (radix-sort fallback only, > 8192 tiles) [1] int[K] Gaussian id of each sorted pair
+ *         [2] ranges int2[2 * tiles]: per virtual tile (2t: core list of tile t, 2t+1: its tail list)
+ *         [3] pos_of int[K]: sorted position of each pair by emission index (= backward partial-sum
+ *         slot order: Gaussian-major, tiles in raster order, core zone first) */
 #define GR_GEOM_PARTS 6
 void gr_geom_layout(int n, size_t offsets_out[GR_GEOM_PARTS]);
-void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[3]);
+void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[4]);
 
 /* Live kernel timing with HIP events on the launch stream (bench.py).  Between begin and end,
  * the timed stages are bracketed by two events each; end() synchronises them and returns the

@@ -45,7 +45,8 @@ def test_layouts_are_aligned_and_ordered(pkg):
                                       __import__("numpy").eye(4, dtype="float32"), 800, 800)
     b = pkg._native.bins_layout(gv, 1000, 12345)
     assert b == sorted(b) and all(o % 256 == 0 for o in b)
-    assert b[2] - b[1] >= 8 * 12345  # sorted (id, slot) pairs
+    assert b[2] - b[1] >= 4 * 12345  # sorted Gaussian ids
+    assert b[3] > b[2]  # pos_of after the ranges
 
 
 def test_struct_sizes_match_header(pkg):

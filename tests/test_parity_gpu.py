@@ -143,7 +143,11 @@ def _native_bins(pkg, scene: orc.Scene, view, proj, W, H, device, cutoff=CUTOFF)
     bins = st.bins.cpu().numpy()
     K = st.num_pairs
     tiles = ((W + 15) // 16) * ((H + 15) // 16)
-    pairs = bins[b_off[1]: b_off[1] + 8 * K].view(np.int32).reshape(K, 2)  # (gaussian id, emission index)
+    ids = bins[b_off[1]: b_off[1] + 4 * K].view(np.int32)  # Gaussian id of each sorted pair
+    pos_of = bins[b_off[3]: b_off[3] + 4 * K].view(np.int32)  # sorted position, by emission index
+    emit = np.full(K, -1, np.int64)
+    emit[pos_of] = np.arange(K)  # emission index of each sorted pair (pos_of is a permutation)
+    pairs = np.stack([ids.astype(np.int64), emit], 1)  # (gaussian id, emission index)
     ranges = bins[b_off[2]: b_off[2] + 16 * tiles].view(np.int32).reshape(2 * tiles, 2)  # per virtual tile
     return dict(rec=rec, rect=rect, core=cnt[:, 0], tail=cnt[:, 1], off=off, pairs=pairs, ranges=ranges, K=K,
                 Kc=int(st.plan.num_core_pairs), slots=int(st.plan.num_slots))
