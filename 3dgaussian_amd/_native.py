@@ -99,6 +99,9 @@ _SIG = {
     "gr_bwd_l1": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P,
                                  ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t,
                                  _P]),
+    "gr_bwd_fit": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P,
+                                  ctypes.c_float, _P, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, ctypes.c_int, _P,
+                                  ctypes.c_size_t, _P]),
     "gr_fwd_render_l1": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P, _P,
                                         ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, ctypes.c_size_t, _P]),
     "gr_bwd_splat": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_size_t, _P]),

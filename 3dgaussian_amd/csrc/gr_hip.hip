@@ -1349,7 +1349,11 @@ struct L1Args {
   const float* t_rgb;   // (H,W,3) target image
   const float* t_mask;  // (H,W) silhouette target or nullptr
   float w_sil, g_scale;
-  float* tile_loss;     // [tiles][2]
+  float* tile_loss;     // [tiles][4]: sums of |out - t|, |alpha - m|, |d_pred - t_d|, and the depth-max term
+  // depth loss (gr_bwd_fit, fit_multiview_stub.py:301-305): w_depth mean|depth / (max(depth) + 1e-6) - t_depth|
+  const float* t_depth = nullptr;  // (H,W) depth target or nullptr (no depth term)
+  float w_depth = 0.0f;
+  const float* dscal = nullptr;    // device scalars: [0] max(depth), [1] the max's gradient per arg-max pixel
 };
 
 __device__ __forceinline__ float sign0(float t) { return t > 0.0f ? 1.0f : (t < 0.0f ? -1.0f : 0.0f); }
@@ -1389,15 +1393,122 @@ __device__ __forceinline__ void pixel_upstream(const ViewK& v, int p, float4 s, 
     ga = g_alpha[p];
   }
   if (has_a && al >= 0.0f && al <= 1.0f) gW += ga / (den * den);
-  if (g_depth) {
+  const bool dfit = l1.t_rgb && l1.t_depth;
+  if (g_depth || dfit) {
     const float d = Dp / dden;
-    if (d >= 0.0f) {
-      const float gd = g_depth[p];
+    if (d >= 0.0f) {  // depth = clamp_min(D / (W + 1e-6), 0): the gradient passes where d >= 0
+      float gd;
+      if (dfit) {  // d (w_depth mean|d / (M + 1e-6) - t|) / d depth, plus the max's share on arg-max pixels
+        const float M = l1.dscal[0], dm = M + 1e-6f;
+        const float t = d / dm - l1.t_depth[p];
+        gd = (sign0(t) * ((l1.w_depth * l1.g_scale) / HWf)) / dm;
+        if (d == M) gd += l1.dscal[1];
+      } else {
+        gd = g_depth[p];
+      }
       gW -= gd * Dp / (dden * dden);
       u[4] = gd / dden;
     }
   }
   u[3] = gW;
+}
+
+// Depth loss of the fused fit backward (gr_bwd_fit): the depth image's maximum M (per tile, then one
+// block: exact, order-free), then per tile the sums of |d / (M + 1e-6) - t|, of the max's chain term
+// sign(.) (d / (M + 1e-6)) / (M + 1e-6) (torch's div backward w.r.t. the denominator, up to its factor) and
+// the count of arg-max pixels; one block turns them into the max's gradient per arg-max pixel
+// (torch's max backward shares it evenly among ties).  Depth = max(D / (W + 1e-6), 0) from the saved sums,
+// exactly as write_pixel made it.
+__device__ __forceinline__ float saved_depth(const float4* __restrict__ saved4, const float* __restrict__ savedD, int p) {
+  const float d = savedD[p] / (saved4[p].x + 1e-6f);
+  return d < 0.0f ? 0.0f : d;
+}
+
+__global__ __launch_bounds__(256) void k_depth_tile_max(ViewK v, const float4* __restrict__ saved4,
+                                                        const float* __restrict__ savedD, float* __restrict__ tile_aux) {
+  const int tile = blockIdx.x, tid = threadIdx.x;
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
+  float m = (x < v.W && y < v.H) ? saved_depth(saved4, savedD, y * v.W + x) : 0.0f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __shared__ float sm[4];
+  if ((tid & 63) == 0) sm[tid >> 6] = m;
+  __syncthreads();
+  if (tid == 0) tile_aux[2 * tile] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+}
+
+__global__ __launch_bounds__(256) void k_depth_max(const float* __restrict__ tile_aux, int tiles, float* __restrict__ dscal) {
+  float m = 0.0f;
+  for (int t = threadIdx.x; t < tiles; t += 256) m = fmaxf(m, tile_aux[2 * t]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __shared__ float sm[4];
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) dscal[0] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+}
+
+__global__ __launch_bounds__(256) void k_depth_tile_sums(ViewK v, const float4* __restrict__ saved4,
+                                                         const float* __restrict__ savedD, const float* __restrict__ t_depth,
+                                                         const float* __restrict__ dscal, float* __restrict__ tile_loss,
+                                                         float* __restrict__ tile_aux) {
+  const int tile = blockIdx.x, tid = threadIdx.x;
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
+  float l = 0.f, sd = 0.f, cnt = 0.f;
+  if (x < v.W && y < v.H) {
+    const int p = y * v.W + x;
+    const float d = saved_depth(saved4, savedD, p), M = dscal[0], dm = M + 1e-6f;
+    const float t = d / dm - t_depth[p];
+    l = fabsf(t);
+    sd = sign0(t) * ((d / dm) / dm);
+    cnt = d == M ? 1.0f : 0.0f;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    l += __shfl_xor(l, o);
+    sd += __shfl_xor(sd, o);
+    cnt += __shfl_xor(cnt, o);
+  }
+  __shared__ float sm[3][4];
+  if ((tid & 63) == 0) {
+    sm[0][tid >> 6] = l;
+    sm[1][tid >> 6] = sd;
+    sm[2][tid >> 6] = cnt;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    tile_loss[4 * tile + 2] = ((sm[0][0] + sm[0][1]) + sm[0][2]) + sm[0][3];
+    tile_loss[4 * tile + 3] = ((sm[1][0] + sm[1][1]) + sm[1][2]) + sm[1][3];
+    tile_aux[2 * tile + 1] = ((sm[2][0] + sm[2][1]) + sm[2][2]) + sm[2][3];
+  }
+}
+
+// dscal[1] = -(w_depth g_scale / HW) sum_p sign(.) (d_p / dm) / dm / (number of arg-max pixels)
+__global__ __launch_bounds__(256) void k_depth_final(const float* __restrict__ tile_loss, const float* __restrict__ tile_aux,
+                                                     int tiles, int64_t HW, float w_depth, float g_scale,
+                                                     float* __restrict__ dscal) {
+  __shared__ double r1[256], r2[256];
+  const int t = threadIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = t; i < tiles; i += 256) {
+    s1 += (double)tile_loss[4 * i + 3];
+    s2 += (double)tile_aux[2 * i + 1];
+  }
+  r1[t] = s1;
+  r2[t] = s2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) {
+      r1[t] += r1[t + w];
+      r2[t] += r2[t + w];
+    }
+    __syncthreads();
+  }
+  if (t != 0) return;
+  const float gM = -((w_depth * g_scale) / (float)HW) * (float)r1[0];
+  dscal[1] = r2[0] > 0.0 ? gM / (float)r2[0] : 0.0f;
 }
 
 // The tile's L1 sums (block of 256 threads, one pixel each): waves, then the 4 wave sums in a fixed order.
@@ -1414,8 +1525,8 @@ __device__ __forceinline__ void tile_loss_sums(int tile, int tid, float l_rgb, f
   }
   __syncthreads();
   if (tid == 0) {
-    tile_loss[2 * tile] = ((sL[0][0] + sL[0][1]) + sL[0][2]) + sL[0][3];
-    tile_loss[2 * tile + 1] = ((sL[1][0] + sL[1][1]) + sL[1][2]) + sL[1][3];
+    tile_loss[4 * tile] = ((sL[0][0] + sL[0][1]) + sL[0][2]) + sL[0][3];
+    tile_loss[4 * tile + 1] = ((sL[1][0] + sL[1][1]) + sL[1][2]) + sL[1][3];
   }
 }
 
@@ -1457,7 +1568,7 @@ __device__ __forceinline__ void tile_fragments(const float (*sU)[TP], uint4* __r
 __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __restrict__ saved4,
                                                      const float* __restrict__ savedD, const float* __restrict__ g_rgb,
                                                      const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
-                                                     uint4* __restrict__ UF, int pieces, L1Args l1) {
+                                                     uint4* __restrict__ UF, int pieces, L1Args l1, bool depth) {
   const int tile = blockIdx.x, tid = threadIdx.x;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
@@ -1472,7 +1583,7 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
 #pragma unroll
   for (int k = 0; k < 5; ++k) sU[k][tid] = u[k];
   __syncthreads();
-  tile_fragments(sU, reinterpret_cast<uint4*>(UF) + (size_t)tile * UF_FRAGS, tid, pieces, g_depth != nullptr);
+  tile_fragments(sU, reinterpret_cast<uint4*>(UF) + (size_t)tile * UF_FRAGS, tid, pieces, depth);
 }
 
 // gr_fwd_render_l1: a finished tile's pixel sums -> the fit loss's upstream fragments (the backward's
@@ -2461,28 +2572,36 @@ __global__ __launch_bounds__(256) void k_l1_final(const float* __restrict__ part
 
 // The view loss of gr_bwd_l1 from its per-tile sums (double, fixed order): mean|out - t| +
 // w_sil mean|alpha - m|, the value k_l1_final gives for the same images.
+// The view loss from the per-tile sums (fixed order, double): mean|out - t| + w_sil mean|alpha - m|
+// (n2 = HW with a mask, else 0) + w_depth mean|d_pred - t_d| (n3 = HW with a depth target, else 0).
 __global__ __launch_bounds__(256) void k_tile_loss_final(const float* __restrict__ tile_loss, int tiles, int64_t n1,
-                                                         int64_t n2, float w_sil, float* __restrict__ loss) {
-  __shared__ double r1[256], r2[256];
+                                                         int64_t n2, float w_sil, int64_t n3, float w_depth,
+                                                         float* __restrict__ loss) {
+  __shared__ double r1[256], r2[256], r3[256];
   const int t = threadIdx.x;
-  double s1 = 0.0, s2 = 0.0;
+  double s1 = 0.0, s2 = 0.0, s3 = 0.0;
   for (int i = t; i < tiles; i += 256) {
-    s1 += (double)tile_loss[2 * i];
-    s2 += (double)tile_loss[2 * i + 1];
+    s1 += (double)tile_loss[4 * i];
+    s2 += (double)tile_loss[4 * i + 1];
+    if (n3 > 0) s3 += (double)tile_loss[4 * i + 2];
   }
   r1[t] = s1;
   r2[t] = s2;
+  r3[t] = s3;
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
     if (t < w) {
       r1[t] += r1[t + w];
       r2[t] += r2[t + w];
+      r3[t] += r3[t + w];
     }
     __syncthreads();
   }
   if (t != 0) return;
-  const float m1 = (float)(r1[0] / (double)n1);
-  *loss = n2 > 0 ? m1 + w_sil * (float)(r2[0] / (double)n2) : m1;
+  float l = (float)(r1[0] / (double)n1);
+  if (n2 > 0) l = l + w_sil * (float)(r2[0] / (double)n2);
+  if (n3 > 0) l = l + w_depth * (float)(r3[0] / (double)n3);
+  *loss = l;
 }
 
 // d/da = g sign(a - b) / n1, d/dc = (w2 g) sign(c - d) / n2 (torch: abs' = sign, sign(0) = 0).
@@ -2612,7 +2731,8 @@ size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan) {
   const size_t tiles = (size_t)tiles_x_of(v->width) * tiles_y_of(v->height);
   const size_t per_tile = UF_FRAGS * sizeof(uint4);
   return align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)) + align_up(tiles * per_tile) +
-         align_up(tiles * 2 * sizeof(float));  // per-tile loss sums (gr_bwd_l1)
+         align_up(tiles * 4 * sizeof(float)) + align_up(tiles * 2 * sizeof(float)) +
+         align_up(4 * sizeof(float));  // per-tile loss sums, per-tile depth max / arg-max counts, depth scalars
 }
 
 // Decode the scanned totals (core, tail pairs) into the plan; a count that does not fit int32 is
@@ -2747,7 +2867,9 @@ gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const floa
 struct BwdWs {
   float* partials;
   uint4* UF;
-  float* tile_loss;
+  float* tile_loss;  // [tiles][4]
+  float* tile_aux;   // [tiles][2]: depth max, arg-max pixels (gr_bwd_fit)
+  float* dscal;      // [4]: max(depth), the max's gradient per arg-max pixel
 };
 static BwdWs bwd_ws(const gr_view* v, const gr_plan* plan, void* ws) {
   const size_t tiles = (size_t)tiles_x_of(v->width) * tiles_y_of(v->height);
@@ -2755,6 +2877,8 @@ static BwdWs bwd_ws(const gr_view* v, const gr_plan* plan, void* ws) {
   w.partials = (float*)ws;
   w.UF = (uint4*)((char*)ws + align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)));
   w.tile_loss = (float*)((char*)w.UF + align_up(tiles * UF_FRAGS * sizeof(uint4)));
+  w.tile_aux = (float*)((char*)w.tile_loss + align_up(tiles * 4 * sizeof(float)));
+  w.dscal = (float*)((char*)w.tile_aux + align_up(tiles * 2 * sizeof(float)));
   return w;
 }
 
@@ -2885,7 +3009,7 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
   GR_HIP_TRY(hipGetLastError());
   if (l1) {
     hipLaunchKernelGGL(k_tile_loss_final, dim3(1), dim3(256), 0, s, (const float*)la.tile_loss, tiles, (int64_t)(3 * HW),
-                       (int64_t)(l1->t_mask ? HW : 0), l1->w_sil, l1_loss_out);
+                       (int64_t)(l1->t_mask ? HW : 0), l1->w_sil, (int64_t)0, 0.0f, l1_loss_out);
     GR_HIP_TRY(hipGetLastError());
   }
   return GR_OK;
@@ -2919,10 +3043,10 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
                           const float* saved, const float* g_rgb, const float* g_alpha, const float* g_depth,
                           const float* t_rgb, const float* t_mask, float w_sil, float g_scale, float* loss_out,
                           float* d_means, float* d_scales, float* d_colors, float* d_opacities, int accumulate, void* ws,
-                          size_t ws_bytes, void* stream) {
+                          size_t ws_bytes, void* stream, const float* t_depth = nullptr, float w_depth = 0.0f) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
-  if (g_depth && v->no_depth_grad)
+  if ((g_depth || (t_rgb && t_depth)) && v->no_depth_grad)
     return set_error(GR_ERR_INVALID_ARGUMENT,
                      "depth gradient for a view rendered with no_depth_grad (render it with depth_grad=True)");
   if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
@@ -2945,22 +3069,38 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
   float* partials = w.partials;
   uint4* UF = w.UF;
   float* tile_loss = w.tile_loss;
-  const L1Args l1{t_rgb, t_mask, w_sil, g_scale, t_rgb ? tile_loss : nullptr};
+  const bool dfit = t_rgb && t_depth;  // fused depth loss (gr_bwd_fit)
+  L1Args l1{t_rgb, t_mask, w_sil, g_scale, t_rgb ? tile_loss : nullptr};
+  if (dfit) {
+    l1.t_depth = t_depth;
+    l1.w_depth = w_depth;
+    l1.dscal = w.dscal;
+    const float4* s4 = (const float4*)saved;
+    const float* sD = saved + 4 * HW;
+    hipLaunchKernelGGL(k_depth_tile_max, dim3(tiles), dim3(256), 0, s, vk, s4, sD, w.tile_aux);
+    hipLaunchKernelGGL(k_depth_max, dim3(1), dim3(256), 0, s, (const float*)w.tile_aux, tiles, w.dscal);
+    hipLaunchKernelGGL(k_depth_tile_sums, dim3(tiles), dim3(256), 0, s, vk, s4, sD, t_depth, (const float*)w.dscal,
+                       tile_loss, w.tile_aux);
+    hipLaunchKernelGGL(k_depth_final, dim3(1), dim3(256), 0, s, (const float*)tile_loss, (const float*)w.tile_aux, tiles,
+                       (int64_t)HW, w_depth, g_scale, w.dscal);
+    GR_HIP_TRY(hipGetLastError());
+  }
+  const bool depth = g_depth != nullptr || dfit;  // an upstream depth gradient reaches the splat
   if (num_pairs > 0 || t_rgb) {
     hipLaunchKernelGGL(k_pixel_grads, dim3(tiles), dim3(256), 0, s, vk, (const float4*)saved, saved + 4 * HW, g_rgb,
-                       g_alpha, g_depth, UF, v->no_depth_grad ? 2 : 3, l1);
+                       g_alpha, g_depth, UF, v->no_depth_grad ? 2 : 3, l1, depth);
     GR_HIP_TRY(hipGetLastError());
   }
   if (t_rgb) {
     hipLaunchKernelGGL(k_tile_loss_final, dim3(1), dim3(256), 0, s, (const float*)tile_loss, tiles, (int64_t)(3 * HW),
-                       (int64_t)(t_mask ? HW : 0), w_sil, loss_out);
+                       (int64_t)(t_mask ? HW : 0), w_sil, (int64_t)(dfit ? HW : 0), w_depth, loss_out);
     GR_HIP_TRY(hipGetLastError());
   }
   if (num_pairs > 0) {
     const int64_t cap = item_cap(2 * tiles, num_pairs);
     prof_mark(PROF_RASTER_BWD, s);
-    auto kern = g_depth != nullptr ? k_raster_bwd_bf16<true, 3>
-                                   : (v->no_depth_grad ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>);
+    auto kern = depth ? k_raster_bwd_bf16<true, 3>
+                      : (v->no_depth_grad ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>);
     hipLaunchKernelGGL(kern, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items,
                        (const int*)b.pairs, (const float4*)g.rec, (const uint4*)UF, partials);
     GR_HIP_TRY(hipGetLastError());
@@ -2969,11 +3109,11 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
   prof_mark(PROF_REDUCE, s);
   {
     // the backward without a depth gradient writes 8-float rows (bwd_item_bf16)
-    const bool row8 = g_depth == nullptr;
+    const bool row8 = !depth;
     auto launch = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
                          (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const int*)b.pos_of, (const float*)partials,
-                         d_means, d_scales, d_colors, d_opacities, g_depth != nullptr ? 1 : 0, accumulate);
+                         d_means, d_scales, d_colors, d_opacities, depth ? 1 : 0, accumulate);
     };
     if (color_dim == 3)
       row8 ? launch(k_reduce_bwd<3, true>) : launch(k_reduce_bwd<3, false>);
@@ -2995,6 +3135,18 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
                  float* d_scales, float* d_colors, float* d_opacities, void* ws, size_t ws_bytes, void* stream) {
   return bwd_impl(v, n, plan, means, scales, colors, color_dim, opacities, geom, bins, saved, g_rgb, g_alpha, g_depth,
                   nullptr, nullptr, 0.0f, 0.0f, nullptr, d_means, d_scales, d_colors, d_opacities, 0, ws, ws_bytes, stream);
+}
+
+gr_status gr_bwd_fit(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
+                     const float* colors, int color_dim, const float* opacities, const void* geom, const void* bins,
+                     const float* saved, const float* target_rgb, const float* target_mask, float w_sil,
+                     const float* target_depth, float w_depth, float g_scale, float* loss_out, float* d_means,
+                     float* d_scales, float* d_colors, float* d_opacities, int accumulate, void* ws, size_t ws_bytes,
+                     void* stream) {
+  if (!target_rgb) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_fit: target_rgb is null");
+  return bwd_impl(v, n, plan, means, scales, colors, color_dim, opacities, geom, bins, saved, nullptr, nullptr, nullptr,
+                  target_rgb, target_mask, w_sil, g_scale, loss_out, d_means, d_scales, d_colors, d_opacities,
+                  accumulate, ws, ws_bytes, stream, target_depth, w_depth);
 }
 
 gr_status gr_bwd_l1(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,

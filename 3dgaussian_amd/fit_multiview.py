@@ -292,6 +292,20 @@ class ViewShardedFitter:
                                core_cutoff=tr.FIT_CUTOFF if fit_view else tr.DEFAULT_CORE_CUTOFF,
                                depth_grad=self._depth_grad(), plan_host=plan_host)
 
+    def _fit_view(self, i: int, device) -> "tr._native.GrView":
+        """The gr_view of view i for the fused path (one FIT_CUTOFF zone, no depth gradient), built once:
+        cameras and background do not change during a fit (saves the host's matrix inverse and copies
+        twice per view and step)."""
+        cache = getattr(self, "_gv_cache", None)
+        if cache is None:
+            self._gv_cache = cache = {}
+        gv = cache.get(i)
+        if gv is None:
+            cam = self.cams[i]
+            gv = cache[i] = tr.make_view(cam.view, cam.proj, self.width, self.height, self._background(device),
+                                         cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
+        return gv
+
     def _plan_pins(self, count: int) -> torch.Tensor:
         """One pinned (count, 3) int64 buffer for the views' plans, kept across steps (a pinned allocation
         per view and step costs host time on the render path)."""
@@ -324,9 +338,9 @@ class ViewShardedFitter:
         return loss
 
     def _direct(self, device) -> bool:
-        """The fused path (step_views_direct): HIP render op, fused L1 losses, no depth term."""
-        return (self.render_fn is hip_render and device.type == "cuda" and FUSED_LOSS and DIRECT_BACKWARD
-                and not self._depth_grad())
+        """The fused path (_views_direct, or _views_direct_depth with a depth term): HIP render op, the
+        view loss and its gradients in the C ABI, no autograd per view."""
+        return self.render_fn is hip_render and device.type == "cuda" and FUSED_LOSS and DIRECT_BACKWARD
 
     def step(self) -> torch.Tensor:
         """One iteration; returns the full (all-rank) loss as a 0-d tensor on the device."""
@@ -337,7 +351,10 @@ class ViewShardedFitter:
         means, scales, colors, opacities = activations(self.params)
         device = means.device
         if self._direct(device) and means.shape[0] > 0:
-            total = self._views_direct(means, scales, colors, opacities)
+            if self._depth_grad():
+                total = self._views_direct_depth(means, scales, colors, opacities)
+            else:
+                total = self._views_direct(means, scales, colors, opacities)
             loss = total / len(self.targets)
             if self.rank == 0:
                 reg = self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean()
@@ -427,7 +444,6 @@ class ViewShardedFitter:
         acc = [tuple(torch.empty_like(t) for t in (m, s, c, o)) for _ in streams]
         for st in streams[1:]:
             st.wait_stream(main)
-        bg = self._background(device)
         w_sil = self.w_sil if (self.masks is not None and self.w_sil > 0.0) else 0.0
         g_scale = 1.0 / len(self.targets)
         # the views' preparations (projection, culling, pair counts) run on a stream of their own,
@@ -444,7 +460,7 @@ class ViewShardedFitter:
         def prepare(j):
             if j < len(views) and j not in ahead:
                 with torch.cuda.stream(prep):
-                    ahead[j] = self._prepare(views[j], m, s, c, o, fit_view=True, plan_host=pins[j])
+                    ahead[j] = tr.prepare_native(m, s, c, o, self._fit_view(views[j], device), plan_host=pins[j])
 
         for j in range(PREP_AHEAD):
             prepare(j)
@@ -471,12 +487,9 @@ class ViewShardedFitter:
             streams[k].wait_event(pv.event)
             pv.geom.record_stream(streams[k])
             with torch.cuda.stream(streams[k]):
-                cam = self.cams[i]
                 # one zone at the core cutoff and no depth channel: the loss reads neither depth nor the
                 # tail-only part of W's footprint (torch_renderer.FIT_CUTOFF)
-                gv = tr.make_view(cam.view, cam.proj, self.width, self.height, bg, cutoff=tr.FIT_CUTOFF,
-                                  core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
-                rs, ws = tr.forward_l1_native(m, s, c, o, gv, pv, self.targets[i],
+                rs, ws = tr.forward_l1_native(m, s, c, o, pv.gv, pv, self.targets[i],
                                               self.masks[i] if w_sil > 0.0 else None, w_sil, g_scale, losses_v[j:j + 1])
                 pv = None
                 tr.backward_splat_native(rs, ws)
@@ -487,6 +500,74 @@ class ViewShardedFitter:
                     sizes[k].pop(0)
         for k in range(ns):
             reduce_pending(k)
+        for st in streams[1:]:
+            main.wait_stream(st)
+        main.wait_stream(prep)
+        used = min(ns, len(views))
+        out = []
+        for q in range(4):
+            t = acc[0][q]
+            for k in range(1, used):
+                t = t + acc[k][q]
+            out.append(t if used > 0 else torch.zeros_like(acc[0][q]))
+        self._acc = tuple(out)
+        return losses_v[:len(views)].sum() if views else torch.zeros((), device=device)
+
+    def _views_direct_depth(self, means, scales, colors, opacities) -> torch.Tensor:
+        """The fused path with the depth term (fit_multiview_stub.py:301-305): per view the HIP forward in the
+        default precision mode (depth output, f32-grade W and D, the depth-gradient footprint), then
+        gr_bwd_fit (L1 + silhouette + depth loss gradients and the render backward) adding the gradient into
+        the stream's accumulator set (in view order: deterministic).  Returns the sum of the view losses."""
+        device = means.device
+        m, s, c, o = (t.detach().contiguous() for t in (means, scales, colors, opacities))
+        views = self.my_views
+        main = torch.cuda.current_stream(device)
+        ns = max(1, min(NUM_STREAMS, len(views)))
+        side = getattr(self, "_side", None)
+        if ns > 1 and (side is None or len(side) != ns - 1 or side[0].device != device):
+            self._side = side = [torch.cuda.Stream(device) for _ in range(ns - 1)]
+        streams = [main] + (side[:ns - 1] if ns > 1 else [])
+        losses_v = torch.empty(max(1, len(views)), dtype=torch.float32, device=device)
+        acc = [tuple(torch.empty_like(t) for t in (m, s, c, o)) for _ in streams]
+        for st in streams[1:]:
+            st.wait_stream(main)
+        w_sil = self.w_sil if (self.masks is not None and self.w_sil > 0.0) else 0.0
+        g_scale = 1.0 / len(self.targets)
+        prep = getattr(self, "_prep", None)
+        if prep is None or prep.device != device:
+            self._prep = prep = torch.cuda.Stream(device)
+        prep.wait_stream(main)
+        pins = self._plan_pins(len(views))
+        cache = getattr(self, "_gvd_cache", None)
+        if cache is None:
+            self._gvd_cache = cache = {}
+        ahead: dict = {}
+
+        def gv_of(i):
+            if i not in cache:
+                cam = self.cams[i]
+                cache[i] = tr.make_view(cam.view, cam.proj, self.width, self.height, self._background(device),
+                                        depth_grad=True)
+            return cache[i]
+
+        def prepare(j):
+            if j < len(views) and j not in ahead:
+                with torch.cuda.stream(prep):
+                    ahead[j] = tr.prepare_native(m, s, c, o, gv_of(views[j]), plan_host=pins[j])
+
+        for j in range(PREP_AHEAD):
+            prepare(j)
+        for j, i in enumerate(views):
+            k = j % ns
+            prepare(j + PREP_AHEAD)
+            pv = ahead.pop(j)
+            streams[k].wait_event(pv.event)
+            pv.geom.record_stream(streams[k])
+            with torch.cuda.stream(streams[k]):
+                _, _, _, rs = tr.forward_native(m, s, c, o, pv.gv, pv)
+                pv = None
+                tr.backward_fit_native(m, s, c, o, rs, self.targets[i], self.masks[i] if w_sil > 0.0 else None, w_sil,
+                                       self.depths[i], self.w_depth, g_scale, losses_v[j:j + 1], acc[k], accumulate=j >= ns)
         for st in streams[1:]:
             main.wait_stream(st)
         main.wait_stream(prep)

@@ -321,6 +321,24 @@ def backward_l1_native(means, scales, colors, opacities, st: RenderState, target
                               _native.ptr(ws), ws.numel(), _stream(dev)), "gr_bwd_l1")
 
 
+def backward_fit_native(means, scales, colors, opacities, st: RenderState, target, mask, w_sil: float, depth_target,
+                        w_depth: float, g_scale: float, loss_out, grads, accumulate: bool) -> None:
+    """gr_bwd_fit on the current stream: as ``backward_l1_native`` with the fit loop's depth term
+    ``w_depth mean|depth / (max(depth) + 1e-6) - depth_target|`` (the view rendered with depth_grad=True)."""
+    L = _native.lib()
+    dev = means.device
+    ws = torch.empty((_ws_round(L.gr_bwd_bytes(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan))),), dtype=torch.uint8,
+                     device=dev)
+    dm, ds, dc, do = grads
+    _native.check(L.gr_bwd_fit(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan), _native.ptr(means), _native.ptr(scales),
+                               _native.ptr(colors), _color_dim(colors), _native.ptr(opacities), _native.ptr(st.geom),
+                               _native.ptr(st.bins), _native.ptr(st.saved), _native.ptr(target), _native.ptr(mask),
+                               ctypes.c_float(w_sil), _native.ptr(depth_target), ctypes.c_float(w_depth),
+                               ctypes.c_float(g_scale), _native.ptr(loss_out), _native.ptr(dm), _native.ptr(ds),
+                               _native.ptr(dc), _native.ptr(do), 1 if accumulate else 0, _native.ptr(ws), ws.numel(),
+                               _stream(dev)), "gr_bwd_fit")
+
+
 def forward_l1_native(means, scales, colors, opacities, gv: _native.GrView, prepared: Prepared, target, mask,
                       w_sil: float, g_scale: float, loss_out):
     """gr_fwd_render_l1 on the current stream (the fused fit path; gv with no_depth_grad, no depth output):
@@ -502,5 +520,5 @@ def render_gaussians_torch(
 
 __all__ = ["Camera", "get_default_device", "perspective", "look_at", "render_gaussians_torch", "rasterize",
            "make_view", "prepare_view", "prepare_native", "Prepared", "forward_native", "backward_native",
-           "backward_l1_native", "forward_l1_native", "backward_splat_native", "reduce_views_native",
+           "backward_l1_native", "backward_fit_native", "forward_l1_native", "backward_splat_native", "reduce_views_native",
            "DEFAULT_CUTOFF", "DEPTH_GRAD_CUTOFF", "DEFAULT_CORE_CUTOFF", "FIT_CUTOFF", "default_cutoff"]

@@ -160,6 +160,19 @@ gr_status gr_bwd_l1(const gr_view* v, int n, const gr_plan* plan, const float* m
                     float* d_means, float* d_scales, float* d_colors, float* d_opacities,
                     int accumulate, void* ws, size_t ws_bytes, void* stream);
 
+/* gr_bwd_l1 with the fit loop's depth term as well (fit_multiview_stub.py:301-305):
+ *   loss = mean|out - target_rgb| + w_sil mean|alpha - target_mask|
+ *          + w_depth mean|depth / (max(depth) + 1e-6) - target_depth|   (target_depth may be NULL)
+ * with torch's gradients of that expression (abs' = sign, max's gradient shared evenly among the
+ * arg-max pixels); the view must be rendered with no_depth_grad = 0 and its depth output.
+ * gr_bwd_l1 = gr_bwd_fit with target_depth = NULL.  Same workspace as gr_bwd. */
+gr_status gr_bwd_fit(const gr_view* v, int n, const gr_plan* plan, const float* means,
+                     const float* scales, const float* colors, int color_dim, const float* opacities,
+                     const void* geom, const void* bins, const float* saved, const float* target_rgb,
+                     const float* target_mask, float w_sil, const float* target_depth, float w_depth,
+                     float g_scale, float* loss_out, float* d_means, float* d_scales, float* d_colors,
+                     float* d_opacities, int accumulate, void* ws, size_t ws_bytes, void* stream);
+
 /* The fused fit path in three calls (fit_multiview.py; views rendered with no_depth_grad = 1):
  *   gr_fwd_render_l1  gr_fwd_render without depth output, whose epilogue also evaluates the fit
  *                     loop's view loss (as gr_bwd_l1) from the pixel sums: the view loss goes to

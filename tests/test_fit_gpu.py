@@ -171,3 +171,45 @@ def test_batched_reduce_matches_per_view_reduce(cuda):
     _, g8b = one_step(8)
     for k in g8:
         assert torch.equal(g8[k], g8b[k]), k
+
+
+@pytest.mark.parametrize("sh", [False, True])
+def test_direct_depth_path_matches_autograd_path(cuda, sh):
+    """The fused path with the depth term (gr_bwd_fit: L1 + silhouette + depth loss
+    w_depth mean|depth / (max depth + 1e-6) - t| and the render backward, gradients accumulated per stream)
+    gives the loss and gradients of the autograd path (torch ops for the loss, gr_bwd, autograd sums)."""
+    import torch
+
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    bench = importlib.import_module("bench")
+    W, H = 96, 80
+    cams = fm.orbit_cameras(5, W, H, cuda)
+    g = torch.Generator(device=cuda).manual_seed(7)
+    targets = [torch.rand((H, W, 3), generator=g, device=cuda) for _ in cams]
+    masks = [(t.mean(dim=2) > 0.5).float() for t in targets]
+    depths = [torch.rand((H, W), generator=g, device=cuda) for _ in cams]
+
+    def one_step(direct):
+        saved = fm.DIRECT_BACKWARD
+        fm.DIRECT_BACKWARD = direct
+        try:
+            params = bench.synthetic_params(8000, cuda)
+            if sh:
+                shc = torch.zeros((8000, 16, 3), device=cuda)
+                shc[:, 0, :] = torch.sigmoid(params.pop("colors_raw").detach())
+                gs = torch.Generator(device=cuda).manual_seed(5)
+                shc[:, 1:, :] = 0.03 * torch.randn((8000, 15, 3), generator=gs, device=cuda)
+                params["sh_raw"] = torch.nn.Parameter(shc)
+            f = fm.ViewShardedFitter(params, cams, targets, W, H, masks=masks, depths=depths)
+            loss = float(f.step())
+            grads = {k: v.grad.detach().clone() for k, v in f.params.items()}
+        finally:
+            fm.DIRECT_BACKWARD = saved
+        return loss, grads
+
+    la, ga = one_step(False)
+    ld, gd = one_step(True)
+    assert abs(la - ld) <= 2e-6 * abs(la)
+    for k in ga:
+        err = float((gd[k] - ga[k]).norm() / ga[k].norm())
+        assert err <= 1e-5, (k, err)

@@ -11,8 +11,8 @@ import glob
 import json
 import sys
 
-KERNELS = ("k_raster_bwd_bf16", "k_raster_bwd_mfma", "k_raster_fwd_mfma", "k_reduce_bwd", "k_emit_zones", "k_tile_place",
-           "k_pixel_grads", "k_fwd_finalize", "k_preprocess")
+KERNELS = ("k_raster_bwd_bf16", "k_raster_bwd_mfma", "k_raster_fwd_mfma", "k_reduce_bwd", "k_reduce_views", "k_emit_zones",
+           "k_tile_place", "k_tile_count", "k_tile_colscan", "k_pixel_grads", "k_fwd_finalize", "k_preprocess")
 
 
 def per_launch(d, counter):
