@@ -1793,11 +1793,27 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
       const float z = DEPTH ? sZ[buf][j] : 0.0f;
       const int myslot = j < nb ? base + j : -1;  // the pair's sorted position = its partial-sum row
       float ex[8], ey[8];
+      if constexpr (!DEPTH && PIECES == 2) {
+        // the lane's 8 pixel slots sit at constant offsets o_q from its first pixel centre, so the exponent
+        // q (d0 + o_q)^2 = q d0^2 + 2 o_q (q d0) + o_q^2 q is two fmas with constant coefficients per slot
+        // (instead of a subtraction and two products); rounding ~|q| o_q^2 ulp, well inside the two-piece
+        // mode's 2^-16 (padding: q d0^2 = -inf, still exactly 0)
+        const float d0x = pxb - a.x, d0y = pyb - a.y;
+        const float tx = a.z * d0x, ty = a.w * d0y;
+        const float cx = tx * d0x, cy = ty * d0y;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float dx = PX0(q) - a.x, dy = PY0(q) - a.y;
-        ex[q] = __builtin_amdgcn_exp2f(dx * a.z * dx);  // exactly 0 for padding
-        ey[q] = __builtin_amdgcn_exp2f(dy * a.w * dy);
+        for (int q = 0; q < 8; ++q) {
+          const float oq = (float)(q < 4 ? q : q + 4);
+          ex[q] = __builtin_amdgcn_exp2f(q == 0 ? cx : fmaf(tx, 2.0f * oq, fmaf(a.z, oq * oq, cx)));
+          ey[q] = __builtin_amdgcn_exp2f(q == 0 ? cy : fmaf(ty, 2.0f * oq, fmaf(a.w, oq * oq, cy)));
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float dx = PX0(q) - a.x, dy = PY0(q) - a.y;
+          ex[q] = __builtin_amdgcn_exp2f(dx * a.z * dx);  // exactly 0 for padding
+          ey[q] = __builtin_amdgcn_exp2f(dy * a.w * dy);
+        }
       }
       // both contractions are issued before either epilogue, so the T epilogue's VALU work runs while
       // the R MFMAs execute
@@ -1819,7 +1835,8 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
 #pragma unroll
         for (int pr = P0; pr < P1; ++pr) DR[pr] = mfma_split2(sUF + (1 * 3 + pr) * 3 * 64, lane, BR);
       }
-      float S[NPART] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      // -0 starts: -0 + x == x for every x, so the first accumulation folds into a plain product
+      float S[NPART] = {-0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f};
       {
       if constexpr (!DEPTH && PIECES == 2) {
         // Moments about the lane's first pixel centre: dy_q = d0 + o_q with o_q = kslot offset (a compile-
@@ -1827,7 +1844,7 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
         // sum t o_q^2: two constant-coefficient fmas per pixel instead of a subtraction, two products and
         // two sums (the same for dx).  Cancellation is bounded by the tile's 16 px (two-piece mode only).
         const float d0y = pyb - a.y, d0x = pxb - a.x;
-        float S6c = 0.f, S8c = 0.f, U0 = 0.f, S5c = 0.f, S7c = 0.f;
+        float S6c = -0.f, S8c = -0.f, U0 = -0.f, S5c = -0.f, S7c = -0.f;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const float oq = (float)(q < 4 ? q : q + 4);
@@ -1837,12 +1854,16 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
           S[2] = fmaf(ey[q], T2, S[2]);
           const float t = ey[q] * fmaf(b.w, T2, fmaf(b.z, T1, fmaf(b.y, T0, T3)));
           S[4] += t;
-          S6c = fmaf(t, oq, S6c);
-          S8c = fmaf(t, oq * oq, S8c);
+          if (q != 0) {  // slot 0 is the origin of the moments
+            S6c = fmaf(t, oq, S6c);
+            S8c = fmaf(t, oq * oq, S8c);
+          }
           const float u = ex[q] * fmaf(b.w, DR[1][q], fmaf(b.z, DR[0][8 + q], fmaf(b.y, DR[0][q], DR[1][8 + q])));
           U0 += u;
-          S5c = fmaf(u, oq, S5c);
-          S7c = fmaf(u, oq * oq, S7c);
+          if (q != 0) {
+            S5c = fmaf(u, oq, S5c);
+            S7c = fmaf(u, oq * oq, S7c);
+          }
         }
         S[6] = fmaf(d0y, S[4], S6c);
         S[8] = fmaf(d0y * d0y, S[4], fmaf(2.0f * d0y, S6c, S8c));
