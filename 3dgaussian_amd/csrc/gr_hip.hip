@@ -1591,13 +1591,15 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
 // of a k_pixel_grads pass over saved sums.  `lds` holds >= 4 x TP free floats; every thread of the block
 // calls this (two barriers).
 __device__ __forceinline__ void l1_tile_epilogue(const ViewK& v, int tile, int tid, const float (&acc)[5], bool inside,
-                                                 int p, const L1Args& l1, uint4* __restrict__ UF, float* lds) {
+                                                 int p, const L1Args& l1, uint4* __restrict__ UF, float* lds,
+                                                 bool fragments = true) {
   float u[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   float l_rgb = 0.f, l_sil = 0.f;
   if (inside)
     pixel_upstream(v, p, make_float4(acc[0], acc[1], acc[2], acc[3]), acc[4], nullptr, nullptr, nullptr, l1, u, l_rgb,
                    l_sil);
   tile_loss_sums(tile, tid, l_rgb, l_sil, l1.tile_loss);  // its barrier also ends every read of lds
+  if (!fragments) return;  // uniform per block
   float (*sU)[TP] = reinterpret_cast<float (*)[TP]>(lds);
 #pragma unroll
   for (int k = 0; k < 4; ++k) sU[k][tid] = u[k];
@@ -1689,7 +1691,8 @@ __global__ __launch_bounds__(256) void k_fwd_finalize(ViewK v, const int2* __res
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
   const bool inside = x < v.W && y < v.H;
   if (inside) write_pixel(v, y * v.W + x, acc, out_rgb, out_alpha, out_depth, saved4, savedD);
-  if (l1.t_rgb) l1_tile_epilogue(v, tile, tid, acc, inside, y * v.W + x, l1, UF, lds);
+  // an empty tile has no backward work item: only its loss terms are needed, not its fragments
+  if (l1.t_rgb) l1_tile_epilogue(v, tile, tid, acc, inside, y * v.W + x, l1, UF, lds, nch > 0);
 }
 
 // Sum over the 4 lane rows (lanes l, l+16, l+32, l+48) of a pair of values with one
