@@ -102,6 +102,11 @@ _SIG = {
     "gr_bwd_fit": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P,
                                   ctypes.c_float, _P, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, ctypes.c_int, _P,
                                   ctypes.c_size_t, _P]),
+    "gr_fit_param_step": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, _P, _P, _P, _P, _P, ctypes.c_float, ctypes.c_int, _P,
+                                         _P, ctypes.c_float, ctypes.c_float, ctypes.c_double, ctypes.c_double, ctypes.c_float,
+                                         _P]),
+    "gr_adam_step": (ctypes.c_int, [ctypes.c_int64, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float, ctypes.c_double,
+                                    ctypes.c_double, ctypes.c_float, _P]),
     "gr_fwd_render_l1": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P, _P,
                                         ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, ctypes.c_size_t, _P]),
     "gr_bwd_splat": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_size_t, _P]),

@@ -2645,6 +2645,60 @@ __global__ __launch_bounds__(256) void k_l1_grad(const float* __restrict__ a, co
   }
 }
 
+// The fit loop's parameter update (fit_multiview_stub.py:268-275 activations, :307-308 regulariser,
+// :311 Adam) for one parameter tensor, fused into one pass over its elements (gr_fit_param_step):
+//   g_raw = act'(raw) * ((acc0 + acc1) + acc2 + reg)      d loss / d raw parameter (torch's backward of
+//                                                         softplus(x) + 1e-3 / sigmoid / identity)
+//   then, with Adam, torch.optim.Adam's foreach update in its own operation order:
+//   m = m + (1 - b1)(g - m); v = v b2 + ((1 - b2) g) g; p = p + step_size m / (sqrt(v) / bc2_sqrt + eps).
+// act: 0 identity, 1 softplus (threshold 20, as torch), 2 sigmoid.
+__global__ __launch_bounds__(256) void k_fit_param_step(int64_t count, int act, float* __restrict__ p,
+                                                        float* __restrict__ grad, const float* __restrict__ acc0,
+                                                        const float* __restrict__ acc1, const float* __restrict__ acc2,
+                                                        float reg, int adam, float* __restrict__ m, float* __restrict__ v,
+                                                        float neg_step, float bc2_sqrt, float b1, float b2, float b2_c,
+                                                        float eps) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < count; e += (int64_t)gridDim.x * 256) {
+    float gact = acc0 ? acc0[e] : 0.0f;
+    if (acc1) gact = gact + acc1[e];
+    if (acc2) gact = gact + acc2[e];
+    gact = gact + reg;
+    const float x = p[e];
+    float g;
+    if (act == 1) {  // softplus backward: g z / (z + 1), z = exp(x) (x <= 20), else g
+      const float z = expf(x);
+      g = x > 20.0f ? gact : gact * z / (z + 1.0f);
+    } else if (act == 2) {  // sigmoid backward: g (1 - y) y
+      const float y = 1.0f / (1.0f + expf(-x));
+      g = gact * (1.0f - y) * y;
+    } else {
+      g = gact;
+    }
+    if (grad) grad[e] = g;
+    if (adam) {  // b1 here is 1 - beta1 and b2 is (beta2, 1 - beta2) rounded from double on the host, as torch's scalars
+      const float mm = fmaf(b1, g - m[e], m[e]);
+      const float vv = fmaf(b2_c, g * g, v[e] * b2);
+      m[e] = mm;
+      v[e] = vv;
+      p[e] = fmaf(neg_step, mm / (sqrtf(vv) / bc2_sqrt + eps), x);
+    }
+  }
+}
+
+// Adam alone on an assembled (e.g. all-reduced) gradient.
+__global__ __launch_bounds__(256) void k_adam_step(int64_t count, float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, float neg_step,
+                                                   float bc2_sqrt, float b1, float b2, float b2_c, float eps) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < count; e += (int64_t)gridDim.x * 256) {
+    const float ge = g[e];
+    const float mm = fmaf(b1, ge - m[e], m[e]);
+    const float vv = fmaf(b2_c, ge * ge, v[e] * b2);
+    m[e] = mm;
+    v[e] = vv;
+    p[e] = fmaf(neg_step, mm / (sqrtf(vv) / bc2_sqrt + eps), p[e]);
+  }
+}
+
 // Optional per-kernel timing with HIP events on the launch stream (gr_profile_begin/end), used by
 // bench.py to time the dominant kernels live.  Off by default; host-side state only.
 enum { PROF_RASTER_FWD = 0, PROF_RASTER_BWD = 1, PROF_REDUCE = 2, PROF_BINNING = 3, PROF_SLOTS = 4 };
@@ -3389,6 +3443,33 @@ gr_status gr_l1_loss_fwd(const float* a, const float* b, int64_t n1, const float
   hipLaunchKernelGGL(k_l1_partial, dim3(LOSS_BLOCKS, 2), dim3(256), 0, s, a, b, n1, c, d, n2, (float*)ws);
   GR_HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_l1_final, dim3(1), dim3(256), 0, s, (const float*)ws, n1, n2, w2, loss);
+  GR_HIP_TRY(hipGetLastError());
+  return GR_OK;
+}
+
+gr_status gr_fit_param_step(int64_t count, int act, float* param, float* grad, const float* acc0, const float* acc1,
+                            const float* acc2, float reg, int adam, float* exp_avg, float* exp_avg_sq, float neg_step_size,
+                            float bias_correction2_sqrt, double beta1, double beta2, float eps, void* stream) {
+  if (count < 0 || act < 0 || act > 2 || !param || (adam && (!exp_avg || !exp_avg_sq)) || (!adam && !grad))
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_param_step: bad arguments");
+  if (count == 0) return GR_OK;
+  const int blocks = (int)std::min<int64_t>((count + 255) / 256, 4096);
+  // torch.optim.Adam passes 1 - beta1 (lerp weight) and 1 - beta2 (addcmul value) as Python floats (double)
+  const float w1 = (float)(1.0 - beta1), w2 = (float)(1.0 - beta2);
+  hipLaunchKernelGGL(k_fit_param_step, dim3(blocks), dim3(256), 0, (hipStream_t)stream, count, act, param, grad, acc0, acc1,
+                     acc2, reg, adam, exp_avg, exp_avg_sq, neg_step_size, bias_correction2_sqrt, w1, (float)beta2, w2, eps);
+  GR_HIP_TRY(hipGetLastError());
+  return GR_OK;
+}
+
+gr_status gr_adam_step(int64_t count, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                       float neg_step_size, float bias_correction2_sqrt, double beta1, double beta2, float eps, void* stream) {
+  if (count < 0 || !param || !grad || !exp_avg || !exp_avg_sq) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_adam_step: bad arguments");
+  if (count == 0) return GR_OK;
+  const int blocks = (int)std::min<int64_t>((count + 255) / 256, 4096);
+  const float w1 = (float)(1.0 - beta1), w2 = (float)(1.0 - beta2);
+  hipLaunchKernelGGL(k_adam_step, dim3(blocks), dim3(256), 0, (hipStream_t)stream, count, param, grad, exp_avg, exp_avg_sq,
+                     neg_step_size, bias_correction2_sqrt, w1, (float)beta2, w2, eps);
   GR_HIP_TRY(hipGetLastError());
   return GR_OK;
 }

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import argparse
 import contextlib
+import ctypes
 import math
 import os
 import sys
@@ -43,6 +44,10 @@ else:
     from . import torch_renderer as tr
 
 RenderFn = Callable[..., tuple]
+
+
+def ctypes_stream(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 DEVICE_DENSIFY_MIN = 100_000  # Gaussians from which densify/prune runs on the device (C5 scale)
 FUSED_LOSS = os.environ.get("GR_FUSED_LOSS", "1") != "0"  # losses.l1_loss for the L1 terms (A/B switch)
 NUM_STREAMS = max(1, int(os.environ.get("GR_STREAMS", "3")))  # HIP streams the views rotate over
@@ -57,6 +62,9 @@ DIRECT_BACKWARD = os.environ.get("GR_DIRECT", "1") != "0"
 # read and the stream's gradient accumulator read and written once per batch instead of once per view
 # (at most REDUCE_BATCH views per batch, a stream's views split into equal batches)
 REDUCE_BATCH = max(1, min(16, int(os.environ.get("GR_REDUCE_BATCH", "16"))))
+# fused path: gradient assembly through the activations and the Adam update in one HIP pass per parameter
+# (gr_fit_param_step) instead of torch's autograd + foreach Adam (0 = torch)
+FUSED_STEP = os.environ.get("GR_FUSED_STEP", "1") != "0"
 # fused path: views prepared ahead of the one being rendered (on the preparation stream)
 PREP_AHEAD = max(1, int(os.environ.get("GR_PREP_AHEAD", "6")))
 
@@ -348,13 +356,32 @@ class ViewShardedFitter:
             self.respatialize()
         self.steps_done += 1
         self.opt.zero_grad(set_to_none=True)
+        device = self.params["means"].device
+        if self._direct(device) and self.params["means"].shape[0] > 0 and self._fused_step_ok():
+            with torch.no_grad():
+                means, scales, colors, opacities = activations(self.params)
+                if self._depth_grad():
+                    total = self._views_direct_depth(means, scales, colors, opacities)
+                else:
+                    total = self._views_direct(means, scales, colors, opacities)
+                loss = total / len(self.targets)
+                if self.rank == 0:
+                    loss = loss + (self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean())
+            return self._fused_param_step(scales, opacities, loss)
         means, scales, colors, opacities = activations(self.params)
-        device = means.device
         if self._direct(device) and means.shape[0] > 0:
             if self._depth_grad():
                 total = self._views_direct_depth(means, scales, colors, opacities)
             else:
                 total = self._views_direct(means, scales, colors, opacities)
+            parts = self._acc_parts
+            acc = []
+            for q in range(4):  # in stream order
+                t = parts[0][q]
+                for pp in parts[1:]:
+                    t = t + pp[q]
+                acc.append(t)
+            self._acc = tuple(acc)
             loss = total / len(self.targets)
             if self.rank == 0:
                 reg = self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean()
@@ -504,13 +531,8 @@ class ViewShardedFitter:
             main.wait_stream(st)
         main.wait_stream(prep)
         used = min(ns, len(views))
-        out = []
-        for q in range(4):
-            t = acc[0][q]
-            for k in range(1, used):
-                t = t + acc[k][q]
-            out.append(t if used > 0 else torch.zeros_like(acc[0][q]))
-        self._acc = tuple(out)
+        # the streams' accumulators (summed in stream order by the caller: gr_fit_param_step or torch adds)
+        self._acc_parts = acc[:used] if used > 0 else [tuple(torch.zeros_like(t) for t in (m, s, c, o))]
         return losses_v[:len(views)].sum() if views else torch.zeros((), device=device)
 
     def _views_direct_depth(self, means, scales, colors, opacities) -> torch.Tensor:
@@ -572,14 +594,80 @@ class ViewShardedFitter:
             main.wait_stream(st)
         main.wait_stream(prep)
         used = min(ns, len(views))
-        out = []
-        for q in range(4):
-            t = acc[0][q]
-            for k in range(1, used):
-                t = t + acc[k][q]
-            out.append(t if used > 0 else torch.zeros_like(acc[0][q]))
-        self._acc = tuple(out)
+        # the streams' accumulators (summed in stream order by the caller: gr_fit_param_step or torch adds)
+        self._acc_parts = acc[:used] if used > 0 else [tuple(torch.zeros_like(t) for t in (m, s, c, o))]
         return losses_v[:len(views)].sum() if views else torch.zeros((), device=device)
+
+    def _fused_step_ok(self) -> bool:
+        """The fused parameter update applies: plain Adam (torch.optim.Adam defaults: no weight decay, no
+        amsgrad, not maximize), one parameter group, the stub's parameter names, float32 on the device."""
+        if not FUSED_STEP or type(self.opt) is not torch.optim.Adam or len(self.opt.param_groups) != 1:
+            return False
+        g = self.opt.param_groups[0]
+        if g["weight_decay"] != 0 or g["amsgrad"] or g.get("maximize", False) or isinstance(g["lr"], torch.Tensor):
+            return False
+        return set(self.params) in ({"means", "scales_raw", "opacities_raw", "colors_raw"},
+                                    {"means", "scales_raw", "opacities_raw", "sh_raw"})
+
+    def _fused_param_step(self, scales, opacities, loss) -> torch.Tensor:
+        """fit_multiview_stub.py:307-311 after the views: d loss / d raw parameters through the activations
+        (softplus + 1e-3, sigmoid, identity) and the regulariser (rank 0), then torch.optim.Adam's update with
+        its own state tensors, one gr_fit_param_step pass per parameter (world size 1), or gradient assembly
+        into the flat all-reduce buffer, the all-reduce, then gr_adam_step per parameter."""
+        L = tr._native.lib()
+        g = self.opt.param_groups[0]
+        lr, (b1, b2), eps = float(g["lr"]), g["betas"], float(g["eps"])
+        parts = self._acc_parts
+        self._acc_parts = None
+        slot = {"means": 0, "scales_raw": 1, "colors_raw": 2, "sh_raw": 2, "opacities_raw": 3}
+        act = {"means": 0, "scales_raw": 1, "colors_raw": 2, "sh_raw": 0, "opacities_raw": 2}
+        # mean()'s backward: the float32 weight divided by the float32 element count, as autograd computes it
+        reg = {"scales_raw": float(np.float32(self.reg_scale) / np.float32(max(1, scales.numel()))),
+               "opacities_raw": float(np.float32(self.reg_opacity) / np.float32(max(1, opacities.numel())))}
+        names = list(self.params)
+        plist = [self.params[k] for k in names]
+        stream = ctypes_stream(plist[0].device)
+        flat = None
+        if self.world > 1:
+            flat = torch.empty(sum(p.numel() for p in plist) + 1, dtype=torch.float32, device=plist[0].device)
+        off = 0
+        steps = []
+        for k, p in zip(names, plist):
+            st = self.opt.state[p]
+            if not st:  # torch.optim.Adam's lazy state, same tensors and layout
+                st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["step"] += 1
+            t = float(st["step"])
+            neg_step = -(lr / (1.0 - b1 ** t))
+            bc2s = (1.0 - b2 ** t) ** 0.5
+            steps.append((neg_step, bc2s))
+            a = [pp[slot[k]] for pp in parts] + [None, None, None]
+            if flat is not None:
+                grad = flat[off:off + p.numel()].view_as(p)
+                off += p.numel()
+            else:
+                grad = torch.empty_like(p)
+            p.grad = grad
+            r = reg.get(k, 0.0) if self.rank == 0 else 0.0
+            tr._native.check(L.gr_fit_param_step(p.numel(), act[k], tr._native.ptr(p.data), tr._native.ptr(grad),
+                                                 tr._native.ptr(a[0]), tr._native.ptr(a[1]), tr._native.ptr(a[2]),
+                                                 ctypes.c_float(r), 0 if flat is not None else 1,
+                                                 tr._native.ptr(st["exp_avg"]), tr._native.ptr(st["exp_avg_sq"]),
+                                                 ctypes.c_float(neg_step), ctypes.c_float(bc2s), ctypes.c_double(b1),
+                                                 ctypes.c_double(b2), ctypes.c_float(eps), stream), "gr_fit_param_step")
+        if flat is None:
+            return loss.detach()
+        flat[off:off + 1].copy_(loss.detach().reshape(1))
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        for (k, p), (neg_step, bc2s) in zip(zip(names, plist), steps):
+            st = self.opt.state[p]
+            tr._native.check(L.gr_adam_step(p.numel(), tr._native.ptr(p.data), tr._native.ptr(p.grad),
+                                            tr._native.ptr(st["exp_avg"]), tr._native.ptr(st["exp_avg_sq"]),
+                                            ctypes.c_float(neg_step), ctypes.c_float(bc2s), ctypes.c_double(b1),
+                                            ctypes.c_double(b2), ctypes.c_float(eps), stream), "gr_adam_step")
+        return flat[off]
 
     def _finish_step(self, loss) -> torch.Tensor:
         plist = list(self.params.values())

@@ -234,6 +234,24 @@ gr_status gr_l1_loss_bwd(const float* a, const float* b, int64_t n1, const float
                          void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
+/* Fit-loop parameter update, the caller's side of the render op (fit_multiview_stub.py:268-275   */
+/* activations, :307-308 regulariser, :311 torch.optim.Adam), one pass per parameter tensor:    */
+/*   grad = act'(param) * ((acc0 + acc1) + acc2 + reg)   (acc1/acc2 may be NULL; act 0 identity,  */
+/*          1 softplus(x) + 1e-3, 2 sigmoid: torch's backward formulas);                          */
+/*   adam != 0: exp_avg / exp_avg_sq / param updated as Adam's foreach step with                 */
+/*   neg_step_size = -lr / (1 - beta1^t), bias_correction2_sqrt = sqrt(1 - beta2^t); the betas are */
+/*   doubles so 1 - beta rounds to float as torch's Python-float scalars do.                     */
+/* gr_adam_step: the Adam update alone on an assembled gradient (after an all-reduce).           */
+/* ------------------------------------------------------------------------------------------ */
+gr_status gr_fit_param_step(int64_t count, int act, float* param, float* grad, const float* acc0,
+                            const float* acc1, const float* acc2, float reg, int adam, float* exp_avg,
+                            float* exp_avg_sq, float neg_step_size, float bias_correction2_sqrt,
+                            double beta1, double beta2, float eps, void* stream);
+gr_status gr_adam_step(int64_t count, float* param, const float* grad, float* exp_avg,
+                       float* exp_avg_sq, float neg_step_size, float bias_correction2_sqrt,
+                       double beta1, double beta2, float eps, void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
 /* Introspection (host-only, no GPU needed).                                                  */
 /* ------------------------------------------------------------------------------------------ */
 
