@@ -18,7 +18,7 @@ Also reported on rank 0:
                 (48 B per pair forward, 84 B per core pair backward, + 40 B per pixel) x the units of one
                 launch / its average launch time (HIP events on its launch stream, gr_profile_begin/end,
                 over one single-stream step after the timed region: the timed steps overlap views on 3
-                streams), vs 8 TB/s; its PMC HBM traffic from profiles/pmc_traffic.json
+                streams and run uninstrumented), vs 8 TB/s; its PMC HBM traffic from profiles/pmc_traffic.json
                 (tools/pmc_traffic.py); the executed bf16 MFMA rate beside it
   hbm_model     the north_star's framing: SURVEY.md 8(d)'s byte model of the tile-binned path per view at
                 this run's pair count (the fit path bins the survey's 5-sigma footprint), the bench value
@@ -225,10 +225,9 @@ def main():
 
     for _ in range(args.warmup):
         fitter.step()
-    if on_gpu:
-        pkg._native.profile_begin()
+    # the timed region runs uninstrumented: HIP event marks around every splat launch cost ~1.5% of the
+    # step (a marker packet per mark on each stream); the launch timings come from the profiled steps below
     elapsed, loss = timed(args.steps)
-    prof_concurrent = pkg._native.profile_end() if on_gpu else None
     pixels = V * R * R * args.steps
     value = pixels / elapsed / 1e6
 
@@ -243,9 +242,15 @@ def main():
             dist.destroy_process_group()
         return
 
-    # Roofline pass: the timed steps rotate views over several HIP streams, so a launch's duration
-    # there includes kernels of other views running beside it.  One more step on a single stream gives
-    # each launch its own duration (with GR_STREAMS=1 the whole run is single-stream and both agree).
+    # One profiled step as the timed ones (views rotating over several HIP streams): a launch's duration
+    # there includes the kernels of other views running beside it.
+    sync()
+    pkg._native.profile_begin()
+    fitter.step()
+    sync()
+    prof_concurrent = pkg._native.profile_end()
+    # Roofline pass: one more step on a single stream gives each launch its own duration (with
+    # GR_STREAMS=1 the whole run is single-stream and both agree).
     streams_saved = fm.NUM_STREAMS
     fm.NUM_STREAMS = 1
     sync()
@@ -313,7 +318,7 @@ def main():
                     "bytes_model": f"{e['unit_bytes']} B x {e['units_desc']} ({int(e['units'])}) + {e['px_bytes']} B x {px} px",
                     "avg_launch_us": round(e["t"] * 1e6, 1), "launches": e["n"],
                     "timing": "HIP events on the launch stream, one single-stream step after the timed region",
-                    "avg_launch_us_in_timed_region": round(e["conc_us"], 1), "streams_in_timed_region": streams_saved,
+                    "avg_launch_us_multi_stream": round(e["conc_us"], 1), "streams_in_timed_region": streams_saved,
                     "mfma": {"executed_bf16_tflops": round(mf, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
                              "frac": round(mf / BF16_MFMA_PEAK_TFLOPS, 4),
                              "f32_equivalent_tflops": round(e["f32"] / e["t"] / 1e12, 1), "f32_peak": F32_MFMA_PEAK_TFLOPS}}

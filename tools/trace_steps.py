@@ -7,7 +7,7 @@ from collections import defaultdict
 
 f = sorted(glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True))[0]
 rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Stream_Id"]) for r in csv.DictReader(open(f)))
-adam = [k for k, r in enumerate(rows) if "multi_tensor_apply" in r[2]]
+adam = [k for k, r in enumerate(rows) if any(m in r[2] for m in ("multi_tensor_apply", "k_fit_param_step", "k_adam_step"))]
 ends = [k for k, nxt in zip(adam, adam[1:] + [None]) if nxt is None or nxt != k + 1]
 lo, hi = ends[-3] + 1, ends[-2] + 1
 rows = rows[lo:hi]
