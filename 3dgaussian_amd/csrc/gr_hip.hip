@@ -2847,7 +2847,8 @@ __device__ __forceinline__ unsigned long long block_exclusive_scan(unsigned long
 // words cannot carry into each other as long as K < 2^31, which is checked against the exact total
 // (the sum of every block's two words) before the plan is trusted.
 __global__ __launch_bounds__(1024) void k_plan(unsigned long long* __restrict__ bsum, int blocks,
-                                               unsigned long long* __restrict__ off_end, gr_plan* plan) {
+                                               unsigned long long* __restrict__ off_end, gr_plan* plan,
+                                               gr_plan* host_plan) {
   __shared__ unsigned long long sh[16];
   const int tid = (int)threadIdx.x, per = (blocks + 1023) / 1024;
   const int b0 = min(blocks, tid * per), b1 = min(blocks, b0 + per);
@@ -2872,6 +2873,12 @@ __global__ __launch_bounds__(1024) void k_plan(unsigned long long* __restrict__ 
   plan->num_pairs = ok ? (long long)exact : -1;
   plan->num_slots = ok ? (long long)exact : -1;  // one partial-sum slot per pair
   plan->num_core_pairs = ok ? (long long)(grand & 0xffffffffull) : -1;
+  if (host_plan) {  // pinned host memory (gr_fwd_prepare_async): no copy command behind the scan
+    host_plan->num_pairs = plan->num_pairs;
+    host_plan->num_slots = plan->num_slots;
+    host_plan->num_core_pairs = plan->num_core_pairs;
+    __threadfence_system();
+  }
 }
 
 // Gaussian level of the offsets scan: offsets[i] = its block's offset + the exclusive scan of the packed
@@ -2913,13 +2920,19 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
   else
     hipLaunchKernelGGL(k_preprocess<48>, dim3(blocks_for(n + 1)), dim3(256), 0, s, vk, n, means, scales, colors, opacities, g);
   GR_HIP_TRY(hipGetLastError());
+  // a plan in pinned (device-mapped) host memory is written by k_plan itself; pageable memory gets a copy
+  gr_plan* mapped = nullptr;
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, plan) == hipSuccess && attr.type == hipMemoryTypeHost && attr.devicePointer)
+    mapped = (gr_plan*)attr.devicePointer;
+  (void)hipGetLastError();  // a pageable pointer leaves an error code behind
   // exclusive scan of the packed counts: blocks (k_plan), then Gaussians (k_offsets)
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, g.total, blocks_for(n + 1), g.offsets + n, g.plan);
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, g.total, blocks_for(n + 1), g.offsets + n, g.plan, mapped);
   GR_HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_offsets, dim3(blocks_for(n)), dim3(256), 0, s, n, (const unsigned long long*)g.counts,
                      (const unsigned long long*)g.total, g.offsets);
   GR_HIP_TRY(hipGetLastError());
-  GR_HIP_TRY(hipMemcpyAsync(plan, g.plan, sizeof(gr_plan), hipMemcpyDeviceToHost, s));
+  if (!mapped) GR_HIP_TRY(hipMemcpyAsync(plan, g.plan, sizeof(gr_plan), hipMemcpyDeviceToHost, s));
   return GR_OK;
 }
 
