@@ -50,7 +50,9 @@ def ctypes_stream(device) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 DEVICE_DENSIFY_MIN = 100_000  # Gaussians from which densify/prune runs on the device (C5 scale)
 FUSED_LOSS = os.environ.get("GR_FUSED_LOSS", "1") != "0"  # losses.l1_loss for the L1 terms (A/B switch)
-NUM_STREAMS = max(1, int(os.environ.get("GR_STREAMS", "3")))  # HIP streams the views rotate over
+# HIP streams the views rotate over (same-box A/B, 20 steps: 4 vs 3 +0.5% at 50 views, +0.8% at the 7 views
+# one rank of 8 renders, +2% at 25; 6 or 8 streams lose)
+NUM_STREAMS = max(1, int(os.environ.get("GR_STREAMS", "4")))
 PREFETCH = max(1, int(os.environ.get("GR_PREFETCH", "3")))  # views prepared ahead of the one rendering
 # steps between re-establishing the Morton order of the moving Gaussians (ViewShardedFitter.respatialize;
 # 0 = only at construction and after densify/prune).  A re-sort costs ~1.2 ms at 1M Gaussians (codes,

@@ -17,7 +17,7 @@ Also reported on rank 0:
                 under "splats") against the HBM roofline: SURVEY.md 8(d)'s algorithmic bytes per unit
                 (48 B per pair forward, 84 B per core pair backward, + 40 B per pixel) x the units of one
                 launch / its average launch time (HIP events on its launch stream, gr_profile_begin/end,
-                over one single-stream step after the timed region: the timed steps overlap views on 3
+                over one single-stream step after the timed region: the timed steps overlap views on 4
                 streams and run uninstrumented), vs 8 TB/s; its PMC HBM traffic from profiles/pmc_traffic.json
                 (tools/pmc_traffic.py); the executed bf16 MFMA rate beside it
   hbm_model     the north_star's framing: SURVEY.md 8(d)'s byte model of the tile-binned path per view at
