@@ -67,6 +67,7 @@ class GrPlan(ctypes.Structure):
 
 
 REDUCE_MAX_VIEWS = 16  # GR_REDUCE_MAX_VIEWS
+PREPARE_MAX_VIEWS = 4  # GR_PREPARE_MAX_VIEWS
 
 
 class GrReduceView(ctypes.Structure):
@@ -89,6 +90,9 @@ _SIG = {
     "gr_geom_bytes": (ctypes.c_size_t, [ctypes.c_int]),
     "gr_fwd_prepare": (ctypes.c_int, [_VP, ctypes.c_int, _P, _P, _P, ctypes.c_int, _P, _P, ctypes.c_size_t, _PP, _P]),
     "gr_fwd_prepare_async": (ctypes.c_int, [_VP, ctypes.c_int, _P, _P, _P, ctypes.c_int, _P, _P, ctypes.c_size_t, _P, _P]),
+    "gr_fwd_prepare_views_async": (ctypes.c_int, [ctypes.c_int, _VP, ctypes.c_int, _P, _P, _P, ctypes.c_int, _P,
+                                                  ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t,
+                                                  ctypes.POINTER(ctypes.c_void_p), _P]),
     "gr_bins_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
     "gr_saved_floats": (ctypes.c_size_t, [_VP]),
     "gr_fwd_scratch_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
@@ -102,7 +106,8 @@ _SIG = {
     "gr_bwd_fit": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P,
                                   ctypes.c_float, _P, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, ctypes.c_int, _P,
                                   ctypes.c_size_t, _P]),
-    "gr_fit_param_step": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, _P, _P, _P, _P, _P, ctypes.c_float, ctypes.c_int, _P,
+    "gr_fit_param_step": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, _P, _P, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                                         ctypes.c_float, ctypes.c_int, _P,
                                          _P, ctypes.c_float, ctypes.c_float, ctypes.c_double, ctypes.c_double, ctypes.c_float,
                                          _P]),
     "gr_adam_step": (ctypes.c_int, [ctypes.c_int64, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float, ctypes.c_double,

@@ -541,17 +541,15 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, int n, const float*
   if (threadIdx.x == 0) g.total[blockIdx.x] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
 }
 
+// One Gaussian in one view from its loaded parameters (k_preprocess, k_preprocess_views).
 template <int CD>
-__device__ __forceinline__ unsigned long long preprocess_one(const ViewK& v, int i, const float* __restrict__ means,
-                                                             const float* __restrict__ scales,
-                                                             const float* __restrict__ colors,
-                                                             const float* __restrict__ opac, Geom& g) {
-  const float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
+__device__ __forceinline__ unsigned long long preprocess_vals(const ViewK& v, int i, float mx, float my, float mz, float s0,
+                                                              float s1, const float* __restrict__ col, float op,
+                                                              const Geom& g) {
   Proj p;
-  project(v, mx, my, mz, scales[3 * i], scales[3 * i + 1], p);
+  project(v, mx, my, mz, s0, s1, p);
   float c[3];
-  eval_color<CD>(v, mx, my, mz, colors + (size_t)CD * i, c);
-  const float op = opac[i];
+  eval_color<CD>(v, mx, my, mz, col, c);
   int4 r;
   const float qx = qcoef(p.sx);
   const float qy = qcoef(p.sy);
@@ -572,6 +570,62 @@ __device__ __forceinline__ unsigned long long preprocess_one(const ViewK& v, int
   g.rect[i] = r;
   g.counts[i] = (unsigned long long)core | ((unsigned long long)tail << 32);
   return (unsigned long long)core | ((unsigned long long)tail << 32);
+}
+
+template <int CD>
+__device__ __forceinline__ unsigned long long preprocess_one(const ViewK& v, int i, const float* __restrict__ means,
+                                                             const float* __restrict__ scales,
+                                                             const float* __restrict__ colors,
+                                                             const float* __restrict__ opac, Geom& g) {
+  return preprocess_vals<CD>(v, i, means[3 * i], means[3 * i + 1], means[3 * i + 2], scales[3 * i], scales[3 * i + 1],
+                             colors + (size_t)CD * i, opac[i], g);
+}
+
+// Several views of the same Gaussians (gr_fwd_prepare_views_async): each thread loads its Gaussian's
+// parameters once and runs the per-view preprocess for every view of the batch (the same float sequence as
+// k_preprocess, view by view); per view the block's packed pair counts go to that view's totals.
+constexpr int PREP_MAX_VIEWS = GR_PREPARE_MAX_VIEWS;
+struct PrepBatch {
+  int nv;
+  ViewK v[PREP_MAX_VIEWS];
+  Geom g[PREP_MAX_VIEWS];
+};
+
+template <int CD>
+__global__ __launch_bounds__(256) void k_preprocess_views(PrepBatch B, int n, const float* __restrict__ means,
+                                                          const float* __restrict__ scales,
+                                                          const float* __restrict__ colors,
+                                                          const float* __restrict__ opac) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  float mx = 0.f, my = 0.f, mz = 0.f, s0 = 0.f, s1 = 0.f, op = 0.f;
+  if (i < n) {
+    mx = means[3 * i];
+    my = means[3 * i + 1];
+    mz = means[3 * i + 2];
+    s0 = scales[3 * i];
+    s1 = scales[3 * i + 1];
+    op = opac[i];
+  }
+  __shared__ unsigned long long wsum[PREP_MAX_VIEWS][4];
+  for (int k = 0; k < B.nv; ++k) {
+    const Geom& g = B.g[k];
+    if (i == n) {
+      g.counts[n] = 0ull;
+      float4* pad = g.rec + (size_t)REC4 * n;
+      pad[0] = make_float4(1e30f, 1e30f, -1.0f, -1.0f);
+      pad[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      g.zr[n] = 0.0f;
+    }
+    unsigned long long kept = 0;
+    if (i < n) kept = preprocess_vals<CD>(B.v[k], i, mx, my, mz, s0, s1, colors + (size_t)CD * i, op, g);
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) kept += __shfl_xor(kept, m);
+    if ((threadIdx.x & 63) == 0) wsum[k][threadIdx.x >> 6] = kept;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < B.nv)
+    B.g[threadIdx.x].total[blockIdx.x] = (wsum[threadIdx.x][0] + wsum[threadIdx.x][1]) +
+                                         (wsum[threadIdx.x][2] + wsum[threadIdx.x][3]);
 }
 
 constexpr int EWIN = 4096;  // pairs staged in LDS per emit block
@@ -2647,21 +2701,22 @@ __global__ __launch_bounds__(256) void k_l1_grad(const float* __restrict__ a, co
 
 // The fit loop's parameter update (fit_multiview_stub.py:268-275 activations, :307-308 regulariser,
 // :311 Adam) for one parameter tensor, fused into one pass over its elements (gr_fit_param_step):
-//   g_raw = act'(raw) * ((acc0 + acc1) + acc2 + reg)      d loss / d raw parameter (torch's backward of
+//   g_raw = act'(raw) * (((acc0 + acc1) + ...) + reg)     d loss / d raw parameter (torch's backward of
 //                                                         softplus(x) + 1e-3 / sigmoid / identity)
 //   then, with Adam, torch.optim.Adam's foreach update in its own operation order:
 //   m = m + (1 - b1)(g - m); v = v b2 + ((1 - b2) g) g; p = p + step_size m / (sqrt(v) / bc2_sqrt + eps).
 // act: 0 identity, 1 softplus (threshold 20, as torch), 2 sigmoid.
+struct AccList {
+  const float* p[GR_FIT_MAX_ACC];
+  int n;
+};
 __global__ __launch_bounds__(256) void k_fit_param_step(int64_t count, int act, float* __restrict__ p,
-                                                        float* __restrict__ grad, const float* __restrict__ acc0,
-                                                        const float* __restrict__ acc1, const float* __restrict__ acc2,
-                                                        float reg, int adam, float* __restrict__ m, float* __restrict__ v,
+                                                        float* __restrict__ grad, AccList acc, float reg, int adam, float* __restrict__ m, float* __restrict__ v,
                                                         float neg_step, float bc2_sqrt, float b1, float b2, float b2_c,
                                                         float eps) {
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < count; e += (int64_t)gridDim.x * 256) {
-    float gact = acc0 ? acc0[e] : 0.0f;
-    if (acc1) gact = gact + acc1[e];
-    if (acc2) gact = gact + acc2[e];
+    float gact = acc.n > 0 ? acc.p[0][e] : 0.0f;
+    for (int a = 1; a < acc.n; ++a) gact = gact + acc.p[a][e];  // in stream order
     gact = gact + reg;
     const float x = p[e];
     float g;
@@ -2846,9 +2901,8 @@ __device__ __forceinline__ unsigned long long block_exclusive_scan(unsigned long
 // block sums) is replaced by its exclusive scan, offsets[n] gets the packed grand total.  The packed
 // words cannot carry into each other as long as K < 2^31, which is checked against the exact total
 // (the sum of every block's two words) before the plan is trusted.
-__global__ __launch_bounds__(1024) void k_plan(unsigned long long* __restrict__ bsum, int blocks,
-                                               unsigned long long* __restrict__ off_end, gr_plan* plan,
-                                               gr_plan* host_plan) {
+__device__ __forceinline__ void plan_scan(unsigned long long* __restrict__ bsum, int blocks,
+                                          unsigned long long* __restrict__ off_end, gr_plan* plan, gr_plan* host_plan) {
   __shared__ unsigned long long sh[16];
   const int tid = (int)threadIdx.x, per = (blocks + 1023) / 1024;
   const int b0 = min(blocks, tid * per), b1 = min(blocks, b0 + per);
@@ -2881,16 +2935,40 @@ __global__ __launch_bounds__(1024) void k_plan(unsigned long long* __restrict__ 
   }
 }
 
+__global__ __launch_bounds__(1024) void k_plan(unsigned long long* __restrict__ bsum, int blocks,
+                                               unsigned long long* __restrict__ off_end, gr_plan* plan,
+                                               gr_plan* host_plan) {
+  plan_scan(bsum, blocks, off_end, plan, host_plan);
+}
+
 // Gaussian level of the offsets scan: offsets[i] = its block's offset + the exclusive scan of the packed
 // counts inside the block (the blocks are k_preprocess's).
+__device__ __forceinline__ void offsets_scan(int n, int b, const unsigned long long* __restrict__ counts,
+                                             const unsigned long long* __restrict__ boff,
+                                             unsigned long long* __restrict__ offsets) {
+  __shared__ unsigned long long sh[4];
+  const int i = (int)(b * 256 + threadIdx.x);
+  unsigned long long tot;
+  const unsigned long long e = block_exclusive_scan<4>(i < n ? counts[i] : 0ull, sh, tot);
+  if (i < n) offsets[i] = boff[b] + e;
+}
 __global__ __launch_bounds__(256) void k_offsets(int n, const unsigned long long* __restrict__ counts,
                                                  const unsigned long long* __restrict__ boff,
                                                  unsigned long long* __restrict__ offsets) {
-  __shared__ unsigned long long sh[4];
-  const int i = (int)(blockIdx.x * 256 + threadIdx.x);
-  unsigned long long tot;
-  const unsigned long long e = block_exclusive_scan<4>(i < n ? counts[i] : 0ull, sh, tot);
-  if (i < n) offsets[i] = boff[blockIdx.x] + e;
+  offsets_scan(n, (int)blockIdx.x, counts, boff, offsets);
+}
+
+// The two scans for a batch of views (gr_fwd_prepare_views_async): block / row k = view k.
+struct HostPlans {
+  gr_plan* p[PREP_MAX_VIEWS];
+};
+__global__ __launch_bounds__(1024) void k_plan_views(PrepBatch B, int n, HostPlans hp) {
+  const Geom& g = B.g[blockIdx.x];
+  plan_scan(g.total, (n + 256) / 256, g.offsets + n, g.plan, hp.p[blockIdx.x]);
+}
+__global__ __launch_bounds__(256) void k_offsets_views(PrepBatch B, int n) {
+  const Geom& g = B.g[blockIdx.y];
+  offsets_scan(n, (int)blockIdx.x, g.counts, g.total, g.offsets);
 }
 
 gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, const float* scales, const float* colors,
@@ -2933,6 +3011,62 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
                      (const unsigned long long*)g.total, g.offsets);
   GR_HIP_TRY(hipGetLastError());
   if (!mapped) GR_HIP_TRY(hipMemcpyAsync(plan, g.plan, sizeof(gr_plan), hipMemcpyDeviceToHost, s));
+  return GR_OK;
+}
+
+gr_status gr_fwd_prepare_views_async(int num_views, const gr_view* views, int n, const float* means,
+                                     const float* scales, const float* colors, int color_dim, const float* opacities,
+                                     void* const* geoms, size_t geom_bytes, gr_plan* const* plans, void* stream) {
+  if (num_views < 1 || num_views > PREP_MAX_VIEWS)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fwd_prepare_views_async: num_views must be in [1, GR_PREPARE_MAX_VIEWS]");
+  if (!views || !geoms || !plans) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+  if (num_views == 1)
+    return gr_fwd_prepare_async(&views[0], n, means, scales, colors, color_dim, opacities, geoms[0], geom_bytes, plans[0],
+                                stream);
+  for (int k = 0; k < num_views; ++k) {
+    gr_status st = check_view(&views[k]);
+    if (st != GR_OK) return st;
+    if (!plans[k] || !geoms[k]) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+  }
+  if (n < 0) return set_error(GR_ERR_INVALID_ARGUMENT, "n must be >= 0");
+  if (color_dim != 3 && color_dim != 12 && color_dim != 48)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");
+  if (n == 0) {
+    for (int k = 0; k < num_views; ++k) *plans[k] = gr_plan{0, 0, 0};
+    return GR_OK;
+  }
+  if (!means || !scales || !colors || !opacities) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+  if (geom_bytes < gr_geom_bytes(n)) return set_error(GR_ERR_WORKSPACE, "geom workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  PrepBatch B;
+  HostPlans hp;
+  bool all_mapped = true;
+  B.nv = num_views;
+  for (int k = 0; k < num_views; ++k) {
+    B.v[k] = make_viewk(&views[k]);
+    B.g[k] = geom_view(geoms[k], n);
+    hipPointerAttribute_t attr;
+    hp.p[k] = nullptr;
+    if (hipPointerGetAttributes(&attr, plans[k]) == hipSuccess && attr.type == hipMemoryTypeHost && attr.devicePointer)
+      hp.p[k] = (gr_plan*)attr.devicePointer;
+    (void)hipGetLastError();
+    all_mapped = all_mapped && hp.p[k];
+  }
+  const int blocks = blocks_for(n + 1);
+  if (color_dim == 3)
+    hipLaunchKernelGGL(k_preprocess_views<3>, dim3(blocks), dim3(256), 0, s, B, n, means, scales, colors, opacities);
+  else if (color_dim == 12)
+    hipLaunchKernelGGL(k_preprocess_views<12>, dim3(blocks), dim3(256), 0, s, B, n, means, scales, colors, opacities);
+  else
+    hipLaunchKernelGGL(k_preprocess_views<48>, dim3(blocks), dim3(256), 0, s, B, n, means, scales, colors, opacities);
+  GR_HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_plan_views, dim3(num_views), dim3(1024), 0, s, B, n, hp);
+  GR_HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_offsets_views, dim3(blocks_for(n), num_views), dim3(256), 0, s, B, n);
+  GR_HIP_TRY(hipGetLastError());
+  if (!all_mapped)
+    for (int k = 0; k < num_views; ++k)
+      if (!hp.p[k]) GR_HIP_TRY(hipMemcpyAsync(plans[k], B.g[k].plan, sizeof(gr_plan), hipMemcpyDeviceToHost, s));
   return GR_OK;
 }
 
@@ -3460,17 +3594,23 @@ gr_status gr_l1_loss_fwd(const float* a, const float* b, int64_t n1, const float
   return GR_OK;
 }
 
-gr_status gr_fit_param_step(int64_t count, int act, float* param, float* grad, const float* acc0, const float* acc1,
-                            const float* acc2, float reg, int adam, float* exp_avg, float* exp_avg_sq, float neg_step_size,
+gr_status gr_fit_param_step(int64_t count, int act, float* param, float* grad, const float* const* accs, int num_accs,
+                            float reg, int adam, float* exp_avg, float* exp_avg_sq, float neg_step_size,
                             float bias_correction2_sqrt, double beta1, double beta2, float eps, void* stream) {
-  if (count < 0 || act < 0 || act > 2 || !param || (adam && (!exp_avg || !exp_avg_sq)) || (!adam && !grad))
+  if (count < 0 || act < 0 || act > 2 || !param || (adam && (!exp_avg || !exp_avg_sq)) || (!adam && !grad) ||
+      num_accs < 0 || num_accs > GR_FIT_MAX_ACC || (num_accs > 0 && !accs))
     return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_param_step: bad arguments");
   if (count == 0) return GR_OK;
+  AccList acc;
+  acc.n = num_accs;
+  for (int a = 0; a < num_accs; ++a) {
+    if (!accs[a]) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_param_step: null accumulator");
+    acc.p[a] = accs[a];
+  }
   const int blocks = (int)std::min<int64_t>((count + 255) / 256, 4096);
   // torch.optim.Adam passes 1 - beta1 (lerp weight) and 1 - beta2 (addcmul value) as Python floats (double)
   const float w1 = (float)(1.0 - beta1), w2 = (float)(1.0 - beta2);
-  hipLaunchKernelGGL(k_fit_param_step, dim3(blocks), dim3(256), 0, (hipStream_t)stream, count, act, param, grad, acc0, acc1,
-                     acc2, reg, adam, exp_avg, exp_avg_sq, neg_step_size, bias_correction2_sqrt, w1, (float)beta2, w2, eps);
+  hipLaunchKernelGGL(k_fit_param_step, dim3(blocks), dim3(256), 0, (hipStream_t)stream, count, act, param, grad, acc, reg, adam, exp_avg, exp_avg_sq, neg_step_size, bias_correction2_sqrt, w1, (float)beta2, w2, eps);
   GR_HIP_TRY(hipGetLastError());
   return GR_OK;
 }

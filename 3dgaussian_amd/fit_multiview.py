@@ -71,6 +71,9 @@ REDUCE_BATCH = max(1, min(16, int(os.environ.get("GR_REDUCE_BATCH", "16"))))
 FUSED_STEP = os.environ.get("GR_FUSED_STEP", "1") != "0"
 # fused path: views prepared ahead of the one being rendered (on the preparation stream)
 PREP_AHEAD = max(1, int(os.environ.get("GR_PREP_AHEAD", "6")))
+L_MAX_ACC = 8  # GR_FIT_MAX_ACC: stream accumulators gr_fit_param_step sums
+# views prepared together (gr_fwd_prepare_views_async: the parameters read once for the group)
+PREP_GROUP = max(1, min(4, int(os.environ.get("GR_PREP_GROUP", "4"))))
 
 
 # ------------------------------------------------------------------------------------------------
@@ -490,8 +493,10 @@ class ViewShardedFitter:
 
         def prepare(j):
             if j < len(views) and j not in ahead:
+                js = range(j, min(len(views), j + PREP_GROUP))  # none of them prepared yet (groups are contiguous)
                 with torch.cuda.stream(prep):
-                    ahead[j] = tr.prepare_native(m, s, c, o, self._fit_view(views[j], device), plan_host=pins[j])
+                    ahead.update(zip(js, tr.prepare_views_native(m, s, c, o, [self._fit_view(views[q], device) for q in js],
+                                                                 [pins[q] for q in js])))
 
         for j in range(PREP_AHEAD):
             prepare(j)
@@ -578,8 +583,10 @@ class ViewShardedFitter:
 
         def prepare(j):
             if j < len(views) and j not in ahead:
+                js = range(j, min(len(views), j + PREP_GROUP))
                 with torch.cuda.stream(prep):
-                    ahead[j] = tr.prepare_native(m, s, c, o, gv_of(views[j]), plan_host=pins[j])
+                    ahead.update(zip(js, tr.prepare_views_native(m, s, c, o, [gv_of(views[q]) for q in js],
+                                                                 [pins[q] for q in js])))
 
         for j in range(PREP_AHEAD):
             prepare(j)
@@ -647,7 +654,13 @@ class ViewShardedFitter:
             neg_step = -(lr / (1.0 - b1 ** t))
             bc2s = (1.0 - b2 ** t) ** 0.5
             steps.append((neg_step, bc2s))
-            a = [pp[slot[k]] for pp in parts] + [None, None, None]
+            a = [pp[slot[k]] for pp in parts]
+            if len(a) > L_MAX_ACC:  # more streams than the kernel sums: fold the rest in stream order first
+                t = a[L_MAX_ACC - 1]
+                for x in a[L_MAX_ACC:]:
+                    t = t + x
+                a = a[:L_MAX_ACC - 1] + [t]
+            accs = (ctypes.c_void_p * max(1, len(a)))(*[x.data_ptr() for x in a])
             if flat is not None:
                 grad = flat[off:off + p.numel()].view_as(p)
                 off += p.numel()
@@ -656,8 +669,7 @@ class ViewShardedFitter:
             p.grad = grad
             r = reg.get(k, 0.0) if self.rank == 0 else 0.0
             tr._native.check(L.gr_fit_param_step(p.numel(), act[k], tr._native.ptr(p.data), tr._native.ptr(grad),
-                                                 tr._native.ptr(a[0]), tr._native.ptr(a[1]), tr._native.ptr(a[2]),
-                                                 ctypes.c_float(r), 0 if flat is not None else 1,
+                                                 accs, len(a), ctypes.c_float(r), 0 if flat is not None else 1,
                                                  tr._native.ptr(st["exp_avg"]), tr._native.ptr(st["exp_avg_sq"]),
                                                  ctypes.c_float(neg_step), ctypes.c_float(bc2s), ctypes.c_double(b1),
                                                  ctypes.c_double(b2), ctypes.c_float(eps), stream), "gr_fit_param_step")

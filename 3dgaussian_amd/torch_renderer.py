@@ -250,6 +250,29 @@ def prepare_native(means, scales, colors, opacities, gv: _native.GrView, plan_ho
     return Prepared(gv, n, geom, plan_host, ev)
 
 
+def prepare_views_native(means, scales, colors, opacities, gvs, plan_hosts) -> list:
+    """gr_fwd_prepare_views_async: up to _native.PREPARE_MAX_VIEWS views of the same Gaussians prepared in one
+    pass over the parameters, on the current stream; ``plan_hosts``: one pinned int64 tensor of 3 elements
+    per view.  Returns one Prepared per view (they share one event)."""
+    L = _native.lib()
+    k = len(gvs)
+    if not 1 <= k <= _native.PREPARE_MAX_VIEWS or len(plan_hosts) != k:
+        raise ValueError(f"1 to {_native.PREPARE_MAX_VIEWS} views, one plan buffer each")
+    dev = means.device
+    n = int(means.shape[0])
+    nbytes = int(L.gr_geom_bytes(n))
+    geoms = [torch.empty((nbytes,), dtype=torch.uint8, device=dev) for _ in range(k)]
+    views = (_native.GrView * k)(*gvs)
+    gptr = (ctypes.c_void_p * k)(*[g.data_ptr() for g in geoms])
+    pptr = (ctypes.c_void_p * k)(*[p.data_ptr() for p in plan_hosts])
+    _native.check(L.gr_fwd_prepare_views_async(k, views, n, _native.ptr(means), _native.ptr(scales), _native.ptr(colors),
+                                               _color_dim(colors), _native.ptr(opacities), gptr, nbytes, pptr,
+                                               _stream(dev)), "gr_fwd_prepare_views_async")
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    return [Prepared(gv, n, g, p, ev) for gv, g, p in zip(gvs, geoms, plan_hosts)]
+
+
 def forward_native(means, scales, colors, opacities, gv: _native.GrView, prepared: Optional[Prepared] = None,
                    want_depth: bool = True):
     """Run gr_fwd_prepare(_async) + gr_fwd_render.  Returns (out, alpha, depth, RenderState).

@@ -106,14 +106,24 @@ gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const floa
                          const float* colors, int color_dim, const float* opacities, void* geom,
                          size_t geom_bytes, gr_plan* plan, void* stream);
 
-/* Same work, stream-ordered: *plan is written by a device-to-host copy enqueued on `stream` and is
- * valid once the stream (or an event recorded after this call) has completed.  A pair count that
+/* Same work, stream-ordered: *plan is written on `stream` (by the device itself when it is pinned
+ * host memory, else by a device-to-host copy) and is valid once the stream (or an event recorded
+ * after this call) has completed.  A pair count that
  * does not fit int32 reads back as num_pairs = -1, which gr_fwd_render reports as
  * GR_ERR_OVERFLOW.  *plan should be pinned host memory (hipHostMalloc / torch pin_memory);
  * pageable memory works but makes the copy synchronous. */
 gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, const float* scales,
                                const float* colors, int color_dim, const float* opacities,
                                void* geom, size_t geom_bytes, gr_plan* plan, void* stream);
+
+/* gr_fwd_prepare_async for up to GR_PREPARE_MAX_VIEWS views of the same Gaussians in one pass: the
+ * parameters are read once per Gaussian, each view's geom (geom_bytes each) and plan are exactly what
+ * gr_fwd_prepare_async writes for that view.  All plans are valid once the stream has completed. */
+#define GR_PREPARE_MAX_VIEWS 4
+gr_status gr_fwd_prepare_views_async(int num_views, const gr_view* views, int n, const float* means,
+                                     const float* scales, const float* colors, int color_dim,
+                                     const float* opacities, void* const* geoms, size_t geom_bytes,
+                                     gr_plan* const* plans, void* stream);
 
 /* Tile-sorted (tile, Gaussian) pair lists, per-tile ranges and work items. */
 size_t gr_bins_bytes(const gr_view* v, int n, const gr_plan* plan);
@@ -236,17 +246,19 @@ gr_status gr_l1_loss_bwd(const float* a, const float* b, int64_t n1, const float
 /* ------------------------------------------------------------------------------------------ */
 /* Fit-loop parameter update, the caller's side of the render op (fit_multiview_stub.py:268-275   */
 /* activations, :307-308 regulariser, :311 torch.optim.Adam), one pass per parameter tensor:    */
-/*   grad = act'(param) * ((acc0 + acc1) + acc2 + reg)   (acc1/acc2 may be NULL; act 0 identity,  */
+/*   grad = act'(param) * (((accs[0] + accs[1]) + ...) + reg)  (up to GR_FIT_MAX_ACC device arrays  */
+/*          of count floats, summed in order; act 0 identity,                                     */
 /*          1 softplus(x) + 1e-3, 2 sigmoid: torch's backward formulas);                          */
 /*   adam != 0: exp_avg / exp_avg_sq / param updated as Adam's foreach step with                 */
 /*   neg_step_size = -lr / (1 - beta1^t), bias_correction2_sqrt = sqrt(1 - beta2^t); the betas are */
 /*   doubles so 1 - beta rounds to float as torch's Python-float scalars do.                     */
 /* gr_adam_step: the Adam update alone on an assembled gradient (after an all-reduce).           */
 /* ------------------------------------------------------------------------------------------ */
-gr_status gr_fit_param_step(int64_t count, int act, float* param, float* grad, const float* acc0,
-                            const float* acc1, const float* acc2, float reg, int adam, float* exp_avg,
-                            float* exp_avg_sq, float neg_step_size, float bias_correction2_sqrt,
-                            double beta1, double beta2, float eps, void* stream);
+#define GR_FIT_MAX_ACC 8
+gr_status gr_fit_param_step(int64_t count, int act, float* param, float* grad, const float* const* accs,
+                            int num_accs, float reg, int adam, float* exp_avg, float* exp_avg_sq,
+                            float neg_step_size, float bias_correction2_sqrt, double beta1, double beta2,
+                            float eps, void* stream);
 gr_status gr_adam_step(int64_t count, float* param, const float* grad, float* exp_avg,
                        float* exp_avg_sq, float neg_step_size, float bias_correction2_sqrt,
                        double beta1, double beta2, float eps, void* stream);

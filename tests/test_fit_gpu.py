@@ -244,3 +244,40 @@ def test_fused_param_step_matches_torch_adam(cuda):
     for k in pa:
         err = float((pf[k] - pa[k]).norm() / pa[k].norm())
         assert err <= 1e-6, (k, err)
+
+
+@pytest.mark.parametrize("sh", [False, True])
+def test_grouped_prepare_matches_single_view_prepare(cuda, sh):
+    """gr_fwd_prepare_views_async (parameters read once for up to 4 views) writes, per view, exactly the geom
+    workspace (records, depths, rectangles, counts, offsets, plan) and the pinned-host plan that
+    gr_fwd_prepare_async writes for that view alone."""
+    import torch
+
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    tr = importlib.import_module("3dgaussian_amd.torch_renderer")
+    bench = importlib.import_module("bench")
+    W, H = 160, 120
+    params = bench.synthetic_params(30_000, cuda)
+    if sh:
+        g = torch.Generator(device=cuda).manual_seed(4)
+        params["sh_raw"] = torch.nn.Parameter(0.1 * torch.randn((30_000, 16, 3), generator=g, device=cuda))
+        del params["colors_raw"]
+    with torch.no_grad():
+        acts = [a.contiguous() for a in fm.activations(params)]
+    cams = fm.orbit_cameras(4, W, H, cuda)
+    gvs = [tr.make_view(c.view, c.proj, W, H, None, cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
+           for c in cams]
+    pins = torch.zeros((8, 3), dtype=torch.int64, pin_memory=True)
+    for k in (4, 3, 2):
+        grouped = tr.prepare_views_native(*acts, gvs[:k], [pins[q] for q in range(k)])
+        single = [tr.prepare_native(*acts, gv, plan_host=pins[4 + (q % 4)]) for q, gv in enumerate(gvs[:k])]
+        for q, (a, b) in enumerate(zip(grouped, single)):
+            pa, pb = a.plan(), b.plan()
+            assert (pa.num_pairs, pa.num_slots, pa.num_core_pairs) == (pb.num_pairs, pb.num_slots, pb.num_core_pairs)
+            assert pa.num_pairs > 0
+            n = acts[0].shape[0]
+            off = tr._native.geom_layout(n)
+            parts = [(off[0], (n + 1) * 36), (off[1], n * 16), (off[2], (n + 1) * 8), (off[3], (n + 1) * 8),
+                     (off[4], 24 + ((n + 256) // 256) * 8)]  # records + depths, rects, counts, offsets, plan + totals
+            for o, nb in parts:
+                assert torch.equal(a.geom[o:o + nb], b.geom[o:o + nb]), (k, q, o)
