@@ -2513,6 +2513,17 @@ __global__ __launch_bounds__(256) void k_preprocess_u8(ViewK v, int n, const flo
   g.counts[i] = (r.z - r.x + 1) * (r.w - r.y + 1);
 }
 
+// Exact 64-bit total of the per-Gaussian pair counts: the int32 scan that places the pairs can wrap
+// past 2^32 back to a positive total, so the total is checked here before anything is sized from it.
+__global__ __launch_bounds__(256) void k_count_total64(int n, const int* __restrict__ counts,
+                                                       unsigned long long* __restrict__ total) {
+  unsigned long long s = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) s += (unsigned)counts[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(total, s);
+}
+
 template <bool SORTED>
 __global__ __launch_bounds__(256) void k_raster_u8(ViewK v, const int2* __restrict__ ranges, const int* __restrict__ ids,
                                                    const float4* __restrict__ ga, const float4* __restrict__ gc,
@@ -3492,6 +3503,7 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
   const size_t o_dk = o; o = align_up(o + nn * sizeof(uint32_t));
   const size_t o_img = o; o = align_up(o + HW * 4);
   const size_t o_scan = o; o = align_up(o + scan_tmp_bytes_t<int>(n));
+  const size_t o_tot = o; o = align_up(o + sizeof(unsigned long long));
   const size_t fixed = o;
   char* d = nullptr;
   GR_HIP_TRY(hipMalloc(&d, fixed));
@@ -3516,11 +3528,16 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
   hipLaunchKernelGGL(k_preprocess_u8, dim3(blocks_for(n + 1)), dim3(256), 0, s, vk, n, din, din + 3 * nn, din + 6 * nn,
                      din + 9 * nn, lr);
   GR_HIP_TRY(hipGetLastError());
+  unsigned long long* tot = (unsigned long long*)(d + o_tot);
+  GR_HIP_TRY(hipMemsetAsync(tot, 0, sizeof(*tot), s));
+  hipLaunchKernelGGL(k_count_total64, dim3(std::min(blocks_for(n), 1024)), dim3(256), 0, s, n, lr.counts, tot);
+  GR_HIP_TRY(hipGetLastError());
   size_t tmp = scan_tmp_bytes_t<int>(n);
   GR_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(d + o_scan, tmp, lr.counts, lr.offsets, n + 1, s));
-  int K = 0;
-  GR_HIP_TRY(hipMemcpy(&K, lr.offsets + n, sizeof(int), hipMemcpyDeviceToHost));
-  if (K < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
+  unsigned long long K64 = 0;
+  GR_HIP_TRY(hipMemcpy(&K64, tot, sizeof(K64), hipMemcpyDeviceToHost));
+  if (K64 >= (1ull << 31)) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
+  const int K = (int)K64;
   // bins: keys_in/out (u32 or u64), ids_in/out, ranges, sort tmp
   const size_t kk = (size_t)(K > 0 ? K : 1);
   const size_t ksz = sorted ? sizeof(uint64_t) : sizeof(uint32_t);

@@ -123,6 +123,10 @@ def sclk_mhz():
     """Current shader clock of the visible GPU (rocm-smi), or None."""
     import subprocess
 
+    # Under rocprofv3 its preloaded library is inherited by the child and initialises the GPU before
+    # rocm-smi's `env python3` hop execs, which the GPU pool refuses: no clock reading there.
+    if "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return None
     try:
         r = subprocess.run(["rocm-smi", "--showclocks", "--json"], capture_output=True, text=True, timeout=20)
         card = next(iter(json.loads(r.stdout).values()))
