@@ -765,14 +765,20 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // One block; virtual tiles are scanned in order, so items are ordered by (virtual tile, chunk) and
 // the core and tail items of a tile are adjacent.  k_work_items reads existing per-virtual-tile
 // ranges (radix-sort path, empty views).
-__global__ __launch_bounds__(1024) void k_work_items(int vtiles, const int2* __restrict__ ranges, int4* __restrict__ items,
+// One workgroup of WI_THREADS (256: it fits beside the splat kernels on a partly occupied CU; a
+// 1024-thread block waits for a whole CU to drain, which under four render streams took up to 1.6 ms).
+#ifndef GR_WI_THREADS
+#define GR_WI_THREADS 256
+#endif
+constexpr int WI_THREADS = GR_WI_THREADS;
+__global__ __launch_bounds__(WI_THREADS) void k_work_items(int vtiles, const int2* __restrict__ ranges, int4* __restrict__ items,
                                                      int* __restrict__ num_items, int* __restrict__ tile_item0) {
-  typedef hipcub::BlockScan<int, 1024> Scan;
+  typedef hipcub::BlockScan<int, WI_THREADS> Scan;
   __shared__ typename Scan::TempStorage tmp;
   __shared__ int carry;
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
-  for (int base = 0; base < vtiles; base += 1024) {
+  for (int base = 0; base < vtiles; base += WI_THREADS) {
     const int t = base + (int)threadIdx.x;
     const int2 r = t < vtiles ? ranges[t] : make_int2(0, 0);
     const int nch = (r.y - r.x + CH - 1) / CH;
@@ -792,16 +798,16 @@ __global__ __launch_bounds__(1024) void k_work_items(int vtiles, const int2* __r
 
 // Counting-sort path: per-tile pair totals of the core region (Tc) and of the tail region (Tt,
 // starting at Kc) are scanned into the virtual-tile ranges (2t: core, 2t+1: tail), then cut.
-__global__ __launch_bounds__(1024) void k_work_items_zones(int tiles, int tiles_x, int Kc, const int* __restrict__ Tc,
+__global__ __launch_bounds__(WI_THREADS) void k_work_items_zones(int tiles, int tiles_x, int Kc, const int* __restrict__ Tc,
                                                            const int* __restrict__ Tt, int2* __restrict__ ranges,
                                                            int4* __restrict__ items, int* __restrict__ num_items,
                                                            int* __restrict__ tile_item0) {
-  typedef hipcub::BlockScan<int, 1024> Scan;
+  typedef hipcub::BlockScan<int, WI_THREADS> Scan;
   __shared__ typename Scan::TempStorage tmp;
   __shared__ int carry, ccarry, tcarry;
   if (threadIdx.x == 0) carry = ccarry = tcarry = 0;
   __syncthreads();
-  for (int base = 0; base < tiles; base += 1024) {
+  for (int base = 0; base < tiles; base += WI_THREADS) {
     const int t = base + (int)threadIdx.x;
     const int nc = (t < tiles && Tc) ? Tc[t] : 0, nt = (t < tiles && Tt) ? Tt[t] : 0;  // null: an empty zone
     int sc, totc, st, tott;
@@ -939,12 +945,20 @@ __global__ __launch_bounds__(256) void k_tile_count(int64_t K, int cw, int cols,
 // CS_T tiles x CS_G column groups; a thread's column run (up to CS_R of them) is loaded at once and kept
 // in registers for the second pass, so the kernel waits on memory about twice instead of once per 8
 // columns and never reads M again.
+// 256 threads per block (16 tiles x 16 column groups): a 1024-thread block needs a whole CU free and
+// waits behind the splat kernels of the other render streams (up to 0.9 ms per launch at C4).
 #ifndef GR_CS_T
 #define GR_CS_T 16
 #endif
-constexpr int CS_T = GR_CS_T, CS_G = 1024 / GR_CS_T, CS_R = 24;
+#ifndef GR_CS_THREADS
+#define GR_CS_THREADS 256
+#endif
+#ifndef GR_CS_R
+#define GR_CS_R 96
+#endif
+constexpr int CS_T = GR_CS_T, CS_G = GR_CS_THREADS / GR_CS_T, CS_R = GR_CS_R;
 
-__global__ __launch_bounds__(1024) void k_tile_colscan(int cols, int tiles, const int* __restrict__ M,
+__global__ __launch_bounds__(GR_CS_THREADS) void k_tile_colscan(int cols, int tiles, const int* __restrict__ M,
                                                        int* __restrict__ S, int* __restrict__ T) {
   __shared__ int part[CS_G][CS_T + 1];
   const int tl = (int)threadIdx.x % CS_T, g = (int)threadIdx.x / CS_T;
@@ -2908,14 +2922,19 @@ __device__ __forceinline__ unsigned long long block_exclusive_scan(unsigned long
 }
 }  // extern "C++"
 
+// One workgroup of PLAN_THREADS (256 fits beside the render streams' splat kernels; see WI_THREADS).
+#ifndef GR_PLAN_THREADS
+#define GR_PLAN_THREADS 256
+#endif
+constexpr int PLAN_THREADS = GR_PLAN_THREADS;
 // Pair totals and the block level of the offsets scan (one workgroup): bsum[b] (k_preprocess's packed
 // block sums) is replaced by its exclusive scan, offsets[n] gets the packed grand total.  The packed
 // words cannot carry into each other as long as K < 2^31, which is checked against the exact total
 // (the sum of every block's two words) before the plan is trusted.
 __device__ __forceinline__ void plan_scan(unsigned long long* __restrict__ bsum, int blocks,
                                           unsigned long long* __restrict__ off_end, gr_plan* plan, gr_plan* host_plan) {
-  __shared__ unsigned long long sh[16];
-  const int tid = (int)threadIdx.x, per = (blocks + 1023) / 1024;
+  __shared__ unsigned long long sh[PLAN_THREADS / 64];
+  const int tid = (int)threadIdx.x, per = (blocks + PLAN_THREADS - 1) / PLAN_THREADS;
   const int b0 = min(blocks, tid * per), b1 = min(blocks, b0 + per);
   unsigned long long acc = 0, ex = 0;
   for (int b = b0; b < b1; ++b) {
@@ -2924,8 +2943,8 @@ __device__ __forceinline__ void plan_scan(unsigned long long* __restrict__ bsum,
     ex += (t & 0xffffffffull) + (t >> 32);
   }
   unsigned long long grand, exact;
-  const unsigned long long base = block_exclusive_scan<16>(acc, sh, grand);
-  (void)block_exclusive_scan<16>(ex, sh, exact);
+  const unsigned long long base = block_exclusive_scan<PLAN_THREADS / 64>(acc, sh, grand);
+  (void)block_exclusive_scan<PLAN_THREADS / 64>(ex, sh, exact);
   unsigned long long run = base;
   for (int b = b0; b < b1; ++b) {
     const unsigned long long t = bsum[b];
@@ -2946,7 +2965,7 @@ __device__ __forceinline__ void plan_scan(unsigned long long* __restrict__ bsum,
   }
 }
 
-__global__ __launch_bounds__(1024) void k_plan(unsigned long long* __restrict__ bsum, int blocks,
+__global__ __launch_bounds__(PLAN_THREADS) void k_plan(unsigned long long* __restrict__ bsum, int blocks,
                                                unsigned long long* __restrict__ off_end, gr_plan* plan,
                                                gr_plan* host_plan) {
   plan_scan(bsum, blocks, off_end, plan, host_plan);
@@ -2973,7 +2992,7 @@ __global__ __launch_bounds__(256) void k_offsets(int n, const unsigned long long
 struct HostPlans {
   gr_plan* p[PREP_MAX_VIEWS];
 };
-__global__ __launch_bounds__(1024) void k_plan_views(PrepBatch B, int n, HostPlans hp) {
+__global__ __launch_bounds__(PLAN_THREADS) void k_plan_views(PrepBatch B, int n, HostPlans hp) {
   const Geom& g = B.g[blockIdx.x];
   plan_scan(g.total, (n + 256) / 256, g.offsets + n, g.plan, hp.p[blockIdx.x]);
 }
@@ -3016,7 +3035,7 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
     mapped = (gr_plan*)attr.devicePointer;
   (void)hipGetLastError();  // a pageable pointer leaves an error code behind
   // exclusive scan of the packed counts: blocks (k_plan), then Gaussians (k_offsets)
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, g.total, blocks_for(n + 1), g.offsets + n, g.plan, mapped);
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(PLAN_THREADS), 0, s, g.total, blocks_for(n + 1), g.offsets + n, g.plan, mapped);
   GR_HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_offsets, dim3(blocks_for(n)), dim3(256), 0, s, n, (const unsigned long long*)g.counts,
                      (const unsigned long long*)g.total, g.offsets);
@@ -3071,7 +3090,7 @@ gr_status gr_fwd_prepare_views_async(int num_views, const gr_view* views, int n,
   else
     hipLaunchKernelGGL(k_preprocess_views<48>, dim3(blocks), dim3(256), 0, s, B, n, means, scales, colors, opacities);
   GR_HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_plan_views, dim3(num_views), dim3(1024), 0, s, B, n, hp);
+  hipLaunchKernelGGL(k_plan_views, dim3(num_views), dim3(PLAN_THREADS), 0, s, B, n, hp);
   GR_HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_offsets_views, dim3(blocks_for(n), num_views), dim3(256), 0, s, B, n);
   GR_HIP_TRY(hipGetLastError());
@@ -3177,7 +3196,7 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
         }
         GR_HIP_TRY(hipGetLastError());
       }
-      hipLaunchKernelGGL(k_work_items_zones, dim3(1), dim3(1024), 0, s, tiles, vk.tiles_x, (int)Kc,
+      hipLaunchKernelGGL(k_work_items_zones, dim3(1), dim3(WI_THREADS), 0, s, tiles, vk.tiles_x, (int)Kc,
                          Kr[0] > 0 ? (const int*)Tz[0] : nullptr, Kr[1] > 0 ? (const int*)Tz[1] : nullptr, b.ranges,
                          b.items, b.num_items, b.tile_item0);
       GR_HIP_TRY(hipGetLastError());
@@ -3206,12 +3225,12 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
       hipLaunchKernelGGL(k_pos_of, dim3(blocks_for(num_pairs)), dim3(256), 0, s, num_pairs, (const int2*)sc.pairs_sorted,
                          b.pairs, b.pos_of);
       GR_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
+      hipLaunchKernelGGL(k_work_items, dim3(1), dim3(WI_THREADS), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
                          b.tile_item0);
     }
   } else {
     GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * vtiles, s));
-    hipLaunchKernelGGL(k_work_items, dim3(1), dim3(1024), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
+    hipLaunchKernelGGL(k_work_items, dim3(1), dim3(WI_THREADS), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
                        b.tile_item0);
   }
   GR_HIP_TRY(hipGetLastError());

@@ -66,6 +66,8 @@ DIRECT_BACKWARD = os.environ.get("GR_DIRECT", "1") != "0"
 # read and the stream's gradient accumulator read and written once per batch instead of once per view
 # (at most REDUCE_BATCH views per batch, a stream's views split into equal batches)
 REDUCE_BATCH = max(1, min(16, int(os.environ.get("GR_REDUCE_BATCH", "16"))))
+# views in the last batch of each stream (0: near-equal batches only)
+REDUCE_TAIL = max(0, int(os.environ.get("GR_REDUCE_TAIL", "2")))
 # fused path: gradient assembly through the activations and the Adam update in one HIP pass per parameter
 # (gr_fit_param_step) instead of torch's autograd + foreach Adam (0 = torch)
 FUSED_STEP = os.environ.get("GR_FUSED_STEP", "1") != "0"
@@ -74,6 +76,7 @@ PREP_AHEAD = max(1, int(os.environ.get("GR_PREP_AHEAD", "6")))
 L_MAX_ACC = 8  # GR_FIT_MAX_ACC: stream accumulators gr_fit_param_step sums
 # views prepared together (gr_fwd_prepare_views_async: the parameters read once for the group)
 PREP_GROUP = max(1, min(4, int(os.environ.get("GR_PREP_GROUP", "4"))))
+PREP_FIRST = max(1, min(PREP_GROUP, int(os.environ.get("GR_PREP_FIRST", "1"))))
 
 
 # ------------------------------------------------------------------------------------------------
@@ -493,7 +496,9 @@ class ViewShardedFitter:
 
         def prepare(j):
             if j < len(views) and j not in ahead:
-                js = range(j, min(len(views), j + PREP_GROUP))  # none of them prepared yet (groups are contiguous)
+                # none of them prepared yet (groups are contiguous); the step's first group is PREP_FIRST views,
+                # so the first render starts after one view's preparation, not a group's
+                js = range(j, min(len(views), j + (PREP_FIRST if j == 0 else PREP_GROUP)))
                 with torch.cuda.stream(prep):
                     ahead.update(zip(js, tr.prepare_views_native(m, s, c, o, [self._fit_view(views[q], device) for q in js],
                                                                  [pins[q] for q in js])))
@@ -506,8 +511,10 @@ class ViewShardedFitter:
         sizes = []
         for k in range(ns):
             p = len(range(k, len(views), ns))
-            nb = max(1, -(-p // REDUCE_BATCH))
-            sizes.append([p // nb + (1 if b < p % nb else 0) for b in range(nb)])
+            # a short last batch (REDUCE_TAIL views): the reductions left when the renders end run alone
+            tail = REDUCE_TAIL if 0 < REDUCE_TAIL < p else 0
+            nb = max(1, -(-(p - tail) // REDUCE_BATCH))
+            sizes.append([(p - tail) // nb + (1 if b < (p - tail) % nb else 0) for b in range(nb)] + ([tail] if tail else []))
 
         def reduce_pending(k):
             if pending[k]:
