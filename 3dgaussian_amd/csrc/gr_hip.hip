@@ -797,48 +797,47 @@ __global__ __launch_bounds__(WI_THREADS) void k_work_items(int vtiles, const int
 }
 
 // Counting-sort path: per-tile pair totals of the core region (Tc) and of the tail region (Tt,
-// starting at Kc) are scanned into the virtual-tile ranges (2t: core, 2t+1: tail), then cut.
+// starting at Kc) are scanned into the virtual-tile ranges (2t: core, 2t+1: tail), then cut.  Thread i
+// owns a contiguous run of tiles: its run's totals are scanned across the block once (three block scans
+// instead of three per 256 tiles), then the run is walked again with running offsets.
 __global__ __launch_bounds__(WI_THREADS) void k_work_items_zones(int tiles, int tiles_x, int Kc, const int* __restrict__ Tc,
                                                            const int* __restrict__ Tt, int2* __restrict__ ranges,
                                                            int4* __restrict__ items, int* __restrict__ num_items,
                                                            int* __restrict__ tile_item0) {
   typedef hipcub::BlockScan<int, WI_THREADS> Scan;
   __shared__ typename Scan::TempStorage tmp;
-  __shared__ int carry, ccarry, tcarry;
-  if (threadIdx.x == 0) carry = ccarry = tcarry = 0;
-  __syncthreads();
-  for (int base = 0; base < tiles; base += WI_THREADS) {
-    const int t = base + (int)threadIdx.x;
-    const int nc = (t < tiles && Tc) ? Tc[t] : 0, nt = (t < tiles && Tt) ? Tt[t] : 0;  // null: an empty zone
-    int sc, totc, st, tott;
-    Scan(tmp).ExclusiveSum(nc, sc, totc);
-    __syncthreads();
-    Scan(tmp).ExclusiveSum(nt, st, tott);
-    __syncthreads();
-    const int2 rc = nc > 0 ? make_int2(ccarry + sc, ccarry + sc + nc) : make_int2(0, 0);
-    const int2 rt = nt > 0 ? make_int2(Kc + tcarry + st, Kc + tcarry + st + nt) : make_int2(0, 0);
-    const int chc = (nc + CH - 1) / CH, cht = (nt + CH - 1) / CH;
-    int excl, total;
-    Scan(tmp).ExclusiveSum(chc + cht, excl, total);
-    const int first = carry + excl;
-    if (t < tiles) {
-      ranges[2 * t] = rc;
-      ranges[2 * t + 1] = rt;
-      tile_item0[2 * t] = first;
-      tile_item0[2 * t + 1] = first + chc;
-      for (int c = 0; c < chc; ++c) items[first + c] = make_int4(2 * t, rc.x + c * CH, min(rc.y, rc.x + (c + 1) * CH), c);
-      for (int c = 0; c < cht; ++c)
-        items[first + chc + c] = make_int4(2 * t + 1, rt.x + c * CH, min(rt.y, rt.x + (c + 1) * CH), c);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      carry += total;
-      ccarry += totc;
-      tcarry += tott;
-    }
-    __syncthreads();
+  const int per = (tiles + WI_THREADS - 1) / WI_THREADS;
+  const int t0 = min(tiles, (int)threadIdx.x * per), t1 = min(tiles, t0 + per);
+  int sc = 0, st = 0, sch = 0;
+  for (int t = t0; t < t1; ++t) {
+    const int nc = Tc ? Tc[t] : 0, nt = Tt ? Tt[t] : 0;  // null: an empty zone
+    sc += nc;
+    st += nt;
+    sch += (nc + CH - 1) / CH + (nt + CH - 1) / CH;
   }
-  if (threadIdx.x == 0) *num_items = carry;
+  int total;
+  Scan(tmp).ExclusiveSum(sc, sc);
+  __syncthreads();
+  Scan(tmp).ExclusiveSum(st, st);
+  __syncthreads();
+  Scan(tmp).ExclusiveSum(sch, sch, total);
+  for (int t = t0; t < t1; ++t) {
+    const int nc = Tc ? Tc[t] : 0, nt = Tt ? Tt[t] : 0;
+    const int2 rc = nc > 0 ? make_int2(sc, sc + nc) : make_int2(0, 0);
+    const int2 rt = nt > 0 ? make_int2(Kc + st, Kc + st + nt) : make_int2(0, 0);
+    const int chc = (nc + CH - 1) / CH, cht = (nt + CH - 1) / CH;
+    ranges[2 * t] = rc;
+    ranges[2 * t + 1] = rt;
+    tile_item0[2 * t] = sch;
+    tile_item0[2 * t + 1] = sch + chc;
+    for (int c = 0; c < chc; ++c) items[sch + c] = make_int4(2 * t, rc.x + c * CH, min(rc.y, rc.x + (c + 1) * CH), c);
+    for (int c = 0; c < cht; ++c)
+      items[sch + chc + c] = make_int4(2 * t + 1, rt.x + c * CH, min(rt.y, rt.x + (c + 1) * CH), c);
+    sc += nc;
+    st += nt;
+    sch += chc + cht;
+  }
+  if (threadIdx.x == 0) *num_items = total;
 }
 
 // Staging pipeline for the 256-wide Gaussian batches of a work item: the records of batch b+1 are

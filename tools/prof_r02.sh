@@ -9,5 +9,5 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 GR_STREAMS=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/stats1 -o run --output-format csv -- python3 $R/bench.py --steps $STEPS --warmup $WARM --no-cpu-baseline --no-extra-modes > $O/bench_prof1.log 2>&1
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/stats3 -o run --output-format csv -- python3 $R/bench.py --steps $STEPS --warmup $WARM --no-cpu-baseline --no-extra-modes > $O/bench_prof3.log 2>&1
-cd $R && python tools/kstats.py $O/stats1 > $O/kernel_stats_1stream.txt && python tools/kstats.py $O/stats3 > $O/kernel_stats_3streams.txt
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/stats4 -o run --output-format csv -- python3 $R/bench.py --steps $STEPS --warmup $WARM --no-cpu-baseline --no-extra-modes > $O/bench_prof3.log 2>&1
+cd $R && python tools/kstats.py $O/stats1 > $O/kernel_stats_1stream.txt && python tools/kstats.py $O/stats4 > $O/kernel_stats_4streams.txt
