@@ -462,7 +462,7 @@ size_t tsort_cells_bound(int64_t K, int tiles) {
 size_t tile_sort_tmp_bytes(int64_t K, int tiles) {
   if (short_keys(tiles)) {
     const int st = tiles / 2;
-    return 3 * align_up(tsort_cells_bound(K, st) * sizeof(int)) + 2 * align_up((size_t)st * sizeof(int));
+    return 4 * align_up(tsort_cells_bound(K, st) * sizeof(int)) + 2 * align_up((size_t)st * sizeof(int));
   }
   size_t tmp = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const int2*)nullptr,
@@ -921,10 +921,37 @@ __device__ __forceinline__ int xcd_item(int b, int nwg) {
 constexpr int TS_RB = 9, TS_RH = 1 << (TS_RB - 1);  // relative tile keys in ts_place
 constexpr int TS_CQ = 8;    // tiles per thread per round of k_tile_place's cursor pass
 
-__global__ __launch_bounds__(256) void k_tile_count(int64_t K, int cw, int cols, int tiles,
-                                                    const uint16_t* __restrict__ keys, int* __restrict__ M) {
+// The two regions (zone 0: core pairs [0, Kc), zone 1: tail pairs [Kc, K)) are sorted by the same three
+// launches: the column blocks of zone 0 come first in the grid, then zone 1's (k_tile_colscan: blockIdx.y).
+struct TZone {
+  int64_t K;              // pairs of the region
+  int cw, cols;           // its tsort_plan
+  int zbase;              // emission index of its first pair
+  const uint16_t* keys;   // its keys and ids (emission order)
+  const int* ids;
+  int* M;                 // its count matrix, column scan and tile totals
+  int* S;
+  int* T;
+};
+struct TZones {
+  TZone z[2];
+};
+// Column block b of the combined grid -> (zone, column), XCD-aware within the grid.
+__device__ __forceinline__ int tzone_of(const TZones& Z, int& c) {
+  const int b = xcd_item(blockIdx.x, Z.z[0].cols + Z.z[1].cols);
+  const int zone = b < Z.z[0].cols ? 0 : 1;
+  c = b - (zone ? Z.z[0].cols : 0);
+  return zone;
+}
+
+__global__ __launch_bounds__(256) void k_tile_count(TZones Z, int tiles) {
   extern __shared__ int hist[];
-  const int c = xcd_item(blockIdx.x, cols);
+  int c;
+  const TZone& zz = Z.z[tzone_of(Z, c)];
+  const int64_t K = zz.K;
+  const int cw = zz.cw;
+  const uint16_t* __restrict__ keys = zz.keys;
+  int* __restrict__ M = zz.M;
   for (int t = threadIdx.x; t < tiles; t += 256) hist[t] = 0;
   __syncthreads();
   const int64_t k0 = (int64_t)c * cw, k1 = min(K, k0 + cw);
@@ -957,8 +984,13 @@ __global__ __launch_bounds__(256) void k_tile_count(int64_t K, int cw, int cols,
 #endif
 constexpr int CS_T = GR_CS_T, CS_G = GR_CS_THREADS / GR_CS_T, CS_R = GR_CS_R;
 
-__global__ __launch_bounds__(GR_CS_THREADS) void k_tile_colscan(int cols, int tiles, const int* __restrict__ M,
-                                                       int* __restrict__ S, int* __restrict__ T) {
+__global__ __launch_bounds__(GR_CS_THREADS) void k_tile_colscan(TZones Z, int tiles) {
+  const TZone& zz = Z.z[blockIdx.y];
+  if (zz.K == 0) return;  // an empty region: no counts, and k_work_items_zones gets no totals for it
+  const int cols = zz.cols;
+  const int* __restrict__ M = zz.M;
+  int* __restrict__ S = zz.S;
+  int* __restrict__ T = zz.T;
   __shared__ int part[CS_G][CS_T + 1];
   const int tl = (int)threadIdx.x % CS_T, g = (int)threadIdx.x / CS_T;
   const int t = (int)blockIdx.x * CS_T + tl;
@@ -1062,13 +1094,18 @@ __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int 
 #ifndef GR_PLACE_WAVES
 #define GR_PLACE_WAVES 3
 #endif
-__global__ __launch_bounds__(256, GR_PLACE_WAVES) void k_tile_place(int64_t K, int cw, int cols, int tiles, int bits,
-                                                    const uint16_t* __restrict__ keys, const int* __restrict__ ids_in,
-                                                    const int* __restrict__ S, const int2* __restrict__ ranges,
-                                                    int zone, int zbase, int* __restrict__ pairs_out,
+__global__ __launch_bounds__(256, GR_PLACE_WAVES) void k_tile_place(TZones Z, int tiles, int bits,
+                                                    const int2* __restrict__ ranges, int* __restrict__ pairs_out,
                                                     int* __restrict__ pos_of) {
   extern __shared__ int cur[];  // [waves][tiles]
-  const int c = xcd_item(blockIdx.x, cols);
+  int c;
+  const int zone = tzone_of(Z, c);
+  const TZone& zz = Z.z[zone];
+  const int64_t K = zz.K;
+  const int cw = zz.cw, zbase = zz.zbase;
+  const uint16_t* __restrict__ keys = zz.keys;
+  const int* __restrict__ ids_in = zz.ids;
+  const int* __restrict__ S = zz.S;
   const int waves = (int)blockDim.x >> 6, w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
   int* my = cur + (size_t)w * tiles;
   const int pw = cw / waves, nseg = pw / (64 * TS_SEG);
@@ -3169,43 +3206,40 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
       hipLaunchKernelGGL((k_emit_zones<uint16_t, false>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
                          (const int4*)g.rect, cnt, offs, (const float4*)g.rec, (uint16_t*)sc.keys_in, sc.ids_in);
       GR_HIP_TRY(hipGetLastError());
-      TSortPlan tp[2];
-      int* Sz[2];
-      int* Tz[2];
+      // one count matrix, column scan and tile totals per region; both regions sorted by the same launches
+      TZones Z;
       char* q = (char*)sc.sort_tmp;
-      int* M = (int*)q;
       const size_t cells = tsort_cells_bound(num_pairs, tiles);
-      q += align_up(cells * sizeof(int));
+      int waves = tsort_waves(tiles);
       for (int z = 0; z < 2; ++z) {
-        tp[z] = tsort_plan(Kr[z], tiles);
-        Sz[z] = (int*)q;
+        const TSortPlan tp = tsort_plan(Kr[z], tiles);
+        TZone& zz = Z.z[z];
+        zz.K = Kr[z];
+        zz.cw = tp.cw;
+        zz.cols = Kr[z] > 0 ? tp.cols : 0;
+        zz.zbase = z == 0 ? 0 : (int)Kc;
+        zz.keys = (const uint16_t*)sc.keys_in + (z == 0 ? 0 : Kc);
+        zz.ids = sc.ids_in + (z == 0 ? 0 : Kc);
+        zz.M = (int*)q;
         q += align_up(cells * sizeof(int));
-        Tz[z] = (int*)q;
+        zz.S = (int*)q;
+        q += align_up(cells * sizeof(int));
+        zz.T = (int*)q;
         q += align_up((size_t)tiles * sizeof(int));
+        waves = tp.waves;
       }
-      const uint16_t* kz[2] = {(const uint16_t*)sc.keys_in, (const uint16_t*)sc.keys_in + Kc};
-      const int* iz[2] = {sc.ids_in, sc.ids_in + Kc};
-      for (int z = 0; z < 2; ++z) {
-        if (Kr[z] > 0) {
-          hipLaunchKernelGGL(k_tile_count, dim3(tp[z].cols), dim3(256), (size_t)tiles * sizeof(int), s, Kr[z], tp[z].cw,
-                             tp[z].cols, tiles, kz[z], M);
-          GR_HIP_TRY(hipGetLastError());
-          hipLaunchKernelGGL(k_tile_colscan, dim3((tiles + CS_T - 1) / CS_T), dim3(CS_T * CS_G), 0, s, tp[z].cols, tiles,
-                             (const int*)M, Sz[z], Tz[z]);
-        }
-        GR_HIP_TRY(hipGetLastError());
-      }
+      const int cols = Z.z[0].cols + Z.z[1].cols;  // >= 1: num_pairs > 0
+      hipLaunchKernelGGL(k_tile_count, dim3(cols), dim3(256), (size_t)tiles * sizeof(int), s, Z, tiles);
+      GR_HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_tile_colscan, dim3((tiles + CS_T - 1) / CS_T, 2), dim3(CS_T * CS_G), 0, s, Z, tiles);
+      GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_work_items_zones, dim3(1), dim3(WI_THREADS), 0, s, tiles, vk.tiles_x, (int)Kc,
-                         Kr[0] > 0 ? (const int*)Tz[0] : nullptr, Kr[1] > 0 ? (const int*)Tz[1] : nullptr, b.ranges,
+                         Kr[0] > 0 ? (const int*)Z.z[0].T : nullptr, Kr[1] > 0 ? (const int*)Z.z[1].T : nullptr, b.ranges,
                          b.items, b.num_items, b.tile_item0);
       GR_HIP_TRY(hipGetLastError());
-      for (int z = 0; z < 2; ++z) {
-        if (Kr[z] == 0) continue;
-        hipLaunchKernelGGL(k_tile_place, dim3(tp[z].cols), dim3(64 * tp[z].waves), (size_t)tiles * sizeof(int) * tp[z].waves,
-                           s, Kr[z], tp[z].cw, tp[z].cols, tiles, bits_for((uint32_t)tiles), kz[z], iz[z],
-                           (const int*)Sz[z], (const int2*)b.ranges, z, z == 0 ? 0 : (int)Kc, b.pairs, b.pos_of);
-        GR_HIP_TRY(hipGetLastError());
-      }
+      hipLaunchKernelGGL(k_tile_place, dim3(cols), dim3(64 * waves), (size_t)tiles * sizeof(int) * waves, s, Z, tiles,
+                         bits_for((uint32_t)tiles), (const int2*)b.ranges, b.pairs, b.pos_of);
+      GR_HIP_TRY(hipGetLastError());
     } else {
       // radix sort of the whole pair array on virtual-tile keys (> TSORT_MAX_TILES tiles)
       hipLaunchKernelGGL((k_emit_zones<uint32_t, true>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
