@@ -3182,7 +3182,7 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
   if (st != GR_OK) return st;
   if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
   if (plan->num_pairs < 0 || plan->num_slots < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
-  if (!l1 && (!out_rgb || !saved)) return set_error(GR_ERR_INVALID_ARGUMENT, "out_rgb and saved are required");
+  if (!l1 && !saved) return set_error(GR_ERR_INVALID_ARGUMENT, "saved is required");
   if (l1 && (!ws || ws_bytes < gr_bwd_bytes(v, n, plan) || !l1_loss_out))
     return set_error(GR_ERR_WORKSPACE, "gr_fwd_render_l1: backward workspace too small (or null loss)");
   if (n > 0 && (!geom || !bins)) return set_error(GR_ERR_INVALID_ARGUMENT, "null workspace");

@@ -604,7 +604,7 @@ class ViewShardedFitter:
             streams[k].wait_event(pv.event)
             pv.geom.record_stream(streams[k])
             with torch.cuda.stream(streams[k]):
-                _, _, _, rs = tr.forward_native(m, s, c, o, pv.gv, pv)
+                _, _, _, rs = tr.forward_native(m, s, c, o, pv.gv, pv, images=False)  # gr_bwd_fit reads the sums
                 pv = None
                 tr.backward_fit_native(m, s, c, o, rs, self.targets[i], self.masks[i] if w_sil > 0.0 else None, w_sil,
                                        self.depths[i], self.w_depth, g_scale, losses_v[j:j + 1], acc[k], accumulate=j >= ns)

@@ -274,10 +274,11 @@ def prepare_views_native(means, scales, colors, opacities, gvs, plan_hosts) -> l
 
 
 def forward_native(means, scales, colors, opacities, gv: _native.GrView, prepared: Optional[Prepared] = None,
-                   want_depth: bool = True):
+                   want_depth: bool = True, images: bool = True):
     """Run gr_fwd_prepare(_async) + gr_fwd_render.  Returns (out, alpha, depth, RenderState).
     ``want_depth=False`` on a no_depth_grad view: no depth output (None) and no depth sums (gr_fwd_render
-    with out_depth = NULL: the forward skips its depth channel)."""
+    with out_depth = NULL: the forward skips its depth channel).  ``images=False``: no output images at
+    all (None, None, None; the saved sums for the backward only, as the fit loop needs)."""
     L = _native.lib()
     dev = means.device
     n = int(means.shape[0])
@@ -292,9 +293,10 @@ def forward_native(means, scales, colors, opacities, gv: _native.GrView, prepare
     plan = prepared.plan()
     bins = torch.empty((_ws_round(L.gr_bins_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8,
                        device=dev)
-    out = torch.empty((H, W, 3), dtype=torch.float32, device=dev)
-    alpha = torch.empty((H, W), dtype=torch.float32, device=dev)
-    depth = torch.empty((H, W), dtype=torch.float32, device=dev) if (want_depth or not gv.no_depth_grad) else None
+    out = torch.empty((H, W, 3), dtype=torch.float32, device=dev) if images else None
+    alpha = torch.empty((H, W), dtype=torch.float32, device=dev) if images else None
+    depth = (torch.empty((H, W), dtype=torch.float32, device=dev)
+             if images and (want_depth or not gv.no_depth_grad) else None)
     saved = torch.empty((int(L.gr_saved_floats(ctypes.byref(gv))),), dtype=torch.float32, device=dev)
     # scratch is released when this function returns; the caching allocator keeps it stream-ordered
     scratch = torch.empty((_ws_round(L.gr_fwd_scratch_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),),

@@ -136,8 +136,9 @@ size_t gr_fwd_scratch_bytes(const gr_view* v, int n, const gr_plan* plan);
 size_t gr_saved_floats(const gr_view* v);
 
 /* Emit pairs + sort by tile + tile ranges + forward splat.  Outputs:
- *   out_rgb (H,W,3) clamp((bg+C)/(1+W),0,1); out_alpha (H,W) (may be NULL); out_depth (H,W)
- *   (may be NULL); saved (5*H*W floats) accumulators kept for gr_bwd.  A view with no_depth_grad
+ *   out_rgb (H,W,3) clamp((bg+C)/(1+W),0,1) (may be NULL: a caller that only needs the backward, as
+ *   the fit loop); out_alpha (H,W) (may be NULL); out_depth (H,W) (may be NULL); saved (5*H*W floats)
+ *   accumulators kept for gr_bwd (required).  A view with no_depth_grad
  *   and out_depth NULL skips the depth channel altogether (its saved depth sums are 0). */
 gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins,
                         size_t bins_bytes, void* scratch, size_t scratch_bytes, float* out_rgb,
