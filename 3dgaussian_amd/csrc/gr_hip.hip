@@ -1715,8 +1715,10 @@ __device__ __forceinline__ void l1_tile_epilogue(const ViewK& v, int tile, int t
 // no_depth_grad); 3: as 2 without the depth channel (no_depth_grad views rendered with no depth output;
 // the saved depth sums are then 0 and unused); 4: as 3, with the fit loss's upstream fragments and tile
 // L1 sums made in the epilogue (gr_fwd_render_l1, the fused fit path).
+// Modes 1/2 at 5 waves per SIMD: at 6 they spill (MODE 1: 5 VGPRs); same-box A/B, C4 depth-loss views,
+// MODE 1: 330/334 -> 320/318 us (profiles/r02o_ab_variants.txt).
 #ifndef GR_FWD_WAVES
-#define GR_FWD_WAVES 6
+#define GR_FWD_WAVES 5
 #endif
 #ifndef GR_FWD_WAVES3
 #define GR_FWD_WAVES3 6
