@@ -1268,6 +1268,49 @@ __device__ __forceinline__ void split3_frag2(const f32x2_t (&v)[4], s16x8 (&f)[3
   split3_frag(u, f);
 }
 
+// f16 two-piece split (forward MODE 3/4 when GR_FWD_F16): the operands are pre-scaled by 2^GR_F16_S
+// (folded into the exponent arguments) so the footprint's smallest weights stay normal in f16.
+// hi = f16(x) truncated (v_cvt_pkrtz), lo = x - hi exact in f32 (one v_fma_mix_f32 per value reads
+// hi's f16 half), truncated to f16: |x - hi - lo| <= 2^-20 |x|; the dropped lo*lo <= 2^-20 of the
+// product.  Four instructions per pair of values instead of five.  Same-box A/B at C4 (fit path):
+// forward 145/154 -> 140/135 us, step 1369-1380 -> 1403-1408 Mpx/s; fit-path errors vs the float64 oracle
+// out 1e-7, gradients <= 1.2e-5 (profiles/r02p_ab_f16.txt).
+#ifndef GR_FWD_F16
+#define GR_FWD_F16 1
+#endif
+#ifndef GR_F16_S
+#define GR_F16_S 12
+#endif
+__device__ __forceinline__ float f16_resid_lo(float x, unsigned h) {  // x - f16(h[15:0])
+  float r;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
+  return r;
+}
+__device__ __forceinline__ float f16_resid_hi(float x, unsigned h) {  // x - f16(h[31:16])
+  float r;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
+  return r;
+}
+__device__ __forceinline__ void split2h_frag2(const f32x2_t (&v)[4], s16x8 (&f)[2]) {
+  unsigned h[4], l[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    h[p] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(v[p].x, v[p].y));
+    l[p] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(f16_resid_lo(v[p].x, h[p]), f16_resid_hi(v[p].y, h[p])));
+  }
+  f[0] = as_frag(make_uint4(h[0], h[1], h[2], h[3]));
+  f[1] = as_frag(make_uint4(l[0], l[1], l[2], l[3]));
+}
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 mfma16h(const s16x8& a, const s16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16h_split2(const s16x8 (&a)[2], const s16x8 (&b)[2], f32x4 c) {
+  c = mfma16h(a[1], b[0], c);
+  c = mfma16h(a[0], b[1], c);
+  return mfma16h(a[0], b[0], c);
+}
+
 // Staged batch layout of the split-precision forward: nine planes of TP floats (px py qx qy o r g b z),
 // one LDS-DMA dword per lane and field.  A lane's eight Gaussians of a step are then consecutive in every
 // plane (two ds_read_b128 per field) and the operand arithmetic runs on packed f32 pairs of Gaussians
@@ -1325,6 +1368,9 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
   int idn = stage_id(k0 + TP + tid, k1, pairs);
   int buf = 0;
   const f32x2_t X = {xc, xc}, Y = {yc, yc};
+  constexpr bool F16 = GR_FWD_F16 && !PRECISE && !ZCH;
+  const f32x2_t SS = {(float)GR_F16_S, (float)GR_F16_S};
+  (void)SS;
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
     stage_wait();
     GR_STAGE_SYNC();
@@ -1354,20 +1400,30 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const f32x2_t dx = X - px[p], dy = Y - py[p];
+#if GR_FWD_F16
+        const f32x2_t tx = F16 ? __builtin_elementwise_fma(dx * qx[p], dx, SS) : (dx * qx[p]) * dx;
+        const f32x2_t ty = F16 ? __builtin_elementwise_fma(dy * qy[p], dy, SS) : (dy * qy[p]) * dy;
+#else
         const f32x2_t tx = (dx * qx[p]) * dx, ty = (dy * qy[p]) * dy;
+#endif
         const f32x2_t ex = {__builtin_amdgcn_exp2f(tx.x), __builtin_amdgcn_exp2f(tx.y)};
         bv[p] = f32x2_t{__builtin_amdgcn_exp2f(ty.x), __builtin_amdgcn_exp2f(ty.y)};
         oe[p] = o[p] * ex;
         aW[p] = oe[p];
         if constexpr (ZCH) aD[p] = oe[p] * z[p];
       }
-      s16x8 fb[3], f3[3];
+      s16x8 fb[3], f3[3], fb2h[2];
       if constexpr (PRECISE) {
         split3_frag2(bv, fb);
         split3_frag2(aW, f3);
         cW = mfma16_split3(f3, fb, cW);
         split3_frag2(aD, f3);
         cD = mfma16_split3(f3, fb, cD);
+      } else if (F16) {  // f16 pieces of the pre-scaled operands (no depth channel)
+        s16x8 f2[2];
+        split2h_frag2(bv, fb2h);
+        split2h_frag2(aW, f2);
+        cW = mfma16h_split2(f2, fb2h, cW);
       } else {  // no depth gradient will follow: W and D need only what the colours need
         s16x8 f2b[2], f2[2];
         split2_frag2(bv, f2b);
@@ -1383,6 +1439,23 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
       if constexpr (!TAIL) {
         f32x2_t c[4], a[4];
         s16x8 f2[2];
+        if constexpr (F16) {
+          ld(5, c);
+#pragma unroll
+          for (int p = 0; p < 4; ++p) a[p] = oe[p] * c[p];
+          split2h_frag2(a, f2);
+          cR = mfma16h_split2(f2, fb2h, cR);
+          ld(6, c);
+#pragma unroll
+          for (int p = 0; p < 4; ++p) a[p] = oe[p] * c[p];
+          split2h_frag2(a, f2);
+          cG = mfma16h_split2(f2, fb2h, cG);
+          ld(7, c);
+#pragma unroll
+          for (int p = 0; p < 4; ++p) a[p] = oe[p] * c[p];
+          split2h_frag2(a, f2);
+          cB = mfma16h_split2(f2, fb2h, cB);
+        } else {
         ld(5, c);
 #pragma unroll
         for (int p = 0; p < 4; ++p) a[p] = oe[p] * c[p];
@@ -1398,6 +1471,7 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
         for (int p = 0; p < 4; ++p) a[p] = oe[p] * c[p];
         split2_frag2(a, f2);
         cB = mfma16_split2<PRECISE>(f2, fb, cB);
+        }
       }
     }
   }
@@ -1748,6 +1822,13 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
     fwd_accumulate_bf16<true, MODE == 1, MODE < 3>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
   else
     fwd_accumulate_bf16<false, MODE == 1, MODE < 3>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
+  if constexpr (GR_FWD_F16 && MODE >= 3) {  // both operands carried 2^GR_F16_S (exact power-of-two rescale)
+    const float sc = __builtin_ldexpf(1.0f, -2 * GR_F16_S);
+    cW *= sc;
+    cR *= sc;
+    cG *= sc;
+    cB *= sc;
+  }
   __syncthreads();
   {  // lane holds C[x = 4*gs + r][y = li]: pixel index y*16 + x, 4 consecutive x
     float* rw = smem + wave * 5 * TP + li * T + 4 * gs;
