@@ -1268,18 +1268,23 @@ __device__ __forceinline__ void split3_frag2(const f32x2_t (&v)[4], s16x8 (&f)[3
   split3_frag(u, f);
 }
 
-// f16 two-piece split (forward MODE 3/4 when GR_FWD_F16): the operands are pre-scaled by 2^GR_F16_S
-// (folded into the exponent arguments) so the footprint's smallest weights stay normal in f16.
+// f16 two-piece split (forward MODE 3/4 when GR_FWD_F16): the operands are pre-scaled (folded into the
+// exponent arguments) so the footprint's smallest weights stay normal in f16: B = ey by 2^GR_F16_SB
+// (ey <= 1, so B <= 2^12), A = o c ex by 2^GR_F16_SA (finite for opacities up to 4094; colours are
+// clamped to [0, 1]); the accumulators are rescaled by 2^-(SA+SB), exactly.
 // hi = f16(x) truncated (v_cvt_pkrtz), lo = x - hi exact in f32 (one v_fma_mix_f32 per value reads
 // hi's f16 half), truncated to f16: |x - hi - lo| <= 2^-20 |x|; the dropped lo*lo <= 2^-20 of the
 // product.  Four instructions per pair of values instead of five.  Same-box A/B at C4 (fit path):
-// forward 145/154 -> 140/135 us, step 1369-1380 -> 1403-1408 Mpx/s; fit-path errors vs the float64 oracle
+// forward 145/154 -> 140/135 us, step 1369-1380 -> 1403-1408 Mpx/s (A/B at SA = SB = 12); fit-path errors vs the float64 oracle
 // out 1e-7, gradients <= 1.2e-5 (profiles/r02p_ab_f16.txt).
 #ifndef GR_FWD_F16
 #define GR_FWD_F16 1
 #endif
-#ifndef GR_F16_S
-#define GR_F16_S 12
+#ifndef GR_F16_SA
+#define GR_F16_SA 4
+#endif
+#ifndef GR_F16_SB
+#define GR_F16_SB 12
 #endif
 __device__ __forceinline__ float f16_resid_lo(float x, unsigned h) {  // x - f16(h[15:0])
   float r;
@@ -1369,8 +1374,9 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
   int buf = 0;
   const f32x2_t X = {xc, xc}, Y = {yc, yc};
   constexpr bool F16 = GR_FWD_F16 && !PRECISE && !ZCH;
-  const f32x2_t SS = {(float)GR_F16_S, (float)GR_F16_S};
-  (void)SS;
+  const f32x2_t SA = {(float)GR_F16_SA, (float)GR_F16_SA}, SB = {(float)GR_F16_SB, (float)GR_F16_SB};
+  (void)SA;
+  (void)SB;
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
     stage_wait();
     GR_STAGE_SYNC();
@@ -1401,8 +1407,8 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
       for (int p = 0; p < 4; ++p) {
         const f32x2_t dx = X - px[p], dy = Y - py[p];
 #if GR_FWD_F16
-        const f32x2_t tx = F16 ? __builtin_elementwise_fma(dx * qx[p], dx, SS) : (dx * qx[p]) * dx;
-        const f32x2_t ty = F16 ? __builtin_elementwise_fma(dy * qy[p], dy, SS) : (dy * qy[p]) * dy;
+        const f32x2_t tx = F16 ? __builtin_elementwise_fma(dx * qx[p], dx, SA) : (dx * qx[p]) * dx;
+        const f32x2_t ty = F16 ? __builtin_elementwise_fma(dy * qy[p], dy, SB) : (dy * qy[p]) * dy;
 #else
         const f32x2_t tx = (dx * qx[p]) * dx, ty = (dy * qy[p]) * dy;
 #endif
@@ -1822,8 +1828,8 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
     fwd_accumulate_bf16<true, MODE == 1, MODE < 3>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
   else
     fwd_accumulate_bf16<false, MODE == 1, MODE < 3>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
-  if constexpr (GR_FWD_F16 && MODE >= 3) {  // both operands carried 2^GR_F16_S (exact power-of-two rescale)
-    const float sc = __builtin_ldexpf(1.0f, -2 * GR_F16_S);
+  if constexpr (GR_FWD_F16 && MODE >= 3) {  // the operands carried 2^SA and 2^SB (exact power-of-two rescale)
+    const float sc = __builtin_ldexpf(1.0f, -(GR_F16_SA + GR_F16_SB));
     cW *= sc;
     cR *= sc;
     cG *= sc;

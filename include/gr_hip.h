@@ -89,6 +89,8 @@ typedef struct gr_view {
 /*   means (N,3), scales (N,3), colors (N,3) [color_dim 3] or SH deg-1 (N,4,3) [color_dim 12]   */
 /*   (extension: degree-3 coefficients (N,16,3) [color_dim 48], basis in DESIGN.md §2),           */
 /*   opacities (N,), all float32 contiguous.                                                   */
+/*   Views rendered with no_depth_grad and no depth output (the fit path) take f16 operand      */
+/*   pieces scaled by 2^4: opacities must stay below 4094 there (sigmoid outputs always do).    */
 /* ------------------------------------------------------------------------------------------ */
 
 /* Sizes produced by gr_fwd_prepare for one view. */

@@ -155,3 +155,31 @@ def test_fit_path_on_fitted_state_vs_dense(pkg, cuda):
     print("fitted C4 state, fit path vs dense sample:", {k: f"{e:.2e}" for k, e in errs.items()})
     for k, e in errs.items():
         assert e <= 1e-4, (k, e)
+
+
+@pytest.mark.parametrize("opac_range", [(1e-4, 1e-3), (0.0, 1.0), (100.0, 3000.0)])
+def test_fit_mode_f16_operand_range(pkg, cuda, opac_range):
+    """The fit-path forward (no depth channel) multiplies on f16 operand pieces pre-scaled by 2^4 (A) and
+    2^12 (B): opacities from 1e-4 (operands near the f16 subnormal range) up to 3000 (near the documented
+    4094 limit, include/gr_hip.h) stay within the parity bar vs the float64 binned oracle."""
+    tr = pkg.torch_renderer
+    rng = np.random.default_rng(7)
+    sc = orc.synthetic_scene(3000, seed=3, scale=0.05)
+    lo, hi = opac_range
+    sc = orc.Scene(sc.means, sc.scales, sc.colors, rng.uniform(lo, hi, sc.opacities.shape).astype(np.float32))
+    view, proj = orc.orbit_cameras(4, 160, 120)[2]
+    W, H = 160, 120
+    g_rgb = rng.standard_normal((H, W, 3)).astype(np.float32)
+    g_a = rng.standard_normal((H, W)).astype(np.float32)
+    t = [torch.from_numpy(a).to(cuda) for a in sc.arrays()]
+    out, alpha, grads = _fit_mode(tr, t, view, proj, W, H, g_rgb, g_a, cuda)
+    v = orc.make_view(view, proj, W, H, None, cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF)
+    o_out, o_a, _ = orc.forward(v, sc, binned=True)
+    o_grads = orc.backward(v, sc, g_rgb, g_a, np.zeros((H, W), np.float32), binned=True)
+    errs = {"out": orc.rel_l2(out.cpu().numpy(), o_out), "alpha": orc.rel_l2(alpha.cpu().numpy(), o_a)}
+    for k, g, og in zip(GRADS, grads, o_grads):
+        errs[k] = orc.rel_l2(g.cpu().numpy(), og)
+    print(f"opacities {opac_range}:", {k: f"{e:.2e}" for k, e in errs.items()})
+    assert np.isfinite(out.cpu().numpy()).all()
+    for k, e in errs.items():
+        assert e <= 1e-4, (k, e)
