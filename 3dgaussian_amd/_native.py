@@ -41,6 +41,7 @@ class GrView(ctypes.Structure):
         ("cutoff", ctypes.c_float),
         ("core_cutoff", ctypes.c_float),
         ("no_depth_grad", ctypes.c_int),
+        ("background_dev", ctypes.c_void_p),  # optional device pointer to the 3 background floats
     ]
 
 
@@ -75,6 +76,12 @@ class GrReduceView(ctypes.Structure):
 
     _fields_ = [("view", GrView), ("plan", GrPlan), ("geom", ctypes.c_void_p), ("bins", ctypes.c_void_p),
                 ("ws", ctypes.c_void_p)]
+
+
+class GrSumsView(ctypes.Structure):
+    """gr_sums_view (include/gr_hip.h): one view of a gr_reduce_sums batch."""
+
+    _fields_ = [("view", GrView), ("sums", ctypes.c_void_p)]
 
 
 class NativeLibraryError(ImportError):
@@ -117,6 +124,10 @@ _SIG = {
     "gr_bwd_splat": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_size_t, _P]),
     "gr_reduce_views": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(GrReduceView), ctypes.c_int, _P, _P, _P, ctypes.c_int,
                                        _P, _P, _P, _P, _P, ctypes.c_int, _P]),
+    "gr_view_sums_floats": (ctypes.c_size_t, [ctypes.c_int]),
+    "gr_gather_view": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, _P, _P]),
+    "gr_reduce_sums": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(GrSumsView), ctypes.c_int, _P, _P, _P, ctypes.c_int,
+                                      _P, _P, _P, _P, _P, ctypes.c_int, _P]),
     "gr_render_u8": (ctypes.c_int, [ctypes.POINTER(GrRenderParams), ctypes.c_int, _P, _P, _P, _P, _P]),
     "gr_geom_layout": (None, [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
     "gr_bins_layout": (None, [_VP, ctypes.c_int, _PP, ctypes.POINTER(ctypes.c_size_t)]),

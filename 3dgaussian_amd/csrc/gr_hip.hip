@@ -89,8 +89,12 @@ struct ViewK {
   float bg[3];
   float cam[3];
   float cutoff;
-  float core;  // core radius of the two-zone footprint (= cutoff: one zone)
+  float core;         // core radius of the two-zone footprint (= cutoff: one zone)
+  const float* bgp;   // gr_view.background_dev: the background read on the device (else bg)
 };
+
+// Background channel k of the view (gr_view.background_dev when set: one cached load).
+__device__ __forceinline__ float view_bg(const ViewK& v, int k) { return v.bgp ? v.bgp[k] : v.bg[k]; }
 
 ViewK make_viewk(const gr_view* v) {
   ViewK k;
@@ -104,6 +108,7 @@ ViewK make_viewk(const gr_view* v) {
   std::memcpy(k.cam, v->cam_pos, sizeof(k.cam));
   k.cutoff = v->cutoff > 0.0f ? v->cutoff : 7.0f;
   k.core = (v->core_cutoff > 0.0f && v->core_cutoff < k.cutoff) ? v->core_cutoff : k.cutoff;
+  k.bgp = v->background_dev;
   return k;
 }
 
@@ -295,12 +300,14 @@ struct Geom {
   unsigned long long* offsets;  // n+1, packed Cnt2
   gr_plan* plan;                // device copy of the plan (gr_fwd_prepare_async copies it to the host)
   unsigned long long* total;    // [blocks of k_preprocess] exact per-block totals of kept pairs (overflow check)
+  float* omax;                  // [blocks of k_preprocess] largest opacity of the block's kept Gaussians
+  int* f16_sa;                  // [1] exponent pre-scale of the f16 forward's A operands (k_plan, f16_sa_of)
   void* scan_tmp;
   size_t scan_tmp_bytes;
 };
 
 // off: [0] records, [1] rect, [2] counts, [3] offsets, [4] device copy of the plan + exact per-block
-//      totals, [5] scan temp (= end of the fixed part)
+//      totals + per-block opacity maxima + the f16 pre-scale, [5] scan temp (= end of the fixed part)
 size_t geom_fixed(int n, size_t off[GR_GEOM_PARTS]) {
   size_t o = 0;
   const size_t nn = (size_t)(n > 0 ? n : 1);
@@ -308,7 +315,7 @@ size_t geom_fixed(int n, size_t off[GR_GEOM_PARTS]) {
   off[1] = o; o = align_up(o + nn * sizeof(int4));
   off[2] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
   off[3] = o; o = align_up(o + (nn + 1) * sizeof(unsigned long long));
-  off[4] = o; o = align_up(o + sizeof(gr_plan) + (nn / 256 + 2) * sizeof(unsigned long long));
+  off[4] = o; o = align_up(o + sizeof(gr_plan) + (nn / 256 + 2) * (sizeof(unsigned long long) + sizeof(float)) + 16);
   off[5] = o;
   return o;
 }
@@ -333,6 +340,8 @@ Geom geom_view(void* base, int n) {
   g.counts = (unsigned long long*)(b + off[2]);
   g.offsets = (unsigned long long*)(b + off[3]);
   g.total = (unsigned long long*)(b + off[4] + sizeof(gr_plan));
+  g.omax = (float*)(g.total + (size_t)n / 256 + 2);
+  g.f16_sa = (int*)(g.omax + (size_t)n / 256 + 2);
   g.scan_tmp = b + fixed;
   g.scan_tmp_bytes = 0;
   return g;
@@ -531,14 +540,26 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, int n, const float*
   }
   unsigned long long kept = 0;
   if (i < n) kept = preprocess_one<CD>(v, i, means, scales, colors, opac, g);
+  // the largest opacity of a kept Gaussian (the f16 forward's operand range, f16_sa_of)
+  float om = kept != 0 ? g.rec[(size_t)REC4 * i + 1].x : 0.0f;
   // the block's packed pair counts (core | tail << 32; a block's counts cannot carry): k_plan scans the
   // blocks, k_offsets the Gaussians inside each block
   __shared__ unsigned long long wsum[4];
+  __shared__ float wmax[4];
 #pragma unroll
-  for (int m = 1; m < 64; m <<= 1) kept += __shfl_xor(kept, m);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = kept;
+  for (int m = 1; m < 64; m <<= 1) {
+    kept += __shfl_xor(kept, m);
+    om = fmaxf(om, __shfl_xor(om, m));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    wsum[threadIdx.x >> 6] = kept;
+    wmax[threadIdx.x >> 6] = om;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) g.total[blockIdx.x] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+  if (threadIdx.x == 0) {
+    g.total[blockIdx.x] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+    g.omax[blockIdx.x] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+  }
 }
 
 // One Gaussian in one view from its loaded parameters (k_preprocess, k_preprocess_views).
@@ -607,6 +628,7 @@ __global__ __launch_bounds__(256) void k_preprocess_views(PrepBatch B, int n, co
     op = opac[i];
   }
   __shared__ unsigned long long wsum[PREP_MAX_VIEWS][4];
+  __shared__ float wmax[PREP_MAX_VIEWS][4];
   for (int k = 0; k < B.nv; ++k) {
     const Geom& g = B.g[k];
     if (i == n) {
@@ -618,14 +640,23 @@ __global__ __launch_bounds__(256) void k_preprocess_views(PrepBatch B, int n, co
     }
     unsigned long long kept = 0;
     if (i < n) kept = preprocess_vals<CD>(B.v[k], i, mx, my, mz, s0, s1, colors + (size_t)CD * i, op, g);
+    float om = kept != 0 ? fmaxf(op, 0.0f) : 0.0f;
 #pragma unroll
-    for (int m = 1; m < 64; m <<= 1) kept += __shfl_xor(kept, m);
-    if ((threadIdx.x & 63) == 0) wsum[k][threadIdx.x >> 6] = kept;
+    for (int m = 1; m < 64; m <<= 1) {
+      kept += __shfl_xor(kept, m);
+      om = fmaxf(om, __shfl_xor(om, m));
+    }
+    if ((threadIdx.x & 63) == 0) {
+      wsum[k][threadIdx.x >> 6] = kept;
+      wmax[k][threadIdx.x >> 6] = om;
+    }
   }
   __syncthreads();
-  if ((int)threadIdx.x < B.nv)
-    B.g[threadIdx.x].total[blockIdx.x] = (wsum[threadIdx.x][0] + wsum[threadIdx.x][1]) +
-                                         (wsum[threadIdx.x][2] + wsum[threadIdx.x][3]);
+  if ((int)threadIdx.x < B.nv) {
+    const int k = threadIdx.x;
+    B.g[k].total[blockIdx.x] = (wsum[k][0] + wsum[k][1]) + (wsum[k][2] + wsum[k][3]);
+    B.g[k].omax[blockIdx.x] = fmaxf(fmaxf(wmax[k][0], wmax[k][1]), fmaxf(wmax[k][2], wmax[k][3]));
+  }
 }
 
 constexpr int EWIN = 4096;  // pairs staged in LDS per emit block
@@ -1286,6 +1317,16 @@ __device__ __forceinline__ void split3_frag2(const f32x2_t (&v)[4], s16x8 (&f)[3
 #ifndef GR_F16_SB
 #define GR_F16_SB 12
 #endif
+// The A pre-scale of a view: 2^GR_F16_SA while its largest opacity (of a kept Gaussian) is below 2^11,
+// lowered by one per binade above, so o * c * ex * 2^sa <= 2^15 always (no inf, whatever the opacities;
+// k_plan computes it from k_preprocess's per-block maxima).  Views with opacities in (0, 2048) - every
+// fit, whose opacities are sigmoid outputs - get exactly GR_F16_SA.
+__device__ __forceinline__ int f16_sa_of(float omax) {
+  if (!(omax <= 3.0e38f)) return GR_F16_SA;  // inf / NaN opacities give inf / NaN outputs in any precision
+  int e = 0;
+  (void)frexpf(omax, &e);  // omax <= 2^e
+  return GR_F16_SA - (e > 11 ? e - 11 : 0);
+}
 __device__ __forceinline__ float f16_resid_lo(float x, unsigned h) {  // x - f16(h[15:0])
   float r;
   asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
@@ -1364,7 +1405,7 @@ __device__ __forceinline__ void glds4_planes(const float4* rec, const float* z, 
 template <bool TAIL, bool PRECISE, bool ZCH = true>
 __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, int k1, int tid, int wave, float xc, float yc,
                                                     int gq, const int* __restrict__ pairs, const float4* __restrict__ rec,
-                                                    f32x4& cW, f32x4& cR, f32x4& cG, f32x4& cB, f32x4& cD) {
+                                                    f32x4& cW, f32x4& cR, f32x4& cG, f32x4& cB, f32x4& cD, float sa) {
   constexpr int BUF = FWD_PLANES * TP;  // floats per buffer
   auto stage = [&](int g, int b) {
     glds4_planes<TAIL, ZCH>(rec_of(g, n, rec), zrec_of(g, n, rec), smem + b * BUF + 64 * wave);
@@ -1374,7 +1415,7 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
   int buf = 0;
   const f32x2_t X = {xc, xc}, Y = {yc, yc};
   constexpr bool F16 = GR_FWD_F16 && !PRECISE && !ZCH;
-  const f32x2_t SA = {(float)GR_F16_SA, (float)GR_F16_SA}, SB = {(float)GR_F16_SB, (float)GR_F16_SB};
+  const f32x2_t SA = {sa, sa}, SB = {(float)GR_F16_SB, (float)GR_F16_SB};
   (void)SA;
   (void)SB;
   for (int base = k0; base < k1; base += TP, buf ^= 1) {
@@ -1423,8 +1464,10 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
         split3_frag2(bv, fb);
         split3_frag2(aW, f3);
         cW = mfma16_split3(f3, fb, cW);
-        split3_frag2(aD, f3);
-        cD = mfma16_split3(f3, fb, cD);
+        if constexpr (ZCH) {
+          split3_frag2(aD, f3);
+          cD = mfma16_split3(f3, fb, cD);
+        }
       } else if (F16) {  // f16 pieces of the pre-scaled operands (no depth channel)
         s16x8 f2[2];
         split2h_frag2(bv, fb2h);
@@ -1491,9 +1534,9 @@ __device__ __forceinline__ void write_pixel(const ViewK& v, int p, const float* 
                                             float4* __restrict__ saved4, float* __restrict__ savedD) {
   const float aW = acc[0], den = 1.0f + aW;
   if (out_rgb) {  // (gr_fwd_render_l1 may render no image: its loss gradients come from the sums)
-    out_rgb[3 * p + 0] = clamp01((v.bg[0] + acc[1]) / den);
-    out_rgb[3 * p + 1] = clamp01((v.bg[1] + acc[2]) / den);
-    out_rgb[3 * p + 2] = clamp01((v.bg[2] + acc[3]) / den);
+    out_rgb[3 * p + 0] = clamp01((view_bg(v, 0) + acc[1]) / den);
+    out_rgb[3 * p + 1] = clamp01((view_bg(v, 1) + acc[2]) / den);
+    out_rgb[3 * p + 2] = clamp01((view_bg(v, 2) + acc[3]) / den);
   }
   if (out_alpha) out_alpha[p] = clamp01(aW / den);
   if (out_depth) {
@@ -1538,6 +1581,7 @@ struct L1Args {
   const float* t_depth = nullptr;  // (H,W) depth target or nullptr (no depth term)
   float w_depth = 0.0f;
   const float* dscal = nullptr;    // device scalars: [0] max(depth), [1] the max's gradient per arg-max pixel
+  int pieces = 2;                  // bf16 pieces of the upstream fragments (gr_fwd_render_l1: 3 at f32 grade)
 };
 
 __device__ __forceinline__ float sign0(float t) { return t > 0.0f ? 1.0f : (t < 0.0f ? -1.0f : 0.0f); }
@@ -1552,7 +1596,7 @@ __device__ __forceinline__ void pixel_upstream(const ViewK& v, int p, float4 s, 
   const float HWf = (float)v.W * (float)v.H;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const float r = (v.bg[k] + C[k]) / den;
+    const float r = (view_bg(v, k) + C[k]) / den;
     float gk;
     if (l1.t_rgb) {
       const float t = clamp01(r) - l1.t_rgb[3 * p + k];
@@ -1788,13 +1832,15 @@ __device__ __forceinline__ void l1_tile_epilogue(const ViewK& v, int tile, int t
 #pragma unroll
   for (int k = 0; k < 4; ++k) sU[k][tid] = u[k];
   __syncthreads();
-  tile_fragments(sU, UF + (size_t)tile * UF_FRAGS, tid, 2, false);
+  tile_fragments(sU, UF + (size_t)tile * UF_FRAGS, tid, l1.pieces, false);
 }
 
 // MODE 1: split bf16, W and D f32-grade; 2: split bf16, W and D within 2^-16 (views rendered with
 // no_depth_grad); 3: as 2 without the depth channel (no_depth_grad views rendered with no depth output;
 // the saved depth sums are then 0 and unused); 4: as 3, with the fit loss's upstream fragments and tile
-// L1 sums made in the epilogue (gr_fwd_render_l1, the fused fit path).
+// L1 sums made in the epilogue (gr_fwd_render_l1, the fused fit path); 5: the fused fit path at
+// f32 grade (no_depth_grad = 2): MODE 1's splits without the depth channel, MODE 4's epilogue with
+// three-piece upstream fragments.
 // Modes 1/2 at 5 waves per SIMD: at 6 they spill (MODE 1: 5 VGPRs); same-box A/B, C4 depth-loss views,
 // MODE 1: 330/334 -> 320/318 us (profiles/r02o_ab_variants.txt).
 #ifndef GR_FWD_WAVES
@@ -1810,7 +1856,7 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
                                                          float* __restrict__ fwd_part, float* __restrict__ out_rgb,
                                                          float* __restrict__ out_alpha, float* __restrict__ out_depth,
                                                          float4* __restrict__ saved4, float* __restrict__ savedD,
-                                                         L1Args l1, uint4* __restrict__ UF) {
+                                                         L1Args l1, uint4* __restrict__ UF, const int* __restrict__ f16_sa) {
   // LDS: two staged record buffers (2 x 9 KiB) during the loop, then the 4-wave reduction (20 KiB).
   __shared__ __attribute__((aligned(16))) float smem[4 * 5 * TP];
   const int nitems = *num_items;
@@ -1824,12 +1870,14 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
   const float xc = (float)(tx * T + li) + 0.5f;  // A row = x
   const float yc = (float)(ty * T + li) + 0.5f;  // B col = y
   f32x4 cW = {0.f, 0.f, 0.f, 0.f}, cR = cW, cG = cW, cB = cW, cD = cW;
+  constexpr bool PREC = MODE == 1 || MODE == 5, ZCHK = MODE < 3, F16K = GR_FWD_F16 && (MODE == 3 || MODE == 4);
+  const int sa = F16K ? *f16_sa : GR_F16_SA;  // the view's A pre-scale (f16_sa_of)
   if (it.x & 1)
-    fwd_accumulate_bf16<true, MODE == 1, MODE < 3>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
+    fwd_accumulate_bf16<true, PREC, ZCHK>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD, (float)sa);
   else
-    fwd_accumulate_bf16<false, MODE == 1, MODE < 3>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD);
-  if constexpr (GR_FWD_F16 && MODE >= 3) {  // the operands carried 2^SA and 2^SB (exact power-of-two rescale)
-    const float sc = __builtin_ldexpf(1.0f, -(GR_F16_SA + GR_F16_SB));
+    fwd_accumulate_bf16<false, PREC, ZCHK>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD, (float)sa);
+  if constexpr (F16K) {  // the operands carried 2^sa and 2^SB (exact power-of-two rescale)
+    const float sc = __builtin_ldexpf(1.0f, -(sa + GR_F16_SB));
     cW *= sc;
     cR *= sc;
     cG *= sc;
@@ -1860,7 +1908,7 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
   const bool inside = x < v.W && y < v.H;
   if (inside) write_pixel(v, y * v.W + x, acc, out_rgb, out_alpha, out_depth, saved4, savedD);
-  if constexpr (MODE == 4) l1_tile_epilogue(v, tile, tid, acc, inside, y * v.W + x, l1, UF, smem);
+  if constexpr (MODE == 4 || MODE == 5) l1_tile_epilogue(v, tile, tid, acc, inside, y * v.W + x, l1, UF, smem);
 }
 
 // Tiles with no Gaussians (background) or split over several work items: sum the items' partial
@@ -2498,6 +2546,136 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_views(RBatch B, int n, const 
   for (int q = 0; q < CD; ++q) out.color(q, gr.c[q]);
 }
 
+// ------------------------------------------------------------------------------------------------
+// The reduction in two stages (gr_gather_view + gr_reduce_sums): the gather of one view's pair rows into
+// per-Gaussian sums runs right after the view's backward splat, as a lean kernel (few registers, no LDS)
+// that fits beside the splat kernels of the other streams on the same SIMDs: its gathers overlap their
+// VALU work instead of taking the CUs from them (the one-pass k_reduce_views needs 117 VGPRs for its chain
+// rule and so never co-resides with a splat).  The chain rule of a batch of views then reads the sums
+// (32 B per Gaussian and view, coalesced) in a short VALU pass.
+// ------------------------------------------------------------------------------------------------
+// Per Gaussian and view: the 8-float sums of its rows [o S0, o S2, S4, S6 | o S1, S8, S5, S7] (no depth
+// gradient).  4 lanes per Gaussian, lane q sums rows q, q+4, ... in order (two rows in flight), the lane
+// sums are combined in a fixed order (xor 1, then xor 2): deterministic.  Lane q writes floats 2q, 2q+1.
+// xor-1 / xor-2 lane exchange inside a quad (DPP quad_perm: no LDS instruction)
+__device__ __forceinline__ float quad_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float quad_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ void add4(float4& x, const float4 a) {
+  x.x += a.x;
+  x.y += a.y;
+  x.z += a.z;
+  x.w += a.w;
+}
+// One row in flight per lane with the next row's position prefetched: ~26 VGPRs, so a wave fits in what
+// the splat kernels leave of a SIMD's registers (backward 4 x 120, forward 6 x 80 of 512).
+__global__ __launch_bounds__(256) void k_gather_view(int n, const Cnt2* __restrict__ offsets, const int* __restrict__ pos_of,
+                                                     const float4* __restrict__ rows, float2* __restrict__ sums) {
+  const int tid = threadIdx.x, q4 = tid & 3;
+  const int i = blockIdx.x * 64 + (tid >> 2);
+  float4 x = {-0.f, -0.f, -0.f, -0.f}, y = x;
+  if (i < n) {
+    const unsigned a = offsets[i].c(), cc = offsets[i + 1].c() - a;
+    const int* pc = pos_of + a;
+    unsigned j = q4;
+    int p = j < cc ? pc[j] : 0;
+    for (; j < cc; j += 4) {
+      const int pn = j + 4 < cc ? pc[j + 4] : 0;
+      add4(x, rows[2 * (size_t)p]);
+      add4(y, rows[2 * (size_t)p + 1]);
+      p = pn;
+    }
+  }
+  x.x += quad_xor1(x.x); x.y += quad_xor1(x.y); x.z += quad_xor1(x.z); x.w += quad_xor1(x.w);
+  y.x += quad_xor1(y.x); y.y += quad_xor1(y.y); y.z += quad_xor1(y.z); y.w += quad_xor1(y.w);
+  x.x += quad_xor2(x.x); x.y += quad_xor2(x.y); x.z += quad_xor2(x.z); x.w += quad_xor2(x.w);
+  y.x += quad_xor2(y.x); y.y += quad_xor2(y.y); y.z += quad_xor2(y.z); y.w += quad_xor2(y.w);
+  if (i < n) {
+    const float2 o = q4 == 0 ? make_float2(x.x, x.y) : q4 == 1 ? make_float2(x.z, x.w) : q4 == 2 ? make_float2(y.x, y.y)
+                                                                                        : make_float2(y.z, y.w);
+    sums[4 * (size_t)i + q4] = o;
+  }
+}
+
+// Chain rule of up to GR_REDUCE_MAX_VIEWS views' gathered sums: one lane per Gaussian, wave w takes
+// views w, w + 4, ... (CRW waves; SH degree 3: wave 0 alone), the wave totals are combined in wave
+// order and written (or added, acc) once.  A Gaussian whose eight sums are all zero touched no tile of
+// that view (its chain rule would add zero).  Deterministic.
+struct SViewK {
+  ViewK v;
+  const float4* sums;  // [n][2]: k_gather_view's output
+};
+struct SBatch {
+  int nv;
+  SViewK r[GR_REDUCE_MAX_VIEWS];
+};
+
+template <int CD>
+__global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const float* __restrict__ means,
+                                                     const float* __restrict__ scales, const float* __restrict__ colors,
+                                                     const float* __restrict__ opac, float* __restrict__ d_means,
+                                                     float* __restrict__ d_scales, float* __restrict__ d_colors,
+                                                     float* __restrict__ d_opac, int acc) {
+  constexpr int CRW = CD == 48 ? 1 : 4;
+  constexpr int NG = 6 + CD;
+  __shared__ float sG[CRW > 1 ? CRW : 1][64][NG + 1];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int gi = blockIdx.x * 64 + lane;
+  GradRegs<CD> gr;
+  if (w < CRW && gi < n) {
+    for (int vi = w; vi < B.nv; vi += CRW) {
+      const float4 a = B.r[vi].sums[2 * (size_t)gi], b = B.r[vi].sums[2 * (size_t)gi + 1];
+      // [o S0, o S2, S4, S6 | o S1, S8, S5, S7] -> S0..S8 (S3, the depth sum, is 0 without a depth gradient)
+      const float Sf[NPART] = {a.x, b.x, a.y, 0.0f, a.z, b.z, a.w, b.w, b.y};
+      const unsigned on = (a.x != 0.f || a.y != 0.f || a.z != 0.f || a.w != 0.f || b.x != 0.f || b.y != 0.f ||
+                           b.z != 0.f || b.w != 0.f) ? 1u : 0u;
+      chain_rule<CD, float>(B.r[vi].v, gi, Sf, on, means, scales, colors, opac, gr);
+    }
+  }
+  if constexpr (CRW > 1) {
+    if (w < CRW) {
+      float* mine = sG[w][lane];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) mine[q] = gr.m[q];
+      mine[3] = gr.s[0];
+      mine[4] = gr.s[1];
+      mine[5] = gr.o;
+#pragma unroll
+      for (int q = 0; q < CD; ++q) mine[6 + q] = gr.c[q];
+    }
+    __syncthreads();
+    if (w != 0 || gi >= n) return;
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      float t = sG[0][lane][q];
+#pragma unroll
+      for (int u = 1; u < CRW; ++u) t += sG[u][lane][q];
+      sG[0][lane][q] = t;
+    }
+    const float* tot = sG[0][lane];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) gr.m[q] = tot[q];
+    gr.s[0] = tot[3];
+    gr.s[1] = tot[4];
+    gr.o = tot[5];
+#pragma unroll
+    for (int q = 0; q < CD; ++q) gr.c[q] = tot[6 + q];
+  }
+  if (w != 0 || gi >= n) return;
+  GradOut out{d_means + 3 * (size_t)gi, d_scales + 3 * (size_t)gi, d_colors + (size_t)CD * gi, d_opac + gi, acc != 0};
+#pragma unroll
+  for (int q = 0; q < 3; ++q) out.mean(q, gr.m[q]);
+  out.scale(0, gr.s[0]);
+  out.scale(1, gr.s[1]);
+  out.scale_z();
+  out.opac(gr.o);
+#pragma unroll
+  for (int q = 0; q < CD; ++q) out.color(q, gr.c[q]);
+}
+
 template <int CD, typename F, typename Out>
 __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, const float* __restrict__ means,
                            const float* __restrict__ scales, const float* __restrict__ colors,
@@ -3057,16 +3235,23 @@ constexpr int PLAN_THREADS = GR_PLAN_THREADS;
 // words cannot carry into each other as long as K < 2^31, which is checked against the exact total
 // (the sum of every block's two words) before the plan is trusted.
 __device__ __forceinline__ void plan_scan(unsigned long long* __restrict__ bsum, int blocks,
-                                          unsigned long long* __restrict__ off_end, gr_plan* plan, gr_plan* host_plan) {
+                                          unsigned long long* __restrict__ off_end, gr_plan* plan, gr_plan* host_plan,
+                                          const float* __restrict__ omax, int* __restrict__ f16_sa) {
   __shared__ unsigned long long sh[PLAN_THREADS / 64];
+  __shared__ float shm[PLAN_THREADS / 64];
   const int tid = (int)threadIdx.x, per = (blocks + PLAN_THREADS - 1) / PLAN_THREADS;
   const int b0 = min(blocks, tid * per), b1 = min(blocks, b0 + per);
   unsigned long long acc = 0, ex = 0;
+  float om = 0.0f;
   for (int b = b0; b < b1; ++b) {
     const unsigned long long t = bsum[b];
     acc += t;
     ex += (t & 0xffffffffull) + (t >> 32);
+    om = fmaxf(om, omax[b]);
   }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) om = fmaxf(om, __shfl_xor(om, m));
+  if ((tid & 63) == 0) shm[tid >> 6] = om;
   unsigned long long grand, exact;
   const unsigned long long base = block_exclusive_scan<PLAN_THREADS / 64>(acc, sh, grand);
   (void)block_exclusive_scan<PLAN_THREADS / 64>(ex, sh, exact);
@@ -3077,6 +3262,9 @@ __device__ __forceinline__ void plan_scan(unsigned long long* __restrict__ bsum,
     run += t;
   }
   if (tid != 0) return;
+#pragma unroll
+  for (int w = 1; w < PLAN_THREADS / 64; ++w) om = fmaxf(om, shm[w]);  // published by the scans' barriers
+  *f16_sa = f16_sa_of(om);
   const bool ok = exact < (1ull << 31);  // then neither packed word carried
   *off_end = grand;
   plan->num_pairs = ok ? (long long)exact : -1;
@@ -3092,8 +3280,9 @@ __device__ __forceinline__ void plan_scan(unsigned long long* __restrict__ bsum,
 
 __global__ __launch_bounds__(PLAN_THREADS) void k_plan(unsigned long long* __restrict__ bsum, int blocks,
                                                unsigned long long* __restrict__ off_end, gr_plan* plan,
-                                               gr_plan* host_plan) {
-  plan_scan(bsum, blocks, off_end, plan, host_plan);
+                                               gr_plan* host_plan, const float* __restrict__ omax,
+                                               int* __restrict__ f16_sa) {
+  plan_scan(bsum, blocks, off_end, plan, host_plan, omax, f16_sa);
 }
 
 // Gaussian level of the offsets scan: offsets[i] = its block's offset + the exclusive scan of the packed
@@ -3119,7 +3308,7 @@ struct HostPlans {
 };
 __global__ __launch_bounds__(PLAN_THREADS) void k_plan_views(PrepBatch B, int n, HostPlans hp) {
   const Geom& g = B.g[blockIdx.x];
-  plan_scan(g.total, (n + 256) / 256, g.offsets + n, g.plan, hp.p[blockIdx.x]);
+  plan_scan(g.total, (n + 256) / 256, g.offsets + n, g.plan, hp.p[blockIdx.x], g.omax, g.f16_sa);
 }
 __global__ __launch_bounds__(256) void k_offsets_views(PrepBatch B, int n) {
   const Geom& g = B.g[blockIdx.y];
@@ -3160,7 +3349,8 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
     mapped = (gr_plan*)attr.devicePointer;
   (void)hipGetLastError();  // a pageable pointer leaves an error code behind
   // exclusive scan of the packed counts: blocks (k_plan), then Gaussians (k_offsets)
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(PLAN_THREADS), 0, s, g.total, blocks_for(n + 1), g.offsets + n, g.plan, mapped);
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(PLAN_THREADS), 0, s, g.total, blocks_for(n + 1), g.offsets + n, g.plan, mapped,
+                     (const float*)g.omax, g.f16_sa);
   GR_HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_offsets, dim3(blocks_for(n)), dim3(256), 0, s, n, (const unsigned long long*)g.counts,
                      (const unsigned long long*)g.total, g.offsets);
@@ -3372,12 +3562,14 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
   float* savedD = saved ? saved + 4 * HW : nullptr;
   if (num_pairs > 0) {
     prof_mark(PROF_RASTER_FWD, s);
-    hipLaunchKernelGGL(l1 ? k_raster_fwd_mfma<4>
-                          : (!v->no_depth_grad ? k_raster_fwd_mfma<1>
-                                               : (out_depth ? k_raster_fwd_mfma<2> : k_raster_fwd_mfma<3>)),
+    // no_depth_grad: 0 default (f32-grade W / D), 1 two-piece splits, 2 f32-grade without a depth gradient
+    const bool f32g = v->no_depth_grad != 1;
+    hipLaunchKernelGGL(l1 ? (f32g ? k_raster_fwd_mfma<5> : k_raster_fwd_mfma<4>)
+                          : (f32g ? k_raster_fwd_mfma<1>
+                                  : (out_depth ? k_raster_fwd_mfma<2> : k_raster_fwd_mfma<3>)),
                        dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
                        (const int*)b.num_items, (const int2*)b.ranges, (const int*)b.pairs, (const float4*)g.rec,
-                       sc.fwd_part, out_rgb, out_alpha, out_depth, saved4, savedD, la, UF);
+                       sc.fwd_part, out_rgb, out_alpha, out_depth, saved4, savedD, la, UF, (const int*)g.f16_sa);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_FWD, s);
   }
@@ -3406,9 +3598,10 @@ gr_status gr_fwd_render_l1(const gr_view* v, int n, const gr_plan* plan, const v
                            float w_sil, float g_scale, float* loss_out, float* out_rgb, float* out_alpha, void* ws,
                            size_t ws_bytes, void* stream) {
   if (!v || !v->no_depth_grad)
-    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fwd_render_l1: the view must have no_depth_grad = 1");
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fwd_render_l1: the view must have no_depth_grad = 1 or 2");
   if (!target_rgb) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fwd_render_l1: target_rgb is null");
-  const L1Args l1{target_rgb, target_mask, w_sil, g_scale, nullptr};
+  L1Args l1{target_rgb, target_mask, w_sil, g_scale, nullptr};
+  l1.pieces = v->no_depth_grad == 1 ? 2 : 3;
   return fwd_impl(v, n, plan, geom, bins, bins_bytes, scratch, scratch_bytes, out_rgb, out_alpha, nullptr, nullptr, stream,
                   &l1, loss_out, ws, ws_bytes);
 }
@@ -3465,7 +3658,7 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
   const bool depth = g_depth != nullptr || dfit;  // an upstream depth gradient reaches the splat
   if (num_pairs > 0 || t_rgb) {
     hipLaunchKernelGGL(k_pixel_grads, dim3(tiles), dim3(256), 0, s, vk, (const float4*)saved, saved + 4 * HW, g_rgb,
-                       g_alpha, g_depth, UF, v->no_depth_grad ? 2 : 3, l1, depth);
+                       g_alpha, g_depth, UF, v->no_depth_grad == 1 ? 2 : 3, l1, depth);
     GR_HIP_TRY(hipGetLastError());
   }
   if (t_rgb) {
@@ -3477,7 +3670,7 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
     const int64_t cap = item_cap(2 * tiles, num_pairs);
     prof_mark(PROF_RASTER_BWD, s);
     auto kern = depth ? k_raster_bwd_bf16<true, 3>
-                      : (v->no_depth_grad ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>);
+                      : (v->no_depth_grad == 1 ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>);
     hipLaunchKernelGGL(kern, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items,
                        (const int*)b.pairs, (const float4*)g.rec, (const uint4*)UF, partials);
     GR_HIP_TRY(hipGetLastError());
@@ -3541,7 +3734,8 @@ gr_status gr_bwd_splat(const gr_view* v, int n, const gr_plan* plan, const void*
                        size_t ws_bytes, void* stream) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
-  if (!v->no_depth_grad) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_splat: the view must have no_depth_grad = 1");
+  if (!v->no_depth_grad)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_splat: the view must have no_depth_grad = 1 or 2");
   if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
   if (plan->num_pairs < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
   if (n <= 0 || plan->num_pairs == 0) return GR_OK;
@@ -3555,8 +3749,9 @@ gr_status gr_bwd_splat(const gr_view* v, int n, const gr_plan* plan, const void*
   const BwdWs w = bwd_ws(v, plan, ws);
   const int64_t cap = item_cap(2 * tiles, plan->num_pairs);
   prof_mark(PROF_RASTER_BWD, s);
-  hipLaunchKernelGGL((k_raster_bwd_bf16<false, 2>), dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
-                     (const int*)b.num_items, (const int*)b.pairs, (const float4*)g.rec, (const uint4*)w.UF, w.partials);
+  hipLaunchKernelGGL((v->no_depth_grad == 1 ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>), dim3((unsigned)cap),
+                     dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items, (const int*)b.pairs,
+                     (const float4*)g.rec, (const uint4*)w.UF, w.partials);
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_RASTER_BWD, s);
   return GR_OK;
@@ -3610,6 +3805,74 @@ gr_status gr_reduce_views(int num_views, const gr_reduce_view* views, int n, con
   return GR_OK;
 }
 
+size_t gr_view_sums_floats(int n) { return (size_t)8 * (size_t)(n > 0 ? n : 0); }
+
+gr_status gr_gather_view(const gr_view* v, int n, const gr_plan* plan, const void* geom, const void* bins, const void* ws,
+                         float* sums, void* stream) {
+  gr_status st = check_view(v);
+  if (st != GR_OK) return st;
+  if (!v->no_depth_grad)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_gather_view: the view must have no_depth_grad = 1 or 2");
+  if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
+  if (plan->num_pairs < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
+  if (n < 0) return set_error(GR_ERR_INVALID_ARGUMENT, "n must be >= 0");
+  if (n == 0) return GR_OK;
+  if (!geom || !sums || (plan->num_pairs > 0 && (!bins || !ws)))
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_gather_view: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  if (plan->num_pairs == 0) {  // no pair: every sum is zero
+    GR_HIP_TRY(hipMemsetAsync(sums, 0, gr_view_sums_floats(n) * sizeof(float), s));
+    return GR_OK;
+  }
+  const ViewK vk = make_viewk(v);
+  const Geom g = geom_view((void*)geom, n);
+  const Bins b = bins_view((void*)bins, 2 * vk.tiles_x * vk.tiles_y, plan->num_pairs);
+  prof_mark(PROF_REDUCE, s);
+  hipLaunchKernelGGL(k_gather_view, dim3((n + 63) / 64), dim3(256), 0, s, n, (const Cnt2*)g.offsets, (const int*)b.pos_of,
+                     (const float4*)ws, (float2*)sums);
+  GR_HIP_TRY(hipGetLastError());
+  prof_mark(PROF_REDUCE, s);
+  return GR_OK;
+}
+
+gr_status gr_reduce_sums(int num_views, const gr_sums_view* views, int n, const float* means, const float* scales,
+                         const float* colors, int color_dim, const float* opacities, float* d_means, float* d_scales,
+                         float* d_colors, float* d_opacities, int accumulate, void* stream) {
+  if (num_views < 0 || num_views > GR_REDUCE_MAX_VIEWS)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_reduce_sums: num_views must be in [0, GR_REDUCE_MAX_VIEWS]");
+  if (color_dim != 3 && color_dim != 12 && color_dim != 48)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");
+  if (n < 0) return set_error(GR_ERR_INVALID_ARGUMENT, "n must be >= 0");
+  if (n == 0) return GR_OK;
+  if (!means || !scales || !colors || !opacities || !d_means || !d_scales || !d_colors || !d_opacities ||
+      (num_views > 0 && !views))
+    return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+  SBatch B;
+  B.nv = num_views;
+  for (int k = 0; k < num_views; ++k) {
+    gr_status st = check_view(&views[k].view);
+    if (st != GR_OK) return st;
+    if (!views[k].sums) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_reduce_sums: null sums");
+    B.r[k].v = make_viewk(&views[k].view);
+    B.r[k].sums = (const float4*)views[k].sums;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  prof_mark(PROF_REDUCE, s);
+  const dim3 grid((n + 63) / 64), block(256);
+  if (color_dim == 3)
+    hipLaunchKernelGGL(k_reduce_sums<3>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
+                       d_colors, d_opacities, accumulate);
+  else if (color_dim == 12)
+    hipLaunchKernelGGL(k_reduce_sums<12>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
+                       d_colors, d_opacities, accumulate);
+  else
+    hipLaunchKernelGGL(k_reduce_sums<48>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
+                       d_colors, d_opacities, accumulate);
+  GR_HIP_TRY(hipGetLastError());
+  prof_mark(PROF_REDUCE, s);
+  return GR_OK;
+}
+
 gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, const float* scales, const float* colors,
                        const float* opacities, uint8_t* rgba) {
   if (!p || !rgba) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
@@ -3620,7 +3883,7 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
     return GR_OK;
   }
   if (!means || !scales || !colors || !opacities) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
-  gr_view gv;
+  gr_view gv{};  // background_dev NULL: the host background of the params
   gv.width = p->width;
   gv.height = p->height;
   std::memcpy(gv.view, p->view, sizeof(gv.view));

@@ -77,6 +77,14 @@ L_MAX_ACC = 8  # GR_FIT_MAX_ACC: stream accumulators gr_fit_param_step sums
 # views prepared together (gr_fwd_prepare_views_async: the parameters read once for the group)
 PREP_GROUP = max(1, min(4, int(os.environ.get("GR_PREP_GROUP", "4"))))
 PREP_FIRST = max(1, min(PREP_GROUP, int(os.environ.get("GR_PREP_FIRST", "1"))))
+# the fused path's reduction in two stages: each view's pair partials gathered into per-Gaussian sums right
+# after its backward splat (gr_gather_view: a lean kernel that runs beside the other streams' splats; the view's
+# workspaces are released at once), the chain rules of a stream's batch of views from those sums
+# (gr_reduce_sums).  0 = the one-pass gr_reduce_views over the batch's kept workspaces.
+GATHER = os.environ.get("GR_GATHER", "1") != "0"
+# the fused path at f32 grade (gr_view.no_depth_grad = 2: three-piece splits in both splats, as the default
+# precision mode) instead of its two-piece mode: the precision reference of the fit path (bench.py f32_grade_fit)
+F32_GRADE = os.environ.get("GR_F32_GRADE", "0") != "0"
 
 
 # ------------------------------------------------------------------------------------------------
@@ -216,6 +224,19 @@ def spatial_order(params: dict) -> dict:
     return {k: torch.nn.Parameter(v.detach()[perm].contiguous()) for k, v in params.items()}
 
 
+def _fit_images(name: str, imgs: Optional[list], shape: tuple, device) -> tuple:
+    """The fused fit path reads the targets / masks / depths through raw device pointers (gr_fwd_render_l1,
+    gr_bwd_fit): each must be exactly ``shape``, float32, contiguous, on the parameters' device.  Returns
+    (images, ok): images normalised to that (a copy only where the dtype, layout or device differ), ok =
+    False when a shape differs (the fit then takes the autograd path, which broadcasts or raises as torch
+    does for the stub's expressions)."""
+    if imgs is None:
+        return None, True
+    if any(tuple(t.shape) != shape for t in imgs):
+        return list(imgs), False
+    return [torch.as_tensor(t).to(device=device, dtype=torch.float32).contiguous() for t in imgs], True
+
+
 def hip_render(means, scales, colors, opacities, cam, width, height, background, prepared=None, depth_grad=True):
     return tr.render_gaussians_torch(means, scales, colors, opacities, cam, width=width, height=height,
                                      background=background, max_gaussians=max(10000, int(means.shape[0])), return_aux=True,
@@ -246,6 +267,11 @@ class ViewShardedFitter:
             self.perm = morton_order(params["means"])
             params = {k: torch.nn.Parameter(v.detach()[self.perm].contiguous()) for k, v in params.items()}
         self.params = params
+        dev = params["means"].device
+        targets, ok_t = _fit_images("targets", targets, (height, width, 3), dev)
+        masks, ok_m = _fit_images("masks", masks, (height, width), dev)
+        depths, ok_d = _fit_images("depths", depths, (height, width), dev)
+        self._images_ok = ok_t and ok_m and ok_d  # the fused path's exact-shape precondition
         self.cams, self.targets, self.masks, self.depths = cams, targets, masks, depths
         self.width, self.height, self.lr = width, height, lr
         self.w_sil, self.w_depth = silhouette_weight, depth_weight
@@ -317,11 +343,14 @@ class ViewShardedFitter:
         cache = getattr(self, "_gv_cache", None)
         if cache is None:
             self._gv_cache = cache = {}
-        gv = cache.get(i)
+        gv = cache.get((i, F32_GRADE))
         if gv is None:
             cam = self.cams[i]
-            gv = cache[i] = tr.make_view(cam.view, cam.proj, self.width, self.height, self._background(device),
-                                         cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
+            gv = cache[(i, F32_GRADE)] = tr.make_view(cam.view, cam.proj, self.width, self.height,
+                                                      self._background(device), cutoff=tr.FIT_CUTOFF,
+                                                      core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
+            if F32_GRADE:
+                gv.no_depth_grad = 2
         return gv
 
     def _plan_pins(self, count: int) -> torch.Tensor:
@@ -357,8 +386,10 @@ class ViewShardedFitter:
 
     def _direct(self, device) -> bool:
         """The fused path (_views_direct, or _views_direct_depth with a depth term): HIP render op, the
-        view loss and its gradients in the C ABI, no autograd per view."""
-        return self.render_fn is hip_render and device.type == "cuda" and FUSED_LOSS and DIRECT_BACKWARD
+        view loss and its gradients in the C ABI, no autograd per view.  Needs float32 parameters and
+        targets / masks / depths of exactly the image's shape (checked at construction)."""
+        return (self.render_fn is hip_render and device.type == "cuda" and FUSED_LOSS and DIRECT_BACKWARD
+                and self._images_ok and all(p.dtype == torch.float32 for p in self.params.values()))
 
     def step(self) -> torch.Tensor:
         """One iteration; returns the full (all-rank) loss as a 0-d tensor on the device."""
@@ -467,7 +498,7 @@ class ViewShardedFitter:
         accumulators are summed in stream order and leave in self._acc for one autograd pass through the
         activations; returns the sum of the view losses (device, 0-d)."""
         device = means.device
-        m, s, c, o = (t.detach().contiguous() for t in (means, scales, colors, opacities))
+        m, s, c, o = (t.detach().float().contiguous() for t in (means, scales, colors, opacities))
         views = self.my_views
         main = torch.cuda.current_stream(device)
         ns = max(1, min(NUM_STREAMS, len(views)))
@@ -519,7 +550,10 @@ class ViewShardedFitter:
         def reduce_pending(k):
             if pending[k]:
                 with torch.cuda.stream(streams[k]):
-                    tr.reduce_views_native(m, s, c, o, pending[k], acc[k], accumulate=started[k])
+                    if GATHER:
+                        tr.reduce_sums_native(m, s, c, o, pending[k], acc[k], accumulate=started[k])
+                    else:
+                        tr.reduce_views_native(m, s, c, o, pending[k], acc[k], accumulate=started[k])
                 started[k] = True
                 pending[k] = []
 
@@ -536,7 +570,11 @@ class ViewShardedFitter:
                                               self.masks[i] if w_sil > 0.0 else None, w_sil, g_scale, losses_v[j:j + 1])
                 pv = None
                 tr.backward_splat_native(rs, ws)
-            pending[k].append((rs, ws))
+                if GATHER:  # the view's sums; its bins, geom and workspace go back to the allocator here
+                    pending[k].append((rs.gv, tr.gather_view_native(rs, ws)))
+                    rs = ws = None
+            if rs is not None:
+                pending[k].append((rs, ws))
             if len(pending[k]) >= sizes[k][0]:
                 reduce_pending(k)
                 if len(sizes[k]) > 1:
@@ -557,7 +595,7 @@ class ViewShardedFitter:
         gr_bwd_fit (L1 + silhouette + depth loss gradients and the render backward) adding the gradient into
         the stream's accumulator set (in view order: deterministic).  Returns the sum of the view losses."""
         device = means.device
-        m, s, c, o = (t.detach().contiguous() for t in (means, scales, colors, opacities))
+        m, s, c, o = (t.detach().float().contiguous() for t in (means, scales, colors, opacities))
         views = self.my_views
         main = torch.cuda.current_stream(device)
         ns = max(1, min(NUM_STREAMS, len(views)))
@@ -618,8 +656,11 @@ class ViewShardedFitter:
 
     def _fused_step_ok(self) -> bool:
         """The fused parameter update applies: plain Adam (torch.optim.Adam defaults: no weight decay, no
-        amsgrad, not maximize), one parameter group, the stub's parameter names, float32 on the device."""
+        amsgrad, not maximize), one parameter group, the stub's parameter names, float32 contiguous tensors on
+        the HIP device (gr_fit_param_step reads them through raw pointers)."""
         if not FUSED_STEP or type(self.opt) is not torch.optim.Adam or len(self.opt.param_groups) != 1:
+            return False
+        if not all(p.dtype == torch.float32 and p.is_cuda and p.is_contiguous() for p in self.params.values()):
             return False
         g = self.opt.param_groups[0]
         if g["weight_decay"] != 0 or g["amsgrad"] or g.get("maximize", False) or isinstance(g["lr"], torch.Tensor):

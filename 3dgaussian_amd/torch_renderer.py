@@ -161,10 +161,19 @@ def make_view(view, proj, width: int, height: int, background=None, cutoff: Opti
     gv.width, gv.height = int(width), int(height)
     gv.view[:] = V.reshape(16).tolist()
     gv.proj[:] = P.reshape(16).tolist()
+    gv.background_dev = None
     if background is None:
         bg = [0.0, 0.0, 0.0]
+    elif isinstance(background, torch.Tensor) and background.device.type == "cuda":
+        # read by the kernels on the device (gr_view.background_dev), stream-ordered: no device-to-host
+        # copy per view.  The caller keeps the tensor alive until the view's kernels have run (rasterize
+        # saves it for the backward); it must be 3 contiguous float32 values.
+        if background.dtype != torch.float32 or background.numel() != 3 or not background.is_contiguous():
+            raise ValueError("a device background must be 3 contiguous float32 values")
+        gv.background_dev = background.data_ptr()
+        bg = [0.0, 0.0, 0.0]
     elif isinstance(background, torch.Tensor):
-        bg = _host_copy(background, (3,)).tolist()
+        bg = background.detach().to(torch.float32).reshape(3).tolist()
     else:
         bg = np.asarray(background, np.float32).reshape(3).tolist()
     gv.background[:] = bg
@@ -258,6 +267,7 @@ def prepare_views_native(means, scales, colors, opacities, gvs, plan_hosts) -> l
     k = len(gvs)
     if not 1 <= k <= _native.PREPARE_MAX_VIEWS or len(plan_hosts) != k:
         raise ValueError(f"1 to {_native.PREPARE_MAX_VIEWS} views, one plan buffer each")
+    _check_params(means, scales, colors, opacities)
     dev = means.device
     n = int(means.shape[0])
     nbytes = int(L.gr_geom_bytes(n))
@@ -352,6 +362,10 @@ def backward_fit_native(means, scales, colors, opacities, st: RenderState, targe
     ``w_depth mean|depth / (max(depth) + 1e-6) - depth_target|`` (the view rendered with depth_grad=True)."""
     L = _native.lib()
     dev = means.device
+    _check_params(means, scales, colors, opacities)
+    _check_operand(target, (st.gv.height, st.gv.width, 3), "target", dev)
+    _check_operand(mask, (st.gv.height, st.gv.width), "mask", dev)
+    _check_operand(depth_target, (st.gv.height, st.gv.width), "depth_target", dev)
     ws = torch.empty((_ws_round(L.gr_bwd_bytes(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan))),), dtype=torch.uint8,
                      device=dev)
     dm, ds, dc, do = grads
@@ -362,6 +376,26 @@ def backward_fit_native(means, scales, colors, opacities, st: RenderState, targe
                                ctypes.c_float(g_scale), _native.ptr(loss_out), _native.ptr(dm), _native.ptr(ds),
                                _native.ptr(dc), _native.ptr(do), 1 if accumulate else 0, _native.ptr(ws), ws.numel(),
                                _stream(dev)), "gr_bwd_fit")
+
+
+def _check_operand(t, shape, name: str, dev) -> None:
+    """A tensor the C ABI reads through its raw pointer (the fused fit path's targets, masks, depths and
+    parameters): exactly ``shape``, float32, contiguous, on ``dev`` - anything else would be read as the
+    wrong bytes, so it raises instead.  None passes (an optional operand)."""
+    if t is None:
+        return
+    if (not isinstance(t, torch.Tensor) or tuple(t.shape) != tuple(shape) or t.dtype != torch.float32
+            or not t.is_contiguous() or t.device != dev):
+        got = (tuple(t.shape), t.dtype, t.device, t.is_contiguous()) if isinstance(t, torch.Tensor) else type(t)
+        raise ValueError(f"{name}: expected a contiguous float32 tensor of shape {tuple(shape)} on {dev}, got {got}")
+
+
+def _check_params(means, scales, colors, opacities) -> None:
+    n, dev = int(means.shape[0]), means.device
+    _check_operand(means, (n, 3), "means", dev)
+    _check_operand(scales, (n, 3), "scales", dev)
+    _check_operand(colors, (n,) + tuple(colors.shape[1:]), "colors", dev)
+    _check_operand(opacities, (n,), "opacities", dev)
 
 
 def forward_l1_native(means, scales, colors, opacities, gv: _native.GrView, prepared: Prepared, target, mask,
@@ -377,6 +411,8 @@ def forward_l1_native(means, scales, colors, opacities, gv: _native.GrView, prep
     if (prepared.n != n or prepared.gv.width != gv.width or prepared.gv.height != gv.height
             or prepared.gv.cutoff != gv.cutoff or prepared.gv.core_cutoff != gv.core_cutoff):
         raise ValueError("prepared view does not match this render (Gaussian count, image size or cutoffs)")
+    _check_operand(target, (gv.height, gv.width, 3), "target", dev)
+    _check_operand(mask, (gv.height, gv.width), "mask", dev)
     plan = prepared.plan()
     bins = torch.empty((_ws_round(L.gr_bins_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8,
                        device=dev)
@@ -407,6 +443,9 @@ def reduce_views_native(means, scales, colors, opacities, batch, grads, accumula
     L = _native.lib()
     if len(batch) > _native.REDUCE_MAX_VIEWS:
         raise ValueError(f"at most {_native.REDUCE_MAX_VIEWS} views per gr_reduce_views batch")
+    _check_params(means, scales, colors, opacities)
+    for g, p, nm in zip(grads, (means, scales, colors, opacities), ("d_means", "d_scales", "d_colors", "d_opacities")):
+        _check_operand(g, tuple(p.shape), nm, means.device)
     arr = (_native.GrReduceView * max(1, len(batch)))()
     for k, (st, ws) in enumerate(batch):
         arr[k].view = st.gv
@@ -419,6 +458,44 @@ def reduce_views_native(means, scales, colors, opacities, batch, grads, accumula
                                     _native.ptr(colors), _color_dim(colors), _native.ptr(opacities), _native.ptr(dm),
                                     _native.ptr(ds), _native.ptr(dc), _native.ptr(do), 1 if accumulate else 0,
                                     _stream(means.device)), "gr_reduce_views")
+
+
+def gather_view_native(st: RenderState, ws, sums=None):
+    """gr_gather_view on the current stream: the per-Gaussian sums (n, 8) of a view's pair partials right
+    after its backward_splat_native; the view's bins / geom / workspace may be dropped once it is enqueued
+    (stream-ordered reuse).  Returns the sums tensor."""
+    L = _native.lib()
+    dev = ws.device
+    if sums is None:
+        sums = torch.empty((st.n, 8), dtype=torch.float32, device=dev)
+    _check_operand(sums, (st.n, 8), "sums", dev)
+    _native.check(L.gr_gather_view(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan), _native.ptr(st.geom),
+                                   _native.ptr(st.bins), _native.ptr(ws), _native.ptr(sums), _stream(dev)),
+                  "gr_gather_view")
+    return sums
+
+
+def reduce_sums_native(means, scales, colors, opacities, batch, grads, accumulate: bool) -> None:
+    """gr_reduce_sums on the current stream: ``batch`` = [(gr_view, sums from gather_view_native), ...] (at
+    most _native.REDUCE_MAX_VIEWS); the views' chain rules summed, written (accumulate=False) or added to
+    ``grads`` = (d_means, d_scales, d_colors, d_opacities)."""
+    L = _native.lib()
+    if len(batch) > _native.REDUCE_MAX_VIEWS:
+        raise ValueError(f"at most {_native.REDUCE_MAX_VIEWS} views per gr_reduce_sums batch")
+    _check_params(means, scales, colors, opacities)
+    n = int(means.shape[0])
+    arr = (_native.GrSumsView * max(1, len(batch)))()
+    for k, (gv, sums) in enumerate(batch):
+        _check_operand(sums, (n, 8), "sums", means.device)
+        arr[k].view = gv
+        arr[k].sums = sums.data_ptr()
+    for g, p, nm in zip(grads, (means, scales, colors, opacities), ("d_means", "d_scales", "d_colors", "d_opacities")):
+        _check_operand(g, tuple(p.shape), nm, means.device)
+    dm, ds, dc, do = grads
+    _native.check(L.gr_reduce_sums(len(batch), arr, n, _native.ptr(means), _native.ptr(scales), _native.ptr(colors),
+                                   _color_dim(colors), _native.ptr(opacities), _native.ptr(dm), _native.ptr(ds),
+                                   _native.ptr(dc), _native.ptr(do), 1 if accumulate else 0, _stream(means.device)),
+                  "gr_reduce_sums")
 
 
 def _grad_background(st: RenderState, background: torch.Tensor, g_out: torch.Tensor) -> torch.Tensor:
@@ -476,6 +553,71 @@ def prepare_view(means, scales, colors, opacities, view, proj, width, height, ba
     return prepare_native(*_device_inputs(means, scales, colors, opacities), gv, plan_host)
 
 
+# ------------------------------------------------------------------------------------------------
+# Preparation ahead for callers that render view after view through the autograd op (the reference fit
+# loop, fit_multiview_stub.py:277-290, calls render_gaussians_torch once per camera with the same
+# activation tensors).  A render needs its view's pair count on the host before the binning can be
+# enqueued; without help that is one host wait per view for a preparation enqueued just before it.
+# After rendering camera A the op enqueues the preparation of the camera that followed A last time,
+# with the same input tensors; the next call uses it when its camera and tensors match (the same live
+# tensor objects at the same versions: weak references, so a freed tensor never matches), and
+# otherwise drops it.  A transition that missed is not speculated the next time.  GR_SPECULATE=0
+# turns this off.
+# ------------------------------------------------------------------------------------------------
+SPECULATE = os.environ.get("GR_SPECULATE", "1") != "0"
+
+
+class _Speculation:
+    __slots__ = ("key", "refs", "versions", "prepared", "src")
+
+    def __init__(self, key, tensors, prepared, src):
+        self.key, self.prepared, self.src = key, prepared, src
+        self.refs = tuple(weakref.ref(t) for t in tensors)
+        self.versions = tuple(t._version for t in tensors)
+
+    def matches(self, key, tensors) -> bool:
+        return key == self.key and all(r() is t and t._version == v
+                                       for r, t, v in zip(self.refs, tensors, self.versions))
+
+
+_SPEC: dict = {"last": None, "next": {}, "views": {}, "cold": set(), "pending": None, "hits": 0, "misses": 0}
+
+
+def _view_key(gv: _native.GrView) -> tuple:
+    return (bytes(gv.view), bytes(gv.proj), gv.width, gv.height, gv.cutoff, gv.core_cutoff, gv.no_depth_grad)
+
+
+def _spec_take(key, tensors) -> Optional[Prepared]:
+    """The speculative preparation of this view, if one is pending for exactly these inputs."""
+    sp, _SPEC["pending"] = _SPEC["pending"], None
+    if sp is None:
+        return None
+    if sp.matches(key, tensors):
+        _SPEC["hits"] += 1
+        _SPEC["cold"].discard((sp.src, key))
+        return sp.prepared
+    _SPEC["misses"] += 1
+    _SPEC["cold"].add((sp.src, sp.key))
+    return None
+
+
+def _spec_after(key, gv, tensors) -> None:
+    """Learn the camera order and enqueue the preparation of the camera expected next."""
+    last = _SPEC["last"]
+    if last is not None:
+        _SPEC["next"][last] = key
+    _SPEC["last"] = key
+    _SPEC["views"][key] = gv
+    if len(_SPEC["views"]) > 4096:
+        _SPEC["views"].clear()
+        _SPEC["next"].clear()
+    nxt = _SPEC["next"].get(key)
+    if nxt is None or (key, nxt) in _SPEC["cold"]:
+        return
+    pv = prepare_native(*tensors, _SPEC["views"][nxt])
+    _SPEC["pending"] = _Speculation(nxt, tensors, pv, key)
+
+
 def rasterize(means, scales, colors, opacities, view, proj, width, height, background=None, cutoff=None,
               prepared: Optional[Prepared] = None, core_cutoff=DEFAULT_CORE_CUTOFF, depth_grad: bool = True):
     """Differentiable render of one view on the HIP device: returns (rgb (H,W,3), alpha (H,W), depth (H,W)).
@@ -492,9 +634,19 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
     m, s, c, o = _device_inputs(means, scales, colors, opacities)
     if background is None:
         background = _default_background(dev)
-    background = background.to(dtype=torch.float32, device=dev)
+    background = background.to(dtype=torch.float32, device=dev).reshape(3).contiguous()
     gv = make_view(view, proj, width, height, background, cutoff, core_cutoff, depth_grad)
-    return _RasterizeGaussians.apply(m, s, c, o, background, gv, prepared)
+    if prepared is not None or not SPECULATE:
+        return _RasterizeGaussians.apply(m, s, c, o, background, gv, prepared)
+    key = _view_key(gv)
+    pv = _spec_take(key, (m, s, c, o))
+    if pv is not None:
+        stream = torch.cuda.current_stream(dev)
+        stream.wait_event(pv.event)
+        pv.geom.record_stream(stream)
+    res = _RasterizeGaussians.apply(m, s, c, o, background, gv, pv)
+    _spec_after(key, gv, (m, s, c, o))
+    return res
 
 
 def render_gaussians_torch(
@@ -546,4 +698,5 @@ def render_gaussians_torch(
 __all__ = ["Camera", "get_default_device", "perspective", "look_at", "render_gaussians_torch", "rasterize",
            "make_view", "prepare_view", "prepare_native", "Prepared", "forward_native", "backward_native",
            "backward_l1_native", "backward_fit_native", "forward_l1_native", "backward_splat_native", "reduce_views_native",
+           "gather_view_native", "reduce_sums_native",
            "DEFAULT_CUTOFF", "DEPTH_GRAD_CUTOFF", "DEFAULT_CORE_CUTOFF", "FIT_CUTOFF", "default_cutoff"]

@@ -26,8 +26,22 @@ Also reported on rank 0:
   default_precision_mode
                 a few more timed steps with a depth term in the loss (the f32-grade mode a depth-loss
                 caller gets; the headline runs the fit's own loss, which has no depth term)
+  f32_grade_fit the headline's fit step with every splat at f32 grade (three-piece splits,
+                gr_view.no_depth_grad = 2): isolates what the two-piece operand splits buy
+  dropin_op     the drop-in op exactly as the unchanged reference fit loop calls it
+                (fit_multiview_stub.py:265-311): per view render_gaussians_torch(..., return_aux=True) with
+                a fresh device background tensor, torch L1 + silhouette losses, loss.backward(),
+                torch.optim.Adam, float(loss) per iteration; same C4 workload
+  psnr_vs_ref   the checker leg (outside every timed region): one view of the final fitted state, the
+                bench's render path and the drop-in default path vs the exact float64 dense render
+                (oracle/gr_oracle.c, every Gaussian at every pixel) at 2048 random pixels
   sclk_mhz      the shader clock before and after (rocm-smi)
-  cpu_baseline  the CPU oracle (oracle/gr_oracle.c, OpenMP) on one view of the same workload.
+  cpu_baseline  the build's CPU path (cpu_renderer.py: the reference's dense semantics, torch on the host
+                cores) fwd+bwd on one view of the same workload; beside it config C1 (the reference stub's
+                CPU plumbing case) through the same op and the float64 oracle on one view.
+  pmc           per-launch HBM bytes and VALU / MFMA issue fractions of the kernels from
+                profiles/pmc_traffic.json (tools/pmc_profile.sh), used only when its source stamp equals
+                the sha256 of this tree's gr_hip.hip (else flagged stale and not used).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--device cpu]
 N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
@@ -100,6 +114,8 @@ def parse():
                          "not a measurement")
     ap.add_argument("--no-reorder", action="store_true",
                     help="keep the synthetic Gaussians in their random order (A/B of the trainer's Morton order)")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the dropin_op measurement")
+    ap.add_argument("--no-psnr", action="store_true", help="skip the psnr_vs_ref checker leg")
     return ap.parse_args()
 
 
@@ -147,22 +163,159 @@ def synthetic_params(n: int, device) -> dict:
     return {k: torch.nn.Parameter(v.to(device)) for k, v in p.items()}
 
 
+def _cpu_op_fwd_bwd(n: int, res: int, views: int, nviews: int) -> float:
+    """Seconds for fwd + bwd of ``nviews`` views through the build's CPU op (render_gaussians_torch on host
+    tensors -> cpu_renderer.py), L1 loss, on the synthetic scene of ``n`` Gaussians."""
+    p = synthetic_params(n, torch.device("cpu"))
+    cams = fm.orbit_cameras(views, res, res, torch.device("cpu"))
+    g = torch.Generator().manual_seed(3)
+    tgt = torch.rand((res, res, 3), generator=g)
+    t0 = time.perf_counter()
+    means, scales, colors, opac = fm.activations(p)
+    total = 0.0
+    for i in range(nviews):
+        out, alpha, _ = tr.render_gaussians_torch(means, scales, colors, opac, cams[i], res, res,
+                                                  max_gaussians=max(10000, n), return_aux=True)
+        total = total + torch.mean(torch.abs(out - tgt))
+    total.backward()
+    return time.perf_counter() - t0
+
+
 def cpu_baseline(n: int, res: int, views: int) -> dict:
-    """Oracle port (float64 accumulation, OpenMP over the host cores) on ONE view of the workload."""
+    """The build's CPU op (cpu_renderer.py, torch on the host cores: the reference's dense semantics) on ONE
+    view of the workload (fwd + bwd), plus config C1 through the same op and the float64 oracle port."""
     from oracle import oracle as orc
 
+    threads = torch.get_num_threads()
+    dt = _cpu_op_fwd_bwd(n, res, views, 1)
+    c1 = _cpu_op_fwd_bwd(1200, 128, 4, 4)
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     scene = orc.synthetic_scene(n, seed=0)
     view, proj = orc.orbit_cameras(views, res, res)[0]
     v = orc.make_view(view, proj, res, res, cutoff=tr.default_cutoff(False), core_cutoff=tr.DEFAULT_CORE_CUTOFF)
-    g = np.random.default_rng(0).standard_normal((res, res, 3)).astype(np.float32)
+    gr = np.random.default_rng(0).standard_normal((res, res, 3)).astype(np.float32)
     t0 = time.perf_counter()
     orc.forward(v, scene, binned=True)
-    orc.backward(v, scene, g, None, None, binned=True)
+    orc.backward(v, scene, gr, None, None, binned=True)
+    dto = time.perf_counter() - t0
+    return {"value": round(res * res / dt / 1e6, 5), "unit": "Mpixels/sec fwd+bwd", "cores": threads, "kind": "port",
+            "sample": f"1 view of the workload ({n} Gaussians, {res}x{res}) fwd+bwd through render_gaussians_torch on "
+                      f"host tensors (cpu_renderer.py, dense: every Gaussian at every pixel, as the reference), torch "
+                      f"with {threads} threads, {dt:.1f} s",
+            "c1": {"value": round(4 * 128 * 128 / c1 / 1e6, 4), "unit": "Mpixels/sec fwd+bwd", "threads": threads,
+                   "sample": f"config C1: 1200 Gaussians, 4 views 128x128, one fit step's fwd+bwd through the same op, "
+                             f"{c1:.2f} s"},
+            "oracle": {"value": round(res * res / dto / 1e6, 5), "unit": "Mpixels/sec fwd+bwd", "cores": cores,
+                       "sample": f"1 view of the workload, oracle/gr_oracle.c binned float64 fwd+bwd, OpenMP {cores} "
+                                 f"threads, {dto:.1f} s"}}
+
+
+def source_sha256() -> str:
+    import hashlib
+
+    with open(os.path.join(REPO, "3dgaussian_amd", "csrc", "gr_hip.hip"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def pmc_table() -> dict:
+    """profiles/pmc_traffic.json (tools/pmc_profile.sh + tools/pmc_summarize.py) when its stamp matches this
+    tree's kernel source; else {"stale": True, ...} and no figures."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return {"stale": True, "reason": "no profiles/pmc_traffic.json"}
+    with open(path) as f:
+        tab = json.load(f)
+    tree = source_sha256()
+    if tab.get("source_sha256") != tree:
+        return {"stale": True, "reason": "collected on another gr_hip.hip", "file_sha256": tab.get("source_sha256"),
+                "tree_sha256": tree}
+    return {"stale": False, "source_sha256": tree, "dir": tab.get("dir"), "kernels": tab.get("kernels", {})}
+
+
+def pmc_of(pmc: dict, prefix: str) -> dict:
+    if pmc.get("stale"):
+        return {}
+    for k, e in pmc["kernels"].items():
+        if k.startswith(prefix):
+            return e
+    return {}
+
+
+def dropin_op(n: int, V: int, R: int, steps: int, warmup: int, device) -> dict:
+    """fit_multiview_stub.py:265-311 as written, on the drop-in module: the unchanged reference loop's use of
+    the op (render_gaussians_torch per view with a fresh device background, torch losses, autograd, Adam,
+    float(loss) per iteration).  Mpx/s over ``steps`` iterations after ``warmup``."""
+    params = synthetic_params(n, device)
+    cams = fm.orbit_cameras(V, R, R, device)
+    g = torch.Generator(device=device).manual_seed(1)
+    targets = [torch.rand((R, R, 3), generator=g, device=device) for _ in range(V)]
+    masks = [(t.mean(dim=2) > 0.5).to(torch.float32) for t in targets]
+    opt = torch.optim.Adam(list(params.values()), lr=0.02)
+
+    def iteration():
+        opt.zero_grad(set_to_none=True)
+        means = params["means"]
+        scales = torch.nn.functional.softplus(params["scales_raw"]) + 1e-3
+        opacities = torch.sigmoid(params["opacities_raw"])
+        colors_eval = torch.sigmoid(params["colors_raw"])
+        total = torch.tensor(0.0, device=device)
+        for i, tgt in enumerate(targets):
+            pred, alpha, depth = tr.render_gaussians_torch(means, scales, colors_eval, opacities, cams[i], width=R,
+                                                           height=R, background=torch.tensor([0.0, 0.0, 0.0], device=device),
+                                                           max_gaussians=max(3000, means.shape[0]), return_aux=True)
+            loss_i = torch.mean(torch.abs(pred - tgt)) + 0.2 * torch.mean(torch.abs(alpha - masks[i]))
+            total = total + loss_i
+        reg = 1e-3 * opacities.mean() + 1e-3 * scales.mean()
+        loss = total / len(targets) + reg
+        loss.backward()
+        opt.step()
+        return float(loss.detach().cpu())
+
+    for _ in range(warmup):
+        iteration()
+    spec0 = dict(tr._SPEC)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        lv = iteration()
+    torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return {"value": round(res * res / dt / 1e6, 5), "unit": "Mpixels/sec fwd+bwd", "cores": cores, "kind": "port",
-            "sample": f"1 view of the workload ({n} Gaussians, {res}x{res}), oracle/gr_oracle.c binned fwd+bwd, "
-                      f"OpenMP {cores} threads, {dt:.1f} s"}
+    return {"value": round(V * R * R * steps / dt / 1e6, 2), "unit": "Mpixels/sec", "steps": steps, "warmup": warmup,
+            "ms_per_step": round(1e3 * dt / steps, 3), "loss": lv,
+            "speculative_preparations": {"hits": tr._SPEC["hits"] - spec0["hits"],
+                                         "misses": tr._SPEC["misses"] - spec0["misses"]},
+            "path": "render_gaussians_torch (autograd op, default precision mode: depth_grad=True, 8/5.5-sigma "
+                    "footprint) as fit_multiview_stub.py:277-311 calls it, unchanged loop"}
+
+
+def psnr_vs_ref(fitter, cams, R: int, device, npix: int = 2048) -> dict:
+    """Checker leg: view 0 of the current fitted state, rendered by the bench's path (fit footprint, no depth
+    channel, two-piece f16/bf16 splits) and by the drop-in default path, against the exact float64 dense
+    render (oracle/gr_oracle.c: every Gaussian at every pixel, no cutoff) at ``npix`` random pixels."""
+    from oracle import oracle as orc
+
+    with torch.no_grad():
+        acts = [a.detach().float().contiguous() for a in fm.activations(fitter.params)]
+    sc = orc.Scene(*(a.cpu().numpy() for a in acts))
+    view, proj = orc.orbit_cameras(len(cams), R, R)[0]
+    v = orc.make_view(view, proj, R, R, None)
+    pix = np.random.default_rng(11).choice(R * R, npix, replace=False).astype(np.int32)
+    t0 = time.perf_counter()
+    d_out, d_a, _ = orc.dense_pixels(v, sc, pix)
+    t_dense = time.perf_counter() - t0
+    res = {}
+    for name, kw in (("bench_path", dict(cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF, depth_grad=False)),
+                     ("dropin_default", {})):
+        gv = tr.make_view(view, proj, R, R, None, **kw)
+        out, alpha, _, _ = tr.forward_native(*acts, gv, want_depth=False)
+        o = out.cpu().numpy().reshape(-1, 3)[pix]
+        a = alpha.cpu().numpy().reshape(-1)[pix]
+        res[name] = {"psnr_db": round(orc.psnr(o, d_out), 2), "rel_l2_rgb": float(f"{orc.rel_l2(o, d_out):.3e}"),
+                     "rel_l2_alpha": float(f"{orc.rel_l2(a, d_a):.3e}")}
+    res.update(value=res["bench_path"]["psnr_db"], unit="dB", target=">= 60 dB (north_star)",
+               sample=f"view 0 of the final fitted state, {npix} random pixels, exact float64 dense reference "
+                      f"({t_dense:.1f} s on the host)")
+    return res
 
 
 def pairs_per_view(fitter, cams, R, cutoff, core_cutoff):
@@ -268,7 +421,7 @@ def main():
 
     # the default precision mode: what a caller with a depth loss gets (f32-grade W / D, three-piece
     # backward with the tail pairs): the same fit with a depth term in the loss (C3's losses)
-    extra = {}
+    extra, f32g = {}, None
     if not args.no_extra_modes:
         gd = torch.Generator(device=device).manual_seed(2)
         fitter.depths = [torch.rand((R, R), generator=gd, device=device) for _ in range(V)]
@@ -279,7 +432,23 @@ def main():
         extra = {"value": round(V * R * R * k / dt / 1e6, 2), "steps": k, "ms_per_step": round(1e3 * dt / k, 3),
                  "mode": "depth_grad=True: forward W/D f32-grade (3-piece bf16 split), backward 3-piece with tail "
                          "pairs; loss L1 + silhouette + 0.05 depth L1 (fit_multiview_stub.py:299-305)"}
+        # the headline's own loss and footprint with every splat at f32 grade (no_depth_grad = 2)
+        fm.F32_GRADE = True
+        fitter.step()
+        dt, _ = timed(k)
+        fm.F32_GRADE = False
+        f32g = {"value": round(V * R * R * k / dt / 1e6, 2), "steps": k, "ms_per_step": round(1e3 * dt / k, 3),
+                "mode": "the headline fit step (L1 + silhouette, 5-sigma fit footprint, fused path) with "
+                        "gr_view.no_depth_grad = 2: forward W three bf16 pieces, colours two pieces x three-piece B, "
+                        "backward three-piece splits (the default precision mode's splats, f32-grade)"}
     clk1 = sclk_mhz() if rank == 0 else None
+    psnr = psnr_vs_ref(fitter, cams, R, device) if (rank == 0 and not args.no_psnr) else None
+    my_views_n = max(len(fitter.my_views), 1)
+    drop = None
+    if rank == 0 and world == 1 and not args.no_dropin:
+        del fitter
+        torch.cuda.empty_cache()
+        drop = dropin_op(n, V, R, steps=2, warmup=1, device=device)
 
     if rank == 0:
         bwd_ms, bwd_n = prof["raster_bwd"]
@@ -288,23 +457,19 @@ def main():
         fwd_conc_us = 1e3 * prof_concurrent["raster_fwd"][0] / max(prof_concurrent["raster_fwd"][1], 1)
         bwd_avg_s = bwd_ms / max(bwd_n, 1) / 1e3
         fwd_avg_s = fwd_ms / max(fwd_n, 1) / 1e3
-        pmc_tab = {}
-        pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                pmc_tab = json.load(f)
+        pmc = pmc_table()
         avg_tail = avg_pairs - avg_core
         px = R * R
         # SURVEY.md 8(d) per-unit bytes: a pair = 12 B key/value + 36 B projected record read once per
         # splat pass; the backward also writes its 36 B of gradient partials; per pixel 20 B of outputs
         # + 20 B of saved state written (forward) / 20 B of upstream grads + 20 B saved read (backward)
         kernels = {
-            "fwd": dict(kernel=FWD_KERNEL, t=fwd_avg_s, n=fwd_n, conc_us=fwd_conc_us, units=avg_pairs,
+            "fwd": dict(kernel=FWD_KERNEL, variant="k_raster_fwd_mfma<4>", t=fwd_avg_s, n=fwd_n, conc_us=fwd_conc_us, units=avg_pairs,
                         unit_bytes=12 + 36, px_bytes=40,
                         units_desc="pairs per launch",
                         flop=BF16_FLOP_PER_CORE_PAIR_FWD * avg_core + BF16_FLOP_PER_TAIL_PAIR_FWD * avg_tail,
                         f32=F32_FLOP_PER_CORE_PAIR_FWD * avg_core + F32_FLOP_PER_TAIL_PAIR_FWD * avg_tail),
-            "bwd": dict(kernel=BWD_KERNEL, t=bwd_avg_s, n=bwd_n, conc_us=bwd_conc_us, units=avg_core,
+            "bwd": dict(kernel=BWD_KERNEL, variant="k_raster_bwd_bf16<false,2>", t=bwd_avg_s, n=bwd_n, conc_us=bwd_conc_us, units=avg_core,
                         unit_bytes=12 + 36 + 36, px_bytes=40,
                         units_desc="core pairs per launch (no upstream depth gradient: tail pairs skipped)",
                         flop=BF16_FLOP_PER_CORE_PAIR_BWD * avg_core, f32=F32_FLOP_PER_CORE_PAIR_BWD * avg_core),
@@ -315,9 +480,12 @@ def main():
             nbytes = e["unit_bytes"] * e["units"] + e["px_bytes"] * px
             ach = nbytes / e["t"] / 1e9
             mf = e["flop"] / e["t"] / 1e12
-            return {"bound": "hbm", "kernel": e["kernel"], "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+            pk = pmc_of(pmc, e["variant"])
+            return {"bound": "hbm", "kernel": e["variant"], "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                    "traffic": pmc_tab.get(e["kernel"], {}).get("hbm_bytes_per_launch"),
+                    "traffic": pk.get("hbm_bytes_per_launch"),
+                    "valu_frac": pk.get("valu_frac"), "mfma_frac": pk.get("mfma_frac"),
+                    "valu_per_32_pair_step": pk.get("valu_per_12_mfma"),
                     "algorithmic_bytes_per_launch": int(nbytes),
                     "bytes_model": f"{e['unit_bytes']} B x {e['units_desc']} ({int(e['units'])}) + {e['px_bytes']} B x {px} px",
                     "avg_launch_us": round(e["t"] * 1e6, 1), "launches": e["n"],
@@ -336,7 +504,7 @@ def main():
                     "frac": round(value / (roof_mpx * world), 4)}
 
         out = {
-            "metric": "Mpixels/sec fwd+bwd @1M Gaussians 800x800",
+            "metric": "Mpixels/sec fwd+bwd @1M Gaussians 800\u00d7800; PSNR vs torch ref",
             "value": round(value, 2),
             "unit": "Mpixels/sec",
             "n_gpus": world,
@@ -364,8 +532,8 @@ def main():
             "roofline": roof(dominant),
             "splats": {"fwd": roof("fwd"), "bwd": roof("bwd")},
             # the batched per-Gaussian reduction (gr_reduce_views), HIP events, per view of the single-stream step
-            "reduce_us_per_view": round(1e3 * prof["reduce_bwd"][0] / max(len(fitter.my_views), 1), 1),
-            "binning_us_per_view": round(1e3 * prof["binning"][0] / max(len(fitter.my_views), 1), 1),
+            "reduce_us_per_view": round(1e3 * prof["reduce_bwd"][0] / my_views_n, 1),
+            "binning_us_per_view": round(1e3 * prof["binning"][0] / my_views_n, 1),
             "hbm_model": dict(hbm_model(avg_pairs),
                               survey_table_roofline_mpx_per_s=SURVEY_C4_ROOF_MPX,
                               frac_of_survey_table=round(value / (SURVEY_C4_ROOF_MPX * world), 4),
@@ -373,6 +541,10 @@ def main():
                                      f"fit path bins one {tr.FIT_CUTOFF:g}-sigma zone, the survey's footprint), and "
                                      f"the survey table's C4 roof (K = 9.41e6 pairs per view at view 0)"),
             "default_precision_mode": extra or None,
+            "f32_grade_fit": f32g,
+            "dropin_op": drop,
+            "psnr_vs_ref": psnr,
+            "pmc": {k: v for k, v in pmc.items() if k != "kernels"},
             "sclk_mhz": {"before": clk0, "after": clk1},
             "loss": float(loss),
         }

@@ -81,7 +81,13 @@ typedef struct gr_view {
                        /* gradient needs (d depth/d w cancels on thin pixels).  1: the caller   */
                        /* will not pass a depth gradient to gr_bwd for this view; W and D are   */
                        /* then accumulated within 2^-16 relative (as the colours), and gr_bwd   */
-                       /* rejects a non-NULL g_depth (GR_ERR_INVALID_ARGUMENT)                  */
+                       /* rejects a non-NULL g_depth (GR_ERR_INVALID_ARGUMENT).  2: no depth    */
+                       /* gradient (as 1) but every splat at the default mode's f32 grade       */
+                       /* (three-piece splits): the fit path's precision reference              */
+  const float* background_dev; /* optional DEVICE pointer to 3 floats: when non-NULL the kernels read */
+                       /* the background colour from it (stream-ordered) instead of background[]: */
+                       /* a caller holding the background in a device tensor (the reference fit   */
+                       /* loop, fit_multiview_stub.py:287) needs no device-to-host read per view  */
 } gr_view;
 
 /* ------------------------------------------------------------------------------------------ */
@@ -90,7 +96,8 @@ typedef struct gr_view {
 /*   (extension: degree-3 coefficients (N,16,3) [color_dim 48], basis in DESIGN.md §2),           */
 /*   opacities (N,), all float32 contiguous.                                                   */
 /*   Views rendered with no_depth_grad and no depth output (the fit path) take f16 operand      */
-/*   pieces scaled by 2^4: opacities must stay below 4094 there (sigmoid outputs always do).    */
+/*   pieces scaled by 2^4; a view whose largest opacity reaches 2^11 gets a smaller power-of-two */
+/*   scale (computed on the device by the preparation), so any opacity gives finite results.     */
 /* ------------------------------------------------------------------------------------------ */
 
 /* Sizes produced by gr_fwd_prepare for one view. */
@@ -223,6 +230,28 @@ gr_status gr_reduce_views(int num_views, const gr_reduce_view* views, int n, con
                           const float* scales, const float* colors, int color_dim,
                           const float* opacities, float* d_means, float* d_scales, float* d_colors,
                           float* d_opacities, int accumulate, void* stream);
+
+/* gr_reduce_views in two stages, so that a fit can release each view's workspaces right after its
+ * backward and the gathers run beside other views' splat kernels (what fit_multiview.py uses):
+ *   gr_gather_view   right after gr_bwd_splat of a view: sums its per-pair partials per Gaussian into
+ *                    `sums` (gr_view_sums_floats(n) device floats, 8 per Gaussian); the view's geom, bins
+ *                    and ws may be released once this has run on the stream.
+ *   gr_reduce_sums   the chain rule of up to GR_REDUCE_MAX_VIEWS gathered views: writes (accumulate = 0)
+ *                    or adds (accumulate != 0) their summed gradient once.
+ * gr_gather_view per view + gr_reduce_sums = gr_reduce_views, up to float summation order (the gathers
+ * sum in f32, gr_reduce_views in f64).  Deterministic.  Replaces the same reference code as
+ * gr_reduce_views (fit_multiview_stub.py:310, the autograd sums over the views). */
+typedef struct gr_sums_view {
+  gr_view view;      /* the view as rendered (its camera: the chain rule)      */
+  const float* sums; /* its gr_gather_view output                              */
+} gr_sums_view;
+size_t gr_view_sums_floats(int n);
+gr_status gr_gather_view(const gr_view* v, int n, const gr_plan* plan, const void* geom, const void* bins,
+                         const void* ws, float* sums, void* stream);
+gr_status gr_reduce_sums(int num_views, const gr_sums_view* views, int n, const float* means,
+                         const float* scales, const float* colors, int color_dim,
+                         const float* opacities, float* d_means, float* d_scales, float* d_colors,
+                         float* d_opacities, int accumulate, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Legacy uint8 surface (host pointers), replaces gr::render_gaussians (renderer.h:33-39).    */

@@ -50,9 +50,10 @@ def test_layouts_are_aligned_and_ordered(pkg):
 
 
 def test_struct_sizes_match_header(pkg):
-    # gr_view: 2 ints + 16 + 16 + 3 + 3 + 2 floats + 1 int; gr_render_params: RenderParams' layout
+    # gr_view: 2 ints + 16 + 16 + 3 + 3 + 2 floats + 1 int, then the background_dev pointer (8-aligned);
+    # gr_render_params: RenderParams' layout
     from oracle import oracle as orc
-    assert ctypes.sizeof(pkg._native.GrView) == 4 * (2 + 16 + 16 + 3 + 3 + 2 + 1)
+    assert ctypes.sizeof(pkg._native.GrView) == 4 * (2 + 16 + 16 + 3 + 3 + 2 + 1) + 4 + 8
     assert [f[0] for f in pkg._native.GrView._fields_] == [f[0] for f in orc.GrView._fields_]
     assert ctypes.sizeof(pkg._native.GrRenderParams) == 4 * (2 + 16 + 16 + 3 + 3)
 
@@ -67,3 +68,46 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     spec.loader.exec_module(mod)
     with pytest.raises(ImportError):
         mod.lib()
+
+
+def _integration_snippet() -> str:
+    """The ctypes example of INTEGRATION.md §4 (the second python block of the file)."""
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    blocks = re.findall(r"```python\n(.*?)```", text, flags=re.S)
+    snip = [b for b in blocks if "gr_fwd_prepare" in b]
+    assert len(snip) == 1
+    return snip[0].replace('ctypes.CDLL("3dgaussian_amd/libgr_hip.so")',
+                           'ctypes.CDLL(os.path.join(REPO, "3dgaussian_amd", "libgr_hip.so"))')
+
+
+def test_integration_ctypes_example_plan_layout(pkg):
+    """The example's GrPlan has the 24-byte layout of gr_plan (the library writes three int64)."""
+    ns = {}
+    snip = _integration_snippet()
+    cls = snip[snip.index("class GrPlan"):snip.index("lib.gr_geom_bytes")]
+    exec("import ctypes\n" + cls, ns)
+    assert ctypes.sizeof(ns["GrPlan"]) == 24 == ctypes.sizeof(pkg._native.GrPlan)
+
+
+@pytest.mark.gpu
+def test_integration_ctypes_example_runs(pkg):
+    """INTEGRATION.md §4's ctypes snippet, run as written against the built library: the plan it
+    reads back equals the one the package's own binding gets."""
+    import numpy as np
+    import torch
+
+    from oracle import oracle as orc
+
+    sc = orc.synthetic_scene(2000, seed=4, scale=0.04)
+    view, proj = orc.orbit_cameras(4, 96, 64)[1]
+    means, scales, colors, opac = (torch.from_numpy(a).cuda() for a in sc.arrays())
+    n = means.shape[0]
+    gv = pkg.torch_renderer.make_view(view, proj, 96, 64)
+    ns = {"os": os, "REPO": REPO, "torch": torch, "view": gv, "n": n, "means": means, "scales": scales,
+          "colors": colors, "opac": opac, "GrRenderParams": pkg._native.GrRenderParams}
+    exec(_integration_snippet(), ns)
+    torch.cuda.synchronize()
+    ref = pkg.torch_renderer.prepare_native(means, scales, colors, opac, gv).plan()
+    got = ns["plan"]
+    assert (got.num_pairs, got.num_core_pairs) == (int(ref.num_pairs), int(ref.num_core_pairs))
+    assert got.num_pairs > 0 and np.isfinite(got.num_pairs)

@@ -157,11 +157,12 @@ def test_fit_path_on_fitted_state_vs_dense(pkg, cuda):
         assert e <= 1e-4, (k, e)
 
 
-@pytest.mark.parametrize("opac_range", [(1e-4, 1e-3), (0.0, 1.0), (100.0, 3000.0)])
+@pytest.mark.parametrize("opac_range", [(1e-4, 1e-3), (0.0, 1.0), (100.0, 3000.0), (3000.0, 6000.0), (0.0, 1e5)])
 def test_fit_mode_f16_operand_range(pkg, cuda, opac_range):
-    """The fit-path forward (no depth channel) multiplies on f16 operand pieces pre-scaled by 2^4 (A) and
-    2^12 (B): opacities from 1e-4 (operands near the f16 subnormal range) up to 3000 (near the documented
-    4094 limit, include/gr_hip.h) stay within the parity bar vs the float64 binned oracle."""
+    """The fit-path forward (no depth channel) multiplies on f16 operand pieces pre-scaled by 2^sa (A) and
+    2^12 (B), sa = 4 while the view's largest opacity is below 2^11 and lower above (f16_sa_of): opacities
+    from 1e-4 (operands near the f16 subnormal range) up to 1e5 (past the fixed 2^4 scale's f16 range of
+    4094) stay finite and within the parity bar vs the float64 binned oracle."""
     tr = pkg.torch_renderer
     rng = np.random.default_rng(7)
     sc = orc.synthetic_scene(3000, seed=3, scale=0.05)
