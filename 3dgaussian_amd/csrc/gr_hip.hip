@@ -1766,7 +1766,10 @@ __device__ __forceinline__ void tile_fragments(const float (*sU)[TP], uint4* __r
     if (!depth && pr == 2) continue;  // never read
     const int r = l & 31, h = l >> 5, ch = pair_channel(pr, r >> 4, depth), i = r & 15;
     uint4* o = fr + ((side * 3 + pr) * 3) * 64 + l;
-    if (pieces == 2) {  // no_depth_grad views: two round-to-nearest pieces (split2_frag)
+    // no_depth_grad views: two round-to-nearest pieces (split2_frag); with a depth gradient the colour
+    // pairs take them too (contracted against three-piece B, mfma_split_a2b3): only the (dW, dD) pair
+    // cancels in the per-pair epilogue and needs the exact three-piece split
+    if (pieces == 2 || (depth && pr < 2)) {
       float val[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -1979,6 +1982,19 @@ __device__ __forceinline__ f32x16 mfma_split(const uint4* __restrict__ A, int la
   return c;
 }
 
+// A in two round-to-nearest pieces (split2_frag), B in an exact three-piece split: the four products of
+// weight >= 2^-17 (a1 b1 ~ 2^-17 is dropped, unbiased: a1 has either sign); the colour channel pairs of
+// the depth-gradient backward.
+__device__ __forceinline__ f32x16 mfma_split_a2b3(const uint4* __restrict__ A, int lane, const s16x8 (&B)[3]) {
+  f32x16 c = {};
+  const s16x8 a0 = as_frag(A[lane]);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(A[64 + lane]), B[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, B[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, B[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, B[0], c, 0, 0, 0);
+  return c;
+}
+
 // A * B over two round-to-nearest pieces each (split2_frag; no_depth_grad views): three products.
 __device__ __forceinline__ f32x16 mfma_split2(const uint4* __restrict__ A, int lane, const s16x8 (&B)[2]) {
   f32x16 c = {};
@@ -2067,9 +2083,13 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
         split_frag(ex, BT);
         split_frag(ey, BR);
 #pragma unroll
-        for (int pr = P0; pr < P1; ++pr) DT[pr] = mfma_split(sUF + (0 * 3 + pr) * 3 * 64, lane, BT);
+        for (int pr = P0; pr < P1; ++pr)
+          DT[pr] = (DEPTH && pr < 2) ? mfma_split_a2b3(sUF + (0 * 3 + pr) * 3 * 64, lane, BT)
+                                     : mfma_split(sUF + (0 * 3 + pr) * 3 * 64, lane, BT);
 #pragma unroll
-        for (int pr = P0; pr < P1; ++pr) DR[pr] = mfma_split(sUF + (1 * 3 + pr) * 3 * 64, lane, BR);
+        for (int pr = P0; pr < P1; ++pr)
+          DR[pr] = (DEPTH && pr < 2) ? mfma_split_a2b3(sUF + (1 * 3 + pr) * 3 * 64, lane, BR)
+                                     : mfma_split(sUF + (1 * 3 + pr) * 3 * 64, lane, BR);
       } else {
         s16x8 BT[2], BR[2];
         split2_frag(ex, BT);

@@ -44,10 +44,11 @@ def _fitter(fm, bench, cuda, views, n=N_C4, seed=1):
 @pytest.mark.timeout(600)
 def test_fit_chain_c4_batch_vs_oracle(cuda):
     fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    tr = importlib.import_module("3dgaussian_amd.torch_renderer")
     bench = importlib.import_module("bench")
     V = 8
     saved = fm.NUM_STREAMS, fm.REDUCE_TAIL, fm.REDUCE_BATCH
-    fm.NUM_STREAMS, fm.REDUCE_TAIL, fm.REDUCE_BATCH = 1, 0, 16  # one stream: one gr_reduce_views of all 8 views
+    fm.NUM_STREAMS, fm.REDUCE_TAIL, fm.REDUCE_BATCH = 1, 0, 16  # one stream: one reduction batch of all 8 views
     try:
         fit, targets, masks = _fitter(fm, bench, cuda, V)
         with torch.no_grad():
@@ -63,23 +64,33 @@ def test_fit_chain_c4_batch_vs_oracle(cuda):
     cams = orc.orbit_cameras(50, W, H)[:V]
     w_sil, g_scale, HW = fit.w_sil, 1.0 / V, H * W
     ora = [np.zeros(a.shape, np.float64) for a in hip]
-    ora_loss = 0.0
+    ora_loss, out_err, flips = 0.0, 0.0, 0
     for i, (view, proj) in enumerate(cams):
-        v = orc.make_view(view, proj, W, H, None, cutoff=fit_cutoff(), core_cutoff=fit_cutoff())
+        v = orc.make_view(view, proj, W, H, None, cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF)
         out, alpha, _ = orc.forward(v, sc, binned=True)
+        # the HIP forward's own images in the fused path's precision mode (the same f16 accumulation as
+        # gr_fwd_render_l1): the L1 kink makes sign(out - t) at near-ties depend on the last float bit, so the
+        # oracle's upstream takes the HIP outputs' signs (how many differ from the oracle's own is printed)
+        gv = tr.make_view(view, proj, W, H, None, cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
+        h_out, h_alpha, _, _ = tr.forward_native(*acts, gv, want_depth=False)
+        h_out, h_alpha = h_out.cpu().numpy().astype(np.float64), h_alpha.cpu().numpy().astype(np.float64)
+        out_err = max(out_err, orc.rel_l2(h_out, out))
         t, m = targets[i].cpu().numpy(), masks[i].cpu().numpy()
         d_rgb, d_a = out.astype(np.float64) - t, alpha.astype(np.float64) - m
+        s_rgb, s_a = np.sign(h_out - t), np.sign(h_alpha - m)
+        flips += int((s_rgb != np.sign(d_rgb)).sum() + (s_a != np.sign(d_a)).sum())
         ora_loss += np.abs(d_rgb).mean() + w_sil * np.abs(d_a).mean()
-        g_rgb = (np.sign(d_rgb) * (g_scale / (3 * HW))).astype(np.float32)
-        g_a = (np.sign(d_a) * (w_sil * g_scale / HW)).astype(np.float32)
+        g_rgb = (s_rgb * (g_scale / (3 * HW))).astype(np.float32)
+        g_a = (s_a * (w_sil * g_scale / HW)).astype(np.float32)
         for k, gk in enumerate(orc.backward(v, sc, g_rgb, g_a, None, binned=True)):
             ora[k] += gk
-    errs = {"loss": abs(hip_loss - ora_loss) / ora_loss}
+    errs = {"loss": abs(hip_loss - ora_loss) / ora_loss, "out (max over views)": out_err}
     for name, h, o in zip(("d_means", "d_scales", "d_colors", "d_opac"), hip, ora):
         if name == "d_scales":  # the render's scale gradient has no z column (the reference's either)
             h, o = h[:, :2], o[:, :2]
         errs[name] = orc.rel_l2(h, o)
-    print("C4 fit chain (8 views, one gr_reduce_views batch) vs float64 oracle:", {k: f"{e:.2e}" for k, e in errs.items()})
+    print(f"C4 fit chain (8 views, one reduction batch) vs float64 oracle ({flips} of {V * 4 * HW} upstream signs "
+          f"differ between the HIP and oracle outputs):", {k: f"{e:.2e}" for k, e in errs.items()})
     assert errs["loss"] <= 1e-5, errs
     for k, e in errs.items():
         assert e <= 1e-4, (k, e)
