@@ -601,8 +601,17 @@ def _spec_take(key, tensors) -> Optional[Prepared]:
     return None
 
 
-def _spec_after(key, gv, tensors) -> None:
-    """Learn the camera order and enqueue the preparation of the camera expected next."""
+def _spec_stream(dev: torch.device) -> "torch.cuda.Stream":
+    st = _SPEC.get(("stream", str(dev)))
+    if st is None:
+        st = _SPEC[("stream", str(dev))] = torch.cuda.Stream(dev)
+    return st
+
+
+def _spec_after(key, gv, tensors, inputs_ready) -> None:
+    """Learn the camera order and enqueue the preparation of the camera expected next, on a stream of its
+    own that waits only for the input tensors (``inputs_ready``, recorded before this view's kernels), so it
+    runs beside this view's render and the host's wait for its plan does not include the render."""
     last = _SPEC["last"]
     if last is not None:
         _SPEC["next"][last] = key
@@ -614,7 +623,12 @@ def _spec_after(key, gv, tensors) -> None:
     nxt = _SPEC["next"].get(key)
     if nxt is None or (key, nxt) in _SPEC["cold"]:
         return
-    pv = prepare_native(*tensors, _SPEC["views"][nxt])
+    ps = _spec_stream(tensors[0].device)
+    ps.wait_event(inputs_ready)
+    for t in tensors:  # read on ps: not reused by the allocator before ps is done with them
+        t.record_stream(ps)
+    with torch.cuda.stream(ps):
+        pv = prepare_native(*tensors, _SPEC["views"][nxt])
     _SPEC["pending"] = _Speculation(nxt, tensors, pv, key)
 
 
@@ -640,12 +654,14 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
         return _RasterizeGaussians.apply(m, s, c, o, background, gv, prepared)
     key = _view_key(gv)
     pv = _spec_take(key, (m, s, c, o))
+    stream = torch.cuda.current_stream(dev)
     if pv is not None:
-        stream = torch.cuda.current_stream(dev)
         stream.wait_event(pv.event)
         pv.geom.record_stream(stream)
+    ready = torch.cuda.Event()
+    ready.record(stream)
     res = _RasterizeGaussians.apply(m, s, c, o, background, gv, pv)
-    _spec_after(key, gv, (m, s, c, o))
+    _spec_after(key, gv, (m, s, c, o), ready)
     return res
 
 

@@ -13,7 +13,7 @@ i=0
 for C in "FETCH_SIZE" "WRITE_SIZE" \
          "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
          "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA GRBM_GUI_ACTIVE"; do
-  timeout -k 10 -s KILL 300 rocprofv3 --kernel-trace --pmc $C -d $R/$OUT/p$i -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-extra-modes --no-dropin "$@" > $R/$OUT/p$i.log 2>&1
+  timeout -k 10 -s KILL 300 rocprofv3 --kernel-trace --pmc $C -d $R/$OUT/p$i -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-extra-modes --no-dropin --no-psnr "$@" > $R/$OUT/p$i.log 2>&1
   i=$((i+1))
 done
 cd $R && python tools/pmc_summarize.py $OUT > $OUT/pmc_summary.txt
