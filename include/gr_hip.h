@@ -78,7 +78,8 @@ typedef struct gr_view {
                        /* D forward and the depth-coupled terms backward; <= 0 or >= cutoff  */
                        /* means one zone (def. 5.5)                                            */
   int no_depth_grad;   /* 0 (default): W and D are accumulated f32-grade, as an upstream depth   */
-                       /* gradient needs (d depth/d w cancels on thin pixels).  1: the caller   */
+                       /* gradient needs (d depth/d w cancels on thin pixels); a backward that  */
+                       /* gets no depth gradient runs the two-piece splat (nothing cancels).  1: the caller   */
                        /* will not pass a depth gradient to gr_bwd for this view; W and D are   */
                        /* then accumulated within 2^-16 relative (as the colours), and gr_bwd   */
                        /* rejects a non-NULL g_depth (GR_ERR_INVALID_ARGUMENT).  2: no depth    */
