@@ -371,7 +371,6 @@ struct Bins {
   int* num_items;      // [1]
   int* tile_item0;     // [tiles] first work item of each tile
   int* pos_of;         // [K] sorted position of each pair, by emission index (k_reduce_bwd's map)
-  int* order;          // [cap] dispatch order of the work items (item_order: largest first per XCD share)
 };
 
 // Forward-only scratch (freed by the caller after gr_fwd_render).
@@ -387,7 +386,7 @@ struct Scratch {
 inline int64_t item_cap(int tiles, int64_t K) { return (K + CH - 1) / CH + tiles; }
 
 // `vtiles` = 2 x tiles (core and tail lists of each tile) on the differentiable path.
-size_t bins_fixed(int vtiles, int64_t K, size_t off[8]) {
+size_t bins_fixed(int vtiles, int64_t K, size_t off[7]) {
   const int tiles = vtiles;
   const size_t kk = (size_t)(K > 0 ? K : 1);
   const size_t cap = (size_t)item_cap(tiles, K);
@@ -399,7 +398,6 @@ size_t bins_fixed(int vtiles, int64_t K, size_t off[8]) {
   off[4] = o; o = align_up(o + sizeof(int));
   off[5] = o; o = align_up(o + (size_t)tiles * sizeof(int));
   off[6] = o; o = align_up(o + kk * sizeof(int));
-  off[7] = o; o = align_up(o + cap * sizeof(int));
   return o;
 }
 
@@ -491,7 +489,7 @@ size_t sort_tmp_bytes(int64_t K, int bits) {
 }
 
 Bins bins_view(void* base, int tiles, int64_t K) {
-  size_t off[8];
+  size_t off[7];
   bins_fixed(tiles, K, off);
   char* b = (char*)base;
   Bins r;
@@ -502,7 +500,6 @@ Bins bins_view(void* base, int tiles, int64_t K) {
   r.num_items = (int*)(b + off[4]);
   r.tile_item0 = (int*)(b + off[5]);
   r.pos_of = (int*)(b + off[6]);
-  r.order = (int*)(b + off[7]);
   return r;
 }
 
@@ -805,49 +802,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define GR_WI_THREADS 256
 #endif
 constexpr int WI_THREADS = GR_WI_THREADS;
-// Dispatch order of the work items (Bins::order, read through xcd_item by the splat kernels): block b
-// runs on XCD b % 8 and takes the (b / 8)-th item of that XCD's contiguous share of the tile-ordered list,
-// so each XCD still renders one compact screen region (its L2 keeps the region's records); inside a share
-// the items are ordered by size, largest first (full CH-pair chunks, then by size), so the launch ends on
-// short items instead of waiting for a full chunk started last.  Counting sort by size bucket with LDS
-// atomics: the order within a bucket may vary, the results do not (every item writes its own slots).
-// Called by every thread of the (single-block) work-item kernels after the items are written.
-constexpr int ORDER_BUCKETS = 34;
-__device__ void item_order(const int4* __restrict__ items, int nitems, int* __restrict__ order) {
-  __shared__ int cnt[8][ORDER_BUCKETS];
-  __syncthreads();  // the items written by the block are visible to all its threads
-  const int tid = threadIdx.x, x = tid / (WI_THREADS / 8), j = tid % (WI_THREADS / 8);
-  constexpr int TPX = WI_THREADS / 8;
-  for (int i = tid; i < 8 * ORDER_BUCKETS; i += WI_THREADS) (&cnt[0][0])[i] = 0;
-  const int q = nitems >> 3, r = nitems & 7;
-  const int start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q, len = q + (x < r ? 1 : 0);
-#if defined(GR_NO_ITEM_ORDER)  // A/B: tile order
-  for (int i = j; i < len; i += TPX) order[start + i] = start + i;
-  return;
-#endif
-  auto bucket = [&](int i) {
-    const int4 it = items[start + i];
-    const int sz = it.z - it.y;
-    return sz >= CH ? 0 : 1 + (CH - 1 - sz) * (ORDER_BUCKETS - 2) / CH;
-  };
-  __syncthreads();
-  for (int i = j; i < len; i += TPX) atomicAdd(&cnt[x][bucket(i)], 1);
-  __syncthreads();
-  if (j == 0) {
-    int run = 0;
-    for (int k = 0; k < ORDER_BUCKETS; ++k) {
-      const int c = cnt[x][k];
-      cnt[x][k] = run;
-      run += c;
-    }
-  }
-  __syncthreads();
-  for (int i = j; i < len; i += TPX) order[start + atomicAdd(&cnt[x][bucket(i)], 1)] = start + i;
-}
-
 __global__ __launch_bounds__(WI_THREADS) void k_work_items(int vtiles, const int2* __restrict__ ranges, int4* __restrict__ items,
-                                                     int* __restrict__ num_items, int* __restrict__ tile_item0,
-                                                     int* __restrict__ order) {
+                                                     int* __restrict__ num_items, int* __restrict__ tile_item0) {
   typedef hipcub::BlockScan<int, WI_THREADS> Scan;
   __shared__ typename Scan::TempStorage tmp;
   __shared__ int carry;
@@ -869,7 +825,6 @@ __global__ __launch_bounds__(WI_THREADS) void k_work_items(int vtiles, const int
     __syncthreads();
   }
   if (threadIdx.x == 0) *num_items = carry;
-  item_order(items, carry, order);
 }
 
 // Counting-sort path: per-tile pair totals of the core region (Tc) and of the tail region (Tt,
@@ -879,7 +834,7 @@ __global__ __launch_bounds__(WI_THREADS) void k_work_items(int vtiles, const int
 __global__ __launch_bounds__(WI_THREADS) void k_work_items_zones(int tiles, int tiles_x, int Kc, const int* __restrict__ Tc,
                                                            const int* __restrict__ Tt, int2* __restrict__ ranges,
                                                            int4* __restrict__ items, int* __restrict__ num_items,
-                                                           int* __restrict__ tile_item0, int* __restrict__ order) {
+                                                           int* __restrict__ tile_item0) {
   typedef hipcub::BlockScan<int, WI_THREADS> Scan;
   __shared__ typename Scan::TempStorage tmp;
   const int per = (tiles + WI_THREADS - 1) / WI_THREADS;
@@ -914,7 +869,6 @@ __global__ __launch_bounds__(WI_THREADS) void k_work_items_zones(int tiles, int 
     sch += chc + cht;
   }
   if (threadIdx.x == 0) *num_items = total;
-  item_order(items, total, order);
 }
 
 // Staging pipeline for the 256-wide Gaussian batches of a work item: the records of batch b+1 are
@@ -1905,13 +1859,12 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
                                                          float* __restrict__ fwd_part, float* __restrict__ out_rgb,
                                                          float* __restrict__ out_alpha, float* __restrict__ out_depth,
                                                          float4* __restrict__ saved4, float* __restrict__ savedD,
-                                                         L1Args l1, uint4* __restrict__ UF, const int* __restrict__ f16_sa,
-                                                         const int* __restrict__ order) {
+                                                         L1Args l1, uint4* __restrict__ UF, const int* __restrict__ f16_sa) {
   // LDS: two staged record buffers (2 x 9 KiB) during the loop, then the 4-wave reduction (20 KiB).
   __shared__ __attribute__((aligned(16))) float smem[4 * 5 * TP];
   const int nitems = *num_items;
   if ((int)blockIdx.x >= nitems) return;
-  const int item = order[xcd_item(blockIdx.x, nitems)];  // item_order: largest first per XCD share
+  const int item = xcd_item(blockIdx.x, nitems);
   const int4 it = items[item];
   const int tile = it.x >> 1, k0 = it.y, k1 = it.z;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
@@ -2271,14 +2224,14 @@ template <bool DEPTH, int PIECES>
 __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void k_raster_bwd_bf16(ViewK v, int n, const int4* __restrict__ items,
                                                            const int* __restrict__ num_items, const int* __restrict__ pairs,
                                                            const float4* __restrict__ rec, const uint4* __restrict__ UF,
-                                                           float* __restrict__ partials, const int* __restrict__ order) {
+                                                           float* __restrict__ partials) {
   __shared__ __attribute__((aligned(16))) float4 sA[2][TP];
   __shared__ __attribute__((aligned(16))) float4 sB[2][TP];
   __shared__ float sZ[2][TP];
   __shared__ __attribute__((aligned(16))) uint4 sUF[UF_FRAGS];
   const int nitems = *num_items;
   if ((int)blockIdx.x >= nitems) return;
-  const int item = order[xcd_item(blockIdx.x, nitems)];  // item_order: largest first per XCD share
+  const int item = xcd_item(blockIdx.x, nitems);
   const int4 it = items[item];
   const bool tail = it.x & 1;
   if (tail && !DEPTH) return;
@@ -3224,7 +3177,7 @@ void gr_geom_layout(int n, size_t offsets_out[GR_GEOM_PARTS]) { geom_fixed(n, of
 
 void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[4]) {
   (void)n;
-  size_t off[8];
+  size_t off[7];
   bins_fixed(vtiles_of(v), plan ? plan->num_pairs : 0, off);
   offsets_out[0] = off[0];
   offsets_out[1] = off[1];
@@ -3241,7 +3194,7 @@ size_t gr_saved_floats(const gr_view* v) { return (size_t)5 * v->width * v->heig
 
 size_t gr_bins_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
-  size_t off[8];
+  size_t off[7];
   return bins_fixed(vtiles_of(v), plan->num_pairs, off);
 }
 
@@ -3581,7 +3534,7 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
       GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_work_items_zones, dim3(1), dim3(WI_THREADS), 0, s, tiles, vk.tiles_x, (int)Kc,
                          Kr[0] > 0 ? (const int*)Z.z[0].T : nullptr, Kr[1] > 0 ? (const int*)Z.z[1].T : nullptr, b.ranges,
-                         b.items, b.num_items, b.tile_item0, b.order);
+                         b.items, b.num_items, b.tile_item0);
       GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_tile_place, dim3(cols), dim3(64 * waves), (size_t)tiles * sizeof(int) * waves, s, Z, tiles,
                          bits_for((uint32_t)tiles), (const int2*)b.ranges, b.pairs, b.pos_of);
@@ -3605,12 +3558,12 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
                          b.pairs, b.pos_of);
       GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_work_items, dim3(1), dim3(WI_THREADS), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
-                         b.tile_item0, b.order);
+                         b.tile_item0);
     }
   } else {
     GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * vtiles, s));
     hipLaunchKernelGGL(k_work_items, dim3(1), dim3(WI_THREADS), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
-                       b.tile_item0, b.order);
+                       b.tile_item0);
   }
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_BINNING, s);
@@ -3636,8 +3589,7 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
                                   : (out_depth ? k_raster_fwd_mfma<2> : k_raster_fwd_mfma<3>)),
                        dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
                        (const int*)b.num_items, (const int2*)b.ranges, (const int*)b.pairs, (const float4*)g.rec,
-                       sc.fwd_part, out_rgb, out_alpha, out_depth, saved4, savedD, la, UF, (const int*)g.f16_sa,
-                       (const int*)b.order);
+                       sc.fwd_part, out_rgb, out_alpha, out_depth, saved4, savedD, la, UF, (const int*)g.f16_sa);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_FWD, s);
   }
@@ -3743,7 +3695,7 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
     prof_mark(PROF_RASTER_BWD, s);
     auto kern = depth ? k_raster_bwd_bf16<true, 3> : (pieces == 2 ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>);
     hipLaunchKernelGGL(kern, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items,
-                       (const int*)b.pairs, (const float4*)g.rec, (const uint4*)UF, partials, (const int*)b.order);
+                       (const int*)b.pairs, (const float4*)g.rec, (const uint4*)UF, partials);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_BWD, s);
   }
@@ -3822,7 +3774,7 @@ gr_status gr_bwd_splat(const gr_view* v, int n, const gr_plan* plan, const void*
   prof_mark(PROF_RASTER_BWD, s);
   hipLaunchKernelGGL((v->no_depth_grad == 1 ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>), dim3((unsigned)cap),
                      dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items, (const int*)b.pairs,
-                     (const float4*)g.rec, (const uint4*)w.UF, w.partials, (const int*)b.order);
+                     (const float4*)g.rec, (const uint4*)w.UF, w.partials);
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_RASTER_BWD, s);
   return GR_OK;
