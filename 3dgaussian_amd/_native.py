@@ -84,6 +84,20 @@ class GrSumsView(ctypes.Structure):
     _fields_ = [("view", GrView), ("sums", ctypes.c_void_p)]
 
 
+class GrFitTarget(ctypes.Structure):
+    """gr_fit_target (include/gr_hip.h): one view of a gr_fit_views call."""
+
+    _fields_ = [("view", GrView), ("target_rgb", ctypes.c_void_p), ("target_mask", ctypes.c_void_p),
+                ("target_depth", ctypes.c_void_p)]
+
+
+class GrFitConfig(ctypes.Structure):
+    """gr_fit_config (include/gr_hip.h): the native fit executor's schedule."""
+
+    _fields_ = [("num_streams", ctypes.c_int), ("prep_ahead", ctypes.c_int), ("prep_group", ctypes.c_int),
+                ("prep_first", ctypes.c_int), ("reduce_batch", ctypes.c_int), ("reduce_tail", ctypes.c_int)]
+
+
 class NativeLibraryError(ImportError):
     pass
 
@@ -128,6 +142,11 @@ _SIG = {
     "gr_gather_view": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, _P, _P]),
     "gr_reduce_sums": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(GrSumsView), ctypes.c_int, _P, _P, _P, ctypes.c_int,
                                       _P, _P, _P, _P, _P, ctypes.c_int, _P]),
+    "gr_executor_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "gr_executor_destroy": (None, [_P]),
+    "gr_fit_views": (ctypes.c_int, [_P, ctypes.POINTER(GrFitConfig), ctypes.c_int, ctypes.POINTER(GrFitTarget), ctypes.c_int,
+                                    _P, _P, _P, ctypes.c_int, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P,
+                                    ctypes.POINTER(ctypes.c_void_p), _P]),
     "gr_render_u8": (ctypes.c_int, [ctypes.POINTER(GrRenderParams), ctypes.c_int, _P, _P, _P, _P, _P]),
     "gr_geom_layout": (None, [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
     "gr_bins_layout": (None, [_VP, ctypes.c_int, _PP, ctypes.POINTER(ctypes.c_size_t)]),
@@ -219,3 +238,16 @@ def bins_layout(gv: GrView, n: int, num_pairs: int):
     plan = GrPlan(int(num_pairs), 0, 0)
     lib().gr_bins_layout(ctypes.byref(gv), int(n), ctypes.byref(plan), out)
     return list(out)
+
+
+_EXECUTORS: dict = {}
+
+
+def executor(device: int) -> ctypes.c_void_p:
+    """The native fit executor of a device (gr_executor_create), created once per process."""
+    ex = _EXECUTORS.get(device)
+    if ex is None:
+        ex = ctypes.c_void_p()
+        check(lib().gr_executor_create(int(device), ctypes.byref(ex)), "gr_executor_create")
+        _EXECUTORS[device] = ex
+    return ex

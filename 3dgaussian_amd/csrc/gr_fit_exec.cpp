@@ -1,0 +1,279 @@
+// gr_fit_exec.cpp — the fit step's per-view schedule as native host code (gr_fit_views, include/gr_hip.h).
+//
+// The reference fit loop renders its views one after another (fit_multiview_stub.py:277-310).  The
+// multi-GPU driver (3dgaussian_amd/fit_multiview.py) runs the same work on several HIP streams with the
+// views' preparations ahead on a stream of their own; this file is that schedule in C++, so a step costs
+// the host a few microseconds per launch instead of the Python driver's per-view interpreter work
+// (the small-view configs and the per-rank share of a multi-GPU step are host-bound in Python).
+//
+// Only the public C ABI (gr_fwd_prepare_views_async, gr_fwd_render_l1, gr_bwd_splat, gr_gather_view,
+// gr_reduce_sums, gr_fwd_render, gr_bwd_fit) and the HIP runtime are used.  Workspaces come from the
+// device's stream-ordered memory pool (hipMallocAsync / hipFreeAsync): a view's bins and workspaces are
+// released on its render stream right after its gather, its geom once its last reader has run.
+// The schedule (streams, preparation groups, reduction batches) is exactly fit_multiview._views_direct's,
+// so both give bit-identical losses and gradients (tests/test_fit_exec_gpu.py).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "../../include/gr_hip.h"
+
+extern "C" gr_status gr_exec_set_error(gr_status st, const char* msg);  // gr_hip.hip: thread-local message
+
+namespace {
+
+struct Sched {
+  int ns;                              // streams used
+  std::vector<std::deque<int>> sizes;  // per stream: its reduction batch sizes, in order
+};
+
+// fit_multiview._views_direct's batches: stream k's views in near-equal batches of at most reduce_batch,
+// the last one reduce_tail views (when 0 < tail < the stream's view count).
+Sched schedule(int views, const gr_fit_config& c) {
+  Sched s;
+  s.ns = std::max(1, std::min(c.num_streams, views));
+  s.sizes.resize(s.ns);
+  for (int k = 0; k < s.ns; ++k) {
+    const int p = views > k ? (views - k + s.ns - 1) / s.ns : 0;
+    const int tail = (c.reduce_tail > 0 && c.reduce_tail < p) ? c.reduce_tail : 0;
+    const int nb = std::max(1, (p - tail + c.reduce_batch - 1) / c.reduce_batch);
+    for (int b = 0; b < nb; ++b) s.sizes[k].push_back((p - tail) / nb + (b < (p - tail) % nb ? 1 : 0));
+    if (tail) s.sizes[k].push_back(tail);
+  }
+  return s;
+}
+
+}  // namespace
+
+struct gr_executor {
+  int device = 0;
+  hipStream_t prep = nullptr;
+  std::vector<hipStream_t> side;   // render streams 1..; stream 0 is the caller's
+  std::vector<hipEvent_t> groups;  // one event per preparation group (reused across steps)
+  hipEvent_t in = nullptr;
+  std::vector<hipEvent_t> done;    // side streams' ends
+  gr_plan* plans = nullptr;        // pinned, mapped: one plan per view (written by the preparation kernels)
+  int plans_cap = 0;
+};
+
+#define GR_EXEC_TRY(expr)                                                            \
+  do {                                                                               \
+    hipError_t e_ = (expr);                                                          \
+    if (e_ != hipSuccess) return gr_exec_set_error(GR_ERR_HIP, hipGetErrorString(e_)); \
+  } while (0)
+#define GR_EXEC_CALL(expr)          \
+  do {                              \
+    gr_status s_ = (expr);          \
+    if (s_ != GR_OK) return s_;     \
+  } while (0)
+
+extern "C" {
+
+gr_status gr_executor_create(int device, gr_executor** out) {
+  if (!out) return gr_exec_set_error(GR_ERR_INVALID_ARGUMENT, "gr_executor_create: null output");
+  *out = nullptr;
+  int cur = 0;
+  GR_EXEC_TRY(hipGetDevice(&cur));
+  GR_EXEC_TRY(hipSetDevice(device));
+  gr_executor* ex = new gr_executor();
+  ex->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&ex->prep, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ex->in, hipEventDisableTiming);
+  // the pool keeps freed workspaces for the next view instead of returning them to the driver
+  hipMemPool_t pool;
+  if (e == hipSuccess) e = hipDeviceGetDefaultMemPool(&pool, device);
+  if (e == hipSuccess) {
+    uint64_t keep = UINT64_MAX;
+    e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  }
+  (void)hipSetDevice(cur);
+  if (e != hipSuccess) {
+    gr_executor_destroy(ex);
+    return gr_exec_set_error(GR_ERR_HIP, hipGetErrorString(e));
+  }
+  *out = ex;
+  return GR_OK;
+}
+
+void gr_executor_destroy(gr_executor* ex) {
+  if (!ex) return;
+  if (ex->prep) (void)hipStreamSynchronize(ex->prep);
+  for (hipStream_t s : ex->side) {
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+  }
+  for (hipEvent_t e : ex->groups) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ex->done) (void)hipEventDestroy(e);
+  if (ex->in) (void)hipEventDestroy(ex->in);
+  if (ex->prep) (void)hipStreamDestroy(ex->prep);
+  if (ex->plans) (void)hipHostFree(ex->plans);
+  delete ex;
+}
+
+gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views, const gr_fit_target* views, int n,
+                       const float* means, const float* scales, const float* colors, int color_dim,
+                       const float* opacities, float w_sil, float w_depth, float g_scale, float* losses,
+                       float* const* acc, void* stream) {
+  if (!ex || !cfg || (num_views > 0 && (!views || !losses || !acc)))
+    return gr_exec_set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views: null argument");
+  if (cfg->num_streams < 1 || cfg->prep_ahead < 1 || cfg->prep_group < 1 || cfg->prep_group > GR_PREPARE_MAX_VIEWS ||
+      cfg->prep_first < 1 || cfg->reduce_batch < 1 || cfg->reduce_batch > GR_REDUCE_MAX_VIEWS || cfg->reduce_tail < 0)
+    return gr_exec_set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views: configuration out of range");
+  if (num_views == 0 || n <= 0) return GR_OK;
+  const bool depth = views[0].target_depth != nullptr;  // the depth-loss path (one form per call)
+  for (int j = 0; j < num_views; ++j) {
+    if ((views[j].target_depth != nullptr) != depth)
+      return gr_exec_set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views: every view or none has a depth target");
+    if (!views[j].target_rgb) return gr_exec_set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views: null target");
+  }
+  const Sched sc = schedule(num_views, *cfg);
+  const int ns = sc.ns;
+  for (int k = 0; k < ns; ++k)
+    for (int q = 0; q < 4; ++q)
+      if (!acc[4 * k + q]) return gr_exec_set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views: null accumulator");
+  hipStream_t main = (hipStream_t)stream;
+  // streams, events and the plan array, grown on demand and kept
+  while ((int)ex->side.size() < ns - 1) {
+    hipStream_t s;
+    GR_EXEC_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    ex->side.push_back(s);
+    hipEvent_t e;
+    GR_EXEC_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ex->done.push_back(e);
+  }
+  const int max_groups = num_views + 1;
+  while ((int)ex->groups.size() < max_groups) {
+    hipEvent_t e;
+    GR_EXEC_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ex->groups.push_back(e);
+  }
+  if (ex->plans_cap < num_views) {
+    if (ex->plans) {
+      GR_EXEC_TRY(hipStreamSynchronize(ex->prep));  // no preparation of an earlier step still writes them
+      GR_EXEC_TRY(hipHostFree(ex->plans));
+    }
+    GR_EXEC_TRY(hipHostMalloc((void**)&ex->plans, sizeof(gr_plan) * num_views, hipHostMallocMapped));
+    ex->plans_cap = num_views;
+  }
+  std::vector<hipStream_t> st(ns);
+  st[0] = main;
+  for (int k = 1; k < ns; ++k) st[k] = ex->side[k - 1];
+  // everything starts after the caller's stream (the activations)
+  GR_EXEC_TRY(hipEventRecord(ex->in, main));
+  GR_EXEC_TRY(hipStreamWaitEvent(ex->prep, ex->in, 0));
+  for (int k = 1; k < ns; ++k) GR_EXEC_TRY(hipStreamWaitEvent(st[k], ex->in, 0));
+
+  const size_t geom_bytes = gr_geom_bytes(n);
+  std::vector<void*> geom(num_views, nullptr);
+  std::vector<int> group_of(num_views, -1);
+  int ngroups = 0, next_prep = 0;
+  auto prepare_upto = [&](int j) -> gr_status {  // views [next_prep, j] prepared (whole groups)
+    while (next_prep < num_views && next_prep <= j) {
+      const int g0 = next_prep, cnt = std::min(num_views - g0, g0 == 0 ? cfg->prep_first : cfg->prep_group);
+      gr_view vs[GR_PREPARE_MAX_VIEWS];
+      void* gs[GR_PREPARE_MAX_VIEWS];
+      gr_plan* ps[GR_PREPARE_MAX_VIEWS];
+      for (int q = 0; q < cnt; ++q) {
+        GR_EXEC_TRY(hipMallocAsync(&geom[g0 + q], geom_bytes, ex->prep));
+        vs[q] = views[g0 + q].view;
+        gs[q] = geom[g0 + q];
+        ps[q] = &ex->plans[g0 + q];
+        group_of[g0 + q] = ngroups;
+      }
+      GR_EXEC_CALL(gr_fwd_prepare_views_async(cnt, vs, n, means, scales, colors, color_dim, opacities, gs, geom_bytes, ps,
+                                              ex->prep));
+      GR_EXEC_TRY(hipEventRecord(ex->groups[ngroups], ex->prep));
+      ++ngroups;
+      next_prep = g0 + cnt;
+    }
+    return GR_OK;
+  };
+
+  struct Pending {
+    gr_view view;
+    float* sums;
+  };
+  std::vector<std::vector<Pending>> pending(ns);
+  std::vector<std::deque<int>> sizes = sc.sizes;
+  std::vector<int> started(ns, 0);
+  const size_t sums_bytes = gr_view_sums_floats(n) * sizeof(float);
+  auto reduce_pending = [&](int k) -> gr_status {
+    if (pending[k].empty()) return GR_OK;
+    gr_sums_view b[GR_REDUCE_MAX_VIEWS];
+    const int nb = (int)pending[k].size();
+    for (int q = 0; q < nb; ++q) {
+      b[q].view = pending[k][q].view;
+      b[q].sums = pending[k][q].sums;
+    }
+    GR_EXEC_CALL(gr_reduce_sums(nb, b, n, means, scales, colors, color_dim, opacities, acc[4 * k + 0], acc[4 * k + 1],
+                                acc[4 * k + 2], acc[4 * k + 3], started[k], st[k]));
+    for (int q = 0; q < nb; ++q) GR_EXEC_TRY(hipFreeAsync(pending[k][q].sums, st[k]));
+    pending[k].clear();
+    started[k] = 1;
+    return GR_OK;
+  };
+
+  GR_EXEC_CALL(prepare_upto(cfg->prep_ahead - 1));
+  for (int j = 0; j < num_views; ++j) {
+    const int k = j % ns;
+    hipStream_t s = st[k];
+    GR_EXEC_CALL(prepare_upto(j + cfg->prep_ahead));
+    const hipEvent_t ev = ex->groups[group_of[j]];
+    GR_EXEC_TRY(hipStreamWaitEvent(s, ev, 0));
+    GR_EXEC_TRY(hipEventSynchronize(ev));  // the plan (pair count) sizes this view's workspaces
+    const gr_plan plan = ex->plans[j];
+    if (plan.num_pairs < 0 || plan.num_slots < 0) return gr_exec_set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
+    const gr_view& v = views[j].view;
+    const size_t bins_bytes = gr_bins_bytes(&v, n, &plan), scratch_bytes = gr_fwd_scratch_bytes(&v, n, &plan);
+    const size_t ws_bytes = gr_bwd_bytes(&v, n, &plan);
+    void *bins = nullptr, *scratch = nullptr, *ws = nullptr;
+    GR_EXEC_TRY(hipMallocAsync(&bins, bins_bytes, s));
+    GR_EXEC_TRY(hipMallocAsync(&scratch, scratch_bytes, s));
+    GR_EXEC_TRY(hipMallocAsync(&ws, ws_bytes, s));
+    if (!depth) {
+      GR_EXEC_CALL(gr_fwd_render_l1(&v, n, &plan, geom[j], bins, bins_bytes, scratch, scratch_bytes, views[j].target_rgb,
+                                    views[j].target_mask, w_sil, g_scale, losses + j, nullptr, nullptr, ws, ws_bytes, s));
+      GR_EXEC_TRY(hipFreeAsync(scratch, s));
+      GR_EXEC_CALL(gr_bwd_splat(&v, n, &plan, geom[j], bins, ws, ws_bytes, s));
+      float* sums = nullptr;
+      GR_EXEC_TRY(hipMallocAsync((void**)&sums, sums_bytes, s));
+      GR_EXEC_CALL(gr_gather_view(&v, n, &plan, geom[j], bins, ws, sums, s));
+      pending[k].push_back({v, sums});
+    } else {
+      float* saved = nullptr;
+      GR_EXEC_TRY(hipMallocAsync((void**)&saved, gr_saved_floats(&v) * sizeof(float), s));
+      GR_EXEC_CALL(gr_fwd_render(&v, n, &plan, geom[j], bins, bins_bytes, scratch, scratch_bytes, nullptr, nullptr,
+                                 nullptr, saved, s));
+      GR_EXEC_TRY(hipFreeAsync(scratch, s));
+      GR_EXEC_CALL(gr_bwd_fit(&v, n, &plan, means, scales, colors, color_dim, opacities, geom[j], bins, saved,
+                              views[j].target_rgb, views[j].target_mask, w_sil, views[j].target_depth, w_depth, g_scale,
+                              losses + j, acc[4 * k + 0], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3], j >= ns ? 1 : 0,
+                              ws, ws_bytes, s));
+      GR_EXEC_TRY(hipFreeAsync(saved, s));
+    }
+    GR_EXEC_TRY(hipFreeAsync(bins, s));
+    GR_EXEC_TRY(hipFreeAsync(ws, s));
+    GR_EXEC_TRY(hipFreeAsync(geom[j], s));
+    geom[j] = nullptr;
+    if (!depth && (int)pending[k].size() >= sizes[k].front()) {
+      GR_EXEC_CALL(reduce_pending(k));
+      if (sizes[k].size() > 1) sizes[k].pop_front();
+    }
+  }
+  for (int k = 0; k < ns; ++k) GR_EXEC_CALL(reduce_pending(k));
+  // the caller's stream waits for every render stream and for the preparation stream
+  for (int k = 1; k < ns; ++k) {
+    GR_EXEC_TRY(hipEventRecord(ex->done[k - 1], st[k]));
+    GR_EXEC_TRY(hipStreamWaitEvent(main, ex->done[k - 1], 0));
+  }
+  GR_EXEC_TRY(hipEventRecord(ex->groups[ngroups], ex->prep));
+  GR_EXEC_TRY(hipStreamWaitEvent(main, ex->groups[ngroups], 0));
+  return GR_OK;
+}
+
+}  // extern "C"

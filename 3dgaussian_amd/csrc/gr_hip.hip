@@ -3145,6 +3145,9 @@ extern "C" {
 
 const char* gr_last_error(void) { return g_last_error.c_str(); }
 
+// the native fit executor (gr_fit_exec.cpp) reports its errors through the same thread-local message
+gr_status gr_exec_set_error(gr_status st, const char* msg) { return set_error(st, msg); }
+
 void gr_profile_begin(void) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
   for (auto& sl : g_prof) sl.used = 0;

@@ -82,6 +82,9 @@ PREP_FIRST = max(1, min(PREP_GROUP, int(os.environ.get("GR_PREP_FIRST", "1"))))
 # workspaces are released at once), the chain rules of a stream's batch of views from those sums
 # (gr_reduce_sums).  0 = the one-pass gr_reduce_views over the batch's kept workspaces.
 GATHER = os.environ.get("GR_GATHER", "1") != "0"
+# the fused paths' per-view schedule as native host code (gr_fit_views, csrc/gr_fit_exec.cpp: the same streams,
+# preparation groups and reduction batches, bit-identical results); 0 = the Python schedule below
+NATIVE_EXEC = os.environ.get("GR_NATIVE_EXEC", "1") != "0"
 # the fused path at f32 grade (gr_view.no_depth_grad = 2: three-piece splits in both splats, as the default
 # precision mode) instead of its two-piece mode: the precision reference of the fit path (bench.py f32_grade_fit)
 F32_GRADE = os.environ.get("GR_F32_GRADE", "0") != "0"
@@ -401,7 +404,9 @@ class ViewShardedFitter:
         if self._direct(device) and self.params["means"].shape[0] > 0 and self._fused_step_ok():
             with torch.no_grad():
                 means, scales, colors, opacities = activations(self.params)
-                if self._depth_grad():
+                if NATIVE_EXEC and GATHER:
+                    total = self._views_native(means, scales, colors, opacities, self._depth_grad())
+                elif self._depth_grad():
                     total = self._views_direct_depth(means, scales, colors, opacities)
                 else:
                     total = self._views_direct(means, scales, colors, opacities)
@@ -488,6 +493,52 @@ class ViewShardedFitter:
             loss = loss + self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean()
         loss.backward()
         return self._finish_step(loss)
+
+    def _views_native(self, means, scales, colors, opacities, depth: bool) -> torch.Tensor:
+        """_views_direct / _views_direct_depth through the native executor (gr_fit_views): one C call per
+        step; returns the sum of the view losses and leaves the stream accumulators in self._acc_parts."""
+        device = means.device
+        m, s, c, o = (t.detach().float().contiguous() for t in (means, scales, colors, opacities))
+        views = self.my_views
+        if not views:
+            self._acc_parts = [tuple(torch.zeros_like(t) for t in (m, s, c, o))]
+            return torch.zeros((), device=device)
+        ns = max(1, min(NUM_STREAMS, len(views)))
+        w_sil = self.w_sil if (self.masks is not None and self.w_sil > 0.0) else 0.0
+        key = (tuple(views), depth, F32_GRADE, w_sil > 0.0, str(device))
+        cache = getattr(self, "_native_targets", None)
+        if cache is None or cache[0] != key:
+            arr = (tr._native.GrFitTarget * len(views))()
+            for j, i in enumerate(views):
+                if depth:
+                    cam = self.cams[i]
+                    gvd = getattr(self, "_gvd_cache", None)
+                    if gvd is None:
+                        self._gvd_cache = gvd = {}
+                    if i not in gvd:
+                        gvd[i] = tr.make_view(cam.view, cam.proj, self.width, self.height, self._background(device),
+                                              depth_grad=True)
+                    arr[j].view = gvd[i]
+                    arr[j].target_depth = self.depths[i].data_ptr()
+                else:
+                    arr[j].view = self._fit_view(i, device)
+                    arr[j].target_depth = None
+                arr[j].target_rgb = self.targets[i].data_ptr()
+                arr[j].target_mask = self.masks[i].data_ptr() if w_sil > 0.0 else None
+            self._native_targets = cache = (key, arr)
+        cfg = tr._native.GrFitConfig(NUM_STREAMS, PREP_AHEAD, PREP_GROUP, PREP_FIRST, REDUCE_BATCH, REDUCE_TAIL)
+        losses_v = torch.empty(len(views), dtype=torch.float32, device=device)
+        acc = [tuple(torch.empty_like(t) for t in (m, s, c, o)) for _ in range(ns)]
+        ptrs = (ctypes.c_void_p * (4 * ns))(*[t.data_ptr() for a in acc for t in a])
+        L = tr._native.lib()
+        tr._native.check(L.gr_fit_views(tr._native.executor(device.index or 0), ctypes.byref(cfg), len(views), cache[1],
+                                        int(m.shape[0]), tr._native.ptr(m), tr._native.ptr(s), tr._native.ptr(c),
+                                        tr._color_dim(c), tr._native.ptr(o), ctypes.c_float(w_sil),
+                                        ctypes.c_float(self.w_depth), ctypes.c_float(1.0 / len(self.targets)),
+                                        tr._native.ptr(losses_v), ptrs, ctypes_stream(device)), "gr_fit_views")
+        self._acc_parts = acc
+        self._native_keep = (m, s, c, o)  # read by the executor's streams until the caller's stream passes them
+        return losses_v.sum()
 
     def _views_direct(self, means, scales, colors, opacities) -> torch.Tensor:
         """This rank's views without autograd: per view, gr_fwd_render_l1 (the HIP forward whose epilogue

@@ -254,6 +254,41 @@ gr_status gr_reduce_sums(int num_views, const gr_sums_view* views, int n, const 
                          const float* opacities, float* d_means, float* d_scales, float* d_colors,
                          float* d_opacities, int accumulate, void* stream);
 
+/* The fit step's views in one call: the per-view schedule of 3dgaussian_amd/fit_multiview.py
+ * (fit_multiview_stub.py:277-310 across several HIP streams) as native host code
+ * (3dgaussian_amd/csrc/gr_fit_exec.cpp).  Per view: its preparation ahead on the executor's preparation
+ * stream (groups of prep_group views, the first of prep_first), then on render stream j % num_streams
+ * (stream 0 = `stream`, the caller's) without a depth target gr_fwd_render_l1 + gr_bwd_splat +
+ * gr_gather_view, every batch of a stream's views (reduce_batch at most, its last reduce_tail views)
+ * gr_reduce_sums into that stream's accumulators; with depth targets gr_fwd_render + gr_bwd_fit.
+ * losses[j] (device) receives view j's loss; acc[4k + 0..3] are stream k's d_means, d_scales, d_colors,
+ * d_opacities accumulators (written by its first batch, then added to), for k < min(num_streams,
+ * num_views): the caller sums them in stream order.  Workspaces come from the device's stream-ordered
+ * memory pool.  Everything is ordered after `stream` and `stream` is ordered after everything when this
+ * returns.  Deterministic; bit-identical to fit_multiview.py's Python schedule with the same settings.
+ * The executor holds the streams, events and pinned plan buffer across steps (one per device). */
+typedef struct gr_executor gr_executor;
+typedef struct gr_fit_target {
+  gr_view view;               /* the view (no_depth_grad 1 or 2 without a depth target, 0 with one) */
+  const float* target_rgb;    /* (H,W,3) float32 device                                           */
+  const float* target_mask;   /* (H,W) or NULL (no silhouette term)                                */
+  const float* target_depth;  /* (H,W) or NULL; all views of a call have one, or none              */
+} gr_fit_target;
+typedef struct gr_fit_config {
+  int num_streams;  /* render streams (the caller's + num_streams - 1 of the executor's)      */
+  int prep_ahead;   /* views prepared ahead of the one rendering                               */
+  int prep_group;   /* views per preparation (<= GR_PREPARE_MAX_VIEWS)                          */
+  int prep_first;   /* views of the first preparation                                           */
+  int reduce_batch; /* views per gr_reduce_sums (<= GR_REDUCE_MAX_VIEWS)                        */
+  int reduce_tail;  /* views in each stream's last batch (0: near-equal batches only)           */
+} gr_fit_config;
+gr_status gr_executor_create(int device, gr_executor** executor);
+void gr_executor_destroy(gr_executor* executor);
+gr_status gr_fit_views(gr_executor* executor, const gr_fit_config* config, int num_views,
+                       const gr_fit_target* views, int n, const float* means, const float* scales,
+                       const float* colors, int color_dim, const float* opacities, float w_sil,
+                       float w_depth, float g_scale, float* losses, float* const* acc, void* stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Legacy uint8 surface (host pointers), replaces gr::render_gaussians (renderer.h:33-39).    */
 /* Semantics of renderer_cpu.cpp: 3-sigma box, w < 1e-5 skip, uint8 round-half-up, A = 255.  */
