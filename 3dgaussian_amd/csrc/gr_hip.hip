@@ -3216,7 +3216,8 @@ size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan) {
   const size_t per_tile = UF_FRAGS * sizeof(uint4);
   return align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)) + align_up(tiles * per_tile) +
          align_up(tiles * 4 * sizeof(float)) + align_up(tiles * 2 * sizeof(float)) +
-         align_up(4 * sizeof(float));  // per-tile loss sums, per-tile depth max / arg-max counts, depth scalars
+         align_up(4 * sizeof(float)) +  // per-tile loss sums, per-tile depth max / arg-max counts, depth scalars
+         align_up((size_t)8 * (n > 0 ? n : 1) * sizeof(float));  // per-Gaussian row sums (gather + chain rule)
 }
 
 // Decode the scanned totals (core, tail pairs) into the plan; a count that does not fit int32 is
@@ -3463,6 +3464,7 @@ struct BwdWs {
   float* tile_loss;  // [tiles][4]
   float* tile_aux;   // [tiles][2]: depth max, arg-max pixels (gr_bwd_fit)
   float* dscal;      // [4]: max(depth), the max's gradient per arg-max pixel
+  float* sums;       // [n][8]: per-Gaussian row sums (k_gather_view) of a backward without a depth gradient
 };
 static BwdWs bwd_ws(const gr_view* v, const gr_plan* plan, void* ws) {
   const size_t tiles = (size_t)tiles_x_of(v->width) * tiles_y_of(v->height);
@@ -3472,6 +3474,7 @@ static BwdWs bwd_ws(const gr_view* v, const gr_plan* plan, void* ws) {
   w.tile_loss = (float*)((char*)w.UF + align_up(tiles * UF_FRAGS * sizeof(uint4)));
   w.tile_aux = (float*)((char*)w.tile_loss + align_up(tiles * 4 * sizeof(float)));
   w.dscal = (float*)((char*)w.tile_aux + align_up(tiles * 2 * sizeof(float)));
+  w.sums = (float*)((char*)w.dscal + align_up(4 * sizeof(float)));
   return w;
 }
 
@@ -3703,7 +3706,27 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
     prof_mark(PROF_RASTER_BWD, s);
   }
   prof_mark(PROF_REDUCE, s);
-  {
+  if (!depth && num_pairs > 0) {
+    // 8-float rows: the lean gather into per-Gaussian sums, then the chain rule of that one view (the two
+    // stages of gr_gather_view + gr_reduce_sums; k_reduce_bwd's one pass needs 117 VGPRs for the chain rule
+    // while it gathers)
+    hipLaunchKernelGGL(k_gather_view, dim3((n + 63) / 64), dim3(256), 0, s, n, (const Cnt2*)g.offsets, (const int*)b.pos_of,
+                       (const float4*)partials, (float2*)w.sums);
+    SBatch B;
+    B.nv = 1;
+    B.r[0].v = vk;
+    B.r[0].sums = (const float4*)w.sums;
+    const dim3 grid((n + 63) / 64), block(256);
+    if (color_dim == 3)
+      hipLaunchKernelGGL(k_reduce_sums<3>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
+                         d_colors, d_opacities, accumulate);
+    else if (color_dim == 12)
+      hipLaunchKernelGGL(k_reduce_sums<12>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
+                         d_colors, d_opacities, accumulate);
+    else
+      hipLaunchKernelGGL(k_reduce_sums<48>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
+                         d_colors, d_opacities, accumulate);
+  } else {
     // the backward without a depth gradient writes 8-float rows (bwd_item_bf16)
     const bool row8 = !depth;
     auto launch = [&](auto kern) {

@@ -109,9 +109,9 @@ def test_direct_path_matches_autograd_path(cuda, sh):
 
 
 def test_batched_reduce_matches_per_view_reduce(cuda):
-    """The fused fit path's three calls (gr_fwd_render_l1, gr_bwd_splat, gr_reduce_views) against
-    gr_fwd_render + gr_bwd_l1 per view: the same view losses bit for bit, a one-view batch the per-view
-    gradient exactly, a batch the sum of the per-view gradients within float summation order; the fit
+    """The fused fit path's calls (gr_fwd_render_l1, gr_bwd_splat, gr_gather_view + gr_reduce_sums or
+    gr_reduce_views) against gr_fwd_render + gr_bwd_l1 per view: the same view losses bit for bit, a one-view
+    two-stage batch the per-view gradient exactly (gr_reduce_views within summation order), a batch the sum of the per-view gradients within float summation order; the fit
     step is the same for every REDUCE_BATCH and deterministic for each."""
     import torch
 
@@ -141,9 +141,14 @@ def test_batched_reduce_matches_per_view_reduce(cuda):
         batch.append((st2, ws))
     assert torch.equal(loss, loss2)  # the forward-epilogue loss is the backward's (same per-tile sums)
     one = tuple(torch.empty_like(t) for t in (m, s, c, o))
-    tr.reduce_views_native(m, s, c, o, batch[:1], one, accumulate=False)
+    # the per-view backward reduces through the same two stages (gather + chain rule of one view): exact
+    tr.reduce_sums_native(m, s, c, o, [(batch[0][0].gv, tr.gather_view_native(*batch[0]))], one, accumulate=False)
     for a, b in zip(one, per_view[0]):
         assert torch.equal(a, b)
+    # the one-pass gr_reduce_views (f64 row sums) within float summation order
+    tr.reduce_views_native(m, s, c, o, batch[:1], one, accumulate=False)
+    for a, b in zip(one, per_view[0]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6 * float(b.abs().max()))
     tot = tuple(torch.empty_like(t) for t in (m, s, c, o))
     tr.reduce_views_native(m, s, c, o, batch, tot, accumulate=False)
     tr.reduce_views_native(m, s, c, o, batch[:2], tot, accumulate=True)  # accumulate adds
