@@ -8,7 +8,7 @@ R=${GRAFT_REPO_ROOT:-$PWD}
 for i in $(seq $REPS); do
   for v in $VIEWS; do
     for e in $SETS; do
-      echo -n "views=$v $e: "; env ${e//,/ } timeout -k 10 300 python $R/bench.py --no-cpu-baseline --no-extra-modes --views $v --steps 20 --warmup 3 2>/dev/null | grep '^{' | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])"
+      echo -n "views=$v $e: "; env ${e//,/ } timeout -k 10 300 python $R/bench.py --no-cpu-baseline --no-extra-modes --no-dropin --no-psnr --views $v --steps 20 --warmup 3 2>/dev/null | grep '^{' | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])"
     done
   done
 done
