@@ -7,9 +7,12 @@
 // (the small-view configs and the per-rank share of a multi-GPU step are host-bound in Python).
 //
 // Only the public C ABI (gr_fwd_prepare_views_async, gr_fwd_render_l1, gr_bwd_splat, gr_gather_view,
-// gr_reduce_sums, gr_fwd_render, gr_bwd_fit) and the HIP runtime are used.  Workspaces come from the
-// device's stream-ordered memory pool (hipMallocAsync / hipFreeAsync): a view's bins and workspaces are
-// released on its render stream right after its gather, its geom once its last reader has run.
+// gr_reduce_sums, gr_fwd_render, gr_bwd_fit) and the HIP runtime are used.  Workspaces are the executor's
+// own, kept across steps and reused only in stream order: each render stream owns its view workspace
+// (bins, forward scratch, backward workspace, saved sums) and a ring of per-view sums for its reduction
+// batch; the geoms are a ring of slots written on the preparation stream, a slot being rewritten only
+// after the preparation stream has waited for the event recorded behind its last reader.  A buffer that
+// must grow is replaced after its stream has drained (rare: the first step, a densify).
 // The schedule (streams, preparation groups, reduction batches) is exactly fit_multiview._views_direct's,
 // so both give bit-identical losses and gradients (tests/test_fit_exec_gpu.py).
 #include <hip/hip_runtime.h>
@@ -50,6 +53,42 @@ Sched schedule(int views, const gr_fit_config& c) {
 
 }  // namespace
 
+// A device buffer that grows: replaced (old one freed after `s` has drained) when a request exceeds it.
+struct Buf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t fit(size_t bytes, hipStream_t s) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) {
+      hipError_t e = hipStreamSynchronize(s);
+      if (e == hipSuccess) e = hipFree(p);
+      if (e != hipSuccess) return e;
+      p = nullptr;
+      cap = 0;
+    }
+    const size_t want = bytes + bytes / 8 + (1u << 20);  // headroom: pair counts drift from step to step
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct StreamWs {  // one render stream's buffers
+  Buf bins, scratch, ws, saved;
+  std::vector<Buf> sums;  // one per view of a reduction batch
+};
+
+struct GeomSlot {
+  Buf buf;
+  hipEvent_t free_ev = nullptr;  // recorded behind the slot's last reader
+  bool pending = false;          // free_ev recorded and not yet waited for by the preparation stream
+};
+
 struct gr_executor {
   int device = 0;
   hipStream_t prep = nullptr;
@@ -59,6 +98,8 @@ struct gr_executor {
   std::vector<hipEvent_t> done;    // side streams' ends
   gr_plan* plans = nullptr;        // pinned, mapped: one plan per view (written by the preparation kernels)
   int plans_cap = 0;
+  std::vector<StreamWs> ws;        // per render stream
+  std::vector<GeomSlot> geoms;     // ring of geom slots
 };
 
 #define GR_EXEC_TRY(expr)                                                            \
@@ -84,13 +125,6 @@ gr_status gr_executor_create(int device, gr_executor** out) {
   ex->device = device;
   hipError_t e = hipStreamCreateWithFlags(&ex->prep, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ex->in, hipEventDisableTiming);
-  // the pool keeps freed workspaces for the next view instead of returning them to the driver
-  hipMemPool_t pool;
-  if (e == hipSuccess) e = hipDeviceGetDefaultMemPool(&pool, device);
-  if (e == hipSuccess) {
-    uint64_t keep = UINT64_MAX;
-    e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-  }
   (void)hipSetDevice(cur);
   if (e != hipSuccess) {
     gr_executor_destroy(ex);
@@ -106,6 +140,18 @@ void gr_executor_destroy(gr_executor* ex) {
   for (hipStream_t s : ex->side) {
     (void)hipStreamSynchronize(s);
     (void)hipStreamDestroy(s);
+  }
+  (void)hipDeviceSynchronize();  // no queued work still uses the executor's buffers
+  for (auto& w : ex->ws) {
+    w.bins.release();
+    w.scratch.release();
+    w.ws.release();
+    w.saved.release();
+    for (auto& b : w.sums) b.release();
+  }
+  for (auto& g : ex->geoms) {
+    g.buf.release();
+    if (g.free_ev) (void)hipEventDestroy(g.free_ev);
   }
   for (hipEvent_t e : ex->groups) (void)hipEventDestroy(e);
   for (hipEvent_t e : ex->done) (void)hipEventDestroy(e);
@@ -146,6 +192,15 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
     GR_EXEC_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ex->done.push_back(e);
   }
+  if ((int)ex->ws.size() < ns) ex->ws.resize(ns);
+  for (int k = 0; k < ns; ++k)
+    if ((int)ex->ws[k].sums.size() < cfg->reduce_batch) ex->ws[k].sums.resize(cfg->reduce_batch);
+  // geom slots: the views prepared ahead, the ones rendering on every stream, and a margin
+  const int nslots = cfg->prep_ahead + cfg->prep_group + ns + 2;
+  while ((int)ex->geoms.size() < nslots) {
+    ex->geoms.emplace_back();
+    GR_EXEC_TRY(hipEventCreateWithFlags(&ex->geoms.back().free_ev, hipEventDisableTiming));
+  }
   const int max_groups = num_views + 1;
   while ((int)ex->groups.size() < max_groups) {
     hipEvent_t e;
@@ -170,6 +225,7 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
 
   const size_t geom_bytes = gr_geom_bytes(n);
   std::vector<void*> geom(num_views, nullptr);
+  std::vector<int> slot_of(num_views, -1);
   std::vector<int> group_of(num_views, -1);
   int ngroups = 0, next_prep = 0;
   auto prepare_upto = [&](int j) -> gr_status {  // views [next_prep, j] prepared (whole groups)
@@ -179,7 +235,15 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
       void* gs[GR_PREPARE_MAX_VIEWS];
       gr_plan* ps[GR_PREPARE_MAX_VIEWS];
       for (int q = 0; q < cnt; ++q) {
-        GR_EXEC_TRY(hipMallocAsync(&geom[g0 + q], geom_bytes, ex->prep));
+        const int sl = (g0 + q) % nslots;
+        GeomSlot& g = ex->geoms[sl];
+        if (g.pending) {  // its previous view's readers first (stream order on the preparation stream)
+          GR_EXEC_TRY(hipStreamWaitEvent(ex->prep, g.free_ev, 0));
+          g.pending = false;
+        }
+        GR_EXEC_TRY(g.buf.fit(geom_bytes, ex->prep));
+        geom[g0 + q] = g.buf.p;
+        slot_of[g0 + q] = sl;
         vs[q] = views[g0 + q].view;
         gs[q] = geom[g0 + q];
         ps[q] = &ex->plans[g0 + q];
@@ -198,6 +262,9 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
     gr_view view;
     float* sums;
   };
+  // a slot's previous view must have been waited for before the slot is refilled: with nslots > prep_ahead
+  // + prep_group + ns the view a slot last held was rendered (and its free event recorded) before the
+  // preparation that refills it is enqueued
   std::vector<std::vector<Pending>> pending(ns);
   std::vector<std::deque<int>> sizes = sc.sizes;
   std::vector<int> started(ns, 0);
@@ -212,7 +279,6 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
     }
     GR_EXEC_CALL(gr_reduce_sums(nb, b, n, means, scales, colors, color_dim, opacities, acc[4 * k + 0], acc[4 * k + 1],
                                 acc[4 * k + 2], acc[4 * k + 3], started[k], st[k]));
-    for (int q = 0; q < nb; ++q) GR_EXEC_TRY(hipFreeAsync(pending[k][q].sums, st[k]));
     pending[k].clear();
     started[k] = 1;
     return GR_OK;
@@ -231,34 +297,32 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
     const gr_view& v = views[j].view;
     const size_t bins_bytes = gr_bins_bytes(&v, n, &plan), scratch_bytes = gr_fwd_scratch_bytes(&v, n, &plan);
     const size_t ws_bytes = gr_bwd_bytes(&v, n, &plan);
-    void *bins = nullptr, *scratch = nullptr, *ws = nullptr;
-    GR_EXEC_TRY(hipMallocAsync(&bins, bins_bytes, s));
-    GR_EXEC_TRY(hipMallocAsync(&scratch, scratch_bytes, s));
-    GR_EXEC_TRY(hipMallocAsync(&ws, ws_bytes, s));
+    StreamWs& W = ex->ws[k];
+    GR_EXEC_TRY(W.bins.fit(bins_bytes, s));
+    GR_EXEC_TRY(W.scratch.fit(scratch_bytes, s));
+    GR_EXEC_TRY(W.ws.fit(ws_bytes, s));
+    void *bins = W.bins.p, *scratch = W.scratch.p, *ws = W.ws.p;
     if (!depth) {
-      GR_EXEC_CALL(gr_fwd_render_l1(&v, n, &plan, geom[j], bins, bins_bytes, scratch, scratch_bytes, views[j].target_rgb,
-                                    views[j].target_mask, w_sil, g_scale, losses + j, nullptr, nullptr, ws, ws_bytes, s));
-      GR_EXEC_TRY(hipFreeAsync(scratch, s));
-      GR_EXEC_CALL(gr_bwd_splat(&v, n, &plan, geom[j], bins, ws, ws_bytes, s));
-      float* sums = nullptr;
-      GR_EXEC_TRY(hipMallocAsync((void**)&sums, sums_bytes, s));
-      GR_EXEC_CALL(gr_gather_view(&v, n, &plan, geom[j], bins, ws, sums, s));
-      pending[k].push_back({v, sums});
+      GR_EXEC_CALL(gr_fwd_render_l1(&v, n, &plan, geom[j], bins, W.bins.cap, scratch, W.scratch.cap, views[j].target_rgb,
+                                    views[j].target_mask, w_sil, g_scale, losses + j, nullptr, nullptr, ws, W.ws.cap, s));
+      GR_EXEC_CALL(gr_bwd_splat(&v, n, &plan, geom[j], bins, ws, W.ws.cap, s));
+      Buf& sb = W.sums[pending[k].size()];
+      GR_EXEC_TRY(sb.fit(sums_bytes, s));
+      GR_EXEC_CALL(gr_gather_view(&v, n, &plan, geom[j], bins, ws, (float*)sb.p, s));
+      pending[k].push_back({v, (float*)sb.p});
     } else {
-      float* saved = nullptr;
-      GR_EXEC_TRY(hipMallocAsync((void**)&saved, gr_saved_floats(&v) * sizeof(float), s));
-      GR_EXEC_CALL(gr_fwd_render(&v, n, &plan, geom[j], bins, bins_bytes, scratch, scratch_bytes, nullptr, nullptr,
-                                 nullptr, saved, s));
-      GR_EXEC_TRY(hipFreeAsync(scratch, s));
-      GR_EXEC_CALL(gr_bwd_fit(&v, n, &plan, means, scales, colors, color_dim, opacities, geom[j], bins, saved,
-                              views[j].target_rgb, views[j].target_mask, w_sil, views[j].target_depth, w_depth, g_scale,
-                              losses + j, acc[4 * k + 0], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3], j >= ns ? 1 : 0,
-                              ws, ws_bytes, s));
-      GR_EXEC_TRY(hipFreeAsync(saved, s));
+      GR_EXEC_TRY(W.saved.fit(gr_saved_floats(&v) * sizeof(float), s));
+      GR_EXEC_CALL(gr_fwd_render(&v, n, &plan, geom[j], bins, W.bins.cap, scratch, W.scratch.cap, nullptr, nullptr,
+                                 nullptr, (float*)W.saved.p, s));
+      GR_EXEC_CALL(gr_bwd_fit(&v, n, &plan, means, scales, colors, color_dim, opacities, geom[j], bins,
+                              (const float*)W.saved.p, views[j].target_rgb, views[j].target_mask, w_sil,
+                              views[j].target_depth, w_depth, g_scale, losses + j, acc[4 * k + 0], acc[4 * k + 1],
+                              acc[4 * k + 2], acc[4 * k + 3], j >= ns ? 1 : 0, ws, W.ws.cap, s));
     }
-    GR_EXEC_TRY(hipFreeAsync(bins, s));
-    GR_EXEC_TRY(hipFreeAsync(ws, s));
-    GR_EXEC_TRY(hipFreeAsync(geom[j], s));
+    // the geom slot may be refilled once this stream has passed its last reader
+    GeomSlot& gsl = ex->geoms[slot_of[j]];
+    GR_EXEC_TRY(hipEventRecord(gsl.free_ev, s));
+    gsl.pending = true;
     geom[j] = nullptr;
     if (!depth && (int)pending[k].size() >= sizes[k].front()) {
       GR_EXEC_CALL(reduce_pending(k));

@@ -240,6 +240,21 @@ def _fit_images(name: str, imgs: Optional[list], shape: tuple, device) -> tuple:
     return [torch.as_tensor(t).to(device=device, dtype=torch.float32).contiguous() for t in imgs], True
 
 
+def bucketed_all_reduce(buckets: list, assemble: Callable[[int], None], finish: Callable[[int], None], group=None) -> None:
+    """The step's one real exchange (SUM over ranks) in buckets, one per parameter tensor (plus the loss in
+    the last): bucket b is assembled (``assemble(b)``, on the current stream) and its all-reduce issued
+    asynchronously at once, so RCCL moves bucket b over xGMI while bucket b + 1 is assembled; then each
+    bucket's update (``finish(b)``) waits for its own all-reduce only.  Summation order per element is the
+    collective's, as for one flat buffer."""
+    works = []
+    for b in range(len(buckets)):
+        assemble(b)
+        works.append(dist.all_reduce(buckets[b], op=dist.ReduceOp.SUM, group=group, async_op=True))
+    for b, w in enumerate(works):
+        w.wait()
+        finish(b)
+
+
 def hip_render(means, scales, colors, opacities, cam, width, height, background, prepared=None, depth_grad=True):
     return tr.render_gaussians_torch(means, scales, colors, opacities, cam, width=width, height=height,
                                      background=background, max_gaussians=max(10000, int(means.shape[0])), return_aux=True,
@@ -742,6 +757,7 @@ class ViewShardedFitter:
             flat = torch.empty(sum(p.numel() for p in plist) + 1, dtype=torch.float32, device=plist[0].device)
         off = 0
         steps = []
+        assembly = []
         for k, p in zip(names, plist):
             st = self.opt.state[p]
             if not st:  # torch.optim.Adam's lazy state, same tensors and layout
@@ -767,21 +783,38 @@ class ViewShardedFitter:
                 grad = torch.empty_like(p)
             p.grad = grad
             r = reg.get(k, 0.0) if self.rank == 0 else 0.0
-            tr._native.check(L.gr_fit_param_step(p.numel(), act[k], tr._native.ptr(p.data), tr._native.ptr(grad),
-                                                 accs, len(a), ctypes.c_float(r), 0 if flat is not None else 1,
-                                                 tr._native.ptr(st["exp_avg"]), tr._native.ptr(st["exp_avg_sq"]),
-                                                 ctypes.c_float(neg_step), ctypes.c_float(bc2s), ctypes.c_double(b1),
-                                                 ctypes.c_double(b2), ctypes.c_float(eps), stream), "gr_fit_param_step")
+
+            def step_call(p=p, grad=grad, accs=accs, a=a, r=r, k=k, st=st, neg_step=neg_step, bc2s=bc2s):
+                tr._native.check(L.gr_fit_param_step(p.numel(), act[k], tr._native.ptr(p.data), tr._native.ptr(grad),
+                                                     accs, len(a), ctypes.c_float(r), 0 if flat is not None else 1,
+                                                     tr._native.ptr(st["exp_avg"]), tr._native.ptr(st["exp_avg_sq"]),
+                                                     ctypes.c_float(neg_step), ctypes.c_float(bc2s), ctypes.c_double(b1),
+                                                     ctypes.c_double(b2), ctypes.c_float(eps), stream), "gr_fit_param_step")
+            assembly.append(step_call)
         if flat is None:
+            for call in assembly:
+                call()
             return loss.detach()
-        flat[off:off + 1].copy_(loss.detach().reshape(1))
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
-        for (k, p), (neg_step, bc2s) in zip(zip(names, plist), steps):
+        bounds, o0 = [], 0
+        for p in plist:
+            bounds.append((o0, o0 + p.numel()))
+            o0 += p.numel()
+        bounds[-1] = (bounds[-1][0], off + 1)  # the loss rides in the last bucket
+
+        def assemble(b):
+            assembly[b]()
+            if b == len(plist) - 1:
+                flat[off:off + 1].copy_(loss.detach().reshape(1))
+
+        def finish(b):
+            p, (neg_step, bc2s) = plist[b], steps[b]
             st = self.opt.state[p]
             tr._native.check(L.gr_adam_step(p.numel(), tr._native.ptr(p.data), tr._native.ptr(p.grad),
                                             tr._native.ptr(st["exp_avg"]), tr._native.ptr(st["exp_avg_sq"]),
                                             ctypes.c_float(neg_step), ctypes.c_float(bc2s), ctypes.c_double(b1),
                                             ctypes.c_double(b2), ctypes.c_float(eps), stream), "gr_adam_step")
+
+        bucketed_all_reduce([flat[a:b] for a, b in bounds], assemble, finish, self.group)
         return flat[off]
 
     def _finish_step(self, loss) -> torch.Tensor:
@@ -791,12 +824,18 @@ class ViewShardedFitter:
                 p.grad = torch.zeros_like(p)
         if self.world > 1:
             flat = torch.cat([p.grad.reshape(-1) for p in plist] + [loss.detach().reshape(1)])
-            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
-            off = 0
+            bounds, off = [], 0
             for p in plist:
-                k = p.numel()
-                p.grad.copy_(flat[off:off + k].view_as(p))
-                off += k
+                bounds.append((off, off + p.numel()))
+                off += p.numel()
+            bounds[-1] = (bounds[-1][0], off + 1)
+            buckets = [flat[a:b] for a, b in bounds]
+
+            def finish(b):
+                p = plist[b]
+                p.grad.copy_(buckets[b][:p.numel()].view_as(p))
+
+            bucketed_all_reduce(buckets, lambda b: None, finish, self.group)
             loss_all = flat[off]
         else:
             loss_all = loss.detach()
