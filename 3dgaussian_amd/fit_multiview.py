@@ -385,7 +385,7 @@ class ViewShardedFitter:
         if self.render_fn is hip_render:
             # without a depth loss the depth output gets no gradient: the forward may accumulate W and D
             # at the colours' precision (gr_view.no_depth_grad)
-            kw["depth_grad"] = self._depth_grad()
+            kw["depth_grad"] = "eager" if self._depth_grad() else False  # a depth loss differentiates depth
         pred, alpha, depth = self.render_fn(means, scales, colors, opacities, self.cams[i], self.width, self.height,
                                             self._background(device), **kw)
         use_sil = self.masks is not None and self.w_sil > 0.0

@@ -48,6 +48,16 @@ DEFAULT_CORE_CUTOFF = 5.5
 FIT_CUTOFF = float(os.environ.get("GR_FIT_CUTOFF", "5.0"))
 
 
+# depth_grad=True (the default, "a depth gradient may follow") renders lazily: the forward runs in the
+# two-piece mode with the no-depth-gradient footprint (what a caller whose loss never differentiates the
+# depth output - the reference fit loop without --depth_dir - needs), and a backward that does receive a
+# depth gradient re-renders the view at f32 grade with the depth-gradient footprint first (gr_bwd then
+# differentiates that render; its outputs equal the returned ones within the parity bar).  A caller that
+# knows it will differentiate the depth passes depth_grad="eager" (one f32-grade render).  GR_LAZY_DEPTH=0
+# makes True eager.
+LAZY_DEPTH = os.environ.get("GR_LAZY_DEPTH", "1") != "0"
+
+
 def default_cutoff(depth_grad: bool = True) -> float:
     """Tail cutoff (in sigma) of a view rendered with/without a depth gradient to follow.  With one, the
     depth-coupled gradient d depth / d w = (z - depth) / (W + 1e-6) amplifies far tails by up to 1e6 on
@@ -55,6 +65,15 @@ def default_cutoff(depth_grad: bool = True) -> float:
     position/scale gradients 4e-5..4e-4 relL2 away, 8 sigma 2.5e-6 (tests/test_scale_gpu.py,
     tools/probe_cutoff.py).  Without one the tail only feeds the alpha/depth outputs: 7 sigma."""
     return DEPTH_GRAD_CUTOFF if depth_grad else DEFAULT_CUTOFF
+
+
+def _eager(depth_grad) -> bool:
+    """depth_grad (True / False / "eager") -> whether the forward renders at f32 grade up front."""
+    if isinstance(depth_grad, str):
+        if depth_grad != "eager":
+            raise ValueError('depth_grad must be True, False or "eager"')
+        return True
+    return bool(depth_grad) and not LAZY_DEPTH
 
 
 @dataclass
@@ -510,12 +529,15 @@ def _grad_background(st: RenderState, background: torch.Tensor, g_out: torch.Ten
 
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, means, scales, colors, opacities, background, gv, prepared):
+    def forward(ctx, means, scales, colors, opacities, background, gv, prepared, gv_depth=None):
+        """gv_depth: the f32-grade view a lazily rendered gv (two-piece mode) re-renders with when a depth
+        gradient arrives (LAZY_DEPTH), else None."""
         out, alpha, depth, st = forward_native(means, scales, colors, opacities, gv, prepared)
         # an output the loss does not use gets a None gradient instead of zeros, so an unused depth
         # output lets the backward skip the tail pairs (gr_bwd with g_depth = NULL)
         ctx.set_materialize_grads(False)
         ctx.st = st
+        ctx.gv_depth = gv_depth
         ctx.save_for_backward(means, scales, colors, opacities, background)
         return out, alpha, depth
 
@@ -529,11 +551,16 @@ class _RasterizeGaussians(torch.autograd.Function):
         g_alpha = None if g_alpha is None else g_alpha.contiguous().float()
         g_depth = None if g_depth is None else g_depth.contiguous().float()
         if g_depth is not None and st.gv.no_depth_grad:
-            raise RuntimeError("the depth output was rendered with depth_grad=False and cannot be differentiated; "
-                               "render with depth_grad=True")
+            if ctx.gv_depth is None:
+                raise RuntimeError("the depth output was rendered with depth_grad=False and cannot be differentiated; "
+                                   "render with depth_grad=True")
+            # lazy default: the depth is differentiated after all - re-render at f32 grade with the
+            # depth-gradient footprint and differentiate that render
+            _, _, _, st = forward_native(means, scales, colors, opacities, ctx.gv_depth, images=False)
+        ctx.st = None
         dm, ds, dc, do = backward_native(means, scales, colors, opacities, st, g_out, g_alpha, g_depth)
         dbg = _grad_background(st, background, g_out) if ctx.needs_input_grad[4] else None
-        return dm, ds, dc, do, dbg, None, None
+        return dm, ds, dc, do, dbg, None, None, None
 
 
 def _device_inputs(means, scales, colors, opacities):
@@ -633,11 +660,12 @@ def _spec_after(key, gv, tensors, inputs_ready) -> None:
 
 
 def rasterize(means, scales, colors, opacities, view, proj, width, height, background=None, cutoff=None,
-              prepared: Optional[Prepared] = None, core_cutoff=DEFAULT_CORE_CUTOFF, depth_grad: bool = True):
+              prepared: Optional[Prepared] = None, core_cutoff=DEFAULT_CORE_CUTOFF, depth_grad=True):
     """Differentiable render of one view on the HIP device: returns (rgb (H,W,3), alpha (H,W), depth (H,W)).
 
     ``prepared`` (from ``prepare_view`` with the same inputs) skips the preparation step;
-    ``depth_grad=False``: see ``make_view``."""
+    ``depth_grad``: True (default: the depth may be differentiated; rendered lazily, see LAZY_DEPTH),
+    "eager" (f32-grade render up front), False (see ``make_view``)."""
     dev = means.device
     if dev.type != "cuda":
         # tensors on the host: the dense CPU op (config C1; cpu_renderer.py).  HIP tensors never take it.
@@ -649,9 +677,18 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
     if background is None:
         background = _default_background(dev)
     background = background.to(dtype=torch.float32, device=dev).reshape(3).contiguous()
-    gv = make_view(view, proj, width, height, background, cutoff, core_cutoff, depth_grad)
+    gv_depth = None
+    if depth_grad is True and not _eager(depth_grad) and cutoff is None:
+        # lazy default: two-piece render with the no-depth-gradient footprint now, f32 grade only if needed
+        gv_depth = make_view(view, proj, width, height, background, None, core_cutoff, True)
+        gv = make_view(view, proj, width, height, background, None, core_cutoff, False)
+    else:
+        gv = make_view(view, proj, width, height, background, cutoff, core_cutoff, bool(depth_grad))
+    if prepared is not None and (prepared.gv.cutoff != gv.cutoff or prepared.gv.no_depth_grad != gv.no_depth_grad):
+        # a preparation made for the eager view (prepare_view(depth_grad=True) with GR_LAZY_DEPTH=0 semantics)
+        gv, gv_depth = prepared.gv, None
     if prepared is not None or not SPECULATE:
-        return _RasterizeGaussians.apply(m, s, c, o, background, gv, prepared)
+        return _RasterizeGaussians.apply(m, s, c, o, background, gv, prepared, gv_depth)
     key = _view_key(gv)
     pv = _spec_take(key, (m, s, c, o))
     stream = torch.cuda.current_stream(dev)
@@ -660,7 +697,7 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
         pv.geom.record_stream(stream)
     ready = torch.cuda.Event()
     ready.record(stream)
-    res = _RasterizeGaussians.apply(m, s, c, o, background, gv, pv)
+    res = _RasterizeGaussians.apply(m, s, c, o, background, gv, pv, gv_depth)
     _spec_after(key, gv, (m, s, c, o), ready)
     return res
 
@@ -680,7 +717,7 @@ def render_gaussians_torch(
     cutoff: Optional[float] = None,
     prepared: Optional[Prepared] = None,
     core_cutoff: float = DEFAULT_CORE_CUTOFF,
-    depth_grad: bool = True,
+    depth_grad=True,
 ):
     """Differentiable Gaussian splat; signature, results and errors of torch_renderer.py:109-203.
 
