@@ -95,7 +95,8 @@ class GrFitConfig(ctypes.Structure):
     """gr_fit_config (include/gr_hip.h): the native fit executor's schedule."""
 
     _fields_ = [("num_streams", ctypes.c_int), ("prep_ahead", ctypes.c_int), ("prep_group", ctypes.c_int),
-                ("prep_first", ctypes.c_int), ("reduce_batch", ctypes.c_int), ("reduce_tail", ctypes.c_int)]
+                ("prep_first", ctypes.c_int), ("reduce_batch", ctypes.c_int), ("reduce_tail", ctypes.c_int),
+                ("render_streams", ctypes.POINTER(ctypes.c_void_p)), ("prep_stream", ctypes.c_void_p)]
 
 
 class NativeLibraryError(ImportError):

@@ -100,6 +100,7 @@ struct gr_executor {
   int plans_cap = 0;
   std::vector<StreamWs> ws;        // per render stream
   std::vector<GeomSlot> geoms;     // ring of geom slots
+  std::vector<hipStream_t> last;   // the previous call's render streams 1.. and preparation stream
 };
 
 #define GR_EXEC_TRY(expr)                                                            \
@@ -123,8 +124,9 @@ gr_status gr_executor_create(int device, gr_executor** out) {
   GR_EXEC_TRY(hipSetDevice(device));
   gr_executor* ex = new gr_executor();
   ex->device = device;
-  hipError_t e = hipStreamCreateWithFlags(&ex->prep, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&ex->in, hipEventDisableTiming);
+  // streams are made on first use, and only when the caller passes none (stream creation order decides the
+  // hardware queue each lands on)
+  hipError_t e = hipEventCreateWithFlags(&ex->in, hipEventDisableTiming);
   (void)hipSetDevice(cur);
   if (e != hipSuccess) {
     gr_executor_destroy(ex);
@@ -184,10 +186,12 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
       if (!acc[4 * k + q]) return gr_exec_set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views: null accumulator");
   hipStream_t main = (hipStream_t)stream;
   // streams, events and the plan array, grown on demand and kept
-  while ((int)ex->side.size() < ns - 1) {
+  while (!cfg->render_streams && (int)ex->side.size() < ns - 1) {
     hipStream_t s;
     GR_EXEC_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     ex->side.push_back(s);
+  }
+  while ((int)ex->done.size() < ns - 1) {
     hipEvent_t e;
     GR_EXEC_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ex->done.push_back(e);
@@ -209,7 +213,7 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
   }
   if (ex->plans_cap < num_views) {
     if (ex->plans) {
-      GR_EXEC_TRY(hipStreamSynchronize(ex->prep));  // no preparation of an earlier step still writes them
+      GR_EXEC_TRY(hipDeviceSynchronize());  // no preparation of an earlier step still writes them
       GR_EXEC_TRY(hipHostFree(ex->plans));
     }
     GR_EXEC_TRY(hipHostMalloc((void**)&ex->plans, sizeof(gr_plan) * num_views, hipHostMallocMapped));
@@ -217,10 +221,22 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
   }
   std::vector<hipStream_t> st(ns);
   st[0] = main;
-  for (int k = 1; k < ns; ++k) st[k] = ex->side[k - 1];
+  for (int k = 1; k < ns; ++k) {
+    st[k] = cfg->render_streams ? (hipStream_t)cfg->render_streams[k - 1] : ex->side[k - 1];
+    if (!st[k]) return gr_exec_set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views: null render stream");
+  }
+  if (!cfg->prep_stream && !ex->prep) GR_EXEC_TRY(hipStreamCreateWithFlags(&ex->prep, hipStreamNonBlocking));
+  const hipStream_t prep = cfg->prep_stream ? (hipStream_t)cfg->prep_stream : ex->prep;
+  // the workspaces of stream k and the geom slots were last used on the previous call's streams: when the
+  // streams change, those finish first
+  std::vector<hipStream_t> now(st.begin() + 1, st.end());
+  now.push_back(prep);
+  if (!ex->last.empty() && ex->last != now)
+    for (hipStream_t s : ex->last) GR_EXEC_TRY(hipStreamSynchronize(s));
+  ex->last = now;
   // everything starts after the caller's stream (the activations)
   GR_EXEC_TRY(hipEventRecord(ex->in, main));
-  GR_EXEC_TRY(hipStreamWaitEvent(ex->prep, ex->in, 0));
+  GR_EXEC_TRY(hipStreamWaitEvent(prep, ex->in, 0));
   for (int k = 1; k < ns; ++k) GR_EXEC_TRY(hipStreamWaitEvent(st[k], ex->in, 0));
 
   const size_t geom_bytes = gr_geom_bytes(n);
@@ -238,10 +254,10 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
         const int sl = (g0 + q) % nslots;
         GeomSlot& g = ex->geoms[sl];
         if (g.pending) {  // its previous view's readers first (stream order on the preparation stream)
-          GR_EXEC_TRY(hipStreamWaitEvent(ex->prep, g.free_ev, 0));
+          GR_EXEC_TRY(hipStreamWaitEvent(prep, g.free_ev, 0));
           g.pending = false;
         }
-        GR_EXEC_TRY(g.buf.fit(geom_bytes, ex->prep));
+        GR_EXEC_TRY(g.buf.fit(geom_bytes, prep));
         geom[g0 + q] = g.buf.p;
         slot_of[g0 + q] = sl;
         vs[q] = views[g0 + q].view;
@@ -250,8 +266,8 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
         group_of[g0 + q] = ngroups;
       }
       GR_EXEC_CALL(gr_fwd_prepare_views_async(cnt, vs, n, means, scales, colors, color_dim, opacities, gs, geom_bytes, ps,
-                                              ex->prep));
-      GR_EXEC_TRY(hipEventRecord(ex->groups[ngroups], ex->prep));
+                                              prep));
+      GR_EXEC_TRY(hipEventRecord(ex->groups[ngroups], prep));
       ++ngroups;
       next_prep = g0 + cnt;
     }
@@ -335,7 +351,7 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
     GR_EXEC_TRY(hipEventRecord(ex->done[k - 1], st[k]));
     GR_EXEC_TRY(hipStreamWaitEvent(main, ex->done[k - 1], 0));
   }
-  GR_EXEC_TRY(hipEventRecord(ex->groups[ngroups], ex->prep));
+  GR_EXEC_TRY(hipEventRecord(ex->groups[ngroups], prep));
   GR_EXEC_TRY(hipStreamWaitEvent(main, ex->groups[ngroups], 0));
   return GR_OK;
 }

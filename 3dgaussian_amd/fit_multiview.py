@@ -85,6 +85,8 @@ GATHER = os.environ.get("GR_GATHER", "1") != "0"
 # the fused paths' per-view schedule as native host code (gr_fit_views, csrc/gr_fit_exec.cpp: the same streams,
 # preparation groups and reduction batches, bit-identical results); 0 = the Python schedule below
 NATIVE_EXEC = os.environ.get("GR_NATIVE_EXEC", "1") != "0"
+# the native executor on this driver's torch streams (1) or on streams of its own (0)
+EXEC_STREAMS = os.environ.get("GR_EXEC_STREAMS", "1") != "0"
 # the fused path at f32 grade (gr_view.no_depth_grad = 2: three-piece splits in both splats, as the default
 # precision mode) instead of its two-piece mode: the precision reference of the fit path (bench.py f32_grade_fit)
 F32_GRADE = os.environ.get("GR_F32_GRADE", "0") != "0"
@@ -542,6 +544,19 @@ class ViewShardedFitter:
                 arr[j].target_mask = self.masks[i].data_ptr() if w_sil > 0.0 else None
             self._native_targets = cache = (key, arr)
         cfg = tr._native.GrFitConfig(NUM_STREAMS, PREP_AHEAD, PREP_GROUP, PREP_FIRST, REDUCE_BATCH, REDUCE_TAIL)
+        if EXEC_STREAMS:
+            # the Python schedule's own torch streams: the same hardware-queue placement (stream creation
+            # order decides it), so the two schedules differ only in their host code
+            side = getattr(self, "_side", None)
+            if ns > 1 and (side is None or len(side) != ns - 1 or side[0].device != device):
+                self._side = side = [torch.cuda.Stream(device) for _ in range(ns - 1)]
+            prep = getattr(self, "_prep", None)
+            if prep is None or prep.device != device:
+                self._prep = prep = torch.cuda.Stream(device)
+            self._exec_streams = rs = (ctypes.c_void_p * max(1, ns - 1))(
+                *[st.cuda_stream for st in (side[:ns - 1] if ns > 1 else [])])
+            cfg.render_streams = rs
+            cfg.prep_stream = prep.cuda_stream
         losses_v = torch.empty(len(views), dtype=torch.float32, device=device)
         acc = [tuple(torch.empty_like(t) for t in (m, s, c, o)) for _ in range(ns)]
         ptrs = (ctypes.c_void_p * (4 * ns))(*[t.data_ptr() for a in acc for t in a])

@@ -263,8 +263,8 @@ gr_status gr_reduce_sums(int num_views, const gr_sums_view* views, int n, const 
  * gr_reduce_sums into that stream's accumulators; with depth targets gr_fwd_render + gr_bwd_fit.
  * losses[j] (device) receives view j's loss; acc[4k + 0..3] are stream k's d_means, d_scales, d_colors,
  * d_opacities accumulators (written by its first batch, then added to), for k < min(num_streams,
- * num_views): the caller sums them in stream order.  Workspaces come from the device's stream-ordered
- * memory pool.  Everything is ordered after `stream` and `stream` is ordered after everything when this
+ * num_views): the caller sums them in stream order.  Workspaces are the executor's own, reused in
+ * stream order (gr_fit_exec.cpp).  Everything is ordered after `stream` and `stream` is ordered after everything when this
  * returns.  Deterministic; bit-identical to fit_multiview.py's Python schedule with the same settings.
  * The executor holds the streams, events and pinned plan buffer across steps (one per device). */
 typedef struct gr_executor gr_executor;
@@ -281,6 +281,13 @@ typedef struct gr_fit_config {
   int prep_first;   /* views of the first preparation                                           */
   int reduce_batch; /* views per gr_reduce_sums (<= GR_REDUCE_MAX_VIEWS)                        */
   int reduce_tail;  /* views in each stream's last batch (0: near-equal batches only)           */
+  /* Optional caller-owned streams (hipStream_t): render streams 1..num_streams-1 and the preparation
+   * stream.  NULL: the executor's own.  HIP maps streams to GPU_MAX_HW_QUEUES hardware queues in creation
+   * order; two render streams on one queue run one after the other, so a caller that already holds
+   * streams on distinct queues passes them here.  A change of streams between calls drains the previous
+   * ones first. */
+  void* const* render_streams;
+  void* prep_stream;
 } gr_fit_config;
 gr_status gr_executor_create(int device, gr_executor** executor);
 void gr_executor_destroy(gr_executor* executor);
