@@ -84,7 +84,7 @@ PREP_FIRST = max(1, min(PREP_GROUP, int(os.environ.get("GR_PREP_FIRST", "1"))))
 GATHER = os.environ.get("GR_GATHER", "1") != "0"
 # the fused paths' per-view schedule as native host code (gr_fit_views, csrc/gr_fit_exec.cpp: the same streams,
 # preparation groups and reduction batches, bit-identical results); 0 = the Python schedule below
-NATIVE_EXEC = os.environ.get("GR_NATIVE_EXEC", "1") != "0"
+NATIVE_EXEC = os.environ.get("GR_NATIVE_EXEC", "0") != "0"
 # the native executor on this driver's torch streams (1) or on streams of its own (0)
 EXEC_STREAMS = os.environ.get("GR_EXEC_STREAMS", "1") != "0"
 # the fused path at f32 grade (gr_view.no_depth_grad = 2: three-piece splits in both splats, as the default
