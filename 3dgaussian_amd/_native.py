@@ -42,6 +42,7 @@ class GrView(ctypes.Structure):
         ("core_cutoff", ctypes.c_float),
         ("no_depth_grad", ctypes.c_int),
         ("background_dev", ctypes.c_void_p),  # optional device pointer to the 3 background floats
+        ("binned", ctypes.c_int),  # 1: gr_fwd_bin already built the bins; the render launches only the splat
     ]
 
 
@@ -119,6 +120,7 @@ _SIG = {
     "gr_saved_floats": (ctypes.c_size_t, [_VP]),
     "gr_fwd_scratch_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
     "gr_fwd_render": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P, _P, _P, _P, _P]),
+    "gr_fwd_bin": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P]),
     "gr_bwd_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
     "gr_bwd": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, _P, _P, _P, ctypes.c_size_t, _P]),

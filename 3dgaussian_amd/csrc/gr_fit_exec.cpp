@@ -300,11 +300,13 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
     return GR_OK;
   };
 
-  GR_EXEC_CALL(prepare_upto(cfg->prep_ahead - 1));
+  // the first two groups, then one more after each render (fit_multiview._prep_groups): the first render is
+  // enqueued before the later groups
+  GR_EXEC_CALL(prepare_upto(std::min(cfg->prep_first, cfg->prep_ahead - 1)));
   for (int j = 0; j < num_views; ++j) {
     const int k = j % ns;
     hipStream_t s = st[k];
-    GR_EXEC_CALL(prepare_upto(j + cfg->prep_ahead));
+    GR_EXEC_CALL(prepare_upto(j));
     const hipEvent_t ev = ex->groups[group_of[j]];
     GR_EXEC_TRY(hipStreamWaitEvent(s, ev, 0));
     GR_EXEC_TRY(hipEventSynchronize(ev));  // the plan (pair count) sizes this view's workspaces
@@ -340,6 +342,7 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
     GR_EXEC_TRY(hipEventRecord(gsl.free_ev, s));
     gsl.pending = true;
     geom[j] = nullptr;
+    GR_EXEC_CALL(prepare_upto(j + cfg->prep_ahead));
     if (!depth && (int)pending[k].size() >= sizes[k].front()) {
       GR_EXEC_CALL(reduce_pending(k));
       if (sizes[k].size() > 1) sizes[k].pop_front();

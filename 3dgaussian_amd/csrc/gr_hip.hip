@@ -2620,10 +2620,12 @@ __global__ __launch_bounds__(256) void k_gather_view(int n, const Cnt2* __restri
   }
 }
 
-// Chain rule of up to GR_REDUCE_MAX_VIEWS views' gathered sums: one lane per Gaussian, wave w takes
-// views w, w + 4, ... (CRW waves; SH degree 3: wave 0 alone), the wave totals are combined in wave
-// order and written (or added, acc) once.  A Gaussian whose eight sums are all zero touched no tile of
-// that view (its chain rule would add zero).  Deterministic.
+// Chain rule of up to GR_REDUCE_MAX_VIEWS views' gathered sums: one lane per Gaussian; the crw waves of a
+// Gaussian group take views u, u + crw, ... (crw = 4 from three views, else the view count, so that no
+// wave idles: a block holds 4 / crw groups of 64 Gaussians; SH degree 3: crw = 1), the wave totals are
+// combined in wave order and written (or added, acc) once.  A Gaussian whose eight sums are all zero
+// touched no tile of that view (its chain rule would add zero).  Deterministic; for a given view count
+// the summation order is fixed (1 or 2 views: the sums a 4-wave group gives, without its idle waves' zeros).
 struct SViewK {
   ViewK v;
   const float4* sums;  // [n][2]: k_gather_view's output
@@ -2632,6 +2634,8 @@ struct SBatch {
   int nv;
   SViewK r[GR_REDUCE_MAX_VIEWS];
 };
+// waves per Gaussian group of k_reduce_sums (host and device)
+__host__ __device__ constexpr int reduce_sums_crw(int nv, int cd) { return cd == 48 ? 1 : (nv >= 3 ? 4 : (nv >= 1 ? nv : 1)); }
 
 template <int CD>
 __global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const float* __restrict__ means,
@@ -2639,14 +2643,15 @@ __global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const floa
                                                      const float* __restrict__ opac, float* __restrict__ d_means,
                                                      float* __restrict__ d_scales, float* __restrict__ d_colors,
                                                      float* __restrict__ d_opac, int acc) {
-  constexpr int CRW = CD == 48 ? 1 : 4;
   constexpr int NG = 6 + CD;
-  __shared__ float sG[CRW > 1 ? CRW : 1][64][NG + 1];
+  __shared__ float sG[CD == 48 ? 1 : 4][64][NG + 1];
+  const int crw = reduce_sums_crw(B.nv, CD);
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int gi = blockIdx.x * 64 + lane;
+  const int gw = w / crw, u = w - gw * crw;
+  const int gi = (blockIdx.x * (4 / crw) + gw) * 64 + lane;
   GradRegs<CD> gr;
-  if (w < CRW && gi < n) {
-    for (int vi = w; vi < B.nv; vi += CRW) {
+  if (gi < n) {
+    for (int vi = u; vi < B.nv; vi += crw) {
       const float4 a = B.r[vi].sums[2 * (size_t)gi], b = B.r[vi].sums[2 * (size_t)gi + 1];
       // [o S0, o S2, S4, S6 | o S1, S8, S5, S7] -> S0..S8 (S3, the depth sum, is 0 without a depth gradient)
       const float Sf[NPART] = {a.x, b.x, a.y, 0.0f, a.z, b.z, a.w, b.w, b.y};
@@ -2655,8 +2660,8 @@ __global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const floa
       chain_rule<CD, float>(B.r[vi].v, gi, Sf, on, means, scales, colors, opac, gr);
     }
   }
-  if constexpr (CRW > 1) {
-    if (w < CRW) {
+  if constexpr (CD != 48) {
+    if (crw > 1) {  // uniform per launch
       float* mine = sG[w][lane];
 #pragma unroll
       for (int q = 0; q < 3; ++q) mine[q] = gr.m[q];
@@ -2665,26 +2670,25 @@ __global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const floa
       mine[5] = gr.o;
 #pragma unroll
       for (int q = 0; q < CD; ++q) mine[6 + q] = gr.c[q];
+      __syncthreads();
+      if (u != 0 || gi >= n) return;
+#pragma unroll
+      for (int q = 0; q < NG; ++q) {
+        float t = sG[w][lane][q];
+        for (int v = 1; v < crw; ++v) t += sG[w + v][lane][q];
+        sG[w][lane][q] = t;
+      }
+      const float* tot = sG[w][lane];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) gr.m[q] = tot[q];
+      gr.s[0] = tot[3];
+      gr.s[1] = tot[4];
+      gr.o = tot[5];
+#pragma unroll
+      for (int q = 0; q < CD; ++q) gr.c[q] = tot[6 + q];
     }
-    __syncthreads();
-    if (w != 0 || gi >= n) return;
-#pragma unroll
-    for (int q = 0; q < NG; ++q) {
-      float t = sG[0][lane][q];
-#pragma unroll
-      for (int u = 1; u < CRW; ++u) t += sG[u][lane][q];
-      sG[0][lane][q] = t;
-    }
-    const float* tot = sG[0][lane];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) gr.m[q] = tot[q];
-    gr.s[0] = tot[3];
-    gr.s[1] = tot[4];
-    gr.o = tot[5];
-#pragma unroll
-    for (int q = 0; q < CD; ++q) gr.c[q] = tot[6 + q];
   }
-  if (w != 0 || gi >= n) return;
+  if (u != 0 || gi >= n) return;
   GradOut out{d_means + 3 * (size_t)gi, d_scales + 3 * (size_t)gi, d_colors + (size_t)CD * gi, d_opac + gi, acc != 0};
 #pragma unroll
   for (int q = 0; q < 3; ++q) out.mean(q, gr.m[q]);
@@ -3478,28 +3482,12 @@ static BwdWs bwd_ws(const gr_view* v, const gr_plan* plan, void* ws) {
   return w;
 }
 
-// l1 != nullptr (gr_fwd_render_l1): no_depth_grad view without depth output; the fit loss's upstream
-// fragments and tile sums go to the backward workspace `ws`, the view loss to l1_loss_out.
-static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins, size_t bins_bytes,
-                          void* scratch, size_t scratch_bytes, float* out_rgb, float* out_alpha, float* out_depth,
-                          float* saved, void* stream, const L1Args* l1, float* l1_loss_out, void* ws, size_t ws_bytes) {
-  gr_status st = check_view(v);
-  if (st != GR_OK) return st;
-  if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
-  if (plan->num_pairs < 0 || plan->num_slots < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
-  if (!l1 && !saved) return set_error(GR_ERR_INVALID_ARGUMENT, "saved is required");
-  if (l1 && (!ws || ws_bytes < gr_bwd_bytes(v, n, plan) || !l1_loss_out))
-    return set_error(GR_ERR_WORKSPACE, "gr_fwd_render_l1: backward workspace too small (or null loss)");
-  if (n > 0 && (!geom || !bins)) return set_error(GR_ERR_INVALID_ARGUMENT, "null workspace");
+// The view's binning (pair emission, the stable counting sort by tile, work items): gr_fwd_bin, or the
+// first half of fwd_impl when the view is not already binned.
+static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const void* geom, const Bins& b,
+                          const Scratch& sc, const ViewK& vk, hipStream_t s) {
   const int64_t num_pairs = plan->num_pairs;
-  if (bins_bytes < gr_bins_bytes(v, n, plan)) return set_error(GR_ERR_WORKSPACE, "bins workspace too small");
-  if (scratch_bytes < gr_fwd_scratch_bytes(v, n, plan) || !scratch)
-    return set_error(GR_ERR_WORKSPACE, "forward scratch workspace too small");
-  hipStream_t s = (hipStream_t)stream;
-  const ViewK vk = make_viewk(v);
   const int tiles = vk.tiles_x * vk.tiles_y, vtiles = 2 * tiles;
-  Bins b = bins_view(bins, vtiles, num_pairs);
-  Scratch sc = scratch_view(scratch, vtiles, num_pairs);
   prof_mark(PROF_BINNING, s);
   if (n > 0 && num_pairs > 0) {
     Geom g = geom_view((void*)geom, n);
@@ -3573,6 +3561,35 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
   }
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_BINNING, s);
+  return GR_OK;
+}
+
+// l1 != nullptr (gr_fwd_render_l1): no_depth_grad view without depth output; the fit loss's upstream
+// fragments and tile sums go to the backward workspace `ws`, the view loss to l1_loss_out.
+static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins, size_t bins_bytes,
+                          void* scratch, size_t scratch_bytes, float* out_rgb, float* out_alpha, float* out_depth,
+                          float* saved, void* stream, const L1Args* l1, float* l1_loss_out, void* ws, size_t ws_bytes) {
+  gr_status st = check_view(v);
+  if (st != GR_OK) return st;
+  if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
+  if (plan->num_pairs < 0 || plan->num_slots < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
+  if (!l1 && !saved) return set_error(GR_ERR_INVALID_ARGUMENT, "saved is required");
+  if (l1 && (!ws || ws_bytes < gr_bwd_bytes(v, n, plan) || !l1_loss_out))
+    return set_error(GR_ERR_WORKSPACE, "gr_fwd_render_l1: backward workspace too small (or null loss)");
+  if (n > 0 && (!geom || !bins)) return set_error(GR_ERR_INVALID_ARGUMENT, "null workspace");
+  const int64_t num_pairs = plan->num_pairs;
+  if (bins_bytes < gr_bins_bytes(v, n, plan)) return set_error(GR_ERR_WORKSPACE, "bins workspace too small");
+  if (scratch_bytes < gr_fwd_scratch_bytes(v, n, plan) || !scratch)
+    return set_error(GR_ERR_WORKSPACE, "forward scratch workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const ViewK vk = make_viewk(v);
+  const int tiles = vk.tiles_x * vk.tiles_y, vtiles = 2 * tiles;
+  Bins b = bins_view(bins, vtiles, num_pairs);
+  Scratch sc = scratch_view(scratch, vtiles, num_pairs);
+  if (!v->binned) {
+    st = bin_impl(v, n, plan, geom, b, sc, vk, s);
+    if (st != GR_OK) return st;
+  }
   Geom g = geom_view((void*)geom, n > 0 ? n : 1);
   const size_t HW = (size_t)v->width * v->height;
   const int64_t cap = item_cap(vtiles, num_pairs);
@@ -3617,6 +3634,22 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
                         float* saved, void* stream) {
   return fwd_impl(v, n, plan, geom, bins, bins_bytes, scratch, scratch_bytes, out_rgb, out_alpha, out_depth, saved, stream,
                   nullptr, nullptr, nullptr, 0);
+}
+
+gr_status gr_fwd_bin(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins, size_t bins_bytes,
+                     void* scratch, size_t scratch_bytes, void* stream) {
+  gr_status st = check_view(v);
+  if (st != GR_OK) return st;
+  if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
+  if (plan->num_pairs < 0 || plan->num_slots < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
+  if (n > 0 && (!geom || !bins)) return set_error(GR_ERR_INVALID_ARGUMENT, "null workspace");
+  if (bins_bytes < gr_bins_bytes(v, n, plan)) return set_error(GR_ERR_WORKSPACE, "bins workspace too small");
+  if (scratch_bytes < gr_fwd_scratch_bytes(v, n, plan) || !scratch)
+    return set_error(GR_ERR_WORKSPACE, "forward scratch workspace too small");
+  const ViewK vk = make_viewk(v);
+  const int vtiles = 2 * vk.tiles_x * vk.tiles_y;
+  return bin_impl(v, n, plan, geom, bins_view(bins, vtiles, plan->num_pairs), scratch_view(scratch, vtiles, plan->num_pairs),
+                  vk, (hipStream_t)stream);
 }
 
 gr_status gr_fwd_render_l1(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins, size_t bins_bytes,
@@ -3716,7 +3749,8 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
     B.nv = 1;
     B.r[0].v = vk;
     B.r[0].sums = (const float4*)w.sums;
-    const dim3 grid((n + 63) / 64), block(256);
+    const int gpb = 64 * (4 / reduce_sums_crw(1, color_dim));
+    const dim3 grid((n + gpb - 1) / gpb), block(256);
     if (color_dim == 3)
       hipLaunchKernelGGL(k_reduce_sums<3>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
                          d_colors, d_opacities, accumulate);
@@ -3907,7 +3941,8 @@ gr_status gr_reduce_sums(int num_views, const gr_sums_view* views, int n, const 
   }
   hipStream_t s = (hipStream_t)stream;
   prof_mark(PROF_REDUCE, s);
-  const dim3 grid((n + 63) / 64), block(256);
+  const int gpb = 64 * (4 / reduce_sums_crw(num_views, color_dim));
+  const dim3 grid((n + gpb - 1) / gpb), block(256);
   if (color_dim == 3)
     hipLaunchKernelGGL(k_reduce_sums<3>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
                        d_colors, d_opacities, accumulate);

@@ -87,6 +87,13 @@ GATHER = os.environ.get("GR_GATHER", "1") != "0"
 NATIVE_EXEC = os.environ.get("GR_NATIVE_EXEC", "0") != "0"
 # the native executor on this driver's torch streams (1) or on streams of its own (0)
 EXEC_STREAMS = os.environ.get("GR_EXEC_STREAMS", "1") != "0"
+# priority of the preparation stream (torch's convention: 0 normal, -1 high).  HIP keeps one pool of hardware
+# queues per priority, so a high-priority preparation stream also stops sharing a queue with a render stream.
+PREP_PRIORITY = int(os.environ.get("GR_PREP_PRIORITY", "0"))
+# the fused path's binning (gr_fwd_bin) on a stream of its own with this priority ("" = off: each view bins on
+# its render stream inside gr_fwd_render_l1).  The binning kernels are latency-bound; behind the other streams'
+# splats they take several times their standalone time while holding CU resources.
+BIN_STREAM = os.environ.get("GR_BIN_STREAM", "")
 # the fused path at f32 grade (gr_view.no_depth_grad = 2: three-piece splits in both splats, as the default
 # precision mode) instead of its two-piece mode: the precision reference of the fit path (bench.py f32_grade_fit)
 F32_GRADE = os.environ.get("GR_F32_GRADE", "0") != "0"
@@ -354,7 +361,26 @@ class ViewShardedFitter:
         return tr.prepare_view(means, scales, colors, opacities, cam.view, cam.proj, self.width, self.height,
                                self._background(means.device), cutoff=cut,
                                core_cutoff=tr.FIT_CUTOFF if fit_view else tr.DEFAULT_CORE_CUTOFF,
-                               depth_grad=self._depth_grad(), plan_host=plan_host)
+                               depth_grad="eager" if self._depth_grad() else False, plan_host=plan_host)
+
+    @staticmethod
+    def _prep_groups(views, ahead: dict, prepare_views: Callable, prep) -> Callable[[int], None]:
+        """prepare_upto(j): the views up to j prepared on stream `prep` (whole groups, in order: the first
+        PREP_FIRST views, then PREP_GROUP at a time; their states go to `ahead`).  Called with the first two
+        groups at once, then after each render (its j + PREP_AHEAD): the step's first render is launched
+        before the host spends time on later groups (a 7-view step waited ~180 us for them)."""
+        nxt = [0]
+
+        def prepare_upto(j):
+            while nxt[0] <= j and nxt[0] < len(views):
+                j0 = nxt[0]
+                js = range(j0, min(len(views), j0 + (PREP_FIRST if j0 == 0 else PREP_GROUP)))
+                with torch.cuda.stream(prep):
+                    ahead.update(zip(js, prepare_views(js)))
+                nxt[0] = js.stop
+
+        prepare_upto(min(PREP_FIRST, PREP_AHEAD - 1))
+        return prepare_upto
 
     def _fit_view(self, i: int, device) -> "tr._native.GrView":
         """The gr_view of view i for the fused path (one FIT_CUTOFF zone, no depth gradient), built once:
@@ -421,6 +447,9 @@ class ViewShardedFitter:
         if self._direct(device) and self.params["means"].shape[0] > 0 and self._fused_step_ok():
             with torch.no_grad():
                 means, scales, colors, opacities = activations(self.params)
+                # the regulariser is enqueued before the views (it needs only the activations), so its small
+                # kernels do not sit between the last reduction and the parameter update
+                reg = (self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean()) if self.rank == 0 else None
                 if NATIVE_EXEC and GATHER:
                     total = self._views_native(means, scales, colors, opacities, self._depth_grad())
                 elif self._depth_grad():
@@ -428,8 +457,8 @@ class ViewShardedFitter:
                 else:
                     total = self._views_direct(means, scales, colors, opacities)
                 loss = total / len(self.targets)
-                if self.rank == 0:
-                    loss = loss + (self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean())
+                if reg is not None:
+                    loss = loss + reg
             return self._fused_param_step(scales, opacities, loss)
         means, scales, colors, opacities = activations(self.params)
         if self._direct(device) and means.shape[0] > 0:
@@ -552,7 +581,7 @@ class ViewShardedFitter:
                 self._side = side = [torch.cuda.Stream(device) for _ in range(ns - 1)]
             prep = getattr(self, "_prep", None)
             if prep is None or prep.device != device:
-                self._prep = prep = torch.cuda.Stream(device)
+                self._prep = prep = torch.cuda.Stream(device, priority=PREP_PRIORITY)
             self._exec_streams = rs = (ctypes.c_void_p * max(1, ns - 1))(
                 *[st.cuda_stream for st in (side[:ns - 1] if ns > 1 else [])])
             cfg.render_streams = rs
@@ -601,22 +630,18 @@ class ViewShardedFitter:
         # starts the first render after enqueueing a few preparations (not all of them)
         prep = getattr(self, "_prep", None)
         if prep is None or prep.device != device:
-            self._prep = prep = torch.cuda.Stream(device)
+            self._prep = prep = torch.cuda.Stream(device, priority=PREP_PRIORITY)
         prep.wait_stream(main)
+        bin_stream = None
+        if BIN_STREAM != "":
+            bin_stream = getattr(self, "_bin", None)
+            if bin_stream is None or bin_stream.device != device:
+                self._bin = bin_stream = torch.cuda.Stream(device, priority=int(BIN_STREAM))
+            bin_stream.wait_stream(main)
         pins = self._plan_pins(len(views))
         ahead: dict = {}
-
-        def prepare(j):
-            if j < len(views) and j not in ahead:
-                # none of them prepared yet (groups are contiguous); the step's first group is PREP_FIRST views,
-                # so the first render starts after one view's preparation, not a group's
-                js = range(j, min(len(views), j + (PREP_FIRST if j == 0 else PREP_GROUP)))
-                with torch.cuda.stream(prep):
-                    ahead.update(zip(js, tr.prepare_views_native(m, s, c, o, [self._fit_view(views[q], device) for q in js],
-                                                                 [pins[q] for q in js])))
-
-        for j in range(PREP_AHEAD):
-            prepare(j)
+        prepare_upto = self._prep_groups(views, ahead, lambda js: tr.prepare_views_native(
+            m, s, c, o, [self._fit_view(views[q], device) for q in js], [pins[q] for q in js]), prep)
         pending: list = [[] for _ in streams]  # per stream: (render state, partials) awaiting their reduction
         started = [False] * ns
         # stream k's views in nb near-equal batches of at most REDUCE_BATCH (sizes in the order they fill)
@@ -640,7 +665,7 @@ class ViewShardedFitter:
 
         for j, i in enumerate(views):
             k = j % ns
-            prepare(j + PREP_AHEAD)
+            prepare_upto(j)
             pv = ahead.pop(j)
             streams[k].wait_event(pv.event)
             pv.geom.record_stream(streams[k])
@@ -648,7 +673,8 @@ class ViewShardedFitter:
                 # one zone at the core cutoff and no depth channel: the loss reads neither depth nor the
                 # tail-only part of W's footprint (torch_renderer.FIT_CUTOFF)
                 rs, ws = tr.forward_l1_native(m, s, c, o, pv.gv, pv, self.targets[i],
-                                              self.masks[i] if w_sil > 0.0 else None, w_sil, g_scale, losses_v[j:j + 1])
+                                              self.masks[i] if w_sil > 0.0 else None, w_sil, g_scale, losses_v[j:j + 1],
+                                              bin_stream=bin_stream)
                 pv = None
                 tr.backward_splat_native(rs, ws)
                 if GATHER:  # the view's sums; its bins, geom and workspace go back to the allocator here
@@ -656,6 +682,7 @@ class ViewShardedFitter:
                     rs = ws = None
             if rs is not None:
                 pending[k].append((rs, ws))
+            prepare_upto(j + PREP_AHEAD)
             if len(pending[k]) >= sizes[k][0]:
                 reduce_pending(k)
                 if len(sizes[k]) > 1:
@@ -665,6 +692,8 @@ class ViewShardedFitter:
         for st in streams[1:]:
             main.wait_stream(st)
         main.wait_stream(prep)
+        if bin_stream is not None:
+            main.wait_stream(bin_stream)
         used = min(ns, len(views))
         # the streams' accumulators (summed in stream order by the caller: gr_fit_param_step or torch adds)
         self._acc_parts = acc[:used] if used > 0 else [tuple(torch.zeros_like(t) for t in (m, s, c, o))]
@@ -692,7 +721,7 @@ class ViewShardedFitter:
         g_scale = 1.0 / len(self.targets)
         prep = getattr(self, "_prep", None)
         if prep is None or prep.device != device:
-            self._prep = prep = torch.cuda.Stream(device)
+            self._prep = prep = torch.cuda.Stream(device, priority=PREP_PRIORITY)
         prep.wait_stream(main)
         pins = self._plan_pins(len(views))
         cache = getattr(self, "_gvd_cache", None)
@@ -707,18 +736,11 @@ class ViewShardedFitter:
                                         depth_grad=True)
             return cache[i]
 
-        def prepare(j):
-            if j < len(views) and j not in ahead:
-                js = range(j, min(len(views), j + PREP_GROUP))
-                with torch.cuda.stream(prep):
-                    ahead.update(zip(js, tr.prepare_views_native(m, s, c, o, [gv_of(views[q]) for q in js],
-                                                                 [pins[q] for q in js])))
-
-        for j in range(PREP_AHEAD):
-            prepare(j)
+        prepare_upto = self._prep_groups(views, ahead, lambda js: tr.prepare_views_native(
+            m, s, c, o, [gv_of(views[q]) for q in js], [pins[q] for q in js]), prep)
         for j, i in enumerate(views):
             k = j % ns
-            prepare(j + PREP_AHEAD)
+            prepare_upto(j)
             pv = ahead.pop(j)
             streams[k].wait_event(pv.event)
             pv.geom.record_stream(streams[k])
@@ -727,6 +749,7 @@ class ViewShardedFitter:
                 pv = None
                 tr.backward_fit_native(m, s, c, o, rs, self.targets[i], self.masks[i] if w_sil > 0.0 else None, w_sil,
                                        self.depths[i], self.w_depth, g_scale, losses_v[j:j + 1], acc[k], accumulate=j >= ns)
+            prepare_upto(j + PREP_AHEAD)
         for st in streams[1:]:
             main.wait_stream(st)
         main.wait_stream(prep)

@@ -22,6 +22,7 @@ libgr_hip.so through a ``torch.autograd.Function`` — not by torch ops.  Differ
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import weakref
@@ -417,13 +418,25 @@ def _check_params(means, scales, colors, opacities) -> None:
     _check_operand(opacities, (n,), "opacities", dev)
 
 
+def _binned(gv: _native.GrView) -> _native.GrView:
+    """gv with binned = 1 (made once per view structure and kept on it)."""
+    b = getattr(gv, "_binned_copy", None)
+    if b is None:
+        b = _native.GrView.from_buffer_copy(gv)
+        b.binned = 1
+        gv._binned_copy = b
+    return b
+
+
 def forward_l1_native(means, scales, colors, opacities, gv: _native.GrView, prepared: Prepared, target, mask,
-                      w_sil: float, g_scale: float, loss_out):
+                      w_sil: float, g_scale: float, loss_out, bin_stream=None):
     """gr_fwd_render_l1 on the current stream (the fused fit path; gv with no_depth_grad, no depth output):
     the forward of one view whose epilogue evaluates the fit loss ``mean|out - target| + w_sil
     mean|alpha - mask|`` (mask may be None) into ``loss_out`` and its upstream gradients (scaled by
     ``g_scale``) into the backward workspace.  No image is written.  Returns (RenderState, workspace):
-    pass them to ``backward_splat_native`` and then ``reduce_views_native``."""
+    pass them to ``backward_splat_native`` and then ``reduce_views_native``.  ``bin_stream``: run the
+    view's binning (gr_fwd_bin) on that stream (after the preparation's event) and only the splat on the
+    current one, which waits for it."""
     L = _native.lib()
     dev = means.device
     n = int(means.shape[0])
@@ -433,12 +446,28 @@ def forward_l1_native(means, scales, colors, opacities, gv: _native.GrView, prep
     _check_operand(target, (gv.height, gv.width, 3), "target", dev)
     _check_operand(mask, (gv.height, gv.width), "mask", dev)
     plan = prepared.plan()
-    bins = torch.empty((_ws_round(L.gr_bins_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8,
-                       device=dev)
+    cur = torch.cuda.current_stream(dev)
+    rv = gv
+    with torch.cuda.stream(bin_stream) if bin_stream is not None else contextlib.nullcontext():
+        bins = torch.empty((_ws_round(L.gr_bins_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8,
+                           device=dev)
+        scratch = torch.empty((_ws_round(L.gr_fwd_scratch_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),),
+                              dtype=torch.uint8, device=dev)
+        if bin_stream is not None:
+            bin_stream.wait_event(prepared.event)
+            prepared.geom.record_stream(bin_stream)
+            _native.check(L.gr_fwd_bin(ctypes.byref(gv), n, ctypes.byref(plan), _native.ptr(prepared.geom),
+                                       _native.ptr(bins), bins.numel(), _native.ptr(scratch), scratch.numel(),
+                                       ctypes.c_void_p(bin_stream.cuda_stream)), "gr_fwd_bin")
+            done = torch.cuda.Event()
+            done.record(bin_stream)
+    if bin_stream is not None:
+        cur.wait_event(done)
+        bins.record_stream(cur)
+        scratch.record_stream(cur)
+        rv = _binned(gv)
     ws = torch.empty((_ws_round(L.gr_bwd_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8, device=dev)
-    scratch = torch.empty((_ws_round(L.gr_fwd_scratch_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),),
-                          dtype=torch.uint8, device=dev)
-    _native.check(L.gr_fwd_render_l1(ctypes.byref(gv), n, ctypes.byref(plan), _native.ptr(prepared.geom),
+    _native.check(L.gr_fwd_render_l1(ctypes.byref(rv), n, ctypes.byref(plan), _native.ptr(prepared.geom),
                                      _native.ptr(bins), bins.numel(), _native.ptr(scratch), scratch.numel(),
                                      _native.ptr(target), _native.ptr(mask), ctypes.c_float(w_sil), ctypes.c_float(g_scale),
                                      _native.ptr(loss_out), None, None, _native.ptr(ws), ws.numel(), _stream(dev)),
@@ -573,10 +602,15 @@ def _device_inputs(means, scales, colors, opacities):
 
 
 def prepare_view(means, scales, colors, opacities, view, proj, width, height, background=None,
-                 cutoff=None, core_cutoff=DEFAULT_CORE_CUTOFF, depth_grad: bool = True, plan_host=None) -> Prepared:
+                 cutoff=None, core_cutoff=DEFAULT_CORE_CUTOFF, depth_grad=True, plan_host=None) -> Prepared:
     """Enqueue the preparation of one view (see ``Prepared``); pass it to ``rasterize(prepared=...)``
-    with the same tensors, cutoffs and ``depth_grad``.  The tensors' values must not change in between."""
-    gv = make_view(view, proj, width, height, background, cutoff, core_cutoff, depth_grad)
+    with the same tensors, cutoffs and ``depth_grad``.  The tensors' values must not change in between.
+    depth_grad=True prepares the view rasterize renders first in the lazy default (the no-depth-gradient
+    footprint); "eager" the f32-grade view."""
+    if depth_grad is True and not _eager(depth_grad) and cutoff is None:
+        gv = make_view(view, proj, width, height, background, None, core_cutoff, False)
+    else:
+        gv = make_view(view, proj, width, height, background, cutoff, core_cutoff, bool(depth_grad))
     return prepare_native(*_device_inputs(means, scales, colors, opacities), gv, plan_host)
 
 
@@ -685,7 +719,7 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
     else:
         gv = make_view(view, proj, width, height, background, cutoff, core_cutoff, bool(depth_grad))
     if prepared is not None and (prepared.gv.cutoff != gv.cutoff or prepared.gv.no_depth_grad != gv.no_depth_grad):
-        # a preparation made for the eager view (prepare_view(depth_grad=True) with GR_LAZY_DEPTH=0 semantics)
+        # a preparation made for the eager view (prepare_view(depth_grad="eager"), or GR_LAZY_DEPTH=0)
         gv, gv_depth = prepared.gv, None
     if prepared is not None or not SPECULATE:
         return _RasterizeGaussians.apply(m, s, c, o, background, gv, prepared, gv_depth)

@@ -89,6 +89,9 @@ typedef struct gr_view {
                        /* the background colour from it (stream-ordered) instead of background[]: */
                        /* a caller holding the background in a device tensor (the reference fit   */
                        /* loop, fit_multiview_stub.py:287) needs no device-to-host read per view  */
+  int binned;          /* 1: gr_fwd_bin has already built this view's bins (same plan, geom, bins   */
+                       /* and scratch, ordered before the render); gr_fwd_render(_l1) then launches */
+                       /* only the splat.  0 (default): the render bins the view itself            */
 } gr_view;
 
 /* ------------------------------------------------------------------------------------------ */
@@ -153,6 +156,12 @@ size_t gr_saved_floats(const gr_view* v);
 gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins,
                         size_t bins_bytes, void* scratch, size_t scratch_bytes, float* out_rgb,
                         float* out_alpha, float* out_depth, float* saved, void* stream);
+
+/* The binning half of gr_fwd_render (pair emission, tile sort, work items) on its own, so a caller can
+ * run it on another stream (e.g. a high-priority one) and then render with gr_view.binned = 1 on the
+ * same plan, geom, bins and scratch. */
+gr_status gr_fwd_bin(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins, size_t bins_bytes,
+                     void* scratch, size_t scratch_bytes, void* stream);
 
 /* Backward workspace: per-pair gradient partials + per-pixel upstream vectors. */
 size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan);

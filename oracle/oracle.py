@@ -39,6 +39,7 @@ class GrView(ctypes.Structure):
         ("core_cutoff", ctypes.c_float),
         ("no_depth_grad", ctypes.c_int),  # product precision mode; the oracle always computes in float64
         ("background_dev", ctypes.c_void_p),  # product only (device background); the oracle reads background
+        ("binned", ctypes.c_int),  # product only (gr_fwd_bin ran); the oracle always bins
     ]
 
 

@@ -1,6 +1,6 @@
 """One steady-state fit step's kernel timeline from a rocprofv3 --kernel-trace CSV run: every kernel's
 start / end (us from the step's first kernel), its queue, and the idle gaps of the whole GPU; the step is
-the span between two consecutive Adam launches (k_adam_step) in the middle of the run.
+the span between two consecutive parameter-update launches (k_adam_step, or k_fit_param_step at world size 1) in the middle of the run.
     python tools/step_timeline.py <dir> [step index from the end, default 3]"""
 import csv
 import glob
@@ -14,12 +14,12 @@ def short(name):
 
 
 def main():
-    f = sorted(glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True))[0]
+    f = sorted(glob.glob(sys.argv[1] + "/**/*k*t*.csv", recursive=True))[0]
     back = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     rows = [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Queue_Id", r.get("Stream_Id", "?")))
             for r in csv.DictReader(open(f))]
     rows.sort(key=lambda r: r[1])
-    adam = [i for i, r in enumerate(rows) if "k_adam_step" in r[0]]
+    adam = [i for i, r in enumerate(rows) if ("k_adam_step" in r[0] or "k_fit_param_step" in r[0])]
     # the last Adam launch of each step: a gap of > 20 launches to the next Adam launch
     ends = [a for a, b in zip(adam, adam[1:]) if b - a > 20] + adam[-1:]
     if len(ends) < back + 1:
