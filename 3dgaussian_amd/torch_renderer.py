@@ -247,10 +247,11 @@ class Prepared:
     the next view before rendering the current one keeps the device busy while the host reads the
     plan (ViewShardedFitter does this)."""
 
-    __slots__ = ("gv", "n", "geom", "plan_host", "event")
+    __slots__ = ("gv", "n", "geom", "plan_host", "event", "binned")
 
     def __init__(self, gv, n, geom, plan_host, event):
         self.gv, self.n, self.geom, self.plan_host, self.event = gv, n, geom, plan_host, event
+        self.binned = None  # (bins, scratch, binned gr_view, event) when the speculation binned it ahead
 
     def plan(self) -> _native.GrPlan:
         self.event.synchronize()
@@ -303,12 +304,56 @@ def prepare_views_native(means, scales, colors, opacities, gvs, plan_hosts) -> l
     return [Prepared(gv, n, g, p, ev) for gv, g, p in zip(gvs, geoms, plan_hosts)]
 
 
+def _bin_launch(L, gv, n, plan, prepared, bin_stream, dev):
+    """gr_fwd_bin of a prepared view on ``bin_stream`` (after the preparation's event), into bins and scratch
+    allocated there.  Returns (bins, scratch, the gr_view with binned = 1, the binning's end event)."""
+    with torch.cuda.stream(bin_stream):
+        bins = torch.empty((_ws_round(L.gr_bins_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8,
+                           device=dev)
+        scratch = torch.empty((_ws_round(L.gr_fwd_scratch_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),),
+                              dtype=torch.uint8, device=dev)
+        bin_stream.wait_event(prepared.event)
+        prepared.geom.record_stream(bin_stream)
+        _native.check(L.gr_fwd_bin(ctypes.byref(gv), n, ctypes.byref(plan), _native.ptr(prepared.geom), _native.ptr(bins),
+                                   bins.numel(), _native.ptr(scratch), scratch.numel(),
+                                   ctypes.c_void_p(bin_stream.cuda_stream)), "gr_fwd_bin")
+        done = torch.cuda.Event()
+        done.record(bin_stream)
+    return bins, scratch, _binned(gv), done
+
+
+def _bin_ahead(L, gv, n, plan, prepared, bin_stream, dev):
+    """The bins and forward scratch of a render (allocated for the current stream); with ``bin_stream``
+    filled by gr_fwd_bin there (_bin_launch), or already binned (``prepared.binned``, the speculation's),
+    the current stream waiting for the binning.  Returns (bins, scratch, the gr_view to render with)."""
+    pre = getattr(prepared, "binned", None) if prepared is not None else None
+    if pre is None and bin_stream is None:
+        bins = torch.empty((_ws_round(L.gr_bins_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8,
+                           device=dev)
+        scratch = torch.empty((_ws_round(L.gr_fwd_scratch_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),),
+                              dtype=torch.uint8, device=dev)
+        return bins, scratch, gv
+    if pre is not None and pre[2].cutoff == gv.cutoff and pre[2].no_depth_grad == gv.no_depth_grad:
+        bins, scratch, _, done = pre
+    else:
+        bins, scratch, _, done = _bin_launch(L, gv, n, plan, prepared, bin_stream or torch.cuda.current_stream(dev), dev)
+    # this render's own view (its background pointer), not the one the binning was launched with
+    rv = _binned(gv)
+    cur = torch.cuda.current_stream(dev)
+    cur.wait_event(done)
+    bins.record_stream(cur)
+    scratch.record_stream(cur)
+    return bins, scratch, rv
+
+
 def forward_native(means, scales, colors, opacities, gv: _native.GrView, prepared: Optional[Prepared] = None,
-                   want_depth: bool = True, images: bool = True):
+                   want_depth: bool = True, images: bool = True, bin_stream=None):
     """Run gr_fwd_prepare(_async) + gr_fwd_render.  Returns (out, alpha, depth, RenderState).
     ``want_depth=False`` on a no_depth_grad view: no depth output (None) and no depth sums (gr_fwd_render
     with out_depth = NULL: the forward skips its depth channel).  ``images=False``: no output images at
-    all (None, None, None; the saved sums for the backward only, as the fit loop needs)."""
+    all (None, None, None; the saved sums for the backward only, as the fit loop needs).  ``bin_stream``
+    (with ``prepared``): the view's binning runs there (gr_fwd_bin), beside whatever the current stream
+    still has queued, and only the splat on the current stream."""
     L = _native.lib()
     dev = means.device
     n = int(means.shape[0])
@@ -321,17 +366,14 @@ def forward_native(means, scales, colors, opacities, gv: _native.GrView, prepare
         raise ValueError("prepared view does not match this render (Gaussian count, image size or cutoffs)")
     geom = prepared.geom
     plan = prepared.plan()
-    bins = torch.empty((_ws_round(L.gr_bins_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8,
-                       device=dev)
+    bins, scratch, rv = _bin_ahead(L, gv, n, plan, prepared, bin_stream, dev)
     out = torch.empty((H, W, 3), dtype=torch.float32, device=dev) if images else None
     alpha = torch.empty((H, W), dtype=torch.float32, device=dev) if images else None
     depth = (torch.empty((H, W), dtype=torch.float32, device=dev)
              if images and (want_depth or not gv.no_depth_grad) else None)
     saved = torch.empty((int(L.gr_saved_floats(ctypes.byref(gv))),), dtype=torch.float32, device=dev)
     # scratch is released when this function returns; the caching allocator keeps it stream-ordered
-    scratch = torch.empty((_ws_round(L.gr_fwd_scratch_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),),
-                          dtype=torch.uint8, device=dev)
-    _native.check(L.gr_fwd_render(ctypes.byref(gv), n, ctypes.byref(plan), _native.ptr(geom), _native.ptr(bins),
+    _native.check(L.gr_fwd_render(ctypes.byref(rv), n, ctypes.byref(plan), _native.ptr(geom), _native.ptr(bins),
                                   bins.numel(), _native.ptr(scratch), scratch.numel(), _native.ptr(out), _native.ptr(alpha),
                                   _native.ptr(depth), _native.ptr(saved), s), "gr_fwd_render")
     del scratch
@@ -446,26 +488,7 @@ def forward_l1_native(means, scales, colors, opacities, gv: _native.GrView, prep
     _check_operand(target, (gv.height, gv.width, 3), "target", dev)
     _check_operand(mask, (gv.height, gv.width), "mask", dev)
     plan = prepared.plan()
-    cur = torch.cuda.current_stream(dev)
-    rv = gv
-    with torch.cuda.stream(bin_stream) if bin_stream is not None else contextlib.nullcontext():
-        bins = torch.empty((_ws_round(L.gr_bins_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8,
-                           device=dev)
-        scratch = torch.empty((_ws_round(L.gr_fwd_scratch_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),),
-                              dtype=torch.uint8, device=dev)
-        if bin_stream is not None:
-            bin_stream.wait_event(prepared.event)
-            prepared.geom.record_stream(bin_stream)
-            _native.check(L.gr_fwd_bin(ctypes.byref(gv), n, ctypes.byref(plan), _native.ptr(prepared.geom),
-                                       _native.ptr(bins), bins.numel(), _native.ptr(scratch), scratch.numel(),
-                                       ctypes.c_void_p(bin_stream.cuda_stream)), "gr_fwd_bin")
-            done = torch.cuda.Event()
-            done.record(bin_stream)
-    if bin_stream is not None:
-        cur.wait_event(done)
-        bins.record_stream(cur)
-        scratch.record_stream(cur)
-        rv = _binned(gv)
+    bins, scratch, rv = _bin_ahead(L, gv, n, plan, prepared, bin_stream, dev)
     ws = torch.empty((_ws_round(L.gr_bwd_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8, device=dev)
     _native.check(L.gr_fwd_render_l1(ctypes.byref(rv), n, ctypes.byref(plan), _native.ptr(prepared.geom),
                                      _native.ptr(bins), bins.numel(), _native.ptr(scratch), scratch.numel(),
@@ -558,10 +581,10 @@ def _grad_background(st: RenderState, background: torch.Tensor, g_out: torch.Ten
 
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, means, scales, colors, opacities, background, gv, prepared, gv_depth=None):
+    def forward(ctx, means, scales, colors, opacities, background, gv, prepared, gv_depth=None, bin_stream=None):
         """gv_depth: the f32-grade view a lazily rendered gv (two-piece mode) re-renders with when a depth
-        gradient arrives (LAZY_DEPTH), else None."""
-        out, alpha, depth, st = forward_native(means, scales, colors, opacities, gv, prepared)
+        gradient arrives (LAZY_DEPTH), else None.  bin_stream: see forward_native."""
+        out, alpha, depth, st = forward_native(means, scales, colors, opacities, gv, prepared, bin_stream=bin_stream)
         # an output the loss does not use gets a None gradient instead of zeros, so an unused depth
         # output lets the backward skip the tail pairs (gr_bwd with g_depth = NULL)
         ctx.set_materialize_grads(False)
@@ -589,7 +612,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.st = None
         dm, ds, dc, do = backward_native(means, scales, colors, opacities, st, g_out, g_alpha, g_depth)
         dbg = _grad_background(st, background, g_out) if ctx.needs_input_grad[4] else None
-        return dm, ds, dc, do, dbg, None, None, None
+        return dm, ds, dc, do, dbg, None, None, None, None
 
 
 def _device_inputs(means, scales, colors, opacities):
@@ -619,13 +642,18 @@ def prepare_view(means, scales, colors, opacities, view, proj, width, height, ba
 # loop, fit_multiview_stub.py:277-290, calls render_gaussians_torch once per camera with the same
 # activation tensors).  A render needs its view's pair count on the host before the binning can be
 # enqueued; without help that is one host wait per view for a preparation enqueued just before it.
-# After rendering camera A the op enqueues the preparation of the camera that followed A last time,
-# with the same input tensors; the next call uses it when its camera and tensors match (the same live
-# tensor objects at the same versions: weak references, so a freed tensor never matches), and
-# otherwise drops it.  A transition that missed is not speculated the next time.  GR_SPECULATE=0
-# turns this off.
+# The op learns the camera order and keeps a two-deep pipeline of the cameras expected next, with the same
+# input tensors, on a stream of its own: after rendering camera A the preparation of the camera two ahead is
+# enqueued, and on entering the render of A the camera after A (prepared one render ago: its plan is on the
+# host) is binned, before A's splat is enqueued, so the binning runs beside A's splat.  A render uses its
+# pipeline entry when camera and tensors match (the same live tensor objects at the same versions: weak
+# references, so a freed tensor never matches) and otherwise drops the pipeline.  A transition that missed
+# is not speculated the next time.  GR_SPECULATE=0 turns this off; GR_SPEC_BIN=0 keeps the binning in the
+# render.
 # ------------------------------------------------------------------------------------------------
 SPECULATE = os.environ.get("GR_SPECULATE", "1") != "0"
+SPEC_BIN = os.environ.get("GR_SPEC_BIN", "1") != "0"
+SPEC_DEPTH = 2
 
 
 class _Speculation:
@@ -641,7 +669,7 @@ class _Speculation:
                                        for r, t, v in zip(self.refs, tensors, self.versions))
 
 
-_SPEC: dict = {"last": None, "next": {}, "views": {}, "cold": set(), "pending": None, "hits": 0, "misses": 0}
+_SPEC: dict = {"last": None, "next": {}, "views": {}, "cold": set(), "pipe": [], "hits": 0, "misses": 0}
 
 
 def _view_key(gv: _native.GrView) -> tuple:
@@ -649,17 +677,24 @@ def _view_key(gv: _native.GrView) -> tuple:
 
 
 def _spec_take(key, tensors) -> Optional[Prepared]:
-    """The speculative preparation of this view, if one is pending for exactly these inputs."""
-    sp, _SPEC["pending"] = _SPEC["pending"], None
-    if sp is None:
+    """The speculative preparation of this view, if the pipeline's head is exactly these inputs; then the
+    next entry is binned on the speculation stream (before this view's kernels are enqueued)."""
+    pipe = _SPEC["pipe"]
+    if not pipe:
         return None
-    if sp.matches(key, tensors):
-        _SPEC["hits"] += 1
-        _SPEC["cold"].discard((sp.src, key))
-        return sp.prepared
-    _SPEC["misses"] += 1
-    _SPEC["cold"].add((sp.src, sp.key))
-    return None
+    sp = pipe.pop(0)
+    if not sp.matches(key, tensors):
+        _SPEC["misses"] += 1
+        _SPEC["cold"].add((sp.src, sp.key))
+        pipe.clear()
+        return None
+    _SPEC["hits"] += 1
+    _SPEC["cold"].discard((sp.src, key))
+    if SPEC_BIN and pipe and pipe[0].prepared.binned is None:
+        nx = pipe[0].prepared
+        nx.binned = _bin_launch(_native.lib(), nx.gv, nx.n, nx.plan(), nx, _spec_stream(tensors[0].device),
+                                tensors[0].device)
+    return sp.prepared
 
 
 def _spec_stream(dev: torch.device) -> "torch.cuda.Stream":
@@ -670,9 +705,9 @@ def _spec_stream(dev: torch.device) -> "torch.cuda.Stream":
 
 
 def _spec_after(key, gv, tensors, inputs_ready) -> None:
-    """Learn the camera order and enqueue the preparation of the camera expected next, on a stream of its
-    own that waits only for the input tensors (``inputs_ready``, recorded before this view's kernels), so it
-    runs beside this view's render and the host's wait for its plan does not include the render."""
+    """Learn the camera order and fill the pipeline with the cameras expected next: their preparations on a
+    stream of their own that waits only for the input tensors (``inputs_ready``, recorded before this
+    view's kernels), so they run beside this view's render."""
     last = _SPEC["last"]
     if last is not None:
         _SPEC["next"][last] = key
@@ -681,16 +716,21 @@ def _spec_after(key, gv, tensors, inputs_ready) -> None:
     if len(_SPEC["views"]) > 4096:
         _SPEC["views"].clear()
         _SPEC["next"].clear()
-    nxt = _SPEC["next"].get(key)
-    if nxt is None or (key, nxt) in _SPEC["cold"]:
-        return
-    ps = _spec_stream(tensors[0].device)
-    ps.wait_event(inputs_ready)
-    for t in tensors:  # read on ps: not reused by the allocator before ps is done with them
-        t.record_stream(ps)
-    with torch.cuda.stream(ps):
-        pv = prepare_native(*tensors, _SPEC["views"][nxt])
-    _SPEC["pending"] = _Speculation(nxt, tensors, pv, key)
+    pipe = _SPEC["pipe"]
+    ps = None
+    while len(pipe) < SPEC_DEPTH:
+        src = pipe[-1].key if pipe else key
+        nxt = _SPEC["next"].get(src)
+        if nxt is None or (src, nxt) in _SPEC["cold"] or nxt == key:
+            return
+        if ps is None:
+            ps = _spec_stream(tensors[0].device)
+            ps.wait_event(inputs_ready)
+            for t in tensors:  # read on ps: not reused by the allocator before ps is done with them
+                t.record_stream(ps)
+        with torch.cuda.stream(ps):
+            pv = prepare_native(*tensors, _SPEC["views"][nxt])
+        pipe.append(_Speculation(nxt, tensors, pv, src))
 
 
 def rasterize(means, scales, colors, opacities, view, proj, width, height, background=None, cutoff=None,
