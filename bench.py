@@ -525,8 +525,8 @@ def main():
             "config": {"workload": f"C4: {n} Gaussians, {V} orbit views {R}x{R}, fwd+bwd+grad all-reduce+Adam per step",
                        "gaussians": n, "views": V, "width": R, "height": R, "cutoff_sigma": tr.FIT_CUTOFF, "core_cutoff_sigma": tr.FIT_CUTOFF,
                        "render_path": "fused fit path: per view gr_fwd_render_l1 (forward, loss and upstream gradients) "
-                                      "+ gr_bwd_splat, then gr_reduce_views per batch of a stream's views "
-                                      "(fit_multiview._views_direct)",
+                                      "+ gr_bwd_splat + gr_gather_view (per-Gaussian sums), then gr_reduce_sums (chain rule) "
+                                      "per batch of a stream's views (fit_multiview._views_direct, 4 HIP streams)",
                        "scale": round(0.1061 * (1200.0 / n) ** (1.0 / 3.0), 5), "seed": 0,
                        "parallelism": f"view-sharded dp{world}", "views_per_rank": views_per_rank,
                        "pairs_per_view": int(avg_pairs), "core_pairs_per_view": int(avg_core),
