@@ -44,6 +44,14 @@
 
 #include "../../include/gr_hip.h"
 
+// Timing experiments only (tools/ab_variant.sh "-DGR_DEBUG_SKIP=<mask>"): launches left out of a variant
+// build to measure their marginal cost in the overlapped fit step - 1 forward splat, 2 backward splat,
+// 4 gather, 8 chain-rule reduction, 16 parameter update.  Results of such a build are wrong; the product
+// build has 0.
+#ifndef GR_DEBUG_SKIP
+#define GR_DEBUG_SKIP 0
+#endif
+
 #define GR_VERSION_STR "gr_hip 0.1.0 (gfx950)"
 
 namespace {
@@ -3603,7 +3611,7 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
   }
   float4* saved4 = saved ? (float4*)saved : nullptr;
   float* savedD = saved ? saved + 4 * HW : nullptr;
-  if (num_pairs > 0) {
+  if (num_pairs > 0 && !(GR_DEBUG_SKIP & 1)) {
     prof_mark(PROF_RASTER_FWD, s);
     // no_depth_grad: 0 default (f32-grade W / D), 1 two-piece splits, 2 f32-grade without a depth gradient
     const bool f32g = v->no_depth_grad != 1;
@@ -3831,6 +3839,7 @@ gr_status gr_bwd_splat(const gr_view* v, int n, const gr_plan* plan, const void*
   const Bins b = bins_view((void*)bins, 2 * tiles, plan->num_pairs);
   const BwdWs w = bwd_ws(v, plan, ws);
   const int64_t cap = item_cap(2 * tiles, plan->num_pairs);
+  if (GR_DEBUG_SKIP & 2) return GR_OK;
   prof_mark(PROF_RASTER_BWD, s);
   hipLaunchKernelGGL((v->no_depth_grad == 1 ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>), dim3((unsigned)cap),
                      dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items, (const int*)b.pairs,
@@ -3910,6 +3919,7 @@ gr_status gr_gather_view(const gr_view* v, int n, const gr_plan* plan, const voi
   const ViewK vk = make_viewk(v);
   const Geom g = geom_view((void*)geom, n);
   const Bins b = bins_view((void*)bins, 2 * vk.tiles_x * vk.tiles_y, plan->num_pairs);
+  if (GR_DEBUG_SKIP & 4) return GR_OK;
   prof_mark(PROF_REDUCE, s);
   hipLaunchKernelGGL(k_gather_view, dim3((n + 63) / 64), dim3(256), 0, s, n, (const Cnt2*)g.offsets, (const int*)b.pos_of,
                      (const float4*)ws, (float2*)sums);
@@ -3940,6 +3950,7 @@ gr_status gr_reduce_sums(int num_views, const gr_sums_view* views, int n, const 
     B.r[k].sums = (const float4*)views[k].sums;
   }
   hipStream_t s = (hipStream_t)stream;
+  if (GR_DEBUG_SKIP & 8) return GR_OK;
   prof_mark(PROF_REDUCE, s);
   const int gpb = 64 * (4 / reduce_sums_crw(num_views, color_dim));
   const dim3 grid((n + gpb - 1) / gpb), block(256);
@@ -4115,6 +4126,7 @@ gr_status gr_fit_param_step(int64_t count, int act, float* param, float* grad, c
   const int blocks = (int)std::min<int64_t>((count + 255) / 256, 4096);
   // torch.optim.Adam passes 1 - beta1 (lerp weight) and 1 - beta2 (addcmul value) as Python floats (double)
   const float w1 = (float)(1.0 - beta1), w2 = (float)(1.0 - beta2);
+  if (GR_DEBUG_SKIP & 16) return GR_OK;
   hipLaunchKernelGGL(k_fit_param_step, dim3(blocks), dim3(256), 0, (hipStream_t)stream, count, act, param, grad, acc, reg, adam, exp_avg, exp_avg_sq, neg_step_size, bias_correction2_sqrt, w1, (float)beta2, w2, eps);
   GR_HIP_TRY(hipGetLastError());
   return GR_OK;
