@@ -447,15 +447,20 @@ class ViewShardedFitter:
         if self._direct(device) and self.params["means"].shape[0] > 0 and self._fused_step_ok():
             with torch.no_grad():
                 means, scales, colors, opacities = activations(self.params)
-                # the regulariser is enqueued before the views (it needs only the activations), so its small
-                # kernels do not sit between the last reduction and the parameter update
-                reg = (self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean()) if self.rank == 0 else None
+                reg_fn = ((lambda: self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean())
+                          if self.rank == 0 else None)
+                reg = None
                 if NATIVE_EXEC and GATHER:
+                    reg = reg_fn() if reg_fn else None
                     total = self._views_native(means, scales, colors, opacities, self._depth_grad())
                 elif self._depth_grad():
+                    reg = reg_fn() if reg_fn else None
                     total = self._views_direct_depth(means, scales, colors, opacities)
                 else:
-                    total = self._views_direct(means, scales, colors, opacities)
+                    # the regulariser's small kernels run on the preparation stream once the last
+                    # preparation is enqueued: neither before the first view nor between the last
+                    # reduction and the parameter update
+                    total, reg = self._views_direct(means, scales, colors, opacities, reg_fn)
                 loss = total / len(self.targets)
                 if reg is not None:
                     loss = loss + reg
@@ -465,7 +470,7 @@ class ViewShardedFitter:
             if self._depth_grad():
                 total = self._views_direct_depth(means, scales, colors, opacities)
             else:
-                total = self._views_direct(means, scales, colors, opacities)
+                total, _ = self._views_direct(means, scales, colors, opacities)
             parts = self._acc_parts
             acc = []
             for q in range(4):  # in stream order
@@ -599,14 +604,15 @@ class ViewShardedFitter:
         self._native_keep = (m, s, c, o)  # read by the executor's streams until the caller's stream passes them
         return losses_v.sum()
 
-    def _views_direct(self, means, scales, colors, opacities) -> torch.Tensor:
+    def _views_direct(self, means, scales, colors, opacities, tail_fn=None):
         """This rank's views without autograd: per view, gr_fwd_render_l1 (the HIP forward whose epilogue
         evaluates the view's L1 + silhouette loss and its upstream gradients, fit_multiview_stub.py:292-299)
         and gr_bwd_splat (the backward splat, :310); every REDUCE_BATCH views of a HIP stream,
         gr_reduce_views adds their gradient w.r.t. the
         activated parameters into that stream's accumulator set (in view order: deterministic).  The
         accumulators are summed in stream order and leave in self._acc for one autograd pass through the
-        activations; returns the sum of the view losses (device, 0-d)."""
+        activations; returns (the sum of the view losses (device, 0-d), tail_fn() evaluated on the
+        preparation stream after the last preparation, or None)."""
         device = means.device
         m, s, c, o = (t.detach().float().contiguous() for t in (means, scales, colors, opacities))
         views = self.my_views
@@ -689,6 +695,10 @@ class ViewShardedFitter:
                     sizes[k].pop(0)
         for k in range(ns):
             reduce_pending(k)
+        tail = None
+        if tail_fn is not None:
+            with torch.cuda.stream(prep):
+                tail = tail_fn()
         for st in streams[1:]:
             main.wait_stream(st)
         main.wait_stream(prep)
@@ -697,7 +707,7 @@ class ViewShardedFitter:
         used = min(ns, len(views))
         # the streams' accumulators (summed in stream order by the caller: gr_fit_param_step or torch adds)
         self._acc_parts = acc[:used] if used > 0 else [tuple(torch.zeros_like(t) for t in (m, s, c, o))]
-        return losses_v[:len(views)].sum() if views else torch.zeros((), device=device)
+        return (losses_v[:len(views)].sum() if views else torch.zeros((), device=device)), tail
 
     def _views_direct_depth(self, means, scales, colors, opacities) -> torch.Tensor:
         """The fused path with the depth term (fit_multiview_stub.py:301-305): per view the HIP forward in the

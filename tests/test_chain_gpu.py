@@ -53,7 +53,7 @@ def test_fit_chain_c4_batch_vs_oracle(cuda):
         fit, targets, masks = _fitter(fm, bench, cuda, V)
         with torch.no_grad():
             acts = [a.detach().float().contiguous() for a in fm.activations(fit.params)]
-            total = fit._views_direct(*acts)
+            total, _ = fit._views_direct(*acts)
             torch.cuda.synchronize()
             (acc,) = fit._acc_parts
             hip = [a.cpu().numpy() for a in acc]
@@ -202,7 +202,7 @@ def test_f32_grade_fit_mode(cuda):
             f = fm.ViewShardedFitter(bench.synthetic_params(40_000, cuda), cams, targets, Wt, Ht, masks=masks)
             with torch.no_grad():
                 acts = [a.detach().float().contiguous() for a in fm.activations(f.params)]
-                total = float(f._views_direct(*acts))
+                total = float(f._views_direct(*acts)[0])
                 parts = f._acc_parts
                 acc = [sum(p[q] for p in parts[1:]) + parts[0][q] if len(parts) > 1 else parts[0][q] for q in range(4)]
             out[f32] = (total, [a.cpu().numpy() for a in acc], acts)
