@@ -149,6 +149,15 @@ def test_batched_reduce_matches_per_view_reduce(cuda):
     tr.reduce_views_native(m, s, c, o, batch[:1], one, accumulate=False)
     for a, b in zip(one, per_view[0]):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6 * float(b.abs().max()))
+    # two-stage batches of 1..5 views (k_reduce_sums groups a Gaussian's views over 1, 2 or 4 waves by the
+    # batch size) against the sum of the per-view gradients
+    sums = [(st.gv, tr.gather_view_native(st, ws)) for st, ws in batch]
+    for k in range(1, len(batch) + 1):
+        got = tuple(torch.empty_like(t) for t in (m, s, c, o))
+        tr.reduce_sums_native(m, s, c, o, sums[:k], got, accumulate=False)
+        for q in range(4):
+            ref = sum(pv[q] for pv in per_view[:k])
+            torch.testing.assert_close(got[q], ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
     tot = tuple(torch.empty_like(t) for t in (m, s, c, o))
     tr.reduce_views_native(m, s, c, o, batch, tot, accumulate=False)
     tr.reduce_views_native(m, s, c, o, batch[:2], tot, accumulate=True)  # accumulate adds
@@ -286,3 +295,29 @@ def test_grouped_prepare_matches_single_view_prepare(cuda, sh):
                      (off[4], 24 + ((n + 256) // 256) * 8)]  # records + depths, rects, counts, offsets, plan + totals
             for o, nb in parts:
                 assert torch.equal(a.geom[o:o + nb], b.geom[o:o + nb]), (k, q, o)
+
+
+def test_binning_on_another_stream_is_exact(cuda):
+    """gr_fwd_bin on a second stream followed by the splat with gr_view.binned = 1 (the drop-in op's
+    speculative binning, torch_renderer._bin_ahead) gives bit-identical outputs and saved sums to the one-call
+    gr_fwd_render, in the default and the no-depth-gradient modes."""
+    import torch
+
+    tr = importlib.import_module("3dgaussian_amd.torch_renderer")
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    bench = importlib.import_module("bench")
+    W, H = 160, 120
+    p = bench.synthetic_params(20_000, cuda)
+    m, s, c, o = (t.detach().contiguous() for t in fm.activations(p))
+    cam = fm.orbit_cameras(3, W, H, cuda)[1]
+    side = torch.cuda.Stream(cuda)
+    for depth_grad in (True, False):
+        gv = tr.make_view(cam.view, cam.proj, W, H, None, depth_grad=depth_grad)
+        res = []
+        for bs in (None, side):
+            prep = tr.prepare_native(m, s, c, o, gv)
+            out, alpha, depth, st = tr.forward_native(m, s, c, o, gv, prep, bin_stream=bs)
+            torch.cuda.synchronize()
+            res.append((out.clone(), alpha.clone(), depth.clone(), st.saved.clone()))
+        for a, b in zip(*res):
+            assert torch.equal(a, b), depth_grad
