@@ -47,7 +47,14 @@
 // Timing experiments only (tools/ab_variant.sh "-DGR_DEBUG_SKIP=<mask>"): launches left out of a variant
 // build to measure their marginal cost in the overlapped fit step - 1 forward splat, 2 backward splat,
 // 4 gather, 8 chain-rule reduction, 16 parameter update.  Results of such a build are wrong; the product
-// build has 0.
+// build has 0.  GR_DEBUG_BIN_REPS / GR_DEBUG_PREP_REPS > 1 repeat a view's binning / a group's
+// preparation (idempotent: same results) to measure their marginal cost the other way round.
+#ifndef GR_DEBUG_PREP_REPS
+#define GR_DEBUG_PREP_REPS 1
+#endif
+#ifndef GR_DEBUG_BIN_REPS
+#define GR_DEBUG_BIN_REPS 1
+#endif
 #ifndef GR_DEBUG_SKIP
 #define GR_DEBUG_SKIP 0
 #endif
@@ -2024,11 +2031,22 @@ __device__ __forceinline__ void split_frag(const float (&v)[8], s16x8 (&f)[3]) {
   f[2] = as_frag(make_uint4(pack_bf16(lo[0], lo[1]), pack_bf16(lo[2], lo[3]), pack_bf16(lo[4], lo[5]), pack_bf16(lo[6], lo[7])));
 }
 
+// LDS image of a tile's A fragments in the backward: NPR channel pairs x NPC pieces per side (the full
+// 3 x 3 with a depth gradient or three pieces; 2 x 2 for the no-depth two-piece kernel, whose smaller
+// footprint lets more blocks share a CU).  Chunk (side, pair, piece) of 64 uint4 at uf_chunk().
+template <bool DEPTH, int PIECES>
+struct UFLayout {
+  static constexpr int NPR = DEPTH ? 3 : 2, NPC = (DEPTH || PIECES == 3) ? 3 : 2;
+  static constexpr int CHUNKS = 2 * NPR * NPC;
+  __device__ static constexpr int chunk(int side, int pr, int piece) { return (side * NPR + pr) * NPC + piece; }
+};
+
 template <bool TAIL, bool DEPTH, int PIECES>
 __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, int wave, int tx, int ty,
                                               const int* __restrict__ pairs, const float4* __restrict__ rec,
                                               float* __restrict__ partials, float4 (*sA)[TP], float4 (*sB)[TP],
-                                              float (*sZ)[TP], const uint4* sUF) {
+                                              float* sZ, const uint4* sUF) {
+  using UL = UFLayout<DEPTH, PIECES>;
   static_assert(DEPTH || !TAIL, "tail items carry only depth-coupled terms");
   constexpr int P0 = TAIL ? 2 : 0;      // first channel pair contracted
   constexpr int P1 = DEPTH ? 3 : 2;     // one past the last (pair_channel)
@@ -2041,7 +2059,7 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
     const float4* p = rec_of(gid, n, rec);
     glds16(p, &sA[b][64 * wave]);
     glds16(p + 1, &sB[b][64 * wave]);
-    if constexpr (DEPTH) glds4(zrec_of(gid, n, rec), &sZ[b][64 * wave]);  // z enters only the depth-coupled terms
+    if constexpr (DEPTH) glds4(zrec_of(gid, n, rec), &sZ[b * TP + 64 * wave]);  // z enters only the depth-coupled terms
   };
   stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1), 0);
   int idn = stage_id(k0 + TP + tid, k1, pairs);  // raw: batch base + TP
@@ -2058,7 +2076,7 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
       const int j = g0 + r;
       const float4 a = sA[buf][j];
       const float4 b = sB[buf][j];
-      const float z = DEPTH ? sZ[buf][j] : 0.0f;
+      const float z = DEPTH ? sZ[buf * TP + j] : 0.0f;
       const int myslot = j < nb ? base + j : -1;  // the pair's sorted position = its partial-sum row
       float ex[8], ey[8];
       if constexpr (!DEPTH && PIECES == 2) {
@@ -2083,6 +2101,9 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
           ey[q] = __builtin_amdgcn_exp2f(dy * a.w * dy);
         }
       }
+      // -0 starts: -0 + x == x for every x, so the first accumulation folds into a plain product
+      float S[NPART] = {-0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f};
+      {
       // both contractions are issued before either epilogue, so the T epilogue's VALU work runs while
       // the R MFMAs execute
       f32x16 DT[3], DR[3];
@@ -2092,23 +2113,21 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
         split_frag(ey, BR);
 #pragma unroll
         for (int pr = P0; pr < P1; ++pr)
-          DT[pr] = (DEPTH && pr < 2) ? mfma_split_a2b3(sUF + (0 * 3 + pr) * 3 * 64, lane, BT)
-                                     : mfma_split(sUF + (0 * 3 + pr) * 3 * 64, lane, BT);
+          DT[pr] = (DEPTH && pr < 2) ? mfma_split_a2b3(sUF + UL::chunk(0, pr, 0) * 64, lane, BT)
+                                     : mfma_split(sUF + UL::chunk(0, pr, 0) * 64, lane, BT);
 #pragma unroll
         for (int pr = P0; pr < P1; ++pr)
-          DR[pr] = (DEPTH && pr < 2) ? mfma_split_a2b3(sUF + (1 * 3 + pr) * 3 * 64, lane, BR)
-                                     : mfma_split(sUF + (1 * 3 + pr) * 3 * 64, lane, BR);
+          DR[pr] = (DEPTH && pr < 2) ? mfma_split_a2b3(sUF + UL::chunk(1, pr, 0) * 64, lane, BR)
+                                     : mfma_split(sUF + UL::chunk(1, pr, 0) * 64, lane, BR);
       } else {
         s16x8 BT[2], BR[2];
         split2_frag(ex, BT);
         split2_frag(ey, BR);
 #pragma unroll
-        for (int pr = P0; pr < P1; ++pr) DT[pr] = mfma_split2(sUF + (0 * 3 + pr) * 3 * 64, lane, BT);
+        for (int pr = P0; pr < P1; ++pr) DT[pr] = mfma_split2(sUF + UL::chunk(0, pr, 0) * 64, lane, BT);
 #pragma unroll
-        for (int pr = P0; pr < P1; ++pr) DR[pr] = mfma_split2(sUF + (1 * 3 + pr) * 3 * 64, lane, BR);
+        for (int pr = P0; pr < P1; ++pr) DR[pr] = mfma_split2(sUF + UL::chunk(1, pr, 0) * 64, lane, BR);
       }
-      // -0 starts: -0 + x == x for every x, so the first accumulation folds into a plain product
-      float S[NPART] = {-0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f};
       {
       if constexpr (!DEPTH && PIECES == 2) {
         // Moments about the lane's first pixel centre: dy_q = d0 + o_q with o_q = kslot offset (a compile-
@@ -2189,6 +2208,7 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
       }
       }
       }
+      }
       // lanes r and r + 32 hold the two halves of Gaussian r's pixels; pair32 leaves half 0 with the
       // total of its first argument, half 1 with that of its second
       if constexpr (!DEPTH) {
@@ -2233,10 +2253,11 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
                                                            const int* __restrict__ num_items, const int* __restrict__ pairs,
                                                            const float4* __restrict__ rec, const uint4* __restrict__ UF,
                                                            float* __restrict__ partials) {
+  using UL = UFLayout<DEPTH, PIECES>;
   __shared__ __attribute__((aligned(16))) float4 sA[2][TP];
   __shared__ __attribute__((aligned(16))) float4 sB[2][TP];
-  __shared__ float sZ[2][TP];
-  __shared__ __attribute__((aligned(16))) uint4 sUF[UF_FRAGS];
+  __shared__ float sZ[2][DEPTH ? TP : 1];
+  __shared__ __attribute__((aligned(16))) uint4 sUF[UL::CHUNKS * 64];
   const int nitems = *num_items;
   if ((int)blockIdx.x >= nitems) return;
   const int item = xcd_item(blockIdx.x, nitems);
@@ -2249,19 +2270,20 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
   {  // the tile's A fragments this item contracts -> LDS (DMA): chunk (side * 3 + pair) * 3 + piece
     const uint4* src = UF + (size_t)tile * UF_FRAGS;
     const int p0 = tail ? 2 : 0, p1 = DEPTH ? 3 : 2;
-    for (int c = wave; c < UF_FRAGS / 64; c += 4) {
-      const int pr = (c / 3) % 3, piece = c % 3;
-      if (piece < PIECES && pr >= p0 && pr < p1) glds16(src + 64 * c + lane, sUF + 64 * c);
+    for (int cc = wave; cc < UL::CHUNKS; cc += 4) {
+      const int side = cc / (UL::NPR * UL::NPC), pr = (cc / UL::NPC) % UL::NPR, piece = cc % UL::NPC;
+      const int c = (side * 3 + pr) * 3 + piece;  // chunk of the tile's full image (tile_fragments)
+      if (piece < PIECES && pr >= p0 && pr < p1) glds16(src + 64 * c + lane, sUF + 64 * cc);
     }
     stage_wait();
     __syncthreads();
   }
   if constexpr (!DEPTH)
-    bwd_item_bf16<false, false, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sUF);
+    bwd_item_bf16<false, false, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF);
   else if (tail)
-    bwd_item_bf16<true, true, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sUF);
+    bwd_item_bf16<true, true, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF);
   else
-    bwd_item_bf16<false, true, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, sZ, sUF);
+    bwd_item_bf16<false, true, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3434,6 +3456,7 @@ gr_status gr_fwd_prepare_views_async(int num_views, const gr_view* views, int n,
     all_mapped = all_mapped && hp.p[k];
   }
   const int blocks = blocks_for(n + 1);
+  for (int rep = 0; rep < GR_DEBUG_PREP_REPS; ++rep) {  // > 1: timing experiments only (idempotent repeats)
   if (color_dim == 3)
     hipLaunchKernelGGL(k_preprocess_views<3>, dim3(blocks), dim3(256), 0, s, B, n, means, scales, colors, opacities);
   else if (color_dim == 12)
@@ -3445,6 +3468,7 @@ gr_status gr_fwd_prepare_views_async(int num_views, const gr_view* views, int n,
   GR_HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_offsets_views, dim3(blocks_for(n), num_views), dim3(256), 0, s, B, n);
   GR_HIP_TRY(hipGetLastError());
+  }
   if (!all_mapped)
     for (int k = 0; k < num_views; ++k)
       if (!hp.p[k]) GR_HIP_TRY(hipMemcpyAsync(plans[k], B.g[k].plan, sizeof(gr_plan), hipMemcpyDeviceToHost, s));
@@ -3595,8 +3619,10 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
   Bins b = bins_view(bins, vtiles, num_pairs);
   Scratch sc = scratch_view(scratch, vtiles, num_pairs);
   if (!v->binned) {
-    st = bin_impl(v, n, plan, geom, b, sc, vk, s);
-    if (st != GR_OK) return st;
+    for (int rep = 0; rep < GR_DEBUG_BIN_REPS; ++rep) {  // > 1: timing experiments only (idempotent repeats)
+      st = bin_impl(v, n, plan, geom, b, sc, vk, s);
+      if (st != GR_OK) return st;
+    }
   }
   Geom g = geom_view((void*)geom, n > 0 ? n : 1);
   const size_t HW = (size_t)v->width * v->height;
