@@ -49,6 +49,13 @@
 // 4 gather, 8 chain-rule reduction, 16 parameter update.  Results of such a build are wrong; the product
 // build has 0.  GR_DEBUG_BIN_REPS / GR_DEBUG_PREP_REPS > 1 repeat a view's binning / a group's
 // preparation (idempotent: same results) to measure their marginal cost the other way round.
+// Tail pairs (the zone between the core and the outer cutoff, where a Gaussian's weight is below
+// o * exp(-core^2/2)) carry only W and D.  GR_TAIL2 = 1: their forward and backward contractions use two
+// pieces per operand (three products) in every precision mode; their terms are at most e^-15 of the
+// Gaussian's peak, so the split's ~2^-16 relative error is far below the f32 grade the core keeps.
+#ifndef GR_TAIL2
+#define GR_TAIL2 1
+#endif
 #ifndef GR_DEBUG_PREP_REPS
 #define GR_DEBUG_PREP_REPS 1
 #endif
@@ -1890,8 +1897,8 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
   f32x4 cW = {0.f, 0.f, 0.f, 0.f}, cR = cW, cG = cW, cB = cW, cD = cW;
   constexpr bool PREC = MODE == 1 || MODE == 5, ZCHK = MODE < 3, F16K = GR_FWD_F16 && (MODE == 3 || MODE == 4);
   const int sa = F16K ? *f16_sa : GR_F16_SA;  // the view's A pre-scale (f16_sa_of)
-  if (it.x & 1)
-    fwd_accumulate_bf16<true, PREC, ZCHK>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD, (float)sa);
+  if (it.x & 1)  // tail items: W and D only, two-piece splits (GR_TAIL2)
+    fwd_accumulate_bf16<true, PREC && !GR_TAIL2, ZCHK>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD, (float)sa);
   else
     fwd_accumulate_bf16<false, PREC, ZCHK>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD, (float)sa);
   if constexpr (F16K) {  // the operands carried 2^sa and 2^SB (exact power-of-two rescale)
@@ -2280,8 +2287,8 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
   }
   if constexpr (!DEPTH)
     bwd_item_bf16<false, false, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF);
-  else if (tail)
-    bwd_item_bf16<true, true, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF);
+  else if (tail)  // the tail's depth-coupled pair on two-piece operands (GR_TAIL2)
+    bwd_item_bf16<true, true, GR_TAIL2 ? 2 : PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF);
   else
     bwd_item_bf16<false, true, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF);
 }
