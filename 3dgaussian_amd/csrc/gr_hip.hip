@@ -2052,7 +2052,7 @@ template <bool TAIL, bool DEPTH, int PIECES>
 __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, int wave, int tx, int ty,
                                               const int* __restrict__ pairs, const float4* __restrict__ rec,
                                               float* __restrict__ partials, float4 (*sA)[TP], float4 (*sB)[TP],
-                                              float* sZ, const uint4* sUF) {
+                                              float* sZ, const uint4* sUF, float* __restrict__ depth3) {
   using UL = UFLayout<DEPTH, PIECES>;
   static_assert(DEPTH || !TAIL, "tail items carry only depth-coupled terms");
   constexpr int P0 = TAIL ? 2 : 0;      // first channel pair contracted
@@ -2227,16 +2227,15 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
           reinterpret_cast<float4*>(partials)[2 * (size_t)myslot + h] =
               h == 0 ? make_float4(b.x * Pa, b.x * Pb, Pc, Pd) : make_float4(b.x * Pa, Pb, Pc, Pd);
       } else {
-        // half 0 ends with the totals of S0, S2, S4, S6, S8, half 1 with S1, S3, S5, S7 (9-float rows)
+        // half 0 ends with the totals of S0, S2, S4, S6, S8, half 1 with S1, S3, S5, S7, S8: the same
+        // 32-byte rows as without a depth gradient (float4 h of the row), the depth sum o S3 in its own
+        // array behind the rows (depth3[slot]), so the gather reads aligned rows either way
         const float P01 = pair32(S[0], S[1]), P23 = pair32(S[2], S[3]), P45 = pair32(S[4], S[5]);
         const float P67 = pair32(S[6], S[7]), P8 = pair32(S[8], S[8]);
-        if (myslot >= 0) {
-          float* dst = partials + (size_t)myslot * NPART + h;
-          dst[0] = b.x * P01;  // colour / depth sums carry the opacity
-          dst[2] = b.x * P23;
-          dst[4] = P45;
-          dst[6] = P67;
-          if (h == 0) dst[8] = P8;
+        if (myslot >= 0) {  // colour / depth sums carry the opacity
+          reinterpret_cast<float4*>(partials)[2 * (size_t)myslot + h] =
+              h == 0 ? make_float4(b.x * P01, b.x * P23, P45, P67) : make_float4(b.x * P01, P8, P45, P67);
+          if (h == 1) depth3[myslot] = b.x * P23;
         }
       }
     }
@@ -2259,7 +2258,7 @@ template <bool DEPTH, int PIECES>
 __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void k_raster_bwd_bf16(ViewK v, int n, const int4* __restrict__ items,
                                                            const int* __restrict__ num_items, const int* __restrict__ pairs,
                                                            const float4* __restrict__ rec, const uint4* __restrict__ UF,
-                                                           float* __restrict__ partials) {
+                                                           float* __restrict__ partials, float* __restrict__ depth3) {
   using UL = UFLayout<DEPTH, PIECES>;
   __shared__ __attribute__((aligned(16))) float4 sA[2][TP];
   __shared__ __attribute__((aligned(16))) float4 sB[2][TP];
@@ -2286,11 +2285,11 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
     __syncthreads();
   }
   if constexpr (!DEPTH)
-    bwd_item_bf16<false, false, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF);
+    bwd_item_bf16<false, false, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF, depth3);
   else if (tail)  // the tail's depth-coupled pair on two-piece operands (GR_TAIL2)
-    bwd_item_bf16<true, true, GR_TAIL2 ? 2 : PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF);
+    bwd_item_bf16<true, true, GR_TAIL2 ? 2 : PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF, depth3);
   else
-    bwd_item_bf16<false, true, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF);
+    bwd_item_bf16<false, true, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF, depth3);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2629,13 +2628,20 @@ __device__ __forceinline__ void add4(float4& x, const float4 a) {
 }
 // One row in flight per lane with the next row's position prefetched: ~26 VGPRs, so a wave fits in what
 // the splat kernels leave of a SIMD's registers (backward 4 x 120, forward 6 x 80 of 512).
+// DEPTH (an upstream depth gradient: tail pairs were contracted too): lane q also sums the Gaussian's
+// tail pairs q, q+4, ... after its core pairs, and the depth sums o S3 (depth3, by sorted position) of
+// both, written to sums3[i].
+template <bool DEPTH>
 __global__ __launch_bounds__(256) void k_gather_view(int n, const Cnt2* __restrict__ offsets, const int* __restrict__ pos_of,
-                                                     const float4* __restrict__ rows, float2* __restrict__ sums) {
+                                                     const float4* __restrict__ rows, float2* __restrict__ sums,
+                                                     const float* __restrict__ depth3, float* __restrict__ sums3) {
   const int tid = threadIdx.x, q4 = tid & 3;
   const int i = blockIdx.x * 64 + (tid >> 2);
   float4 x = {-0.f, -0.f, -0.f, -0.f}, y = x;
+  float z3 = -0.f;
   if (i < n) {
-    const unsigned a = offsets[i].c(), cc = offsets[i + 1].c() - a;
+    const Cnt2 o0 = offsets[i], o1 = offsets[i + 1];
+    const unsigned a = o0.c(), cc = o1.c() - a;
     const int* pc = pos_of + a;
     unsigned j = q4;
     int p = j < cc ? pc[j] : 0;
@@ -2643,8 +2649,24 @@ __global__ __launch_bounds__(256) void k_gather_view(int n, const Cnt2* __restri
       const int pn = j + 4 < cc ? pc[j + 4] : 0;
       add4(x, rows[2 * (size_t)p]);
       add4(y, rows[2 * (size_t)p + 1]);
+      if constexpr (DEPTH) z3 += depth3[p];
       p = pn;
     }
+    if constexpr (DEPTH) {
+      const unsigned tc = o1.t() - o0.t();
+      const int* pt = pos_of + (size_t)offsets[n].c() + o0.t();
+      for (j = q4; j < tc; j += 4) {
+        const int pp = pt[j];
+        add4(x, rows[2 * (size_t)pp]);
+        add4(y, rows[2 * (size_t)pp + 1]);
+        z3 += depth3[pp];
+      }
+    }
+  }
+  if constexpr (DEPTH) {
+    z3 += quad_xor1(z3);
+    z3 += quad_xor2(z3);
+    if (i < n && q4 == 0) sums3[i] = z3;
   }
   x.x += quad_xor1(x.x); x.y += quad_xor1(x.y); x.z += quad_xor1(x.z); x.w += quad_xor1(x.w);
   y.x += quad_xor1(y.x); y.y += quad_xor1(y.y); y.z += quad_xor1(y.z); y.w += quad_xor1(y.w);
@@ -2666,6 +2688,7 @@ __global__ __launch_bounds__(256) void k_gather_view(int n, const Cnt2* __restri
 struct SViewK {
   ViewK v;
   const float4* sums;  // [n][2]: k_gather_view's output
+  const float* sums3;  // [n] depth sums o S3 (k_gather_view<true>), or null (no depth gradient: S3 = 0)
 };
 struct SBatch {
   int nv;
@@ -2691,9 +2714,10 @@ __global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const floa
     for (int vi = u; vi < B.nv; vi += crw) {
       const float4 a = B.r[vi].sums[2 * (size_t)gi], b = B.r[vi].sums[2 * (size_t)gi + 1];
       // [o S0, o S2, S4, S6 | o S1, S8, S5, S7] -> S0..S8 (S3, the depth sum, is 0 without a depth gradient)
-      const float Sf[NPART] = {a.x, b.x, a.y, 0.0f, a.z, b.z, a.w, b.w, b.y};
+      const float s3 = B.r[vi].sums3 ? B.r[vi].sums3[gi] : 0.0f;
+      const float Sf[NPART] = {a.x, b.x, a.y, s3, a.z, b.z, a.w, b.w, b.y};
       const unsigned on = (a.x != 0.f || a.y != 0.f || a.z != 0.f || a.w != 0.f || b.x != 0.f || b.y != 0.f ||
-                           b.z != 0.f || b.w != 0.f) ? 1u : 0u;
+                           b.z != 0.f || b.w != 0.f || s3 != 0.f) ? 1u : 0u;
       chain_rule<CD, float>(B.r[vi].v, gi, Sf, on, means, scales, colors, opac, gr);
     }
   }
@@ -3258,7 +3282,8 @@ size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan) {
   return align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)) + align_up(tiles * per_tile) +
          align_up(tiles * 4 * sizeof(float)) + align_up(tiles * 2 * sizeof(float)) +
          align_up(4 * sizeof(float)) +  // per-tile loss sums, per-tile depth max / arg-max counts, depth scalars
-         align_up((size_t)8 * (n > 0 ? n : 1) * sizeof(float));  // per-Gaussian row sums (gather + chain rule)
+         align_up((size_t)8 * (n > 0 ? n : 1) * sizeof(float)) +  // per-Gaussian row sums (gather + chain rule)
+         align_up((size_t)(n > 0 ? n : 1) * sizeof(float));       // and depth sums
 }
 
 // Decode the scanned totals (core, tail pairs) into the plan; a count that does not fit int32 is
@@ -3507,9 +3532,10 @@ struct BwdWs {
   float* tile_loss;  // [tiles][4]
   float* tile_aux;   // [tiles][2]: depth max, arg-max pixels (gr_bwd_fit)
   float* dscal;      // [4]: max(depth), the max's gradient per arg-max pixel
-  float* sums;       // [n][8]: per-Gaussian row sums (k_gather_view) of a backward without a depth gradient
+  float* sums;       // [n][8]: per-Gaussian row sums (k_gather_view)
+  float* sums3;      // [n]: per-Gaussian depth sums (k_gather_view<true>, with an upstream depth gradient)
 };
-static BwdWs bwd_ws(const gr_view* v, const gr_plan* plan, void* ws) {
+static BwdWs bwd_ws(const gr_view* v, int n, const gr_plan* plan, void* ws) {
   const size_t tiles = (size_t)tiles_x_of(v->width) * tiles_y_of(v->height);
   BwdWs w;
   w.partials = (float*)ws;
@@ -3518,6 +3544,7 @@ static BwdWs bwd_ws(const gr_view* v, const gr_plan* plan, void* ws) {
   w.tile_aux = (float*)((char*)w.tile_loss + align_up(tiles * 4 * sizeof(float)));
   w.dscal = (float*)((char*)w.tile_aux + align_up(tiles * 2 * sizeof(float)));
   w.sums = (float*)((char*)w.dscal + align_up(4 * sizeof(float)));
+  w.sums3 = (float*)((char*)w.sums + align_up((size_t)8 * (n > 0 ? n : 1) * sizeof(float)));
   return w;
 }
 
@@ -3637,7 +3664,7 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
   L1Args la{nullptr, nullptr, 0.f, 0.f, nullptr};
   uint4* UF = nullptr;
   if (l1) {
-    const BwdWs w = bwd_ws(v, plan, ws);
+    const BwdWs w = bwd_ws(v, n, plan, ws);
     la = *l1;
     la.tile_loss = w.tile_loss;
     UF = w.UF;
@@ -3735,7 +3762,7 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
   Geom g = geom_view((void*)geom, n);
   Bins b = bins_view((void*)bins, 2 * tiles, num_pairs);
   const size_t HW = (size_t)v->width * v->height;
-  const BwdWs w = bwd_ws(v, plan, ws);
+  const BwdWs w = bwd_ws(v, n, plan, ws);
   float* partials = w.partials;
   uint4* UF = w.UF;
   float* tile_loss = w.tile_loss;
@@ -3775,21 +3802,29 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
     prof_mark(PROF_RASTER_BWD, s);
     auto kern = depth ? k_raster_bwd_bf16<true, 3> : (pieces == 2 ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>);
     hipLaunchKernelGGL(kern, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items,
-                       (const int*)b.pairs, (const float4*)g.rec, (const uint4*)UF, partials);
+                       (const int*)b.pairs, (const float4*)g.rec, (const uint4*)UF, partials,
+                       partials + 8 * (size_t)plan->num_slots);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_BWD, s);
   }
   prof_mark(PROF_REDUCE, s);
-  if (!depth && num_pairs > 0) {
-    // 8-float rows: the lean gather into per-Gaussian sums, then the chain rule of that one view (the two
-    // stages of gr_gather_view + gr_reduce_sums; k_reduce_bwd's one pass needs 117 VGPRs for the chain rule
-    // while it gathers)
-    hipLaunchKernelGGL(k_gather_view, dim3((n + 63) / 64), dim3(256), 0, s, n, (const Cnt2*)g.offsets, (const int*)b.pos_of,
-                       (const float4*)partials, (float2*)w.sums);
+  if (num_pairs > 0) {
+    // 32-byte rows: the lean gather into per-Gaussian sums (with a depth gradient also the tail pairs and
+    // the depth sums), then the chain rule of that one view (the two stages of gr_gather_view +
+    // gr_reduce_sums; k_reduce_bwd's one pass needs 117 VGPRs for the chain rule while it gathers)
+    float* depth3 = partials + 8 * (size_t)plan->num_slots;
+    if (depth)
+      hipLaunchKernelGGL(k_gather_view<true>, dim3((n + 63) / 64), dim3(256), 0, s, n, (const Cnt2*)g.offsets,
+                         (const int*)b.pos_of, (const float4*)partials, (float2*)w.sums, (const float*)depth3, w.sums3);
+    else
+      hipLaunchKernelGGL(k_gather_view<false>, dim3((n + 63) / 64), dim3(256), 0, s, n, (const Cnt2*)g.offsets,
+                         (const int*)b.pos_of, (const float4*)partials, (float2*)w.sums, (const float*)nullptr,
+                         (float*)nullptr);
     SBatch B;
     B.nv = 1;
     B.r[0].v = vk;
     B.r[0].sums = (const float4*)w.sums;
+    B.r[0].sums3 = depth ? w.sums3 : nullptr;
     const int gpb = 64 * (4 / reduce_sums_crw(1, color_dim));
     const dim3 grid((n + gpb - 1) / gpb), block(256);
     if (color_dim == 3)
@@ -3870,13 +3905,13 @@ gr_status gr_bwd_splat(const gr_view* v, int n, const gr_plan* plan, const void*
   const int tiles = vk.tiles_x * vk.tiles_y;
   const Geom g = geom_view((void*)geom, n);
   const Bins b = bins_view((void*)bins, 2 * tiles, plan->num_pairs);
-  const BwdWs w = bwd_ws(v, plan, ws);
+  const BwdWs w = bwd_ws(v, n, plan, ws);
   const int64_t cap = item_cap(2 * tiles, plan->num_pairs);
   if (GR_DEBUG_SKIP & 2) return GR_OK;
   prof_mark(PROF_RASTER_BWD, s);
   hipLaunchKernelGGL((v->no_depth_grad == 1 ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>), dim3((unsigned)cap),
                      dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items, (const int*)b.pairs,
-                     (const float4*)g.rec, (const uint4*)w.UF, w.partials);
+                     (const float4*)g.rec, (const uint4*)w.UF, w.partials, (float*)nullptr);
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_RASTER_BWD, s);
   return GR_OK;
@@ -3954,8 +3989,8 @@ gr_status gr_gather_view(const gr_view* v, int n, const gr_plan* plan, const voi
   const Bins b = bins_view((void*)bins, 2 * vk.tiles_x * vk.tiles_y, plan->num_pairs);
   if (GR_DEBUG_SKIP & 4) return GR_OK;
   prof_mark(PROF_REDUCE, s);
-  hipLaunchKernelGGL(k_gather_view, dim3((n + 63) / 64), dim3(256), 0, s, n, (const Cnt2*)g.offsets, (const int*)b.pos_of,
-                     (const float4*)ws, (float2*)sums);
+  hipLaunchKernelGGL(k_gather_view<false>, dim3((n + 63) / 64), dim3(256), 0, s, n, (const Cnt2*)g.offsets,
+                     (const int*)b.pos_of, (const float4*)ws, (float2*)sums, (const float*)nullptr, (float*)nullptr);
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_REDUCE, s);
   return GR_OK;
@@ -3981,6 +4016,7 @@ gr_status gr_reduce_sums(int num_views, const gr_sums_view* views, int n, const 
     if (!views[k].sums) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_reduce_sums: null sums");
     B.r[k].v = make_viewk(&views[k].view);
     B.r[k].sums = (const float4*)views[k].sums;
+    B.r[k].sums3 = nullptr;
   }
   hipStream_t s = (hipStream_t)stream;
   if (GR_DEBUG_SKIP & 8) return GR_OK;
