@@ -83,8 +83,12 @@ PREP_FIRST = max(1, min(PREP_GROUP, int(os.environ.get("GR_PREP_FIRST", "1"))))
 # (gr_reduce_sums).  0 = the one-pass gr_reduce_views over the batch's kept workspaces.
 GATHER = os.environ.get("GR_GATHER", "1") != "0"
 # the fused paths' per-view schedule as native host code (gr_fit_views, csrc/gr_fit_exec.cpp: the same streams,
-# preparation groups and reduction batches, bit-identical results); 0 = the Python schedule below
-NATIVE_EXEC = os.environ.get("GR_NATIVE_EXEC", "0") != "0"
+# preparation groups and reduction batches, bit-identical results); 0 = the Python schedule below, 1 = always,
+# auto (default) = for views of at most NATIVE_EXEC_MAX_PIXELS, where the per-view GPU work is short enough for the
+# host's per-view enqueue time to show (C2, 8 views 512x512: 1.33 -> 1.10 ms per step; at 800x800 the step is
+# GPU-bound and the Python schedule is level or 1-2% ahead: profiles/r03_ab_native_exec.txt)
+NATIVE_EXEC = os.environ.get("GR_NATIVE_EXEC", "auto")
+NATIVE_EXEC_MAX_PIXELS = 512 * 512
 # the native executor on this driver's torch streams (1) or on streams of its own (0)
 EXEC_STREAMS = os.environ.get("GR_EXEC_STREAMS", "1") != "0"
 # priority of the preparation stream (torch's convention: 0 normal, -1 high).  HIP keeps one pool of hardware
@@ -450,7 +454,7 @@ class ViewShardedFitter:
                 reg_fn = ((lambda: self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean())
                           if self.rank == 0 else None)
                 reg = None
-                if NATIVE_EXEC and GATHER:
+                if self._native_exec() and GATHER:
                     reg = reg_fn() if reg_fn else None
                     total = self._views_native(means, scales, colors, opacities, self._depth_grad())
                 elif self._depth_grad():
@@ -544,6 +548,12 @@ class ViewShardedFitter:
             loss = loss + self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean()
         loss.backward()
         return self._finish_step(loss)
+
+    def _native_exec(self) -> bool:
+        """Whether this step's views go through the native executor (GR_NATIVE_EXEC)."""
+        if NATIVE_EXEC == "auto":
+            return self.width * self.height <= NATIVE_EXEC_MAX_PIXELS
+        return str(NATIVE_EXEC) not in ("0", "False", "")
 
     def _views_native(self, means, scales, colors, opacities, depth: bool) -> torch.Tensor:
         """_views_direct / _views_direct_depth through the native executor (gr_fit_views): one C call per

@@ -26,12 +26,15 @@ def test_native_executor_matches_python_schedule(cuda, streams, depth):
     saved = fm.NATIVE_EXEC, fm.NUM_STREAMS
     try:
         for native in (False, True):
-            fm.NATIVE_EXEC, fm.NUM_STREAMS = native, streams
+            fm.NATIVE_EXEC, fm.NUM_STREAMS = ("1" if native else "0"), streams
             f = fm.ViewShardedFitter(bench.synthetic_params(50_000, cuda), cams, targets, W, H, masks=masks, depths=depths)
             losses = [float(f.step()) for _ in range(2)]
             res[native] = (losses, {k: v.detach().clone() for k, v in f.params.items()})
     finally:
         fm.NATIVE_EXEC, fm.NUM_STREAMS = saved
     assert res[True][0] == res[False][0]
+    # the default ("auto") takes the native executor for views this small
+    f = fm.ViewShardedFitter(bench.synthetic_params(1000, cuda), cams, targets, W, H)
+    assert fm.NATIVE_EXEC != "auto" or f._native_exec()
     for k in res[False][1]:
         assert torch.equal(res[True][1][k], res[False][1][k]), k
