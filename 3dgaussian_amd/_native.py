@@ -68,6 +68,7 @@ class GrPlan(ctypes.Structure):
     _fields_ = [("num_pairs", ctypes.c_int64), ("num_slots", ctypes.c_int64), ("num_core_pairs", ctypes.c_int64)]
 
 
+CAMERA_GRADS = 35  # GR_CAMERA_GRADS: d view (16), d proj (16), d cam_pos (3)
 REDUCE_MAX_VIEWS = 16  # GR_REDUCE_MAX_VIEWS
 PREPARE_MAX_VIEWS = 4  # GR_PREPARE_MAX_VIEWS
 
@@ -124,6 +125,8 @@ _SIG = {
     "gr_bwd_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
     "gr_bwd": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, _P, _P, _P, ctypes.c_size_t, _P]),
+    "gr_bwd_camera": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, ctypes.c_size_t, ctypes.c_int,
+                                     _P, _P]),
     "gr_bwd_l1": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P,
                                  ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, ctypes.c_int, _P, ctypes.c_size_t,
                                  _P]),

@@ -114,6 +114,16 @@ struct gr_executor {
     if (s_ != GR_OK) return s_;     \
   } while (0)
 
+static gr_status fit_views_on_device(gr_executor* ex, const gr_fit_config* cfg, int num_views, const gr_fit_target* views,
+                                     int n, const float* means, const float* scales, const float* colors, int color_dim,
+                                     const float* opacities, float w_sil, float w_depth, float g_scale, float* losses,
+                                     float* const* acc, void* stream);
+static gr_status enqueue_views(gr_executor* ex, const gr_fit_config* cfg, int num_views, const gr_fit_target* views, int n,
+                               const float* means, const float* scales, const float* colors, int color_dim,
+                               const float* opacities, float w_sil, float w_depth, float g_scale, float* losses,
+                               float* const* acc, const Sched& sc, const std::vector<hipStream_t>& st, hipStream_t prep,
+                               bool depth, int nslots, int& ngroups);
+
 extern "C" {
 
 gr_status gr_executor_create(int device, gr_executor** out) {
@@ -169,8 +179,11 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
                        float* const* acc, void* stream) {
   if (!ex || !cfg || (num_views > 0 && (!views || !losses || !acc)))
     return gr_exec_set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views: null argument");
+  // every batch of a stream (its last one holds reduce_tail views) and every preparation group must fit the
+  // fixed-size view arrays of gr_reduce_sums / gr_fwd_prepare_views_async (and the per-stream sums ring)
   if (cfg->num_streams < 1 || cfg->prep_ahead < 1 || cfg->prep_group < 1 || cfg->prep_group > GR_PREPARE_MAX_VIEWS ||
-      cfg->prep_first < 1 || cfg->reduce_batch < 1 || cfg->reduce_batch > GR_REDUCE_MAX_VIEWS || cfg->reduce_tail < 0)
+      cfg->prep_first < 1 || cfg->prep_first > GR_PREPARE_MAX_VIEWS || cfg->reduce_batch < 1 ||
+      cfg->reduce_batch > GR_REDUCE_MAX_VIEWS || cfg->reduce_tail < 0 || cfg->reduce_tail > cfg->reduce_batch)
     return gr_exec_set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views: configuration out of range");
   if (num_views == 0 || n <= 0) return GR_OK;
   const bool depth = views[0].target_depth != nullptr;  // the depth-loss path (one form per call)
@@ -179,6 +192,23 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
       return gr_exec_set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views: every view or none has a depth target");
     if (!views[j].target_rgb) return gr_exec_set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views: null target");
   }
+  // the executor's streams, events and buffers belong to its device: make it current for this call
+  int prev_dev = 0;
+  GR_EXEC_TRY(hipGetDevice(&prev_dev));
+  GR_EXEC_TRY(hipSetDevice(ex->device));
+  const gr_status st = fit_views_on_device(ex, cfg, num_views, views, n, means, scales, colors, color_dim, opacities, w_sil,
+                                           w_depth, g_scale, losses, acc, stream);
+  (void)hipSetDevice(prev_dev);
+  return st;
+}
+
+}  // extern "C"
+
+static gr_status fit_views_on_device(gr_executor* ex, const gr_fit_config* cfg, int num_views, const gr_fit_target* views,
+                                     int n, const float* means, const float* scales, const float* colors, int color_dim,
+                                     const float* opacities, float w_sil, float w_depth, float g_scale, float* losses,
+                                     float* const* acc, void* stream) {
+  const bool depth = views[0].target_depth != nullptr;
   const Sched sc = schedule(num_views, *cfg);
   const int ns = sc.ns;
   for (int k = 0; k < ns; ++k)
@@ -227,9 +257,9 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
   }
   if (!cfg->prep_stream && !ex->prep) GR_EXEC_TRY(hipStreamCreateWithFlags(&ex->prep, hipStreamNonBlocking));
   const hipStream_t prep = cfg->prep_stream ? (hipStream_t)cfg->prep_stream : ex->prep;
-  // the workspaces of stream k and the geom slots were last used on the previous call's streams: when the
-  // streams change, those finish first
-  std::vector<hipStream_t> now(st.begin() + 1, st.end());
+  // the workspaces of every render stream (stream 0's on the caller's stream) and the geom slots were last used on
+  // the previous call's streams: when any of them changes, those finish first
+  std::vector<hipStream_t> now(st.begin(), st.end());
   now.push_back(prep);
   if (!ex->last.empty() && ex->last != now)
     for (hipStream_t s : ex->last) GR_EXEC_TRY(hipStreamSynchronize(s));
@@ -238,12 +268,33 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
   GR_EXEC_TRY(hipEventRecord(ex->in, main));
   GR_EXEC_TRY(hipStreamWaitEvent(prep, ex->in, 0));
   for (int k = 1; k < ns; ++k) GR_EXEC_TRY(hipStreamWaitEvent(st[k], ex->in, 0));
+  // From here work is enqueued on the executor's streams: whatever happens below, the caller's stream is ordered
+  // after all of it before this returns (an error part-way must not let the caller free buffers still in use).
+  int ngroups = 0;
+  auto join = [&]() {
+    for (int k = 1; k < ns; ++k)
+      if (hipEventRecord(ex->done[k - 1], st[k]) != hipSuccess || hipStreamWaitEvent(main, ex->done[k - 1], 0) != hipSuccess)
+        (void)hipStreamSynchronize(st[k]);
+    if (hipEventRecord(ex->groups[ngroups], prep) != hipSuccess || hipStreamWaitEvent(main, ex->groups[ngroups], 0) != hipSuccess)
+      (void)hipStreamSynchronize(prep);
+  };
+  const gr_status status = enqueue_views(ex, cfg, num_views, views, n, means, scales, colors, color_dim, opacities, w_sil,
+                                         w_depth, g_scale, losses, acc, sc, st, prep, depth, nslots, ngroups);
+  join();
+  return status;
+}
 
+static gr_status enqueue_views(gr_executor* ex, const gr_fit_config* cfg, int num_views, const gr_fit_target* views, int n,
+                               const float* means, const float* scales, const float* colors, int color_dim,
+                               const float* opacities, float w_sil, float w_depth, float g_scale, float* losses,
+                               float* const* acc, const Sched& sc, const std::vector<hipStream_t>& st, hipStream_t prep,
+                               bool depth, int nslots, int& ngroups) {
+  const int ns = sc.ns;
   const size_t geom_bytes = gr_geom_bytes(n);
   std::vector<void*> geom(num_views, nullptr);
   std::vector<int> slot_of(num_views, -1);
   std::vector<int> group_of(num_views, -1);
-  int ngroups = 0, next_prep = 0;
+  int next_prep = 0;
   auto prepare_upto = [&](int j) -> gr_status {  // views [next_prep, j] prepared (whole groups)
     while (next_prep < num_views && next_prep <= j) {
       const int g0 = next_prep, cnt = std::min(num_views - g0, g0 == 0 ? cfg->prep_first : cfg->prep_group);
@@ -349,14 +400,5 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
     }
   }
   for (int k = 0; k < ns; ++k) GR_EXEC_CALL(reduce_pending(k));
-  // the caller's stream waits for every render stream and for the preparation stream
-  for (int k = 1; k < ns; ++k) {
-    GR_EXEC_TRY(hipEventRecord(ex->done[k - 1], st[k]));
-    GR_EXEC_TRY(hipStreamWaitEvent(main, ex->done[k - 1], 0));
-  }
-  GR_EXEC_TRY(hipEventRecord(ex->groups[ngroups], prep));
-  GR_EXEC_TRY(hipStreamWaitEvent(main, ex->groups[ngroups], 0));
-  return GR_OK;
+  return GR_OK;  // the caller joins the streams (fit_views_on_device)
 }
-
-}  // extern "C"

@@ -1342,7 +1342,9 @@ __device__ __forceinline__ void split3_frag2(const f32x2_t (&v)[4], s16x8 (&f)[3
 // The A pre-scale of a view: 2^GR_F16_SA while its largest opacity (of a kept Gaussian) is below 2^11,
 // lowered by one per binade above, so o * c * ex * 2^sa <= 2^15 always (no inf, whatever the opacities;
 // k_plan computes it from k_preprocess's per-block maxima).  Views with opacities in (0, 2048) - every
-// fit, whose opacities are sigmoid outputs - get exactly GR_F16_SA.
+// fit, whose opacities are sigmoid outputs - get exactly GR_F16_SA.  The A operands are o c ex with o = max(op, 0)
+// (the record's clamp, torch_renderer.py:177) and c clamped to [0, 1] (:144), so |A| <= 2^sa max(op, 0): a negative
+// opacity contributes nothing and needs no range (tests/test_scale_gpu.py, opacities down to -1e5).
 __device__ __forceinline__ int f16_sa_of(float omax) {
   if (!(omax <= 3.0e38f)) return GR_F16_SA;  // inf / NaN opacities give inf / NaN outputs in any precision
   int e = 0;
@@ -2761,6 +2763,90 @@ __global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const floa
   for (int q = 0; q < CD; ++q) out.color(q, gr.c[q]);
 }
 
+// The projection half of the chain rule (torch_renderer.py:57-78, 146-150) from a Gaussian's sums S (SURVEY.md
+// App. A): the gradients of its clamped sigmas, of its camera-space point pc and of its clip-space point (shared
+// by chain_rule and the camera gradient, k_camera_grad).
+template <typename F>
+struct ProjGrad {
+  F dsx, dsy;   // d L / d sigma_x, sigma_y (zero where the clamp at 1 is active)
+  F dpc[4];     // d L / d pc (through the clip point, and through z_abs into the depth and the sigmas)
+  F dclip[4];   // d L / d clip
+};
+template <typename F>
+__device__ __forceinline__ void proj_grads(const ViewK& v, const Proj& p, F o, const F* S, ProjGrad<F>& g) {
+  const F sx = p.sx, sy = p.sy;
+  // ge = o * gw * E  ->  sums over ge carry a factor o.
+  const F dpx = o * S[5] / (sx * sx), dpy = o * S[6] / (sy * sy);
+  F dsx = o * S[7] / (sx * sx * sx), dsy = o * S[8] / (sy * sy * sy);
+  if (!(p.sxr >= 1.0f)) dsx = F(0);
+  if (!(p.syr >= 1.0f)) dsy = F(0);
+  g.dsx = dsx;
+  g.dsy = dsy;
+  const F dza = S[3] - dsx * p.sxr / p.za - dsy * p.syr / p.za;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) g.dpc[j] = F(0);
+  if (fabsf(p.pc[2]) >= 1e-6f) g.dpc[2] += dza * (p.pc[2] > 0.f ? F(1) : (p.pc[2] < 0.f ? F(-1) : F(0)));
+  const F dndx = dpx * F(0.5) * (v.W - 1);
+  const F dndy = -dpy * F(0.5) * (v.H - 1);
+  g.dclip[0] = dndx / p.ws;
+  g.dclip[1] = dndy / p.ws;
+  g.dclip[2] = F(0);
+  g.dclip[3] = (fabsf(p.clip[3]) < 1e-8f) ? F(0) : -(dndx * p.clip[0] + dndy * p.clip[1]) / ((F)p.ws * p.ws);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) g.dpc[j] += (F)v.P[r * 4 + j] * g.dclip[r];
+}
+
+// The colour half (torch_renderer.py:86-106, 144): d L / d colour before the clamp (inclusive clamp mask), and
+// for SH colours d L / d (cam - m) of the view direction (gd: through the normalisation; zero for RGB).
+template <int CD, typename F>
+struct ColGrad {
+  F dcol[3];
+  F d[3];    // unit view direction (SH)
+  F dd[3];   // d L / d (cam - m)
+};
+template <int CD, typename F>
+__device__ __forceinline__ void color_grads(const ViewK& v, float mx, float my, float mz, const float* __restrict__ col,
+                                            const F* S, ColGrad<CD, F>& c) {
+  float cpre[3];
+  eval_color<CD>(v, mx, my, mz, col, cpre);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) c.dcol[k] = (cpre[k] >= 0.0f && cpre[k] <= 1.0f) ? S[k] : F(0);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) c.dd[j] = F(0);
+  if constexpr (CD != 3) {
+    const F vv[3] = {(F)v.cam[0] - mx, (F)v.cam[1] - my, (F)v.cam[2] - mz};
+    const F nn = std::sqrt(vv[0] * vv[0] + vv[1] * vv[1] + vv[2] * vv[2]);
+    const F ne = nn + F(1e-8);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) c.d[j] = vv[j] / ne;
+    F gd[3] = {F(0), F(0), F(0)};
+    if constexpr (CD == 12) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) gd[j] += c.dcol[k] * (F)col[(1 + j) * 3 + k];
+    } else {  // degree 3: d col / d d = sum_i k_i dY_i/dd
+      F G[16][3];
+      sh3_basis_grad(c.d[0], c.d[1], c.d[2], G);
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const F t = c.dcol[k] * (F)col[3 * i + k];
+#pragma unroll
+          for (int j = 0; j < 3; ++j) gd[j] += t * G[i][j];
+        }
+    }
+    if (nn > F(0)) {
+      const F vg = vv[0] * gd[0] + vv[1] * gd[1] + vv[2] * gd[2];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) c.dd[j] = gd[j] / ne - vv[j] * vg / (nn * ne * ne);
+    }
+  }
+}
+
 template <int CD, typename F, typename Out>
 __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, const float* __restrict__ means,
                            const float* __restrict__ scales, const float* __restrict__ colors,
@@ -2776,87 +2862,124 @@ __device__ void chain_rule(const ViewK& v, int i, const F* S, unsigned cnt, cons
   Proj p;
   project(v, mx, my, mz, s0, s1, p);
   const F o = op < 0.0f ? F(0) : (F)op;
-  const F sx = p.sx, sy = p.sy;
-  // ge = o * gw * E  ->  sums over ge carry a factor o.
-  const F dpx = o * S[5] / (sx * sx), dpy = o * S[6] / (sy * sy);
-  F dsx = o * S[7] / (sx * sx * sx), dsy = o * S[8] / (sy * sy * sy);
-  if (!(p.sxr >= 1.0f)) dsx = F(0);
-  if (!(p.syr >= 1.0f)) dsy = F(0);
+  ProjGrad<F> pg;
+  proj_grads<F>(v, p, o, S, pg);
   const F fx = fabsf(v.P[0]), fy = fabsf(v.P[5]);
   const F kx = F(0.5) * v.W * fx / p.za, ky = F(0.5) * v.H * fy / p.za;
   const F sgx = s0 > 0.f ? F(1) : (s0 < 0.f ? F(-1) : F(0));
   const F sgy = s1 > 0.f ? F(1) : (s1 < 0.f ? F(-1) : F(0));
-  out.scale(0, (float)(dsx * kx * sgx));
-  out.scale(1, (float)(dsy * ky * sgy));
+  out.scale(0, (float)(pg.dsx * kx * sgx));
+  out.scale(1, (float)(pg.dsy * ky * sgy));
   out.scale_z();
-  const F dza = S[3] - dsx * p.sxr / p.za - dsy * p.syr / p.za;
-  F dpc[4] = {F(0), F(0), F(0), F(0)};
-  if (fabsf(p.pc[2]) >= 1e-6f) dpc[2] += dza * (p.pc[2] > 0.f ? F(1) : (p.pc[2] < 0.f ? F(-1) : F(0)));
-  const F dndx = dpx * F(0.5) * (v.W - 1);
-  const F dndy = -dpy * F(0.5) * (v.H - 1);
-  F dclip[4];
-  dclip[0] = dndx / p.ws;
-  dclip[1] = dndy / p.ws;
-  dclip[2] = F(0);
-  dclip[3] = (fabsf(p.clip[3]) < 1e-8f) ? F(0) : -(dndx * p.clip[0] + dndy * p.clip[1]) / ((F)p.ws * p.ws);
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) dpc[j] += (F)v.P[r * 4 + j] * dclip[r];
   F dm[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     dm[j] = F(0);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) dm[j] += (F)v.V[r * 4 + j] * dpc[r];
+    for (int r = 0; r < 4; ++r) dm[j] += (F)v.V[r * 4 + j] * pg.dpc[r];
   }
   out.opac((float)((op >= 0.0f) ? S[4] : F(0)));
-  float cpre[3];
-  eval_color<CD>(v, mx, my, mz, col, cpre);
-  F dcol[3];
+  ColGrad<CD, F> cg;
+  color_grads<CD, F>(v, mx, my, mz, col, S, cg);
 #pragma unroll
-  for (int k = 0; k < 3; ++k) dcol[k] = (cpre[k] >= 0.0f && cpre[k] <= 1.0f) ? S[k] : F(0);
-  if constexpr (CD == 3) {
+  for (int k = 0; k < 3; ++k) out.color(k, (float)cg.dcol[k]);
+  if constexpr (CD == 12) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) out.color(k, (float)dcol[k]);
-  } else {
-    const F vv[3] = {(F)v.cam[0] - mx, (F)v.cam[1] - my, (F)v.cam[2] - mz};
-    const F nn = std::sqrt(vv[0] * vv[0] + vv[1] * vv[1] + vv[2] * vv[2]);
-    const F ne = nn + F(1e-8);
-    const F d[3] = {vv[0] / ne, vv[1] / ne, vv[2] / ne};
-    F gd[3] = {F(0), F(0), F(0)};
-    if constexpr (CD == 12) {
+    for (int k = 0; k < 3; ++k)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        out.color(k, (float)dcol[k]);
+      for (int j = 0; j < 3; ++j) out.color((1 + j) * 3 + k, (float)(cg.dcol[k] * cg.d[j]));
+  } else if constexpr (CD == 48) {  // d col / d k_i = Y_i(d)
+    F Y[16];
+    sh3_basis(cg.d[0], cg.d[1], cg.d[2], Y);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          out.color((1 + j) * 3 + k, (float)(dcol[k] * d[j]));
-          gd[j] += dcol[k] * (F)col[(1 + j) * 3 + k];
+    for (int i = 1; i < 16; ++i)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) out.color(3 * i + k, (float)(cg.dcol[k] * Y[i]));
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) out.mean(j, (float)(dm[j] - cg.dd[j]));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Camera gradient (gr_bwd_camera).  The reference's camera is differentiable: view and proj are ordinary
+// torch operands of _project, of the SH view direction (cam = inv(view)[:3,3]) and of the sigma rule
+// (torch_renderer.py:57-83, 140-150), so a caller whose camera tensors require grad gets d view / d proj.
+// From a view's per-Gaussian sums (k_gather_view's output, the same the chain rule reads), each Gaussian's
+//   d view += d pc (m, 1)^T,   d proj += d clip pc^T,   d proj[0][0] += d sigma_x |s0| W / (2 z) sign(P00)
+//   (the same for [1][1]),   d cam += d L / d (cam - m)  (SH colours),
+// summed per block in double (wave butterfly, then the four waves in order) and over the blocks by
+// k_camera_final (one wave per component, fixed order): deterministic.  The host turns d cam into
+// d view through the inverse (torch_renderer.py:81-83).
+// ------------------------------------------------------------------------------------------------
+constexpr int CAM_GRADS = 35;  // d view (16, row-major), d proj (16), d cam_pos (3)
+template <int CD>
+__global__ __launch_bounds__(256) void k_camera_grad(ViewK v, int n, const float* __restrict__ means,
+                                                     const float* __restrict__ scales, const float* __restrict__ colors,
+                                                     const float* __restrict__ opac, const float4* __restrict__ sums,
+                                                     const float* __restrict__ sums3, double* __restrict__ part) {
+  double acc[CAM_GRADS];
+#pragma unroll
+  for (int q = 0; q < CAM_GRADS; ++q) acc[q] = 0.0;
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  if (i < n) {
+    const float4 a = sums[2 * (size_t)i], b = sums[2 * (size_t)i + 1];
+    const float s3 = sums3 ? sums3[i] : 0.0f;
+    const float S[NPART] = {a.x, b.x, a.y, s3, a.z, b.z, a.w, b.w, b.y};
+    const bool on = a.x != 0.f || a.y != 0.f || a.z != 0.f || a.w != 0.f || b.x != 0.f || b.y != 0.f || b.z != 0.f ||
+                    b.w != 0.f || s3 != 0.f;
+    if (on) {
+      const float mx = means[3 * i], my = means[3 * i + 1], mz = means[3 * i + 2];
+      const float s0 = scales[3 * i], s1 = scales[3 * i + 1];
+      const float op = opac[i];
+      Proj p;
+      project(v, mx, my, mz, s0, s1, p);
+      ProjGrad<float> pg;
+      proj_grads<float>(v, p, op < 0.0f ? 0.0f : op, S, pg);
+      const float mh[4] = {mx, my, mz, 1.0f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[r * 4 + j] = (double)pg.dpc[r] * (double)mh[j];
+          acc[16 + r * 4 + j] = (double)pg.dclip[r] * (double)p.pc[j];
         }
+      const float sg0 = v.P[0] > 0.f ? 1.f : (v.P[0] < 0.f ? -1.f : 0.f);
+      const float sg5 = v.P[5] > 0.f ? 1.f : (v.P[5] < 0.f ? -1.f : 0.f);
+      acc[16 + 0] += (double)(pg.dsx * (fabsf(s0) * 0.5f * (float)v.W / p.za) * sg0);
+      acc[16 + 5] += (double)(pg.dsy * (fabsf(s1) * 0.5f * (float)v.H / p.za) * sg5);
+      if constexpr (CD != 3) {
+        ColGrad<CD, float> cg;
+        color_grads<CD, float>(v, mx, my, mz, colors + (size_t)CD * i, S, cg);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[32 + j] = (double)cg.dd[j];
       }
-    } else {  // degree 3: d col / d k_i = Y_i(d), d col / d d = sum_i k_i dY_i/dd
-      F Y[16], G[16][3];
-      sh3_basis(d[0], d[1], d[2], Y);
-      sh3_basis_grad(d[0], d[1], d[2], G);
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          out.color(3 * i + k, (float)(dcol[k] * Y[i]));
-          const F t = dcol[k] * (F)col[3 * i + k];
-#pragma unroll
-          for (int j = 0; j < 3; ++j) gd[j] += t * G[i][j];
-        }
-    }
-    if (nn > F(0)) {
-      const F vg = vv[0] * gd[0] + vv[1] * gd[1] + vv[2] * gd[2];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) dm[j] -= gd[j] / ne - vv[j] * vg / (nn * ne * ne);
     }
   }
 #pragma unroll
-  for (int j = 0; j < 3; ++j) out.mean(j, (float)dm[j]);
+  for (int q = 0; q < CAM_GRADS; ++q)
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) acc[q] += __shfl_xor(acc[q], m);
+  __shared__ double sh[4][CAM_GRADS];
+  const int w = (int)threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int q = 0; q < CAM_GRADS; ++q) sh[w][q] = acc[q];
+  __syncthreads();
+  if ((int)threadIdx.x < CAM_GRADS) {
+    const int q = threadIdx.x;
+    part[(size_t)blockIdx.x * CAM_GRADS + q] = ((sh[0][q] + sh[1][q]) + sh[2][q]) + sh[3][q];
+  }
+}
+
+// Block partials -> the view's camera gradient: block q sums component q over the blocks (lane l takes blocks
+// l, l + 64, ..., then a butterfly), in a fixed order.
+__global__ __launch_bounds__(64) void k_camera_final(const double* __restrict__ part, int blocks, float* __restrict__ out) {
+  const int q = blockIdx.x, lane = threadIdx.x;
+  double s = 0.0;
+  for (int b = lane; b < blocks; b += 64) s += part[(size_t)b * CAM_GRADS + q];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+  if (lane == 0) out[q] = (float)s;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3283,7 +3406,8 @@ size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan) {
          align_up(tiles * 4 * sizeof(float)) + align_up(tiles * 2 * sizeof(float)) +
          align_up(4 * sizeof(float)) +  // per-tile loss sums, per-tile depth max / arg-max counts, depth scalars
          align_up((size_t)8 * (n > 0 ? n : 1) * sizeof(float)) +  // per-Gaussian row sums (gather + chain rule)
-         align_up((size_t)(n > 0 ? n : 1) * sizeof(float));       // and depth sums
+         align_up((size_t)(n > 0 ? n : 1) * sizeof(float)) +      // and depth sums
+         align_up((size_t)blocks_for(n > 0 ? n : 1) * CAM_GRADS * sizeof(double));  // camera-gradient partials
 }
 
 // Decode the scanned totals (core, tail pairs) into the plan; a count that does not fit int32 is
@@ -3534,6 +3658,7 @@ struct BwdWs {
   float* dscal;      // [4]: max(depth), the max's gradient per arg-max pixel
   float* sums;       // [n][8]: per-Gaussian row sums (k_gather_view)
   float* sums3;      // [n]: per-Gaussian depth sums (k_gather_view<true>, with an upstream depth gradient)
+  double* cam_part;  // [blocks][CAM_GRADS]: per-block camera-gradient partials (gr_bwd_camera)
 };
 static BwdWs bwd_ws(const gr_view* v, int n, const gr_plan* plan, void* ws) {
   const size_t tiles = (size_t)tiles_x_of(v->width) * tiles_y_of(v->height);
@@ -3545,6 +3670,7 @@ static BwdWs bwd_ws(const gr_view* v, int n, const gr_plan* plan, void* ws) {
   w.dscal = (float*)((char*)w.tile_aux + align_up(tiles * 2 * sizeof(float)));
   w.sums = (float*)((char*)w.dscal + align_up(4 * sizeof(float)));
   w.sums3 = (float*)((char*)w.sums + align_up((size_t)8 * (n > 0 ? n : 1) * sizeof(float)));
+  w.cam_part = (double*)((char*)w.sums3 + align_up((size_t)(n > 0 ? n : 1) * sizeof(float)));
   return w;
 }
 
@@ -4034,6 +4160,45 @@ gr_status gr_reduce_sums(int num_views, const gr_sums_view* views, int n, const 
                        d_colors, d_opacities, accumulate);
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_REDUCE, s);
+  return GR_OK;
+}
+
+gr_status gr_bwd_camera(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
+                        const float* colors, int color_dim, const float* opacities, void* ws, size_t ws_bytes, int depth,
+                        float* d_camera, void* stream) {
+  gr_status st = check_view(v);
+  if (st != GR_OK) return st;
+  if (!plan || !d_camera) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_camera: null plan or output");
+  if (plan->num_pairs < 0) return set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
+  if (color_dim != 3 && color_dim != 12 && color_dim != 48)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");
+  if (n < 0) return set_error(GR_ERR_INVALID_ARGUMENT, "n must be >= 0");
+  if (depth && v->no_depth_grad)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_camera: depth sums of a view rendered with no_depth_grad");
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0 || plan->num_pairs == 0) {  // no pair reached the backward: every term is zero
+    GR_HIP_TRY(hipMemsetAsync(d_camera, 0, CAM_GRADS * sizeof(float), s));
+    return GR_OK;
+  }
+  if (!means || !scales || !colors || !opacities || !ws) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+  if (ws_bytes < gr_bwd_bytes(v, n, plan)) return set_error(GR_ERR_WORKSPACE, "backward workspace too small");
+  const ViewK vk = make_viewk(v);
+  const BwdWs w = bwd_ws(v, n, plan, ws);
+  const int blocks = blocks_for(n);
+  const float4* sums = (const float4*)w.sums;
+  const float* sums3 = depth ? (const float*)w.sums3 : nullptr;
+  if (color_dim == 3)
+    hipLaunchKernelGGL(k_camera_grad<3>, dim3(blocks), dim3(256), 0, s, vk, n, means, scales, colors, opacities, sums, sums3,
+                       w.cam_part);
+  else if (color_dim == 12)
+    hipLaunchKernelGGL(k_camera_grad<12>, dim3(blocks), dim3(256), 0, s, vk, n, means, scales, colors, opacities, sums, sums3,
+                       w.cam_part);
+  else
+    hipLaunchKernelGGL(k_camera_grad<48>, dim3(blocks), dim3(256), 0, s, vk, n, means, scales, colors, opacities, sums, sums3,
+                       w.cam_part);
+  GR_HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_camera_final, dim3(CAM_GRADS), dim3(64), 0, s, (const double*)w.cam_part, blocks, d_camera);
+  GR_HIP_TRY(hipGetLastError());
   return GR_OK;
 }
 

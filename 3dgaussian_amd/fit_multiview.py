@@ -67,7 +67,7 @@ DIRECT_BACKWARD = os.environ.get("GR_DIRECT", "1") != "0"
 # (at most REDUCE_BATCH views per batch, a stream's views split into equal batches)
 REDUCE_BATCH = max(1, min(16, int(os.environ.get("GR_REDUCE_BATCH", "16"))))
 # views in the last batch of each stream (0: near-equal batches only)
-REDUCE_TAIL = max(0, int(os.environ.get("GR_REDUCE_TAIL", "2")))
+REDUCE_TAIL = max(0, min(REDUCE_BATCH, int(os.environ.get("GR_REDUCE_TAIL", "2"))))  # a batch holds <= REDUCE_BATCH
 # fused path: gradient assembly through the activations and the Adam update in one HIP pass per parameter
 # (gr_fit_param_step) instead of torch's autograd + foreach Adam (0 = torch)
 FUSED_STEP = os.environ.get("GR_FUSED_STEP", "1") != "0"

@@ -15,7 +15,9 @@ libgr_hip.so through a ``torch.autograd.Function`` — not by torch ops.  Differ
   dense reference to <=5e-6 relative L2 on its own fixtures, with and without depth gradients, and to
   <=1e-4 on sampled dense checks at configs C4 and C5 (tests/test_scale_gpu.py);
 * ``chunk_size`` is accepted and ignored (no chunk loop);
-* gradients flow to means, scales, colours/SH, opacities and background; not to the camera matrices;
+* gradients flow to means, scales, colours/SH, opacities, background and - when their tensors require
+  grad, as the reference's autograd gives them (:57-83, 140-150) - to camera.view / camera.proj
+  (gr_bwd_camera);
 * the op dispatches on the tensors' device like the reference: HIP tensors always run the HIP kernels
   (a missing libgr_hip.so raises ImportError; nothing falls back), CPU tensors run ``cpu_renderer``'s
   dense torch op (config C1, the reference's own CPU plumbing case; no tile cutoff there).
@@ -380,8 +382,9 @@ def forward_native(means, scales, colors, opacities, gv: _native.GrView, prepare
     return out, alpha, depth, RenderState(gv, n, plan, geom, bins, saved)
 
 
-def backward_native(means, scales, colors, opacities, st: RenderState, g_out, g_alpha, g_depth):
-    """Run gr_bwd.  Returns (d_means, d_scales, d_colors, d_opacities)."""
+def backward_native(means, scales, colors, opacities, st: RenderState, g_out, g_alpha, g_depth, want_ws: bool = False):
+    """Run gr_bwd.  Returns (d_means, d_scales, d_colors, d_opacities) (+ the backward workspace with
+    ``want_ws``: it holds the per-Gaussian sums camera_grad_native reads)."""
     L = _native.lib()
     dev = means.device
     cd = _color_dim(colors)
@@ -396,7 +399,37 @@ def backward_native(means, scales, colors, opacities, st: RenderState, g_out, g_
                            _native.ptr(st.saved), _native.ptr(g_out), _native.ptr(g_alpha), _native.ptr(g_depth),
                            _native.ptr(dm), _native.ptr(ds), _native.ptr(dc), _native.ptr(do), _native.ptr(ws), ws.numel(),
                            _stream(dev)), "gr_bwd")
-    return dm, ds, dc, do
+    return (dm, ds, dc, do, ws) if want_ws else (dm, ds, dc, do)
+
+
+def camera_grad_native(means, scales, colors, opacities, st: RenderState, ws, depth: bool) -> torch.Tensor:
+    """gr_bwd_camera on the current stream, after backward_native(..., want_ws=True) of the same render:
+    (35,) device floats = d view (16, row-major), d proj (16), d cam_pos (3, SH colours only)."""
+    L = _native.lib()
+    out = torch.empty((_native.CAMERA_GRADS,), dtype=torch.float32, device=means.device)
+    _native.check(L.gr_bwd_camera(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan), _native.ptr(means), _native.ptr(scales),
+                                  _native.ptr(colors), _color_dim(colors), _native.ptr(opacities), _native.ptr(ws), ws.numel(),
+                                  1 if depth else 0, _native.ptr(out), _stream(means.device)), "gr_bwd_camera")
+    return out
+
+
+def _camera_grads(d: torch.Tensor, view: Optional[torch.Tensor], proj: Optional[torch.Tensor], need_view: bool,
+                  need_proj: bool, sh: bool):
+    """gr_bwd_camera's 35 floats -> (d view, d proj) in the camera tensors' dtype and device.  With SH colours the
+    camera centre cam = inv(view)[:3,3] (torch_renderer.py:81-83) also depends on view:
+    d view += -inv(view)^T G inv(view)^T with G = d cam in column 3 (the inverse's differential)."""
+    dview = dproj = None
+    if need_view:
+        dv = d[:16].view(4, 4).double()
+        if sh:
+            Vi = torch.linalg.inv(view.detach().to(device=d.device, dtype=torch.float64))
+            G = torch.zeros((4, 4), dtype=torch.float64, device=d.device)
+            G[:3, 3] = d[32:35].double()
+            dv = dv - Vi.t() @ G @ Vi.t()
+        dview = dv.to(dtype=view.dtype, device=view.device)
+    if need_proj:
+        dproj = d[16:32].view(4, 4).to(dtype=proj.dtype, device=proj.device)
+    return dview, dproj
 
 
 def backward_l1_native(means, scales, colors, opacities, st: RenderState, target, mask, w_sil: float, g_scale: float,
@@ -581,22 +614,26 @@ def _grad_background(st: RenderState, background: torch.Tensor, g_out: torch.Ten
 
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, means, scales, colors, opacities, background, gv, prepared, gv_depth=None, bin_stream=None):
-        """gv_depth: the f32-grade view a lazily rendered gv (two-piece mode) re-renders with when a depth
-        gradient arrives (LAZY_DEPTH), else None.  bin_stream: see forward_native."""
+    def forward(ctx, means, scales, colors, opacities, background, view, proj, gv, prepared, gv_depth=None,
+                bin_stream=None):
+        """view / proj: the camera tensors (their gradients, gr_bwd_camera) or None; the render itself uses gv's
+        host copy of them.  gv_depth: the f32-grade view a lazily rendered gv (two-piece mode) re-renders with
+        when a depth gradient arrives (LAZY_DEPTH), else None.  bin_stream: see forward_native."""
         out, alpha, depth, st = forward_native(means, scales, colors, opacities, gv, prepared, bin_stream=bin_stream)
         # an output the loss does not use gets a None gradient instead of zeros, so an unused depth
         # output lets the backward skip the tail pairs (gr_bwd with g_depth = NULL)
         ctx.set_materialize_grads(False)
-        ctx.st = st
+        ctx.meta = (st.gv, st.n, st.plan)
         ctx.gv_depth = gv_depth
-        ctx.save_for_backward(means, scales, colors, opacities, background)
+        # the render state's device buffers are saved tensors: autograd releases them after this node's backward
+        # unless the graph is retained (a second backward through it then finds them)
+        ctx.save_for_backward(means, scales, colors, opacities, background, view, proj, st.geom, st.bins, st.saved)
         return out, alpha, depth
 
     @staticmethod
     def backward(ctx, g_out, g_alpha, g_depth):
-        means, scales, colors, opacities, background = ctx.saved_tensors
-        st = ctx.st
+        means, scales, colors, opacities, background, view, proj, geom, bins, saved = ctx.saved_tensors
+        st = RenderState(*ctx.meta, geom, bins, saved)
         if g_out is None:
             g_out = torch.zeros((st.gv.height, st.gv.width, 3), dtype=torch.float32, device=means.device)
         g_out = g_out.contiguous().float()
@@ -609,10 +646,14 @@ class _RasterizeGaussians(torch.autograd.Function):
             # lazy default: the depth is differentiated after all - re-render at f32 grade with the
             # depth-gradient footprint and differentiate that render
             _, _, _, st = forward_native(means, scales, colors, opacities, ctx.gv_depth, images=False)
-        ctx.st = None
-        dm, ds, dc, do = backward_native(means, scales, colors, opacities, st, g_out, g_alpha, g_depth)
+        need_view, need_proj = ctx.needs_input_grad[5], ctx.needs_input_grad[6]
+        dm, ds, dc, do, ws = backward_native(means, scales, colors, opacities, st, g_out, g_alpha, g_depth, want_ws=True)
         dbg = _grad_background(st, background, g_out) if ctx.needs_input_grad[4] else None
-        return dm, ds, dc, do, dbg, None, None, None, None
+        dview = dproj = None
+        if need_view or need_proj:
+            d = camera_grad_native(means, scales, colors, opacities, st, ws, g_depth is not None)
+            dview, dproj = _camera_grads(d, view, proj, need_view, need_proj, colors.dim() == 3)
+        return dm, ds, dc, do, dbg, dview, dproj, None, None, None, None
 
 
 def _device_inputs(means, scales, colors, opacities):
@@ -761,8 +802,11 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
     if prepared is not None and (prepared.gv.cutoff != gv.cutoff or prepared.gv.no_depth_grad != gv.no_depth_grad):
         # a preparation made for the eager view (prepare_view(depth_grad="eager"), or GR_LAZY_DEPTH=0)
         gv, gv_depth = prepared.gv, None
+    # the camera tensors enter the autograd op only when a gradient is wanted for them (gr_bwd_camera)
+    cam_v = view if isinstance(view, torch.Tensor) and view.requires_grad else None
+    cam_p = proj if isinstance(proj, torch.Tensor) and proj.requires_grad else None
     if prepared is not None or not SPECULATE:
-        return _RasterizeGaussians.apply(m, s, c, o, background, gv, prepared, gv_depth)
+        return _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, prepared, gv_depth)
     key = _view_key(gv)
     pv = _spec_take(key, (m, s, c, o))
     stream = torch.cuda.current_stream(dev)
@@ -771,7 +815,7 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
         pv.geom.record_stream(stream)
     ready = torch.cuda.Event()
     ready.record(stream)
-    res = _RasterizeGaussians.apply(m, s, c, o, background, gv, pv, gv_depth)
+    res = _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, pv, gv_depth)
     _spec_after(key, gv, (m, s, c, o), ready)
     return res
 

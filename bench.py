@@ -101,8 +101,8 @@ SURVEY_C4_ROOF_MPX = 2830.0  # the north_star targ
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--gaussians", type=int, default=1_000_000)
     ap.add_argument("--views", type=int, default=50)
     ap.add_argument("--res", type=int, default=800)
@@ -203,6 +203,7 @@ def cpu_baseline(n: int, res: int, views: int) -> dict:
     orc.backward(v, scene, gr, None, None, binned=True)
     dto = time.perf_counter() - t0
     return {"value": round(res * res / dt / 1e6, 5), "unit": "Mpixels/sec fwd+bwd", "cores": threads, "kind": "port",
+            "host_cpu_count": os.cpu_count(), "torch_threads": threads,
             "sample": f"1 view of the workload at {res}x{res} fwd+bwd through render_gaussians_torch on host tensors "
                       f"(cpu_renderer.py, dense: every Gaussian at every pixel, as the reference), torch with {threads} "
                       f"threads, timed on {sub} of the {n} Gaussians ({dt * sub / n:.1f} s) and scaled by {n / sub:g} "

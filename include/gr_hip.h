@@ -175,6 +175,18 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
                  const float* g_alpha, const float* g_depth, float* d_means, float* d_scales,
                  float* d_colors, float* d_opacities, void* ws, size_t ws_bytes, void* stream);
 
+/* Camera gradient of a view after gr_bwd (its workspace ws still holds the per-Gaussian sums gr_bwd formed).
+ * Replaces the autograd path of the reference's camera operands: python/torch_renderer.py:140-150 moves
+ * camera.view / camera.proj into _project (:57-78), the SH view direction (cam = inv(view)[:3,3], :81-83) and the
+ * sigma rule (fx = |proj[0,0]|, fy = |proj[1,1]|), so a caller whose camera tensors require grad gets their
+ * gradients.  d_camera (device, 35 floats) receives d view (16, row-major), d proj (16) and d cam_pos (3; zero for
+ * RGB colours: the caller adds its chain through inv(view)).  depth != 0: gr_bwd was given g_depth (its depth sums
+ * enter too).  Deterministic (fixed-order double sums). */
+#define GR_CAMERA_GRADS 35
+gr_status gr_bwd_camera(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
+                        const float* colors, int color_dim, const float* opacities, void* ws, size_t ws_bytes, int depth,
+                        float* d_camera, void* stream);
+
 /* Backward of gr_fwd_render fused with the fit loop's view loss (fit_multiview_stub.py:292-299):
  *   loss = mean|out - target_rgb| + w_sil * mean|alpha - target_mask|   (target_mask may be NULL)
  * The upstream gradients are those of g_scale * loss (torch's abs' = sign, sign(0) = 0), computed

@@ -12,6 +12,9 @@ Sources of truth (nothing from the reference is copied into the repo; only input
     oracle/build_ref.sh (oracle/_ref/libref.so), OIT and depth-sorted modes.
   * F4 fit curve: /root/reference/python/fit_multiview_stub.py run on CPU with
     torch.manual_seed(1234) on the tiny synthetic targets in tests/golden/fit_targets/.
+  * F5 camera gradients (``make_golden.py camera`` writes only these): the same imported
+    torch_renderer.py with camera.view / camera.proj requiring grad; autograd's d view / d proj of the F1
+    loss with and without its depth term.
 """
 from __future__ import annotations
 
@@ -185,5 +188,42 @@ def main():
     print("F4 losses", losses)
 
 
+def camera_main():
+    """F5: camera-gradient fixtures (view / proj requiring grad in the reference's autograd)."""
+    torch.set_num_threads(8)
+    cases = [("f5_cam_n64_64x48", edge_scene(64, seed=501), 64, 48, orc.look_at([0.3, 0.5, 2.4], [0, 0, 0], [0, 1, 0])),
+             ("f5_cam_n300_64x48_sh", edge_scene(300, seed=502, sh=True), 64, 48,
+              orc.look_at([-0.4, 0.6, 2.3], [0, 0, 0], [0, 1, 0])),
+             ("f5_cam_c1_view1", orc.synthetic_scene(1200, seed=0, scale=0.1061), 128, 128, orc.orbit_cameras(4, 128, 128)[1][0])]
+    for ci, (name, scene, W, H, view) in enumerate(cases):
+        proj = orc.perspective(60.0, W / H, 0.01, 100.0)
+        bg = np.array([0.1, 0.2, 0.3], np.float32)
+        g = np.random.default_rng(600 + ci)
+        g_rgb = g.standard_normal((H, W, 3)).astype(np.float32)
+        g_a = g.standard_normal((H, W)).astype(np.float32)
+        g_d = g.standard_normal((H, W)).astype(np.float32)
+        d = dict(width=np.int32(W), height=np.int32(H), view=np.asarray(view, np.float32), proj=np.asarray(proj, np.float32),
+                 background=bg, means=scene.means, scales=scene.scales, colors=scene.colors, opacities=scene.opacities,
+                 g_rgb=g_rgb, g_alpha=g_a, g_depth=g_d)
+        for tag, with_depth in (("", True), ("_nodepth", False)):
+            vt = torch.from_numpy(np.asarray(view, np.float32).copy()).requires_grad_(True)
+            pt = torch.from_numpy(np.asarray(proj, np.float32).copy()).requires_grad_(True)
+            m, s, c, o = (torch.from_numpy(a.copy()) for a in scene.arrays())
+            rgb, alpha, depth = ref.render_gaussians_torch(m, s, c, o, ref.Camera(view=vt, proj=pt), W, H,
+                                                           background=torch.from_numpy(bg), max_gaussians=10000,
+                                                           return_aux=True)
+            loss = (rgb * torch.from_numpy(g_rgb)).sum() + (alpha * torch.from_numpy(g_a)).sum()
+            if with_depth:
+                loss = loss + (depth * torch.from_numpy(g_d)).sum()
+            loss.backward()
+            d["d_view" + tag] = vt.grad.numpy().astype(np.float32)
+            d["d_proj" + tag] = pt.grad.numpy().astype(np.float32)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
+        print("wrote", name, float(np.abs(d["d_view"]).max()), float(np.abs(d["d_proj"]).max()))
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "camera":
+        camera_main()
+    else:
+        main()

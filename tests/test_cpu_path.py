@@ -128,10 +128,10 @@ def test_fit_driver_on_cpu_reproduces_reference_curve(pkg, tmp_path):
 
     from conftest import GOLDEN
 
-    d = golden("f4_fit_curve")
+    d = golden("f4_fit_curve")  # the F4 run is square (make_golden.py: --width 48 --height 48; no height key stored)
     fm = importlib.import_module("3dgaussian_amd.fit_multiview")
     fm.main(["--targets_dir", os.path.join(GOLDEN, "fit_targets"), "--out_dir", str(tmp_path), "--iters", str(int(d["iters"])),
-             "--width", str(int(d["width"])), "--height", str(int(d["width"])), "--num_gaussians", str(int(d["num_gaussians"])),
+             "--width", str(int(d["width"])), "--height", str(int(d["height"] if "height" in d else d["width"])), "--num_gaussians", str(int(d["num_gaussians"])),
              "--max_gaussians", str(int(d["max_gaussians"])), "--densify_interval", str(int(d["densify_interval"])),
              "--prune_interval", str(int(d["densify_interval"])), "--seed", str(int(d["seed"])), "--device", "cpu"])
     losses = np.array([float(x) for x in (tmp_path / "loss.txt").read_text().split()])

@@ -3,6 +3,7 @@ driver's per-view schedule (fit_multiview._views_direct / _views_direct_depth: s
 groups, reduction batches) and gives bit-identical losses and parameters after a fit step."""
 from __future__ import annotations
 
+import ctypes
 import importlib
 
 import pytest
@@ -38,3 +39,62 @@ def test_native_executor_matches_python_schedule(cuda, streams, depth):
     assert fm.NATIVE_EXEC != "auto" or f._native_exec()
     for k in res[False][1]:
         assert torch.equal(res[True][1][k], res[False][1][k]), k
+
+
+def test_native_executor_at_c4_size(cuda):
+    """The size at which the executor's first design faulted (commit 3f15cae: cross-stream pool reuse at C4):
+    1M Gaussians, 13 views of 800x800 (several views per stream and a second reduction batch), two steps, the
+    second one reusing every workspace and geom slot; bit-identical to the Python schedule (VERDICT r03 #4)."""
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    bench = importlib.import_module("bench")
+    R, V = 800, 13
+    cams = fm.orbit_cameras(V, R, R, cuda)
+    g = torch.Generator(device=cuda).manual_seed(4)
+    targets = [torch.rand((R, R, 3), generator=g, device=cuda) for _ in range(V)]
+    masks = [(t.mean(dim=2) > 0.5).float() for t in targets]
+    res = {}
+    saved = fm.NATIVE_EXEC, fm.REDUCE_BATCH
+    try:
+        for native in (False, True):
+            fm.NATIVE_EXEC, fm.REDUCE_BATCH = ("1" if native else "0"), 2
+            f = fm.ViewShardedFitter(bench.synthetic_params(1_000_000, cuda), cams, targets, R, R, masks=masks)
+            losses = [float(f.step()) for _ in range(2)]
+            torch.cuda.synchronize()
+            res[native] = (losses, {k: v.detach().clone() for k, v in f.params.items()})
+            del f
+            torch.cuda.empty_cache()
+    finally:
+        fm.NATIVE_EXEC, fm.REDUCE_BATCH = saved
+    assert res[True][0] == res[False][0]
+    for k in res[False][1]:
+        assert torch.equal(res[True][1][k], res[False][1][k]), k
+
+
+def test_native_executor_rejects_out_of_range_config(pkg, cuda):
+    """ADVICE r03: a configuration whose batches or preparation groups would not fit the fixed-size view arrays
+    returns GR_ERR_INVALID_ARGUMENT (raised as ValueError) before anything is enqueued."""
+    tr = pkg.torch_renderer
+    nat = pkg._native
+    L = nat.lib()
+    n = 64
+    p = [torch.zeros((n, 3), device=cuda), torch.ones((n, 3), device=cuda), torch.zeros((n, 3), device=cuda),
+         torch.zeros((n,), device=cuda)]
+    cam = importlib.import_module("3dgaussian_amd.fit_multiview").orbit_cameras(1, 32, 32, cuda)[0]
+    tgt = torch.zeros((32, 32, 3), device=cuda)
+    arr = (nat.GrFitTarget * 1)()
+    arr[0].view = tr.make_view(cam.view, cam.proj, 32, 32, None, depth_grad=False)
+    arr[0].target_rgb = tgt.data_ptr()
+    acc = [torch.empty_like(t) for t in p]
+    accp = (ctypes.c_void_p * 4)(*[t.data_ptr() for t in acc])
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    losses = torch.empty(1, device=cuda)
+    bad = [dict(reduce_tail=17), dict(reduce_tail=5, reduce_batch=4), dict(prep_first=5), dict(prep_group=5),
+           dict(reduce_batch=17)]
+    for b in bad:
+        c = dict(num_streams=1, prep_ahead=2, prep_group=2, prep_first=1, reduce_batch=4, reduce_tail=0)
+        c.update(b)
+        cfg = nat.GrFitConfig(c["num_streams"], c["prep_ahead"], c["prep_group"], c["prep_first"], c["reduce_batch"],
+                              c["reduce_tail"])
+        st = L.gr_fit_views(nat.executor(0), ctypes.byref(cfg), 1, arr, n, *[nat.ptr(t) for t in p[:3]], 3, nat.ptr(p[3]),
+                            0.0, 0.0, 1.0, nat.ptr(losses), accp, stream)
+        assert st == nat.GR_ERR_INVALID_ARGUMENT, (b, st)

@@ -157,7 +157,10 @@ def test_fit_path_on_fitted_state_vs_dense(pkg, cuda):
         assert e <= 1e-4, (k, e)
 
 
-@pytest.mark.parametrize("opac_range", [(1e-4, 1e-3), (0.0, 1.0), (100.0, 3000.0), (3000.0, 6000.0), (0.0, 1e5)])
+# (-1e5, 2.0): large negative opacities - the record keeps max(o, 0) and the colours clamp to [0, 1], so
+# the A operands o c ex stay within max(o, 0) of the scale f16_sa_of sizes them by
+@pytest.mark.parametrize("opac_range", [(1e-4, 1e-3), (0.0, 1.0), (100.0, 3000.0), (3000.0, 6000.0), (0.0, 1e5),
+                                        (-1e5, 2.0)])
 def test_fit_mode_f16_operand_range(pkg, cuda, opac_range):
     """The fit-path forward (no depth channel) multiplies on f16 operand pieces pre-scaled by 2^sa (A) and
     2^12 (B), sa = 4 while the view's largest opacity is below 2^11 and lower above (f16_sa_of): opacities
