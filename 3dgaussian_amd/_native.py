@@ -83,7 +83,7 @@ class GrReduceView(ctypes.Structure):
 class GrSumsView(ctypes.Structure):
     """gr_sums_view (include/gr_hip.h): one view of a gr_reduce_sums batch."""
 
-    _fields_ = [("view", GrView), ("sums", ctypes.c_void_p)]
+    _fields_ = [("view", GrView), ("sums", ctypes.c_void_p), ("sums3", ctypes.c_void_p)]
 
 
 class GrFitTarget(ctypes.Structure):
@@ -121,10 +121,14 @@ _SIG = {
     "gr_saved_floats": (ctypes.c_size_t, [_VP]),
     "gr_fwd_scratch_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
     "gr_fwd_render": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P, _P, _P, _P, _P]),
+    "gr_fwd_render_saved": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P, _P]),
+    "gr_fwd_compose": (ctypes.c_int, [_VP, _P, _P, _P, _P, _P]),
     "gr_fwd_bin": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P]),
     "gr_bwd_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
     "gr_bwd": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, _P, _P, _P, ctypes.c_size_t, _P]),
+    "gr_bwd_indexed": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P,
+                                      _P, _P, _P, _P, _P, ctypes.c_size_t, _P]),
     "gr_bwd_camera": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, ctypes.c_size_t, ctypes.c_int,
                                      _P, _P]),
     "gr_bwd_l1": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P,
@@ -146,6 +150,8 @@ _SIG = {
                                        _P, _P, _P, _P, _P, ctypes.c_int, _P]),
     "gr_view_sums_floats": (ctypes.c_size_t, [ctypes.c_int]),
     "gr_gather_view": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, _P, _P]),
+    "gr_bwd_fit_gather": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, _P, _P, ctypes.c_float, _P, ctypes.c_float,
+                                         ctypes.c_float, _P, _P, ctypes.c_size_t, _P, _P, _P]),
     "gr_reduce_sums": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(GrSumsView), ctypes.c_int, _P, _P, _P, ctypes.c_int,
                                       _P, _P, _P, _P, _P, ctypes.c_int, _P]),
     "gr_executor_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),

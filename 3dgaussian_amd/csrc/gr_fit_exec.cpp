@@ -80,7 +80,7 @@ struct Buf {
 
 struct StreamWs {  // one render stream's buffers
   Buf bins, scratch, ws, saved;
-  std::vector<Buf> sums;  // one per view of a reduction batch
+  std::vector<Buf> sums, sums3;  // one per view of a reduction batch (sums3: the depth-loss path's depth sums)
 };
 
 struct GeomSlot {
@@ -160,6 +160,7 @@ void gr_executor_destroy(gr_executor* ex) {
     w.ws.release();
     w.saved.release();
     for (auto& b : w.sums) b.release();
+    for (auto& b : w.sums3) b.release();
   }
   for (auto& g : ex->geoms) {
     g.buf.release();
@@ -228,7 +229,10 @@ static gr_status fit_views_on_device(gr_executor* ex, const gr_fit_config* cfg, 
   }
   if ((int)ex->ws.size() < ns) ex->ws.resize(ns);
   for (int k = 0; k < ns; ++k)
-    if ((int)ex->ws[k].sums.size() < cfg->reduce_batch) ex->ws[k].sums.resize(cfg->reduce_batch);
+    if ((int)ex->ws[k].sums.size() < cfg->reduce_batch) {
+      ex->ws[k].sums.resize(cfg->reduce_batch);
+      ex->ws[k].sums3.resize(cfg->reduce_batch);
+    }
   // geom slots: the views prepared ahead, the ones rendering on every stream, and a margin
   const int nslots = cfg->prep_ahead + cfg->prep_group + ns + 2;
   while ((int)ex->geoms.size() < nslots) {
@@ -328,6 +332,7 @@ static gr_status enqueue_views(gr_executor* ex, const gr_fit_config* cfg, int nu
   struct Pending {
     gr_view view;
     float* sums;
+    float* sums3;  // depth sums (depth-loss path) or null
   };
   // a slot's previous view must have been waited for before the slot is refilled: with nslots > prep_ahead
   // + prep_group + ns the view a slot last held was rendered (and its free event recorded) before the
@@ -343,6 +348,7 @@ static gr_status enqueue_views(gr_executor* ex, const gr_fit_config* cfg, int nu
     for (int q = 0; q < nb; ++q) {
       b[q].view = pending[k][q].view;
       b[q].sums = pending[k][q].sums;
+      b[q].sums3 = pending[k][q].sums3;
     }
     GR_EXEC_CALL(gr_reduce_sums(nb, b, n, means, scales, colors, color_dim, opacities, acc[4 * k + 0], acc[4 * k + 1],
                                 acc[4 * k + 2], acc[4 * k + 3], started[k], st[k]));
@@ -378,15 +384,19 @@ static gr_status enqueue_views(gr_executor* ex, const gr_fit_config* cfg, int nu
       Buf& sb = W.sums[pending[k].size()];
       GR_EXEC_TRY(sb.fit(sums_bytes, s));
       GR_EXEC_CALL(gr_gather_view(&v, n, &plan, geom[j], bins, ws, (float*)sb.p, s));
-      pending[k].push_back({v, (float*)sb.p});
+      pending[k].push_back({v, (float*)sb.p, nullptr});
     } else {
       GR_EXEC_TRY(W.saved.fit(gr_saved_floats(&v) * sizeof(float), s));
       GR_EXEC_CALL(gr_fwd_render(&v, n, &plan, geom[j], bins, W.bins.cap, scratch, W.scratch.cap, nullptr, nullptr,
                                  nullptr, (float*)W.saved.p, s));
-      GR_EXEC_CALL(gr_bwd_fit(&v, n, &plan, means, scales, colors, color_dim, opacities, geom[j], bins,
-                              (const float*)W.saved.p, views[j].target_rgb, views[j].target_mask, w_sil,
-                              views[j].target_depth, w_depth, g_scale, losses + j, acc[4 * k + 0], acc[4 * k + 1],
-                              acc[4 * k + 2], acc[4 * k + 3], j >= ns ? 1 : 0, ws, W.ws.cap, s));
+      Buf& sb = W.sums[pending[k].size()];
+      Buf& s3 = W.sums3[pending[k].size()];
+      GR_EXEC_TRY(sb.fit(sums_bytes, s));
+      GR_EXEC_TRY(s3.fit((size_t)n * sizeof(float), s));
+      GR_EXEC_CALL(gr_bwd_fit_gather(&v, n, &plan, geom[j], bins, (const float*)W.saved.p, views[j].target_rgb,
+                                     views[j].target_mask, w_sil, views[j].target_depth, w_depth, g_scale, losses + j, ws,
+                                     W.ws.cap, (float*)sb.p, (float*)s3.p, s));
+      pending[k].push_back({v, (float*)sb.p, (float*)s3.p});
     }
     // the geom slot may be refilled once this stream has passed its last reader
     GeomSlot& gsl = ex->geoms[slot_of[j]];
@@ -394,7 +404,7 @@ static gr_status enqueue_views(gr_executor* ex, const gr_fit_config* cfg, int nu
     gsl.pending = true;
     geom[j] = nullptr;
     GR_EXEC_CALL(prepare_upto(j + cfg->prep_ahead));
-    if (!depth && (int)pending[k].size() >= sizes[k].front()) {
+    if ((int)pending[k].size() >= sizes[k].front()) {
       GR_EXEC_CALL(reduce_pending(k));
       if (sizes[k].size() > 1) sizes[k].pop_front();
     }

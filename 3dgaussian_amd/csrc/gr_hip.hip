@@ -15,7 +15,8 @@
 //   k_work_items_zones  per-(virtual) tile ranges, work items of <= CH pairs.
 //   k_raster_fwd_mfma   per work item: records staged through LDS by LDS-DMA, the separable splat as
 //                    a contraction on bf16 MFMA with split operands;
-//                    k_fwd_finalize combines tiles split over several items; out/alpha/depth + saved.
+//                    a tile split over several items is finished by its last item (arrival ticket);
+//                    out/alpha/depth + saved, with the fit loss its upstream fragments and the view loss.
 //   k_pixel_grads    per pixel upstream vector U = (dC, dW, dD), pre-split into MFMA fragments.
 //   k_raster_bwd_bf16   per work item: the two K = 16 contractions (over x, over y) of U with the
 //                    Gaussians' exponentials; 8- or 9-float partial rows at the pairs' sorted positions.
@@ -274,6 +275,27 @@ __device__ __forceinline__ float tile_emax(const ViewK& v, float px, float py, f
 
 __device__ __forceinline__ float radius_thr(float R) { return (-0.5f * LOG2E) * (R * R); }
 
+// tile_emax in its column and row terms, ex(tx) + ey(ty) (the same float operations, so the same value bit for bit):
+// the tile loops of the preparation and of the emission evaluate the row term once per row.
+__device__ __forceinline__ float tile_ex(const ViewK& v, float px, float qx, int tx) {
+  const int xe = min(tx * T + T - 1, v.W - 1);
+  const float lox = (float)(tx * T) + 0.5f, hix = (float)xe + 0.5f;
+  const float cx = px < lox ? lox : (px > hix ? hix : px);
+  const float dx = cx - px;
+  return (dx * dx) * qx;
+}
+__device__ __forceinline__ float tile_ey(const ViewK& v, float py, float qy, int ty) {
+  const int ye = min(ty * T + T - 1, v.H - 1);
+  const float loy = (float)(ty * T) + 0.5f, hiy = (float)ye + 0.5f;
+  const float cy = py < loy ? loy : (py > hiy ? hiy : py);
+  const float dy = cy - py;
+  return (dy * dy) * qy;
+}
+// tile_class from the two terms and the view's two thresholds (radius_thr of the cutoff and of the core)
+__device__ __forceinline__ int tile_class_e(float e, float thr_cut, float thr_core) {
+  return !(e >= thr_cut) ? 0 : (e >= thr_core ? 2 : 1);
+}
+
 // Tile culling inside the rectangle: keep tile (tx,ty) iff the Gaussian's largest weight over it is
 // >= o * exp(-cutoff^2/2).
 __device__ __forceinline__ bool tile_pass(const ViewK& v, float px, float py, float qx, float qy, int tx, int ty) {
@@ -393,6 +415,8 @@ struct Bins {
   int* num_items;      // [1]
   int* tile_item0;     // [tiles] first work item of each tile
   int* pos_of;         // [K] sorted position of each pair, by emission index (k_reduce_bwd's map)
+  int* ticket;         // [tiles + 1] arrivals of a split tile's items, then of finished tiles (k_raster_fwd_mfma);
+                       // zeroed by the work-item builder, left zero by the forward
 };
 
 // Forward-only scratch (freed by the caller after gr_fwd_render).
@@ -408,7 +432,7 @@ struct Scratch {
 inline int64_t item_cap(int tiles, int64_t K) { return (K + CH - 1) / CH + tiles; }
 
 // `vtiles` = 2 x tiles (core and tail lists of each tile) on the differentiable path.
-size_t bins_fixed(int vtiles, int64_t K, size_t off[7]) {
+size_t bins_fixed(int vtiles, int64_t K, size_t off[8]) {
   const int tiles = vtiles;
   const size_t kk = (size_t)(K > 0 ? K : 1);
   const size_t cap = (size_t)item_cap(tiles, K);
@@ -420,6 +444,7 @@ size_t bins_fixed(int vtiles, int64_t K, size_t off[7]) {
   off[4] = o; o = align_up(o + sizeof(int));
   off[5] = o; o = align_up(o + (size_t)tiles * sizeof(int));
   off[6] = o; o = align_up(o + kk * sizeof(int));
+  off[7] = o; o = align_up(o + ((size_t)tiles / 2 + 1) * sizeof(int));
   return o;
 }
 
@@ -438,9 +463,9 @@ size_t scratch_fixed(int vtiles, int64_t K, size_t off[5]) {
   return o;
 }
 
-// Pair order by tile.  Pairs leave k_emit in Gaussian order; the forward and backward need them
+// Pair order by tile.  Pairs leave the emission in Gaussian order; the forward and backward need them
 // grouped by tile with ascending Gaussian ids inside a tile (a stable sort by tile).  Up to
-// TSORT_MAX_TILES tiles this is a stable counting sort over 16-bit tile keys (k_tile_count ..
+// TSORT_MAX_TILES tiles this is a stable counting sort over 16-bit tile keys (k_emit_cols, k_tile_colscan,
 // k_tile_place below): the keys are read twice and the ids once, instead of a radix sort's
 // histogram + two scatter passes over keys and values.  Larger images use the hipcub radix sort on
 // 32-bit keys.
@@ -448,52 +473,42 @@ size_t scratch_fixed(int vtiles, int64_t K, size_t off[5]) {
 // Waves per column block: the per-wave tile counters (tiles ints per wave) stay within 64 KB LDS.
 inline int tsort_waves(int tiles) { return tiles <= 4096 ? 4 : tiles <= 8192 ? 2 : 1; }
 
-struct TSortPlan {
-  int waves, cw, cols;  // waves per column, pairs per column, columns
-  size_t cells;         // tiles * cols
-};
-
-// 64 * TS_SEG pairs per wave (k_tile_place's register-resident segment); more segments per wave only when
-// the count matrix would pass 2^28 cells.
-#ifndef GR_TSORT_NSEG
-#define GR_TSORT_NSEG 1
-#endif
 #ifndef GR_TS_SEG
 #define GR_TS_SEG 24
 #endif
 constexpr int TS_SEG = GR_TS_SEG;  // 64-pair steps per register-resident segment (1536 pairs per wave;
                                    // 16 and 32 (2048) were slower, two segments per wave much slower)
-inline TSortPlan tsort_plan(int64_t K, int tiles) {
-  TSortPlan p;
-  p.waves = tsort_waves(tiles);
-  int64_t pw = 64 * TS_SEG * GR_TSORT_NSEG;
-  const int64_t kk = K > 0 ? K : 1;
-  // Wider columns (more segments per wave) while the count matrix would outweigh half the
-  // keys and there are columns to spare: at many tiles (1080p: 8160) and many pairs the matrices
-  // (M and its scan, tiles x columns ints, each read and written) otherwise dominate the sort.
-  auto cols_of = [&](int64_t w) { return (kk + w * p.waves - 1) / (w * p.waves); };
-  while ((int64_t)tiles * cols_of(pw) > (1ll << 28) ||
-         ((int64_t)tiles * cols_of(pw) > kk / 2 && cols_of(2 * pw) >= 1024))
-    pw *= 2;
-  p.cw = (int)(pw * p.waves);
-  p.cols = (int)((kk + p.cw - 1) / p.cw);
-  p.cells = (size_t)tiles * p.cols;
+
+// Columns of the counting sort: column c = the pairs of the G = 256 J consecutive Gaussians [c G, c G + G), one
+// k_emit_cols block each (which counts them per tile as it emits them), so the per-column tile counts need no pass
+// of their own.  J is chosen from the view's plan so that a column holds about one register segment per place
+// wave (64 TS_SEG pairs), and wider while the count matrix (tiles x columns ints, written, scanned and read) would
+// outweigh half the keys (many tiles: 1080p).  Columns follow the Gaussians, so their pair counts vary with the
+// scene (Morton order: near and far parts of the cloud); k_tile_place walks a long column in several segments.
+struct ColPlan {
+  int J, G, cols;
+};
+constexpr int COL_MAX_J = 64;
+inline ColPlan col_plan(int n, int64_t K, int tiles) {
+  ColPlan p;
+  const int64_t nn = n > 0 ? n : 1, kk = K > 0 ? K : 1;
+  const int64_t pt = 64ll * TS_SEG * tsort_waves(tiles);  // pairs per column aimed at
+  int64_t J = (pt * nn + 128 * kk) / (256 * kk);           // round(pt n / (256 K))
+  const int64_t Jc = (2 * (int64_t)tiles * nn + 256 * kk - 1) / (256 * kk);  // tiles x cols <= K / 2
+  J = std::max<int64_t>(1, std::min<int64_t>(COL_MAX_J, std::max(J, std::min<int64_t>(Jc, COL_MAX_J))));
+  p.J = (int)J;
+  p.G = 256 * p.J;
+  p.cols = (int)((nn + p.G - 1) / p.G);
   return p;
 }
 
-// Scratch behind the fixed part: counting sort = count matrix M, its row scan S, tile totals T;
-// radix sort = its temp storage.
-// `tiles` = virtual tiles (2 x screen tiles).  Counting sort: one count matrix M (reused by the two
-// regions), per region its row scan S and tile totals T.  Every matrix is bounded by the cells of the
-// whole array at the smallest column width (a region's plan never has more).
-size_t tsort_cells_bound(int64_t K, int tiles) {
-  const int64_t cw = 64ll * TS_SEG * GR_TSORT_NSEG * tsort_waves(tiles), kk = K > 0 ? K : 1;
-  return (size_t)tiles * (size_t)((kk + cw - 1) / cw);
-}
-size_t tile_sort_tmp_bytes(int64_t K, int tiles) {
+// Scratch behind the fixed part: counting sort = per region its count matrix M, its column scan S and its tile
+// totals T (`tiles` = virtual tiles, 2 x screen tiles); radix sort = its temp storage.
+size_t tile_sort_tmp_bytes(int n, int64_t K, int tiles) {
   if (short_keys(tiles)) {
     const int st = tiles / 2;
-    return 4 * align_up(tsort_cells_bound(K, st) * sizeof(int)) + 2 * align_up((size_t)st * sizeof(int));
+    const size_t cells = (size_t)st * col_plan(n, K, st).cols;
+    return 4 * align_up(cells * sizeof(int)) + 2 * align_up((size_t)st * sizeof(int));
   }
   size_t tmp = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const int2*)nullptr,
@@ -511,7 +526,7 @@ size_t sort_tmp_bytes(int64_t K, int bits) {
 }
 
 Bins bins_view(void* base, int tiles, int64_t K) {
-  size_t off[7];
+  size_t off[8];
   bins_fixed(tiles, K, off);
   char* b = (char*)base;
   Bins r;
@@ -522,6 +537,7 @@ Bins bins_view(void* base, int tiles, int64_t K) {
   r.num_items = (int*)(b + off[4]);
   r.tile_item0 = (int*)(b + off[5]);
   r.pos_of = (int*)(b + off[6]);
+  r.ticket = (int*)(b + off[7]);
   return r;
 }
 
@@ -542,6 +558,31 @@ Scratch scratch_view(void* base, int tiles, int64_t K) {
 // ------------------------------------------------------------------------------------------------
 // Kernels: binning.
 // ------------------------------------------------------------------------------------------------
+// Exclusive scan of one value per thread over a block of NW waves (wave shuffles, then the wave totals
+// through LDS); `total` = the block's sum.
+template <int NW>
+__device__ __forceinline__ unsigned long long block_exclusive_scan(unsigned long long x, unsigned long long* sh,
+                                                                   unsigned long long& total) {
+  const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
+  unsigned long long inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  __syncthreads();  // sh may still be read by a previous call
+  if (lane == 63) sh[w] = inc;
+  __syncthreads();
+  unsigned long long base = 0, all = 0;
+#pragma unroll
+  for (int u = 0; u < NW; ++u) {
+    base += u < w ? sh[u] : 0ull;
+    all += sh[u];
+  }
+  total = all;
+  return base + inc - x;
+}
+
 template <int CD>
 __device__ __forceinline__ unsigned long long preprocess_one(const ViewK& v, int i, const float* __restrict__ means,
                                                              const float* __restrict__ scales,
@@ -563,7 +604,8 @@ __global__ __launch_bounds__(256) void k_preprocess(ViewK v, int n, const float*
   unsigned long long kept = 0;
   if (i < n) kept = preprocess_one<CD>(v, i, means, scales, colors, opac, g);
   // the largest opacity of a kept Gaussian (the f16 forward's operand range, f16_sa_of)
-  float om = kept != 0 ? g.rec[(size_t)REC4 * i + 1].x : 0.0f;
+  // (times max(1, z): the depth channel's operand o z ex)
+  float om = kept != 0 ? g.rec[(size_t)REC4 * i + 1].x * fmaxf(1.0f, g.zr[i]) : 0.0f;
   // the block's packed pair counts (core | tail << 32; a block's counts cannot carry): k_plan scans the
   // blocks, k_offsets the Gaussians inside each block
   __shared__ unsigned long long wsum[4];
@@ -599,12 +641,15 @@ __device__ __forceinline__ unsigned long long preprocess_vals(const ViewK& v, in
   int core = 0, tail = 0;
   const int area = tile_rect(v, p, op, r);
   if (area > 0) {
-    for (int ty = r.y; ty <= r.w; ++ty)
+    const float thr_cut = radius_thr(v.cutoff), thr_core = radius_thr(v.core);
+    for (int ty = r.y; ty <= r.w; ++ty) {
+      const float ey = tile_ey(v, p.py, qy, ty);
       for (int tx = r.x; tx <= r.z; ++tx) {
-        const int cls = tile_class(v, p.px, p.py, qx, qy, tx, ty);
+        const int cls = tile_class_e(tile_ex(v, p.px, qx, tx) + ey, thr_cut, thr_core);
         core += cls == 2;
         tail += cls == 1;
       }
+    }
   }
   float4* rec = g.rec + (size_t)REC4 * i;
   rec[0] = make_float4(p.px, p.py, qx, qy);
@@ -662,7 +707,7 @@ __global__ __launch_bounds__(256) void k_preprocess_views(PrepBatch B, int n, co
     }
     unsigned long long kept = 0;
     if (i < n) kept = preprocess_vals<CD>(B.v[k], i, mx, my, mz, s0, s1, colors + (size_t)CD * i, op, g);
-    float om = kept != 0 ? fmaxf(op, 0.0f) : 0.0f;
+    float om = kept != 0 ? fmaxf(op, 0.0f) * fmaxf(1.0f, g.zr[i]) : 0.0f;  // as k_preprocess
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) {
       kept += __shfl_xor(kept, m);
@@ -776,6 +821,83 @@ __global__ __launch_bounds__(256) void k_emit_zones(ViewK v, int n, const int4* 
   }
 }
 
+// Differentiable path, counting-sort views: one block per column of the sort (ColPlan: Gaussians [c G, c G + G),
+// G = 256 J, thread t taking Gaussians c G + t J .. c G + t J + J - 1).  The block
+//   - scans its Gaussians' packed pair counts (core | tail << 32) on top of the column's offset (k_plan's exclusive
+//     scan of the 256-Gaussian block totals) and writes every Gaussian's offsets (the gather and the reductions
+//     read them): no separate offsets pass;
+//   - emits its pairs, core pairs at [0, Kc) and tail pairs at [Kc, K), each in Gaussian order with the tiles in
+//     raster order (a pair's index is its partial-sum slot), staged in LDS and written with coalesced stores (direct
+//     scattered stores when the column overflows the window);
+//   - counts them per tile and zone in LDS and writes its row of each zone's count matrix M: no counting pass.
+constexpr int EWIN_COL = 6144;  // pairs staged in LDS per column block
+inline size_t emit_cols_lds(int tiles, bool tail) { return (size_t)tiles * (tail ? 2 : 1) * sizeof(int) + EWIN_COL * 6; }
+__global__ __launch_bounds__(256) void k_emit_cols(ViewK v, int n, int J, int tiles, const int4* __restrict__ rect,
+                                                   const Cnt2* __restrict__ counts, const unsigned long long* __restrict__ bsum,
+                                                   Cnt2* __restrict__ offsets, const float4* __restrict__ rec,
+                                                   uint16_t* __restrict__ keys, int* __restrict__ ids, int* __restrict__ Mc,
+                                                   int* __restrict__ Mt) {
+  extern __shared__ __attribute__((aligned(16))) int esm[];
+  int* hc = esm;                              // [tiles] core pairs per tile
+  int* ht = hc + tiles;                       // [tiles] tail pairs per tile (Mt != null)
+  int* sI = ht + (Mt ? tiles : 0);            // [EWIN_COL] staged Gaussian ids
+  uint16_t* sK = (uint16_t*)(sI + EWIN_COL);  // [EWIN_COL] staged tile keys
+  __shared__ unsigned long long wsum[4];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const int i0 = c * 256 * J + tid * J, i1 = min(n, i0 + J);
+  for (int t = tid; t < (Mt ? 2 : 1) * tiles; t += 256) hc[t] = 0;
+  unsigned long long own = 0;
+  for (int i = i0; i < i1; ++i) own += counts[i].v;
+  unsigned long long tot;
+  const unsigned long long ex = block_exclusive_scan<4>(own, wsum, tot);  // its barriers publish the zeroed counters
+  const Cnt2 cb{bsum[(size_t)c * J]};
+  const int Kc = (int)offsets[n].c();
+  const int c0 = (int)cb.c(), t0 = (int)cb.t();         // the column's first core pair, first tail pair (after Kc)
+  const int nc = (int)(tot & 0xffffffffull), nt = (int)(tot >> 32);
+  const bool staged = nc + nt <= EWIN_COL;              // uniform per block
+  unsigned long long run = cb.v + ex;
+  for (int i = i0; i < i1; ++i) {
+    const Cnt2 cn = counts[i];
+    offsets[i].v = run;
+    if (cn.v != 0) {
+      const int4 r = rect[i];
+      const float4 a = rec[(size_t)REC4 * i];
+      int kc = (int)(run & 0xffffffffull), kt = (int)(run >> 32);
+      const float thr_cut = radius_thr(v.cutoff), thr_core = radius_thr(v.core);
+      for (int ty = r.y; ty <= r.w; ++ty) {
+        const float ey = tile_ey(v, a.y, a.w, ty);
+        for (int tx = r.x; tx <= r.z; ++tx) {
+          const int cls = tile_class_e(tile_ex(v, a.x, a.z, tx) + ey, thr_cut, thr_core);
+          if (cls == 0) continue;
+          const int t = ty * v.tiles_x + tx;
+          const int e = cls == 2 ? kc++ - c0 : nc + (kt++ - t0);  // index in the column's window
+          atomicAdd(cls == 2 ? &hc[t] : &ht[t], 1);
+          if (staged) {
+            sK[e] = (uint16_t)t;
+            sI[e] = i;
+          } else {
+            const int k = e < nc ? c0 + e : Kc + t0 + (e - nc);
+            keys[k] = (uint16_t)t;
+            ids[k] = i;
+          }
+        }
+      }
+    }
+    run += cn.v;
+  }
+  __syncthreads();
+  if (staged)
+    for (int e = tid; e < nc + nt; e += 256) {
+      const int k = e < nc ? c0 + e : Kc + t0 + (e - nc);
+      keys[k] = sK[e];
+      ids[k] = sI[e];
+    }
+  for (int t = tid; t < tiles; t += 256) {
+    Mc[(size_t)c * tiles + t] = hc[t];
+    if (Mt) Mt[(size_t)c * tiles + t] = ht[t];
+  }
+}
+
 // Radix-sort path: the sorted (id, emission index) values -> the Gaussian ids and the sorted position of
 // each pair by emission index (the counting sort writes both in k_tile_place).
 __global__ __launch_bounds__(256) void k_pos_of(int64_t K, const int2* __restrict__ sorted, int* __restrict__ ids,
@@ -814,83 +936,53 @@ __global__ __launch_bounds__(256) void k_ranges(int64_t K, const KeyT* __restric
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // Work items: each non-empty (virtual) tile's pair list is cut into chunks of CH Gaussians, so every
-// workgroup gets about the same amount of work however unevenly Gaussians fall on tiles.
-// One block; virtual tiles are scanned in order, so items are ordered by (virtual tile, chunk) and
-// the core and tail items of a tile are adjacent.  k_work_items reads existing per-virtual-tile
-// ranges (radix-sort path, empty views).
+// workgroup gets about the same amount of work however unevenly Gaussians fall on tiles; a tile with no pair in
+// either zone gets one empty item (its pixels are background: the forward writes them, and their loss terms).
+// Items are ordered by (virtual tile, chunk), so the core and tail items of a tile are adjacent.  The builders
+// also zero the forward's arrival tickets (Bins::ticket).  k_work_items reads existing per-virtual-tile ranges
+// (radix-sort path, empty views); the counting sort's k_tile_place cuts them from the tile totals
+// (work_items_zones).
 // One workgroup of WI_THREADS (256: it fits beside the splat kernels on a partly occupied CU; a
 // 1024-thread block waits for a whole CU to drain, which under four render streams took up to 1.6 ms).
 #ifndef GR_WI_THREADS
 #define GR_WI_THREADS 256
 #endif
 constexpr int WI_THREADS = GR_WI_THREADS;
+__device__ __forceinline__ int chunks_of(int len) { return (len + CH - 1) / CH; }
 __global__ __launch_bounds__(WI_THREADS) void k_work_items(int vtiles, const int2* __restrict__ ranges, int4* __restrict__ items,
-                                                     int* __restrict__ num_items, int* __restrict__ tile_item0) {
+                                                     int* __restrict__ num_items, int* __restrict__ tile_item0,
+                                                     int* __restrict__ ticket) {
   typedef hipcub::BlockScan<int, WI_THREADS> Scan;
   __shared__ typename Scan::TempStorage tmp;
   __shared__ int carry;
+  const int tiles = vtiles / 2;
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
-  for (int base = 0; base < vtiles; base += WI_THREADS) {
+  for (int base = 0; base < tiles; base += WI_THREADS) {
     const int t = base + (int)threadIdx.x;
-    const int2 r = t < vtiles ? ranges[t] : make_int2(0, 0);
-    const int nch = (r.y - r.x + CH - 1) / CH;
+    const int2 rc = t < tiles ? ranges[2 * t] : make_int2(0, 0), rt = t < tiles ? ranges[2 * t + 1] : make_int2(0, 0);
+    const int chc = chunks_of(rc.y - rc.x), cht = chunks_of(rt.y - rt.x);
+    const int nch = t < tiles ? max(1, chc + cht) : 0;  // an empty tile: one empty item
     int excl, total;
     Scan(tmp).ExclusiveSum(nch, excl, total);
     const int first = carry + excl;
-    if (t < vtiles) {
-      tile_item0[t] = first;
-      for (int c = 0; c < nch; ++c) items[first + c] = make_int4(t, r.x + c * CH, min(r.y, r.x + (c + 1) * CH), c);
+    if (t < tiles) {
+      ticket[t] = 0;
+      tile_item0[2 * t] = first;
+      tile_item0[2 * t + 1] = first + chc;
+      for (int c = 0; c < chc; ++c) items[first + c] = make_int4(2 * t, rc.x + c * CH, min(rc.y, rc.x + (c + 1) * CH), c);
+      for (int c = 0; c < cht; ++c)
+        items[first + chc + c] = make_int4(2 * t + 1, rt.x + c * CH, min(rt.y, rt.x + (c + 1) * CH), c);
+      if (chc + cht == 0) items[first] = make_int4(2 * t, 0, 0, 0);
     }
     __syncthreads();
     if (threadIdx.x == 0) carry += total;
     __syncthreads();
   }
-  if (threadIdx.x == 0) *num_items = carry;
-}
-
-// Counting-sort path: per-tile pair totals of the core region (Tc) and of the tail region (Tt,
-// starting at Kc) are scanned into the virtual-tile ranges (2t: core, 2t+1: tail), then cut.  Thread i
-// owns a contiguous run of tiles: its run's totals are scanned across the block once (three block scans
-// instead of three per 256 tiles), then the run is walked again with running offsets.
-__global__ __launch_bounds__(WI_THREADS) void k_work_items_zones(int tiles, int tiles_x, int Kc, const int* __restrict__ Tc,
-                                                           const int* __restrict__ Tt, int2* __restrict__ ranges,
-                                                           int4* __restrict__ items, int* __restrict__ num_items,
-                                                           int* __restrict__ tile_item0) {
-  typedef hipcub::BlockScan<int, WI_THREADS> Scan;
-  __shared__ typename Scan::TempStorage tmp;
-  const int per = (tiles + WI_THREADS - 1) / WI_THREADS;
-  const int t0 = min(tiles, (int)threadIdx.x * per), t1 = min(tiles, t0 + per);
-  int sc = 0, st = 0, sch = 0;
-  for (int t = t0; t < t1; ++t) {
-    const int nc = Tc ? Tc[t] : 0, nt = Tt ? Tt[t] : 0;  // null: an empty zone
-    sc += nc;
-    st += nt;
-    sch += (nc + CH - 1) / CH + (nt + CH - 1) / CH;
+  if (threadIdx.x == 0) {
+    *num_items = carry;
+    ticket[tiles] = 0;
   }
-  int total;
-  Scan(tmp).ExclusiveSum(sc, sc);
-  __syncthreads();
-  Scan(tmp).ExclusiveSum(st, st);
-  __syncthreads();
-  Scan(tmp).ExclusiveSum(sch, sch, total);
-  for (int t = t0; t < t1; ++t) {
-    const int nc = Tc ? Tc[t] : 0, nt = Tt ? Tt[t] : 0;
-    const int2 rc = nc > 0 ? make_int2(sc, sc + nc) : make_int2(0, 0);
-    const int2 rt = nt > 0 ? make_int2(Kc + st, Kc + st + nt) : make_int2(0, 0);
-    const int chc = (nc + CH - 1) / CH, cht = (nt + CH - 1) / CH;
-    ranges[2 * t] = rc;
-    ranges[2 * t + 1] = rt;
-    tile_item0[2 * t] = sch;
-    tile_item0[2 * t + 1] = sch + chc;
-    for (int c = 0; c < chc; ++c) items[sch + c] = make_int4(2 * t, rc.x + c * CH, min(rc.y, rc.x + (c + 1) * CH), c);
-    for (int c = 0; c < cht; ++c)
-      items[sch + chc + c] = make_int4(2 * t + 1, rt.x + c * CH, min(rt.y, rt.x + (c + 1) * CH), c);
-    sc += nc;
-    st += nt;
-    sch += chc + cht;
-  }
-  if (threadIdx.x == 0) *num_items = total;
 }
 
 // Staging pipeline for the 256-wide Gaussian batches of a work item: the records of batch b+1 are
@@ -959,26 +1051,25 @@ __device__ __forceinline__ int xcd_item(int b, int nwg) {
 }
 
 // ---- Stable counting sort of the pairs by tile -------------------------------------------------
-// The emitted pairs are cut into columns of cw consecutive pairs, one workgroup of `waves` waves
-// per column, wave w owning the w-th part of its column.
-//   k_tile_count    counts each column's pairs per tile into M[column][tile];
-//   k_tile_colscan  scans M over the columns of each tile (S = start of (column, tile) within the
-//                   tile) and writes the tile's total T[tile];
-//   k_work_items    scans T into the tile ranges (and cuts the work items);
-//   k_tile_place    re-counts per wave, turns ranges + S into per-wave cursors and walks each wave's
-//                   pairs in order, 64 at a time.  Lanes holding the same tile in one step are ranked
-//                   by bit-plane ballots (one ballot per key bit: the lanes agreeing with this lane on
-//                   every bit), and the highest lane of each group advances the tile's cursor.
+// The emitted pairs of each region (zone 0: core pairs [0, Kc), zone 1: tail pairs [Kc, K)) are cut into columns:
+// column c = the region's pairs of the Gaussians [c G, c G + G) (ColPlan), three dependent launches:
+//   k_emit_cols     emits the pairs and counts each column's pairs per tile into M[column][tile] (and writes the
+//                   Gaussians' offsets);
+//   k_tile_colscan  scans M over the columns of each tile (S = start of (column, tile) within the tile) and
+//                   writes the tile's total T[tile];
+//   k_tile_place    one block per (region, column): scans T into the tile starts itself, re-counts per wave,
+//                   turns tile starts + S into per-wave cursors and walks each wave's pairs in order, 64 at a
+//                   time.  Lanes holding the same tile in one step are ranked by bit-plane ballots (one ballot
+//                   per key bit: the lanes agreeing with this lane on every bit), and the highest lane of each
+//                   group advances the tile's cursor.  Block 0 of the launch instead cuts the per-virtual-tile
+//                   ranges and work items the splats read (work_items_zones), beside the placing blocks.
 // Everything is walked in pair order, so the Gaussian ids inside each tile come out ascending:
 // exactly the oracle's stable sort (oracle/gr_oracle.c gro_bin), and deterministic.
 constexpr int TS_RB = 9, TS_RH = 1 << (TS_RB - 1);  // relative tile keys in ts_place
-constexpr int TS_CQ = 8;    // tiles per thread per round of k_tile_place's cursor pass
 
-// The two regions (zone 0: core pairs [0, Kc), zone 1: tail pairs [Kc, K)) are sorted by the same three
-// launches: the column blocks of zone 0 come first in the grid, then zone 1's (k_tile_colscan: blockIdx.y).
 struct TZone {
   int64_t K;              // pairs of the region
-  int cw, cols;           // its tsort_plan
+  int cols;               // its columns (0: an empty region)
   int zbase;              // emission index of its first pair
   const uint16_t* keys;   // its keys and ids (emission order)
   const int* ids;
@@ -988,36 +1079,21 @@ struct TZone {
 };
 struct TZones {
   TZone z[2];
+  const Cnt2* offsets;  // the Gaussians' packed offsets (k_emit_cols; offsets[n] = the region totals)
+  int n, G;             // Gaussians, Gaussians per column
 };
 // Column block b of the combined grid -> (zone, column), XCD-aware within the grid.
-__device__ __forceinline__ int tzone_of(const TZones& Z, int& c) {
-  const int b = xcd_item(blockIdx.x, Z.z[0].cols + Z.z[1].cols);
+__device__ __forceinline__ int tzone_of(const TZones& Z, int b, int& c) {
+  b = xcd_item(b, Z.z[0].cols + Z.z[1].cols);
   const int zone = b < Z.z[0].cols ? 0 : 1;
   c = b - (zone ? Z.z[0].cols : 0);
   return zone;
 }
-
-__global__ __launch_bounds__(256) void k_tile_count(TZones Z, int tiles) {
-  extern __shared__ int hist[];
-  int c;
-  const TZone& zz = Z.z[tzone_of(Z, c)];
-  const int64_t K = zz.K;
-  const int cw = zz.cw;
-  const uint16_t* __restrict__ keys = zz.keys;
-  int* __restrict__ M = zz.M;
-  for (int t = threadIdx.x; t < tiles; t += 256) hist[t] = 0;
-  __syncthreads();
-  const int64_t k0 = (int64_t)c * cw, k1 = min(K, k0 + cw);
-  for (int64_t kb = k0 + threadIdx.x; kb < k1; kb += 256 * 8) {
-    int d[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] = kb + j * 256 < k1 ? (int)keys[kb + j * 256] : -1;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (d[j] >= 0) atomicAdd(&hist[d[j]], 1);
-  }
-  __syncthreads();
-  for (int t = threadIdx.x; t < tiles; t += 256) M[(size_t)c * tiles + t] = hist[t];
+// Pairs [k0, k1) of column c in region `zone`, relative to the region's first pair.
+__device__ __forceinline__ void column_range(const TZones& Z, int zone, int c, int64_t& k0, int64_t& k1) {
+  const Cnt2 a = Z.offsets[min(Z.n, c * Z.G)], b = Z.offsets[min(Z.n, (c + 1) * Z.G)];
+  k0 = zone ? a.t() : a.c();
+  k1 = zone ? b.t() : b.c();
 }
 
 // Column scan of M: S[c][t] = sum of M[c'][t] over c' < c, T[t] = the tile's total.  A block takes
@@ -1039,7 +1115,7 @@ constexpr int CS_T = GR_CS_T, CS_G = GR_CS_THREADS / GR_CS_T, CS_R = GR_CS_R;
 
 __global__ __launch_bounds__(GR_CS_THREADS) void k_tile_colscan(TZones Z, int tiles) {
   const TZone& zz = Z.z[blockIdx.y];
-  if (zz.K == 0) return;  // an empty region: no counts, and k_work_items_zones gets no totals for it
+  if (zz.K == 0) return;  // an empty region: no counts, and the work items get no totals for it
   const int cols = zz.cols;
   const int* __restrict__ M = zz.M;
   int* __restrict__ S = zz.S;
@@ -1143,42 +1219,106 @@ __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int 
   }
 }
 
-// ranges: per virtual tile; this region's pairs go to tile t's list 2t + zone.
+// Counting-sort views: the per-tile totals of the core region (Tc) and of the tail region (Tt, starting at Kc)
+// scanned into the virtual-tile ranges (2t: core, 2t+1: tail), then cut into work items of <= CH pairs.  Thread i
+// owns a contiguous run of tiles: its run's totals are scanned across the block once (three block scans instead of
+// three per NT tiles), then the run is walked again with running offsets.  Block 0 of k_tile_place.
+template <int NT>
+__device__ __forceinline__ void work_items_zones(int tiles, int Kc, const int* __restrict__ Tc, const int* __restrict__ Tt,
+                                                 int2* __restrict__ ranges, int4* __restrict__ items,
+                                                 int* __restrict__ num_items, int* __restrict__ tile_item0,
+                                                 int* __restrict__ ticket) {
+  typedef hipcub::BlockScan<int, NT> Scan;
+  __shared__ typename Scan::TempStorage tmp;
+  const int per = (tiles + NT - 1) / NT;
+  const int t0 = min(tiles, (int)threadIdx.x * per), t1 = min(tiles, t0 + per);
+  int sc = 0, st = 0, sch = 0;
+  for (int t = t0; t < t1; ++t) {
+    const int nc = Tc ? Tc[t] : 0, nt = Tt ? Tt[t] : 0;  // null: an empty zone
+    sc += nc;
+    st += nt;
+    sch += max(1, chunks_of(nc) + chunks_of(nt));  // an empty tile: one empty item
+  }
+  int total;
+  Scan(tmp).ExclusiveSum(sc, sc);
+  __syncthreads();
+  Scan(tmp).ExclusiveSum(st, st);
+  __syncthreads();
+  Scan(tmp).ExclusiveSum(sch, sch, total);
+  for (int t = t0; t < t1; ++t) {
+    const int nc = Tc ? Tc[t] : 0, nt = Tt ? Tt[t] : 0;
+    const int2 rc = nc > 0 ? make_int2(sc, sc + nc) : make_int2(0, 0);
+    const int2 rt = nt > 0 ? make_int2(Kc + st, Kc + st + nt) : make_int2(0, 0);
+    const int chc = chunks_of(nc), cht = chunks_of(nt);
+    ranges[2 * t] = rc;
+    ranges[2 * t + 1] = rt;
+    tile_item0[2 * t] = sch;
+    tile_item0[2 * t + 1] = sch + chc;
+    ticket[t] = 0;
+    for (int c = 0; c < chc; ++c) items[sch + c] = make_int4(2 * t, rc.x + c * CH, min(rc.y, rc.x + (c + 1) * CH), c);
+    for (int c = 0; c < cht; ++c)
+      items[sch + chc + c] = make_int4(2 * t + 1, rt.x + c * CH, min(rt.y, rt.x + (c + 1) * CH), c);
+    if (chc + cht == 0) items[sch] = make_int4(2 * t, 0, 0, 0);
+    sc += nc;
+    st += nt;
+    sch += max(1, chc + cht);
+  }
+  if (threadIdx.x == 0) {
+    *num_items = total;
+    ticket[tiles] = 0;
+  }
+}
+
+// Grid: 1 + the columns of both regions (block 0: the work items).  LDS: the per-wave cursors [waves][tiles].
 #ifndef GR_PLACE_WAVES
 #define GR_PLACE_WAVES 3
 #endif
-__global__ __launch_bounds__(256, GR_PLACE_WAVES) void k_tile_place(TZones Z, int tiles, int bits,
-                                                    const int2* __restrict__ ranges, int* __restrict__ pairs_out,
-                                                    int* __restrict__ pos_of) {
-  extern __shared__ int cur[];  // [waves][tiles]
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES, GR_PLACE_WAVES) void k_tile_place(TZones Z, int tiles, int bits,
+                                                                    int2* __restrict__ ranges, int4* __restrict__ items,
+                                                                    int* __restrict__ num_items, int* __restrict__ tile_item0,
+                                                                    int* __restrict__ ticket, int* __restrict__ pairs_out,
+                                                                    int* __restrict__ pos_of) {
+  if (blockIdx.x == 0) {
+    work_items_zones<64 * WAVES>(tiles, Z.z[1].zbase, Z.z[0].K > 0 ? Z.z[0].T : nullptr, Z.z[1].K > 0 ? Z.z[1].T : nullptr,
+                                 ranges, items, num_items, tile_item0, ticket);
+    return;
+  }
+  extern __shared__ int cur[];  // [WAVES][tiles]
+  __shared__ int wsc[WAVES];
   int c;
-  const int zone = tzone_of(Z, c);
+  const int zone = tzone_of(Z, (int)blockIdx.x - 1, c);
   const TZone& zz = Z.z[zone];
   const int64_t K = zz.K;
-  const int cw = zz.cw, zbase = zz.zbase;
+  const int zbase = zz.zbase;
   const uint16_t* __restrict__ keys = zz.keys;
   const int* __restrict__ ids_in = zz.ids;
   const int* __restrict__ S = zz.S;
-  const int waves = (int)blockDim.x >> 6, w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+  const int* __restrict__ T = zz.T;
+  constexpr int NT = 64 * WAVES;
+  const int w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
   int* my = cur + (size_t)w * tiles;
-  const int pw = cw / waves, nseg = pw / (64 * TS_SEG);
-  const int64_t k0 = (int64_t)c * cw + (int64_t)w * pw, k1 = min(K, k0 + pw);
+  int64_t kc0, kc1;
+  column_range(Z, zone, c, kc0, kc1);
+  // this wave's part of the column: whole 64-pair steps, the parts in wave order
+  const int64_t steps = (kc1 - kc0 + 63) / 64, wsteps = (steps + WAVES - 1) / WAVES;
+  const int64_t k0 = min(kc1, kc0 + (int64_t)w * wsteps * 64), k1 = min(kc1, k0 + wsteps * 64);
+  const int nseg = (int)((wsteps + TS_SEG - 1) / TS_SEG);
   int d[TS_SEG], id[TS_SEG];
-  ts_load(k0, k1, K - 1, lane, keys, ids_in, d, id);  // in flight while the counters are cleared
-  // Tile bases (tile start + this column's start within the tile) of the cursor pass, TS_CQ tiles per
-  // thread per round, loaded together (one memory latency per round, not one per tile); the first
-  // round is issued here, under the count pass.
-  int rx[TS_CQ], sx[TS_CQ];
-  auto load_bases = [&](int t0) {
-#pragma unroll
-    for (int q = 0; q < TS_CQ; ++q) {
-      const int t = min(t0 + q * (int)blockDim.x, tiles - 1);
-      rx[q] = ranges[2 * t + zone].x;
-      sx[q] = S[(size_t)c * tiles + t];
-    }
-  };
-  load_bases((int)threadIdx.x);
+  ts_load(k0, k1, K - 1, lane, keys, ids_in, d, id);  // in flight while the tile starts are scanned
   for (int t = lane; t < tiles; t += 64) my[t] = 0;
+  // tile starts: thread i owns the contiguous tiles [i per, i per + per); their totals' exclusive scan over the block
+  const int per = (tiles + NT - 1) / NT;
+  const int tb = min(tiles, (int)threadIdx.x * per), te = min(tiles, tb + per);
+  int own = 0;
+  for (int t = tb; t < te; ++t) own += T[t];
+  int incl = own;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsc[w] = incl;
   __builtin_amdgcn_wave_barrier();
   for (int seg = 0; seg < nseg; ++seg) {  // this wave's count per tile
     if (seg > 0) ts_load(k0 + (int64_t)seg * 64 * TS_SEG, k1, K - 1, lane, keys, ids_in, d, id);
@@ -1189,19 +1329,17 @@ __global__ __launch_bounds__(256, GR_PLACE_WAVES) void k_tile_place(TZones Z, in
     for (int j = 0; j < TS_SEG; ++j) atomicAdd(&my[d[j] < 0 ? 0 : d[j]], (d[j] < 0 ? 0 : 1) + (id[j] >> 31));
   }
   __syncthreads();
-  // cursor of (tile, wave) = tile start + column start within the tile + lower waves' counts
-  for (int t0 = threadIdx.x; t0 < tiles; t0 += TS_CQ * (int)blockDim.x) {
-    if (t0 != (int)threadIdx.x) load_bases(t0);
+  // cursor of (tile, wave) = region start + tile start + column start within the tile + lower waves' counts
+  int run = zbase + incl - own;
+  for (int u = 0; u < w; ++u) run += wsc[u];
+  for (int t = tb; t < te; ++t) {
+    int r = run + S[(size_t)c * tiles + t];
+    run += T[t];
 #pragma unroll
-    for (int q = 0; q < TS_CQ; ++q) {
-      const int t = t0 + q * (int)blockDim.x;
-      if (t >= tiles) break;
-      int run = rx[q] + sx[q];
-      for (int u = 0; u < waves; ++u) {
-        const int n = cur[(size_t)u * tiles + t];
-        cur[(size_t)u * tiles + t] = run;
-        run += n;
-      }
+    for (int u = 0; u < WAVES; ++u) {
+      const int m = cur[(size_t)u * tiles + t];
+      cur[(size_t)u * tiles + t] = r;
+      r += m;
     }
   }
   __syncthreads();
@@ -1339,10 +1477,11 @@ __device__ __forceinline__ void split3_frag2(const f32x2_t (&v)[4], s16x8 (&f)[3
 #ifndef GR_F16_SB
 #define GR_F16_SB 12
 #endif
-// The A pre-scale of a view: 2^GR_F16_SA while its largest opacity (of a kept Gaussian) is below 2^11,
-// lowered by one per binade above, so o * c * ex * 2^sa <= 2^15 always (no inf, whatever the opacities;
-// k_plan computes it from k_preprocess's per-block maxima).  Views with opacities in (0, 2048) - every
-// fit, whose opacities are sigmoid outputs - get exactly GR_F16_SA.  The A operands are o c ex with o = max(op, 0)
+// The A pre-scale of a view: 2^GR_F16_SA while the largest o max(1, z) of its kept Gaussians is below 2^11,
+// lowered by one per binade above, so o * c * ex * 2^sa and the depth channel's o * z * ex * 2^sa stay <= 2^15
+// (no inf, whatever the opacities and depths; k_plan computes it from k_preprocess's per-block maxima).  Views with
+// o z below 2048 - every fit, whose opacities are sigmoid outputs, at any sane camera distance - get exactly
+// GR_F16_SA.  The A operands are o c ex with o = max(op, 0)
 // (the record's clamp, torch_renderer.py:177) and c clamped to [0, 1] (:144), so |A| <= 2^sa max(op, 0): a negative
 // opacity contributes nothing and needs no range (tests/test_scale_gpu.py, opacities down to -1e5).
 __device__ __forceinline__ int f16_sa_of(float omax) {
@@ -1438,7 +1577,9 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
   int idn = stage_id(k0 + TP + tid, k1, pairs);
   int buf = 0;
   const f32x2_t X = {xc, xc}, Y = {yc, yc};
-  constexpr bool F16 = GR_FWD_F16 && !PRECISE && !ZCH;
+  // core items outside f32 grade take f16 pieces (W, the colours and D); tail items (their small weights would be
+  // f16 subnormals) two bf16 pieces
+  constexpr bool F16 = GR_FWD_F16 && !PRECISE && !TAIL;
   const f32x2_t SA = {sa, sa}, SB = {(float)GR_F16_SB, (float)GR_F16_SB};
   (void)SA;
   (void)SB;
@@ -1492,11 +1633,15 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
           split3_frag2(aD, f3);
           cD = mfma16_split3(f3, fb, cD);
         }
-      } else if (F16) {  // f16 pieces of the pre-scaled operands (no depth channel)
+      } else if (F16) {  // f16 pieces of the pre-scaled operands
         s16x8 f2[2];
         split2h_frag2(bv, fb2h);
         split2h_frag2(aW, f2);
         cW = mfma16h_split2(f2, fb2h, cW);
+        if constexpr (ZCH) {  // o z ex 2^sa: f16_sa_of sized sa by the view's largest o max(1, z)
+          split2h_frag2(aD, f2);
+          cD = mfma16h_split2(f2, fb2h, cD);
+        }
       } else {  // no depth gradient will follow: W and D need only what the colours need
         s16x8 f2b[2], f2[2];
         split2_frag2(bv, f2b);
@@ -1573,6 +1718,17 @@ __device__ __forceinline__ void write_pixel(const ViewK& v, int p, const float* 
   }
 }
 
+// gr_fwd_compose: a view's outputs from its saved pixel sums (write_pixel), with the view's background.
+__global__ __launch_bounds__(256) void k_compose(ViewK v, int hw, const float4* __restrict__ saved4,
+                                                 const float* __restrict__ savedD, float* __restrict__ out_rgb,
+                                                 float* __restrict__ out_alpha, float* __restrict__ out_depth) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= hw) return;
+  const float4 a = saved4[p];
+  const float acc[5] = {a.x, a.y, a.z, a.w, savedD[p]};
+  write_pixel(v, p, acc, out_rgb, out_alpha, out_depth, nullptr, nullptr);
+}
+
 // bf16 split-precision backward (k_raster_bwd_bf16): per tile, A fragments of v_mfma_f32_32x32x16_bf16
 // for 2 sides (T: contraction over x, R: over y) x 3 channel pairs x 3 bf16 pieces x 64 lanes, 16 B each.
 constexpr int UF_FRAGS = 2 * 3 * 3 * 64;  // uint4 per tile
@@ -1606,7 +1762,63 @@ struct L1Args {
   float w_depth = 0.0f;
   const float* dscal = nullptr;    // device scalars: [0] max(depth), [1] the max's gradient per arg-max pixel
   int pieces = 2;                  // bf16 pieces of the upstream fragments (gr_fwd_render_l1: 3 at f32 grade)
+  // gr_fwd_render_l1: the view loss, written by the forward's last finished tile (photometric / silhouette element
+  // counts n1 / n2, as k_tile_loss_final)
+  float* loss_out = nullptr;
+  int64_t n1 = 0, n2 = 0;
 };
+
+// Write-through (sc1) stores and loads of data handed from one workgroup to another inside a launch, with an
+// arrival ticket (MI355X_MICROARCH.md, Valid forms, first row of the hand-off table: every store and load of the
+// handed-off bytes sc1; each storing wave drained, a barrier, then one lane's agent-scope atomic add; the workgroup
+// whose add returns count - 1 reads after its add has returned and a barrier).
+__device__ __forceinline__ void st_through(float* p, float x) { __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ float ld_through(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Every thread of the block calls this after its write-through stores: true in the block that arrives last of
+// `count` (uniform per block).  `flag`: one LDS word.
+__device__ __forceinline__ bool arrive_last(int* ticket, int count, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have completed
+  __syncthreads();                                   // ... and every wave's
+  if (threadIdx.x == 0) *flag = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == count - 1;
+  __syncthreads();
+  return *flag != 0;
+}
+
+// The view loss from the per-tile L1 sums (one block of 256 threads; double sums in a fixed order):
+// mean |out - t| + w_sil mean |alpha - m| (+ w_depth mean |d_pred - t_d| with n3 > 0).  THROUGH: the sums were
+// written in the same launch (write-through, arrive_last).
+template <bool THROUGH>
+__device__ __forceinline__ void tile_loss_total(const float* __restrict__ tile_loss, int tiles, int64_t n1, int64_t n2,
+                                                float w_sil, int64_t n3, float w_depth, float* __restrict__ loss,
+                                                double (*r)[256]) {
+  const int t = threadIdx.x;
+  auto ld = [&](int i) { return THROUGH ? ld_through(tile_loss + i) : tile_loss[i]; };
+  double s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  for (int i = t; i < tiles; i += 256) {
+    s1 += (double)ld(4 * i);
+    s2 += (double)ld(4 * i + 1);
+    if (n3 > 0) s3 += (double)ld(4 * i + 2);
+  }
+  r[0][t] = s1;
+  r[1][t] = s2;
+  r[2][t] = s3;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) {
+      r[0][t] += r[0][t + w];
+      r[1][t] += r[1][t + w];
+      r[2][t] += r[2][t + w];
+    }
+    __syncthreads();
+  }
+  if (t != 0) return;
+  float l = (float)(r[0][0] / (double)n1);
+  if (n2 > 0) l = l + w_sil * (float)(r[1][0] / (double)n2);
+  if (n3 > 0) l = l + w_depth * (float)(r[2][0] / (double)n3);
+  *loss = l;
+}
 
 __device__ __forceinline__ float sign0(float t) { return t > 0.0f ? 1.0f : (t < 0.0f ? -1.0f : 0.0f); }
 
@@ -1777,8 +1989,9 @@ __device__ __forceinline__ void tile_loss_sums(int tile, int tid, float l_rgb, f
   }
   __syncthreads();
   if (tid == 0) {
-    tile_loss[4 * tile] = ((sL[0][0] + sL[0][1]) + sL[0][2]) + sL[0][3];
-    tile_loss[4 * tile + 1] = ((sL[1][0] + sL[1][1]) + sL[1][2]) + sL[1][3];
+    // write-through: the forward's last finished tile reads them in the same launch (arrive_last)
+    st_through(&tile_loss[4 * tile], ((sL[0][0] + sL[0][1]) + sL[0][2]) + sL[0][3]);
+    st_through(&tile_loss[4 * tile + 1], ((sL[1][0] + sL[1][1]) + sL[1][2]) + sL[1][3]);
   }
 }
 
@@ -1883,9 +2096,11 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
                                                          float* __restrict__ fwd_part, float* __restrict__ out_rgb,
                                                          float* __restrict__ out_alpha, float* __restrict__ out_depth,
                                                          float4* __restrict__ saved4, float* __restrict__ savedD,
-                                                         L1Args l1, uint4* __restrict__ UF, const int* __restrict__ f16_sa) {
+                                                         L1Args l1, uint4* __restrict__ UF, const int* __restrict__ f16_sa,
+                                                         const int* __restrict__ tile_item0, int* __restrict__ ticket) {
   // LDS: two staged record buffers (2 x 9 KiB) during the loop, then the 4-wave reduction (20 KiB).
   __shared__ __attribute__((aligned(16))) float smem[4 * 5 * TP];
+  __shared__ int last_flag;
   const int nitems = *num_items;
   if ((int)blockIdx.x >= nitems) return;
   const int item = xcd_item(blockIdx.x, nitems);
@@ -1897,18 +2112,21 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
   const float xc = (float)(tx * T + li) + 0.5f;  // A row = x
   const float yc = (float)(ty * T + li) + 0.5f;  // B col = y
   f32x4 cW = {0.f, 0.f, 0.f, 0.f}, cR = cW, cG = cW, cB = cW, cD = cW;
-  constexpr bool PREC = MODE == 1 || MODE == 5, ZCHK = MODE < 3, F16K = GR_FWD_F16 && (MODE == 3 || MODE == 4);
-  const int sa = F16K ? *f16_sa : GR_F16_SA;  // the view's A pre-scale (f16_sa_of)
-  if (it.x & 1)  // tail items: W and D only, two-piece splits (GR_TAIL2)
-    fwd_accumulate_bf16<true, PREC && !GR_TAIL2, ZCHK>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD, (float)sa);
-  else
-    fwd_accumulate_bf16<false, PREC, ZCHK>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD, (float)sa);
-  if constexpr (F16K) {  // the operands carried 2^sa and 2^SB (exact power-of-two rescale)
+  constexpr bool PREC = MODE == 1 || MODE == 5, ZCHK = MODE < 3, F16K = GR_FWD_F16 && MODE >= 2 && MODE <= 4;
+  const int sa = F16K && f16_sa ? *f16_sa : GR_F16_SA;  // the view's A pre-scale (f16_sa_of; none: no pair to scale)
+  if (k1 > k0) {  // (an empty tile's one item has no pair)
+    if (it.x & 1)  // tail items: W and D only, two-piece splits (GR_TAIL2)
+      fwd_accumulate_bf16<true, PREC && !GR_TAIL2, ZCHK>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD, (float)sa);
+    else
+      fwd_accumulate_bf16<false, PREC, ZCHK>(smem, n, k0, k1, tid, wave, xc, yc, gs, pairs, rec, cW, cR, cG, cB, cD, (float)sa);
+  }
+  if (F16K && !(it.x & 1)) {  // a core item's operands carried 2^sa and 2^SB (exact power-of-two rescale)
     const float sc = __builtin_ldexpf(1.0f, -(sa + GR_F16_SB));
     cW *= sc;
     cR *= sc;
     cG *= sc;
     cB *= sc;
+    cD *= sc;
   }
   __syncthreads();
   {  // lane holds C[x = 4*gs + r][y = li]: pixel index y*16 + x, 4 consecutive x
@@ -1925,42 +2143,36 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
   for (int c = 0; c < 5; ++c)
     acc[c] = ((smem[0 * 5 * TP + c * TP + tid] + smem[1 * 5 * TP + c * TP + tid]) + smem[2 * 5 * TP + c * TP + tid]) +
              smem[3 * 5 * TP + c * TP + tid];
-  if (tile_chunks(ranges[2 * tile]) + tile_chunks(ranges[2 * tile + 1]) > 1) {
-    // tile split over several items: combine in k_fwd_finalize
+  const int nch = tile_chunks(ranges[2 * tile]) + tile_chunks(ranges[2 * tile + 1]);
+  if (nch > 1) {
+    // a tile split over several items: each leaves its partial sums (write-through) and takes the tile's ticket;
+    // the last to arrive sums every item's partials in item order (deterministic) and finishes the tile
     float* dst = fwd_part + (size_t)item * 5 * TP;
 #pragma unroll
-    for (int c = 0; c < 5; ++c) dst[c * TP + tid] = acc[c];
-    return;
+    for (int c = 0; c < 5; ++c) st_through(dst + c * TP + tid, acc[c]);
+    if (!arrive_last(&ticket[tile], nch, &last_flag)) return;
+    const float* src = fwd_part + (size_t)tile_item0[2 * tile] * 5 * TP;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) acc[c] = 0.f;
+    for (int q = 0; q < nch; ++q)
+#pragma unroll
+      for (int c = 0; c < 5; ++c) acc[c] += ld_through(src + (size_t)q * 5 * TP + c * TP + tid);
+    if (tid == 0) ticket[tile] = 0;  // left zero for a later render of the same bins
   }
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
   const bool inside = x < v.W && y < v.H;
   if (inside) write_pixel(v, y * v.W + x, acc, out_rgb, out_alpha, out_depth, saved4, savedD);
-  if constexpr (MODE == 4 || MODE == 5) l1_tile_epilogue(v, tile, tid, acc, inside, y * v.W + x, l1, UF, smem);
-}
-
-// Tiles with no Gaussians (background) or split over several work items: sum the items' partial
-// accumulators in item order (core chunks, then tail chunks: deterministic) and write the outputs
-// (and with l1.t_rgb the fit loss's upstream fragments, as k_raster_fwd_mfma<4>).
-__global__ __launch_bounds__(256) void k_fwd_finalize(ViewK v, const int2* __restrict__ ranges,
-                                                      const int* __restrict__ tile_item0, const float* __restrict__ fwd_part,
-                                                      float* __restrict__ out_rgb, float* __restrict__ out_alpha,
-                                                      float* __restrict__ out_depth, float4* __restrict__ saved4,
-                                                      float* __restrict__ savedD, L1Args l1, uint4* __restrict__ UF) {
-  __shared__ float lds[4 * TP];
-  const int tile = blockIdx.x, tid = threadIdx.x;
-  const int nch = tile_chunks(ranges[2 * tile]) + tile_chunks(ranges[2 * tile + 1]);
-  if (nch == 1) return;  // written by k_raster_fwd_mfma
-  float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  const float* src = fwd_part + (size_t)(nch > 0 ? tile_item0[2 * tile] : 0) * 5 * TP;
-  for (int c = 0; c < nch; ++c)
-#pragma unroll
-    for (int q = 0; q < 5; ++q) acc[q] += src[(size_t)c * 5 * TP + q * TP + tid];
-  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
-  const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
-  const bool inside = x < v.W && y < v.H;
-  if (inside) write_pixel(v, y * v.W + x, acc, out_rgb, out_alpha, out_depth, saved4, savedD);
-  // an empty tile has no backward work item: only its loss terms are needed, not its fragments
-  if (l1.t_rgb) l1_tile_epilogue(v, tile, tid, acc, inside, y * v.W + x, l1, UF, lds, nch > 0);
+  if constexpr (MODE == 4 || MODE == 5) {
+    // an empty tile has no backward work item: only its loss terms are needed, not its fragments
+    l1_tile_epilogue(v, tile, tid, acc, inside, y * v.W + x, l1, UF, smem, nch > 0);
+    // the view loss: the last tile to finish sums the tiles' L1 sums (k_tile_loss_final's order)
+    const int tiles = v.tiles_x * v.tiles_y;
+    if (arrive_last(&ticket[tiles], tiles, &last_flag)) {
+      tile_loss_total<true>(l1.tile_loss, tiles, l1.n1, l1.n2, l1.w_sil, 0, 0.0f, l1.loss_out,
+                            reinterpret_cast<double (*)[256]>(smem));
+      if (tid == 0) ticket[tiles] = 0;
+    }
+  }
 }
 
 // Sum over the 4 lane rows (lanes l, l+16, l+32, l+48) of a pair of values with one
@@ -2273,6 +2485,7 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
   const bool tail = it.x & 1;
   if (tail && !DEPTH) return;
   const int tile = it.x >> 1, k0 = it.y, k1 = it.z;
+  if (k1 <= k0) return;  // an empty tile's item: nothing to differentiate
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   {  // the tile's A fragments this item contracts -> LDS (DMA): chunk (side * 3 + pair) * 3 + piece
@@ -2353,7 +2566,8 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
                                                     const Cnt2* __restrict__ offsets, const int* __restrict__ pos_of,
                                                     const float* __restrict__ partials, float* __restrict__ d_means,
                                                     float* __restrict__ d_scales, float* __restrict__ d_colors,
-                                                    float* __restrict__ d_opac, int depth, int acc) {
+                                                    float* __restrict__ d_opac, int depth, int acc,
+                                                    const int* __restrict__ out_index) {
   const int g0 = blockIdx.x * RG;
   const int tid = threadIdx.x, q4 = tid & 3;
   const int i = g0 + (tid >> 2);
@@ -2435,7 +2649,8 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
 #pragma unroll
   for (int q = 0; q < NPART; ++q) Sf[q] = sS[tid][q];
   const int gi = g0 + tid;
-  GradOut out{d_means + 3 * (size_t)gi, d_scales + 3 * (size_t)gi, d_colors + (size_t)CD * gi, d_opac + gi, acc != 0};
+  const size_t go = out_index ? (size_t)out_index[gi] : (size_t)gi;  // the row of Gaussian gi in the gradients
+  GradOut out{d_means + 3 * go, d_scales + 3 * go, d_colors + (size_t)CD * go, d_opac + go, acc != 0};
   chain_rule<CD, float>(v, gi, Sf, sS[tid][NPART] != 0.0f ? 1u : 0u, means, scales, colors, opac, out);
 }
 
@@ -2704,7 +2919,7 @@ __global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const floa
                                                      const float* __restrict__ scales, const float* __restrict__ colors,
                                                      const float* __restrict__ opac, float* __restrict__ d_means,
                                                      float* __restrict__ d_scales, float* __restrict__ d_colors,
-                                                     float* __restrict__ d_opac, int acc) {
+                                                     float* __restrict__ d_opac, int acc, const int* __restrict__ out_index) {
   constexpr int NG = 6 + CD;
   __shared__ float sG[CD == 48 ? 1 : 4][64][NG + 1];
   const int crw = reduce_sums_crw(B.nv, CD);
@@ -2752,7 +2967,8 @@ __global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const floa
     }
   }
   if (u != 0 || gi >= n) return;
-  GradOut out{d_means + 3 * (size_t)gi, d_scales + 3 * (size_t)gi, d_colors + (size_t)CD * gi, d_opac + gi, acc != 0};
+  const size_t go = out_index ? (size_t)out_index[gi] : (size_t)gi;  // the row of Gaussian gi in the gradients
+  GradOut out{d_means + 3 * go, d_scales + 3 * go, d_colors + (size_t)CD * go, d_opac + go, acc != 0};
 #pragma unroll
   for (int q = 0; q < 3; ++q) out.mean(q, gr.m[q]);
   out.scale(0, gr.s[0]);
@@ -3191,31 +3407,8 @@ __global__ __launch_bounds__(256) void k_l1_final(const float* __restrict__ part
 __global__ __launch_bounds__(256) void k_tile_loss_final(const float* __restrict__ tile_loss, int tiles, int64_t n1,
                                                          int64_t n2, float w_sil, int64_t n3, float w_depth,
                                                          float* __restrict__ loss) {
-  __shared__ double r1[256], r2[256], r3[256];
-  const int t = threadIdx.x;
-  double s1 = 0.0, s2 = 0.0, s3 = 0.0;
-  for (int i = t; i < tiles; i += 256) {
-    s1 += (double)tile_loss[4 * i];
-    s2 += (double)tile_loss[4 * i + 1];
-    if (n3 > 0) s3 += (double)tile_loss[4 * i + 2];
-  }
-  r1[t] = s1;
-  r2[t] = s2;
-  r3[t] = s3;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (t < w) {
-      r1[t] += r1[t + w];
-      r2[t] += r2[t + w];
-      r3[t] += r3[t + w];
-    }
-    __syncthreads();
-  }
-  if (t != 0) return;
-  float l = (float)(r1[0] / (double)n1);
-  if (n2 > 0) l = l + w_sil * (float)(r2[0] / (double)n2);
-  if (n3 > 0) l = l + w_depth * (float)(r3[0] / (double)n3);
-  *loss = l;
+  __shared__ double r[3][256];
+  tile_loss_total<false>(tile_loss, tiles, n1, n2, w_sil, n3, w_depth, loss, r);
 }
 
 // d/da = g sign(a - b) / n1, d/dc = (w2 g) sign(c - d) / n2 (torch: abs' = sign, sign(0) = 0).
@@ -3368,7 +3561,7 @@ void gr_geom_layout(int n, size_t offsets_out[GR_GEOM_PARTS]) { geom_fixed(n, of
 
 void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[4]) {
   (void)n;
-  size_t off[7];
+  size_t off[8];
   bins_fixed(vtiles_of(v), plan ? plan->num_pairs : 0, off);
   offsets_out[0] = off[0];
   offsets_out[1] = off[1];
@@ -3385,15 +3578,14 @@ size_t gr_saved_floats(const gr_view* v) { return (size_t)5 * v->width * v->heig
 
 size_t gr_bins_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
-  size_t off[7];
+  size_t off[8];
   return bins_fixed(vtiles_of(v), plan->num_pairs, off);
 }
 
 size_t gr_fwd_scratch_bytes(const gr_view* v, int n, const gr_plan* plan) {
-  (void)n;
   const int vtiles = vtiles_of(v);
   size_t off[5];
-  return scratch_fixed(vtiles, plan->num_pairs, off) + align_up(tile_sort_tmp_bytes(plan->num_pairs, vtiles));
+  return scratch_fixed(vtiles, plan->num_pairs, off) + align_up(tile_sort_tmp_bytes(n, plan->num_pairs, vtiles));
 }
 
 // Backward workspace: pair partials (one 9-float slot per rectangle tile) + per-pixel upstream
@@ -3414,30 +3606,7 @@ size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan) {
 // flagged as num_pairs = -1 (gr_fwd_render then reports the overflow).
 // Exclusive scan of one value per thread over a block of NW waves (wave shuffles, then the wave totals
 // through LDS); `total` = the block's sum.
-extern "C++" {  // inside the C-ABI section
-template <int NW>
-__device__ __forceinline__ unsigned long long block_exclusive_scan(unsigned long long x, unsigned long long* sh,
-                                                                   unsigned long long& total) {
-  const int lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
-  unsigned long long inc = x;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long y = __shfl_up(inc, o);
-    if (lane >= o) inc += y;
-  }
-  __syncthreads();  // sh may still be read by a previous call
-  if (lane == 63) sh[w] = inc;
-  __syncthreads();
-  unsigned long long base = 0, all = 0;
-#pragma unroll
-  for (int u = 0; u < NW; ++u) {
-    base += u < w ? sh[u] : 0ull;
-    all += sh[u];
-  }
-  total = all;
-  return base + inc - x;
-}
-}  // extern "C++"
+
 
 // One workgroup of PLAN_THREADS (256 fits beside the render streams' splat kernels; see WI_THREADS).
 #ifndef GR_PLAN_THREADS
@@ -3524,10 +3693,6 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_plan_views(PrepBatch B, int n,
   const Geom& g = B.g[blockIdx.x];
   plan_scan(g.total, (n + 256) / 256, g.offsets + n, g.plan, hp.p[blockIdx.x], g.omax, g.f16_sa);
 }
-__global__ __launch_bounds__(256) void k_offsets_views(PrepBatch B, int n) {
-  const Geom& g = B.g[blockIdx.y];
-  offsets_scan(n, (int)blockIdx.x, g.counts, g.total, g.offsets);
-}
 
 gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, const float* scales, const float* colors,
                                int color_dim, const float* opacities, void* geom, size_t geom_bytes, gr_plan* plan,
@@ -3562,12 +3727,10 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
   if (hipPointerGetAttributes(&attr, plan) == hipSuccess && attr.type == hipMemoryTypeHost && attr.devicePointer)
     mapped = (gr_plan*)attr.devicePointer;
   (void)hipGetLastError();  // a pageable pointer leaves an error code behind
-  // exclusive scan of the packed counts: blocks (k_plan), then Gaussians (k_offsets)
+  // exclusive scan of the packed counts over the 256-Gaussian blocks (k_plan); the Gaussian level of the scan is
+  // the binning's (k_emit_cols writes the offsets as it emits)
   hipLaunchKernelGGL(k_plan, dim3(1), dim3(PLAN_THREADS), 0, s, g.total, blocks_for(n + 1), g.offsets + n, g.plan, mapped,
                      (const float*)g.omax, g.f16_sa);
-  GR_HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_offsets, dim3(blocks_for(n)), dim3(256), 0, s, n, (const unsigned long long*)g.counts,
-                     (const unsigned long long*)g.total, g.offsets);
   GR_HIP_TRY(hipGetLastError());
   if (!mapped) GR_HIP_TRY(hipMemcpyAsync(plan, g.plan, sizeof(gr_plan), hipMemcpyDeviceToHost, s));
   return GR_OK;
@@ -3621,8 +3784,6 @@ gr_status gr_fwd_prepare_views_async(int num_views, const gr_view* views, int n,
     hipLaunchKernelGGL(k_preprocess_views<48>, dim3(blocks), dim3(256), 0, s, B, n, means, scales, colors, opacities);
   GR_HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_plan_views, dim3(num_views), dim3(PLAN_THREADS), 0, s, B, n, hp);
-  GR_HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_offsets_views, dim3(blocks_for(n), num_views), dim3(256), 0, s, B, n);
   GR_HIP_TRY(hipGetLastError());
   }
   if (!all_mapped)
@@ -3686,22 +3847,21 @@ static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const vo
     const Cnt2* cnt = (const Cnt2*)g.counts;
     const Cnt2* offs = (const Cnt2*)g.offsets;
     if (short_keys(vtiles)) {
-      // counting sort of each region (core pairs [0, Kc), tail pairs [Kc, K)) on 16-bit tile keys
+      // counting sort of each region (core pairs [0, Kc), tail pairs [Kc, K)) on 16-bit tile keys, columns of G
+      // Gaussians: emission + per-column counts + offsets, the column scan, the placement + work items
       const int64_t Kc = plan->num_core_pairs, Kr[2] = {Kc, num_pairs - Kc};
-      hipLaunchKernelGGL((k_emit_zones<uint16_t, false>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
-                         (const int4*)g.rect, cnt, offs, (const float4*)g.rec, (uint16_t*)sc.keys_in, sc.ids_in);
-      GR_HIP_TRY(hipGetLastError());
-      // one count matrix, column scan and tile totals per region; both regions sorted by the same launches
+      const ColPlan cp = col_plan(n, num_pairs, tiles);
+      const size_t cells = (size_t)tiles * cp.cols;
+      const int waves = tsort_waves(tiles);
       TZones Z;
+      Z.offsets = offs;
+      Z.n = n;
+      Z.G = cp.G;
       char* q = (char*)sc.sort_tmp;
-      const size_t cells = tsort_cells_bound(num_pairs, tiles);
-      int waves = tsort_waves(tiles);
       for (int z = 0; z < 2; ++z) {
-        const TSortPlan tp = tsort_plan(Kr[z], tiles);
         TZone& zz = Z.z[z];
         zz.K = Kr[z];
-        zz.cw = tp.cw;
-        zz.cols = Kr[z] > 0 ? tp.cols : 0;
+        zz.cols = Kr[z] > 0 ? cp.cols : 0;
         zz.zbase = z == 0 ? 0 : (int)Kc;
         zz.keys = (const uint16_t*)sc.keys_in + (z == 0 ? 0 : Kc);
         zz.ids = sc.ids_in + (z == 0 ? 0 : Kc);
@@ -3711,22 +3871,33 @@ static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const vo
         q += align_up(cells * sizeof(int));
         zz.T = (int*)q;
         q += align_up((size_t)tiles * sizeof(int));
-        waves = tp.waves;
       }
-      const int cols = Z.z[0].cols + Z.z[1].cols;  // >= 1: num_pairs > 0
-      hipLaunchKernelGGL(k_tile_count, dim3(cols), dim3(256), (size_t)tiles * sizeof(int), s, Z, tiles);
+      const bool tail = Kr[1] > 0;
+      hipLaunchKernelGGL(k_emit_cols, dim3(cp.cols), dim3(256), emit_cols_lds(tiles, tail), s, vk, n, cp.J, tiles,
+                         (const int4*)g.rect, cnt, (const unsigned long long*)g.total, (Cnt2*)g.offsets, (const float4*)g.rec,
+                         (uint16_t*)sc.keys_in, sc.ids_in, Z.z[0].M, tail ? Z.z[1].M : (int*)nullptr);
       GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_tile_colscan, dim3((tiles + CS_T - 1) / CS_T, 2), dim3(CS_T * CS_G), 0, s, Z, tiles);
       GR_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_work_items_zones, dim3(1), dim3(WI_THREADS), 0, s, tiles, vk.tiles_x, (int)Kc,
-                         Kr[0] > 0 ? (const int*)Z.z[0].T : nullptr, Kr[1] > 0 ? (const int*)Z.z[1].T : nullptr, b.ranges,
-                         b.items, b.num_items, b.tile_item0);
-      GR_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_tile_place, dim3(cols), dim3(64 * waves), (size_t)tiles * sizeof(int) * waves, s, Z, tiles,
-                         bits_for((uint32_t)tiles), (const int2*)b.ranges, b.pairs, b.pos_of);
+      const int blocks = 1 + Z.z[0].cols + Z.z[1].cols;  // block 0: the work items
+      const size_t lds = (size_t)tiles * sizeof(int) * waves;
+      const int bits = bits_for((uint32_t)tiles);
+      if (waves == 4)
+        hipLaunchKernelGGL(k_tile_place<4>, dim3(blocks), dim3(256), lds, s, Z, tiles, bits, b.ranges, b.items, b.num_items,
+                           b.tile_item0, b.ticket, b.pairs, b.pos_of);
+      else if (waves == 2)
+        hipLaunchKernelGGL(k_tile_place<2>, dim3(blocks), dim3(128), lds, s, Z, tiles, bits, b.ranges, b.items, b.num_items,
+                           b.tile_item0, b.ticket, b.pairs, b.pos_of);
+      else
+        hipLaunchKernelGGL(k_tile_place<1>, dim3(blocks), dim3(64), lds, s, Z, tiles, bits, b.ranges, b.items, b.num_items,
+                           b.tile_item0, b.ticket, b.pairs, b.pos_of);
       GR_HIP_TRY(hipGetLastError());
     } else {
-      // radix sort of the whole pair array on virtual-tile keys (> TSORT_MAX_TILES tiles)
+      // radix sort of the whole pair array on virtual-tile keys (> TSORT_MAX_TILES tiles); the Gaussians' offsets
+      // first (the counting-sort path's emission writes them itself)
+      hipLaunchKernelGGL(k_offsets, dim3(blocks_for(n)), dim3(256), 0, s, n, (const unsigned long long*)g.counts,
+                         (const unsigned long long*)g.total, g.offsets);
+      GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL((k_emit_zones<uint32_t, true>), dim3(blocks_for(n)), dim3(256), 0, s, vk, n,
                          (const int4*)g.rect, cnt, offs, (const float4*)g.rec, sc.keys_in, sc.ids_in);
       GR_HIP_TRY(hipGetLastError());
@@ -3735,7 +3906,7 @@ static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const vo
       GR_HIP_TRY(hipGetLastError());
       GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * vtiles, s));
       const int bits = bits_for((uint32_t)vtiles);
-      size_t tmp = tile_sort_tmp_bytes(num_pairs, vtiles);
+      size_t tmp = tile_sort_tmp_bytes(n, num_pairs, vtiles);
       GR_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp, tmp, sc.keys_in, b.keys, sc.pairs_in, sc.pairs_sorted,
                                                     (int)num_pairs, 0, bits, s));
       hipLaunchKernelGGL(k_ranges<uint32_t>, dim3(blocks_for(num_pairs)), dim3(256), 0, s, num_pairs, b.keys, b.ranges);
@@ -3744,12 +3915,14 @@ static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const vo
                          b.pairs, b.pos_of);
       GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_work_items, dim3(1), dim3(WI_THREADS), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
-                         b.tile_item0);
+                         b.tile_item0, b.ticket);
     }
   } else {
+    // no pair: the Gaussians' offsets (written by the emission otherwise) are all zero
+    if (n > 0) GR_HIP_TRY(hipMemsetAsync(geom_view((void*)geom, n).offsets, 0, (size_t)n * sizeof(unsigned long long), s));
     GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * vtiles, s));
     hipLaunchKernelGGL(k_work_items, dim3(1), dim3(WI_THREADS), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
-                       b.tile_item0);
+                       b.tile_item0, b.ticket);
   }
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_BINNING, s);
@@ -3760,7 +3933,8 @@ static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const vo
 // fragments and tile sums go to the backward workspace `ws`, the view loss to l1_loss_out.
 static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins, size_t bins_bytes,
                           void* scratch, size_t scratch_bytes, float* out_rgb, float* out_alpha, float* out_depth,
-                          float* saved, void* stream, const L1Args* l1, float* l1_loss_out, void* ws, size_t ws_bytes) {
+                          float* saved, void* stream, const L1Args* l1, float* l1_loss_out, void* ws, size_t ws_bytes,
+                          bool depth_sums = false) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
   if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
@@ -3793,30 +3967,29 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
     const BwdWs w = bwd_ws(v, n, plan, ws);
     la = *l1;
     la.tile_loss = w.tile_loss;
+    la.loss_out = l1_loss_out;
+    la.n1 = (int64_t)(3 * HW);
+    la.n2 = (int64_t)(l1->t_mask ? HW : 0);
     UF = w.UF;
   }
   float4* saved4 = saved ? (float4*)saved : nullptr;
   float* savedD = saved ? saved + 4 * HW : nullptr;
-  if (num_pairs > 0 && !(GR_DEBUG_SKIP & 1)) {
+  if (!(GR_DEBUG_SKIP & 1)) {
+    // every tile has a work item (an empty tile its one empty item): the splat writes every output pixel, finishes
+    // the tiles split over several items (the last item to arrive) and, with the fit loss, the view loss (the last
+    // tile to finish)
     prof_mark(PROF_RASTER_FWD, s);
     // no_depth_grad: 0 default (f32-grade W / D), 1 two-piece splits, 2 f32-grade without a depth gradient
     const bool f32g = v->no_depth_grad != 1;
     hipLaunchKernelGGL(l1 ? (f32g ? k_raster_fwd_mfma<5> : k_raster_fwd_mfma<4>)
                           : (f32g ? k_raster_fwd_mfma<1>
-                                  : (out_depth ? k_raster_fwd_mfma<2> : k_raster_fwd_mfma<3>)),
+                                  : (out_depth || depth_sums ? k_raster_fwd_mfma<2> : k_raster_fwd_mfma<3>)),
                        dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
                        (const int*)b.num_items, (const int2*)b.ranges, (const int*)b.pairs, (const float4*)g.rec,
-                       sc.fwd_part, out_rgb, out_alpha, out_depth, saved4, savedD, la, UF, (const int*)g.f16_sa);
+                       sc.fwd_part, out_rgb, out_alpha, out_depth, saved4, savedD, la, UF,
+                       (const int*)(n > 0 && num_pairs > 0 ? g.f16_sa : nullptr), (const int*)b.tile_item0, b.ticket);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_FWD, s);
-  }
-  hipLaunchKernelGGL(k_fwd_finalize, dim3(tiles), dim3(256), 0, s, vk, (const int2*)b.ranges, (const int*)b.tile_item0,
-                     (const float*)sc.fwd_part, out_rgb, out_alpha, out_depth, saved4, savedD, la, UF);
-  GR_HIP_TRY(hipGetLastError());
-  if (l1) {
-    hipLaunchKernelGGL(k_tile_loss_final, dim3(1), dim3(256), 0, s, (const float*)la.tile_loss, tiles, (int64_t)(3 * HW),
-                       (int64_t)(l1->t_mask ? HW : 0), l1->w_sil, (int64_t)0, 0.0f, l1_loss_out);
-    GR_HIP_TRY(hipGetLastError());
   }
   return GR_OK;
 }
@@ -3828,6 +4001,24 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
                         float* saved, void* stream) {
   return fwd_impl(v, n, plan, geom, bins, bins_bytes, scratch, scratch_bytes, out_rgb, out_alpha, out_depth, saved, stream,
                   nullptr, nullptr, nullptr, 0);
+}
+
+gr_status gr_fwd_render_saved(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins,
+                              size_t bins_bytes, void* scratch, size_t scratch_bytes, float* saved, void* stream) {
+  return fwd_impl(v, n, plan, geom, bins, bins_bytes, scratch, scratch_bytes, nullptr, nullptr, nullptr, saved, stream,
+                  nullptr, nullptr, nullptr, 0, true);
+}
+
+gr_status gr_fwd_compose(const gr_view* v, const float* saved, float* out_rgb, float* out_alpha, float* out_depth,
+                         void* stream) {
+  gr_status st = check_view(v);
+  if (st != GR_OK) return st;
+  if (!saved) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fwd_compose: saved is null");
+  const int hw = v->width * v->height;
+  hipLaunchKernelGGL(k_compose, dim3(blocks_for(hw)), dim3(256), 0, (hipStream_t)stream, make_viewk(v), hw,
+                     (const float4*)saved, saved + 4 * (size_t)hw, out_rgb, out_alpha, out_depth);
+  GR_HIP_TRY(hipGetLastError());
+  return GR_OK;
 }
 
 gr_status gr_fwd_bin(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins, size_t bins_bytes,
@@ -3866,7 +4057,8 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
                           const float* saved, const float* g_rgb, const float* g_alpha, const float* g_depth,
                           const float* t_rgb, const float* t_mask, float w_sil, float g_scale, float* loss_out,
                           float* d_means, float* d_scales, float* d_colors, float* d_opacities, int accumulate, void* ws,
-                          size_t ws_bytes, void* stream, const float* t_depth = nullptr, float w_depth = 0.0f) {
+                          size_t ws_bytes, void* stream, const float* t_depth = nullptr, float w_depth = 0.0f,
+                          const int* out_index = nullptr, float* g_sums = nullptr, float* g_sums3 = nullptr) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
   if ((g_depth || (t_rgb && t_depth)) && v->no_depth_grad)
@@ -3876,7 +4068,9 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
   if (color_dim != 3 && color_dim != 12 && color_dim != 48)
     return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");
   if (n == 0) return GR_OK;
-  if ((!g_rgb && !t_rgb) || !saved || !geom || !bins || !d_means || !d_scales || !d_colors || !d_opacities)
+  const bool gather_only = g_sums != nullptr;  // gr_bwd_fit_gather: the per-Gaussian sums to the caller, no chain rule
+  if ((!g_rgb && !t_rgb) || !saved || !geom || !bins ||
+      (!gather_only && (!d_means || !d_scales || !d_colors || !d_opacities)))
     return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
   if (t_rgb && (!loss_out || !ws)) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_l1: null loss or workspace");
   const int64_t num_pairs = plan->num_pairs;
@@ -3939,13 +4133,21 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
     // the depth sums), then the chain rule of that one view (the two stages of gr_gather_view +
     // gr_reduce_sums; k_reduce_bwd's one pass needs 117 VGPRs for the chain rule while it gathers)
     float* depth3 = partials + 8 * (size_t)plan->num_slots;
+    float* sums = gather_only ? g_sums : w.sums;
+    float* sums3 = gather_only ? g_sums3 : w.sums3;
     if (depth)
       hipLaunchKernelGGL(k_gather_view<true>, dim3((n + 63) / 64), dim3(256), 0, s, n, (const Cnt2*)g.offsets,
-                         (const int*)b.pos_of, (const float4*)partials, (float2*)w.sums, (const float*)depth3, w.sums3);
+                         (const int*)b.pos_of, (const float4*)partials, (float2*)sums, (const float*)depth3, sums3);
     else
       hipLaunchKernelGGL(k_gather_view<false>, dim3((n + 63) / 64), dim3(256), 0, s, n, (const Cnt2*)g.offsets,
-                         (const int*)b.pos_of, (const float4*)partials, (float2*)w.sums, (const float*)nullptr,
+                         (const int*)b.pos_of, (const float4*)partials, (float2*)sums, (const float*)nullptr,
                          (float*)nullptr);
+    if (gather_only) {
+      if (!depth && sums3) GR_HIP_TRY(hipMemsetAsync(sums3, 0, (size_t)n * sizeof(float), s));
+      GR_HIP_TRY(hipGetLastError());
+      prof_mark(PROF_REDUCE, s);
+      return GR_OK;
+    }
     SBatch B;
     B.nv = 1;
     B.r[0].v = vk;
@@ -3955,20 +4157,23 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
     const dim3 grid((n + gpb - 1) / gpb), block(256);
     if (color_dim == 3)
       hipLaunchKernelGGL(k_reduce_sums<3>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
-                         d_colors, d_opacities, accumulate);
+                         d_colors, d_opacities, accumulate, out_index);
     else if (color_dim == 12)
       hipLaunchKernelGGL(k_reduce_sums<12>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
-                         d_colors, d_opacities, accumulate);
+                         d_colors, d_opacities, accumulate, out_index);
     else
       hipLaunchKernelGGL(k_reduce_sums<48>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
-                         d_colors, d_opacities, accumulate);
+                         d_colors, d_opacities, accumulate, out_index);
+  } else if (gather_only) {  // no pair: every sum is zero
+    GR_HIP_TRY(hipMemsetAsync(g_sums, 0, gr_view_sums_floats(n) * sizeof(float), s));
+    if (g_sums3) GR_HIP_TRY(hipMemsetAsync(g_sums3, 0, (size_t)n * sizeof(float), s));
   } else {
     // the backward without a depth gradient writes 8-float rows (bwd_item_bf16)
     const bool row8 = !depth;
     auto launch = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
                          (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const int*)b.pos_of, (const float*)partials,
-                         d_means, d_scales, d_colors, d_opacities, depth ? 1 : 0, accumulate);
+                         d_means, d_scales, d_colors, d_opacities, depth ? 1 : 0, accumulate, out_index);
     };
     if (color_dim == 3)
       row8 ? launch(k_reduce_bwd<3, true>) : launch(k_reduce_bwd<3, false>);
@@ -3992,6 +4197,16 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
                   nullptr, nullptr, 0.0f, 0.0f, nullptr, d_means, d_scales, d_colors, d_opacities, 0, ws, ws_bytes, stream);
 }
 
+gr_status gr_bwd_indexed(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
+                         const float* colors, int color_dim, const float* opacities, const void* geom, const void* bins,
+                         const float* saved, const float* g_rgb, const float* g_alpha, const float* g_depth,
+                         const int* index, float* d_means, float* d_scales, float* d_colors, float* d_opacities, void* ws,
+                         size_t ws_bytes, void* stream) {
+  return bwd_impl(v, n, plan, means, scales, colors, color_dim, opacities, geom, bins, saved, g_rgb, g_alpha, g_depth,
+                  nullptr, nullptr, 0.0f, 0.0f, nullptr, d_means, d_scales, d_colors, d_opacities, 0, ws, ws_bytes, stream,
+                  nullptr, 0.0f, index);
+}
+
 gr_status gr_bwd_fit(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
                      const float* colors, int color_dim, const float* opacities, const void* geom, const void* bins,
                      const float* saved, const float* target_rgb, const float* target_mask, float w_sil,
@@ -4002,6 +4217,17 @@ gr_status gr_bwd_fit(const gr_view* v, int n, const gr_plan* plan, const float* 
   return bwd_impl(v, n, plan, means, scales, colors, color_dim, opacities, geom, bins, saved, nullptr, nullptr, nullptr,
                   target_rgb, target_mask, w_sil, g_scale, loss_out, d_means, d_scales, d_colors, d_opacities,
                   accumulate, ws, ws_bytes, stream, target_depth, w_depth);
+}
+
+gr_status gr_bwd_fit_gather(const gr_view* v, int n, const gr_plan* plan, const void* geom, const void* bins,
+                            const float* saved, const float* target_rgb, const float* target_mask, float w_sil,
+                            const float* target_depth, float w_depth, float g_scale, float* loss_out, void* ws,
+                            size_t ws_bytes, float* sums, float* sums3, void* stream) {
+  if (!target_rgb) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_fit_gather: target_rgb is null");
+  if (!sums) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_bwd_fit_gather: sums is null");
+  return bwd_impl(v, n, plan, nullptr, nullptr, nullptr, 3, nullptr, geom, bins, saved, nullptr, nullptr, nullptr,
+                  target_rgb, target_mask, w_sil, g_scale, loss_out, nullptr, nullptr, nullptr, nullptr, 0, ws, ws_bytes,
+                  stream, target_depth, w_depth, nullptr, sums, sums3);
 }
 
 gr_status gr_bwd_l1(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
@@ -4142,7 +4368,7 @@ gr_status gr_reduce_sums(int num_views, const gr_sums_view* views, int n, const 
     if (!views[k].sums) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_reduce_sums: null sums");
     B.r[k].v = make_viewk(&views[k].view);
     B.r[k].sums = (const float4*)views[k].sums;
-    B.r[k].sums3 = nullptr;
+    B.r[k].sums3 = views[k].sums3;
   }
   hipStream_t s = (hipStream_t)stream;
   if (GR_DEBUG_SKIP & 8) return GR_OK;
@@ -4151,13 +4377,13 @@ gr_status gr_reduce_sums(int num_views, const gr_sums_view* views, int n, const 
   const dim3 grid((n + gpb - 1) / gpb), block(256);
   if (color_dim == 3)
     hipLaunchKernelGGL(k_reduce_sums<3>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
-                       d_colors, d_opacities, accumulate);
+                       d_colors, d_opacities, accumulate, (const int*)nullptr);
   else if (color_dim == 12)
     hipLaunchKernelGGL(k_reduce_sums<12>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
-                       d_colors, d_opacities, accumulate);
+                       d_colors, d_opacities, accumulate, (const int*)nullptr);
   else
     hipLaunchKernelGGL(k_reduce_sums<48>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
-                       d_colors, d_opacities, accumulate);
+                       d_colors, d_opacities, accumulate, (const int*)nullptr);
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_REDUCE, s);
   return GR_OK;

@@ -39,9 +39,11 @@ if __package__ in (None, ""):
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import losses  # type: ignore
     import torch_renderer as tr  # type: ignore
+    from spatial import _spread3, morton_order  # type: ignore  # noqa: F401
 else:
     from . import losses
     from . import torch_renderer as tr
+    from .spatial import _spread3, morton_order  # noqa: F401
 
 RenderFn = Callable[..., tuple]
 
@@ -207,30 +209,6 @@ def densify_and_prune_device(params: dict, max_gaussians: int, densify_ratio: fl
     return {k: torch.nn.Parameter(v.contiguous()) for k, v in out.items()}
 
 
-def _spread3(v: torch.Tensor) -> torch.Tensor:
-    """Bits 0..9 of v moved to bits 0, 3, 6, .. 27 (Morton interleave of one axis)."""
-    v = (v | (v << 16)) & 0x030000FF
-    v = (v | (v << 8)) & 0x0300F00F
-    v = (v | (v << 4)) & 0x030C30C3
-    return (v | (v << 2)) & 0x09249249
-
-
-def morton_order(means: torch.Tensor) -> torch.Tensor:
-    """Permutation that puts the Gaussians in 3-D Morton (Z-curve) order of their centres, 10 bits per
-    axis over the bounding box; stable, so every rank computes the same permutation from the same
-    means.  Neighbours in this order are neighbours in space, hence on screen in every view: the
-    pairs one wave emits land in few tiles (the tile sort writes runs instead of scattered 8-byte
-    pairs) and a tile's records are gathered from few cache lines."""
-    with torch.no_grad():
-        m = means.detach()
-        mt = m.t().contiguous()  # (3, N): row reductions (a dim-0 reduction of (N,3) is a slow strided kernel)
-        lo = mt.amin(1)
-        ext = (mt.amax(1) - lo).clamp_min(1e-20)
-        q = ((m - lo) / ext * 1023.0).round().to(torch.int64).clamp_(0, 1023)
-        key = _spread3(q[:, 0]) | (_spread3(q[:, 1]) << 1) | (_spread3(q[:, 2]) << 2)
-        return torch.argsort(key, stable=True)
-
-
 def spatial_order(params: dict) -> dict:
     """The same Gaussians, permuted into morton_order (a layout choice of the trainer: the rendered
     images and the loss do not depend on the order of the Gaussians beyond float summation order)."""
@@ -251,6 +229,19 @@ def _fit_images(name: str, imgs: Optional[list], shape: tuple, device) -> tuple:
     if any(tuple(t.shape) != shape for t in imgs):
         return list(imgs), False
     return [torch.as_tensor(t).to(device=device, dtype=torch.float32).contiguous() for t in imgs], True
+
+
+def _batch_sizes(ns: int, nviews: int) -> list:
+    """Per stream (views j = k, k + ns, ...): its views' reduction batches, near-equal and at most REDUCE_BATCH, in
+    the order they fill; a short last batch of REDUCE_TAIL views (the reductions left when the renders end run alone).
+    The native executor's schedule() is the same rule."""
+    sizes = []
+    for k in range(ns):
+        p = len(range(k, nviews, ns))
+        tail = min(REDUCE_TAIL, REDUCE_BATCH) if 0 < REDUCE_TAIL < p else 0  # (gr_fit_views: tail <= batch)
+        nb = max(1, -(-(p - tail) // REDUCE_BATCH))
+        sizes.append([(p - tail) // nb + (1 if b < (p - tail) % nb else 0) for b in range(nb)] + ([tail] if tail else []))
+    return sizes
 
 
 def bucketed_all_reduce(buckets: list, assemble: Callable[[int], None], finish: Callable[[int], None], group=None) -> None:
@@ -587,7 +578,7 @@ class ViewShardedFitter:
                 arr[j].target_rgb = self.targets[i].data_ptr()
                 arr[j].target_mask = self.masks[i].data_ptr() if w_sil > 0.0 else None
             self._native_targets = cache = (key, arr)
-        cfg = tr._native.GrFitConfig(NUM_STREAMS, PREP_AHEAD, PREP_GROUP, PREP_FIRST, REDUCE_BATCH, REDUCE_TAIL)
+        cfg = tr._native.GrFitConfig(NUM_STREAMS, PREP_AHEAD, PREP_GROUP, PREP_FIRST, REDUCE_BATCH, min(REDUCE_TAIL, REDUCE_BATCH))
         if EXEC_STREAMS:
             # the Python schedule's own torch streams: the same hardware-queue placement (stream creation
             # order decides it), so the two schedules differ only in their host code
@@ -660,14 +651,7 @@ class ViewShardedFitter:
             m, s, c, o, [self._fit_view(views[q], device) for q in js], [pins[q] for q in js]), prep)
         pending: list = [[] for _ in streams]  # per stream: (render state, partials) awaiting their reduction
         started = [False] * ns
-        # stream k's views in nb near-equal batches of at most REDUCE_BATCH (sizes in the order they fill)
-        sizes = []
-        for k in range(ns):
-            p = len(range(k, len(views), ns))
-            # a short last batch (REDUCE_TAIL views): the reductions left when the renders end run alone
-            tail = REDUCE_TAIL if 0 < REDUCE_TAIL < p else 0
-            nb = max(1, -(-(p - tail) // REDUCE_BATCH))
-            sizes.append([(p - tail) // nb + (1 if b < (p - tail) % nb else 0) for b in range(nb)] + ([tail] if tail else []))
+        sizes = _batch_sizes(ns, len(views))
 
         def reduce_pending(k):
             if pending[k]:
@@ -758,6 +742,19 @@ class ViewShardedFitter:
 
         prepare_upto = self._prep_groups(views, ahead, lambda js: tr.prepare_views_native(
             m, s, c, o, [gv_of(views[q]) for q in js], [pins[q] for q in js]), prep)
+        # per view its render and the depth-loss backward up to the per-Gaussian sums (gr_bwd_fit_gather); per batch
+        # of a stream's views one chain-rule pass (gr_reduce_sums with the depth sums), as _views_direct
+        pending: list = [[] for _ in streams]
+        started = [False] * ns
+        sizes = _batch_sizes(ns, len(views))
+
+        def reduce_pending(k):
+            if pending[k]:
+                with torch.cuda.stream(streams[k]):
+                    tr.reduce_sums_native(m, s, c, o, pending[k], acc[k], accumulate=started[k])
+                started[k] = True
+                pending[k] = []
+
         for j, i in enumerate(views):
             k = j % ns
             prepare_upto(j)
@@ -765,11 +762,20 @@ class ViewShardedFitter:
             streams[k].wait_event(pv.event)
             pv.geom.record_stream(streams[k])
             with torch.cuda.stream(streams[k]):
-                _, _, _, rs = tr.forward_native(m, s, c, o, pv.gv, pv, images=False)  # gr_bwd_fit reads the sums
+                _, _, _, rs = tr.forward_native(m, s, c, o, pv.gv, pv, images=False)  # the backward reads the sums
                 pv = None
-                tr.backward_fit_native(m, s, c, o, rs, self.targets[i], self.masks[i] if w_sil > 0.0 else None, w_sil,
-                                       self.depths[i], self.w_depth, g_scale, losses_v[j:j + 1], acc[k], accumulate=j >= ns)
+                sums, sums3 = tr.backward_fit_gather_native(rs, self.targets[i], self.masks[i] if w_sil > 0.0 else None,
+                                                            w_sil, self.depths[i], self.w_depth, g_scale,
+                                                            losses_v[j:j + 1])
+                pending[k].append((rs.gv, sums, sums3))
+                rs = None
             prepare_upto(j + PREP_AHEAD)
+            if len(pending[k]) >= sizes[k][0]:
+                reduce_pending(k)
+                if len(sizes[k]) > 1:
+                    sizes[k].pop(0)
+        for k in range(ns):
+            reduce_pending(k)
         for st in streams[1:]:
             main.wait_stream(st)
         main.wait_stream(prep)

@@ -35,10 +35,11 @@ import numpy as np
 import torch
 
 try:  # package import (3dgaussian_amd.torch_renderer) or flat import (drop-in on sys.path)
-    from . import _native, cpu_renderer
+    from . import _native, cpu_renderer, spatial
 except ImportError:  # pragma: no cover
     import _native  # type: ignore
     import cpu_renderer  # type: ignore
+    import spatial  # type: ignore
 
 DEFAULT_CUTOFF = 7.0  # tail zone (W and D) when no depth gradient will follow (depth_grad=False)
 DEPTH_GRAD_CUTOFF = 8.0  # tail zone when the depth output may be differentiated (the default mode)
@@ -249,11 +250,12 @@ class Prepared:
     the next view before rendering the current one keeps the device busy while the host reads the
     plan (ViewShardedFitter does this)."""
 
-    __slots__ = ("gv", "n", "geom", "plan_host", "event", "binned")
+    __slots__ = ("gv", "n", "geom", "plan_host", "event", "binned", "rendered")
 
     def __init__(self, gv, n, geom, plan_host, event):
         self.gv, self.n, self.geom, self.plan_host, self.event = gv, n, geom, plan_host, event
         self.binned = None  # (bins, scratch, binned gr_view, event) when the speculation binned it ahead
+        self.rendered = None  # (saved sums, event) when the speculation also rendered it ahead (_render_launch)
 
     def plan(self) -> _native.GrPlan:
         self.event.synchronize()
@@ -324,6 +326,25 @@ def _bin_launch(L, gv, n, plan, prepared, bin_stream, dev):
     return bins, scratch, _binned(gv), done
 
 
+def _render_launch(L, prepared: Prepared, stream, dev) -> None:
+    """The splat of a speculatively prepared view, ahead of its call, on ``stream``: its binning (_bin_launch, unless
+    done) and gr_fwd_render_saved into saved sums; the call then only composes the outputs with its own background
+    (forward_native).  Sets ``prepared.binned`` and ``prepared.rendered``."""
+    plan = prepared.plan()
+    if prepared.binned is None:
+        prepared.binned = _bin_launch(L, prepared.gv, prepared.n, plan, prepared, stream, dev)
+    bins, scratch, bgv, done = prepared.binned
+    with torch.cuda.stream(stream):
+        stream.wait_event(done)
+        saved = torch.empty((int(L.gr_saved_floats(ctypes.byref(bgv))),), dtype=torch.float32, device=dev)
+        _native.check(L.gr_fwd_render_saved(ctypes.byref(bgv), prepared.n, ctypes.byref(plan), _native.ptr(prepared.geom),
+                                            _native.ptr(bins), bins.numel(), _native.ptr(scratch), scratch.numel(),
+                                            _native.ptr(saved), ctypes.c_void_p(stream.cuda_stream)), "gr_fwd_render_saved")
+        ev = torch.cuda.Event()
+        ev.record(stream)
+    prepared.rendered = (saved, ev)
+
+
 def _bin_ahead(L, gv, n, plan, prepared, bin_stream, dev):
     """The bins and forward scratch of a render (allocated for the current stream); with ``bin_stream``
     filled by gr_fwd_bin there (_bin_launch), or already binned (``prepared.binned``, the speculation's),
@@ -368,6 +389,21 @@ def forward_native(means, scales, colors, opacities, gv: _native.GrView, prepare
         raise ValueError("prepared view does not match this render (Gaussian count, image size or cutoffs)")
     geom = prepared.geom
     plan = prepared.plan()
+    ahead = getattr(prepared, "rendered", None)
+    if ahead is not None and images and prepared.binned[2].no_depth_grad == gv.no_depth_grad:
+        # rendered ahead (the speculation's gr_fwd_render_saved): only the outputs, with this call's background
+        saved, ev = ahead
+        bins = prepared.binned[0]
+        cur = torch.cuda.current_stream(dev)
+        cur.wait_event(ev)
+        for t in (saved, bins, geom):
+            t.record_stream(cur)
+        out = torch.empty((H, W, 3), dtype=torch.float32, device=dev)
+        alpha = torch.empty((H, W), dtype=torch.float32, device=dev)
+        depth = torch.empty((H, W), dtype=torch.float32, device=dev)
+        _native.check(L.gr_fwd_compose(ctypes.byref(gv), _native.ptr(saved), _native.ptr(out), _native.ptr(alpha),
+                                       _native.ptr(depth), s), "gr_fwd_compose")
+        return out, alpha, depth, RenderState(gv, n, plan, geom, bins, saved)
     bins, scratch, rv = _bin_ahead(L, gv, n, plan, prepared, bin_stream, dev)
     out = torch.empty((H, W, 3), dtype=torch.float32, device=dev) if images else None
     alpha = torch.empty((H, W), dtype=torch.float32, device=dev) if images else None
@@ -382,9 +418,11 @@ def forward_native(means, scales, colors, opacities, gv: _native.GrView, prepare
     return out, alpha, depth, RenderState(gv, n, plan, geom, bins, saved)
 
 
-def backward_native(means, scales, colors, opacities, st: RenderState, g_out, g_alpha, g_depth, want_ws: bool = False):
+def backward_native(means, scales, colors, opacities, st: RenderState, g_out, g_alpha, g_depth, want_ws: bool = False,
+                    index=None):
     """Run gr_bwd.  Returns (d_means, d_scales, d_colors, d_opacities) (+ the backward workspace with
-    ``want_ws``: it holds the per-Gaussian sums camera_grad_native reads)."""
+    ``want_ws``: it holds the per-Gaussian sums camera_grad_native reads).  ``index`` (int32 device, n): the
+    rendered Gaussians are a permuted copy, Gaussian i's gradients go to row index[i] (gr_bwd_indexed)."""
     L = _native.lib()
     dev = means.device
     cd = _color_dim(colors)
@@ -394,11 +432,19 @@ def backward_native(means, scales, colors, opacities, st: RenderState, g_out, g_
     ds = torch.empty_like(scales)
     dc = torch.empty_like(colors)
     do = torch.empty_like(opacities)
-    _native.check(L.gr_bwd(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan), _native.ptr(means), _native.ptr(scales),
-                           _native.ptr(colors), cd, _native.ptr(opacities), _native.ptr(st.geom), _native.ptr(st.bins),
-                           _native.ptr(st.saved), _native.ptr(g_out), _native.ptr(g_alpha), _native.ptr(g_depth),
-                           _native.ptr(dm), _native.ptr(ds), _native.ptr(dc), _native.ptr(do), _native.ptr(ws), ws.numel(),
-                           _stream(dev)), "gr_bwd")
+    if index is None:
+        _native.check(L.gr_bwd(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan), _native.ptr(means), _native.ptr(scales),
+                               _native.ptr(colors), cd, _native.ptr(opacities), _native.ptr(st.geom), _native.ptr(st.bins),
+                               _native.ptr(st.saved), _native.ptr(g_out), _native.ptr(g_alpha), _native.ptr(g_depth),
+                               _native.ptr(dm), _native.ptr(ds), _native.ptr(dc), _native.ptr(do), _native.ptr(ws),
+                               ws.numel(), _stream(dev)), "gr_bwd")
+    else:
+        _native.check(L.gr_bwd_indexed(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan), _native.ptr(means),
+                                       _native.ptr(scales), _native.ptr(colors), cd, _native.ptr(opacities),
+                                       _native.ptr(st.geom), _native.ptr(st.bins), _native.ptr(st.saved), _native.ptr(g_out),
+                                       _native.ptr(g_alpha), _native.ptr(g_depth), _native.ptr(index), _native.ptr(dm),
+                                       _native.ptr(ds), _native.ptr(dc), _native.ptr(do), _native.ptr(ws), ws.numel(),
+                                       _stream(dev)), "gr_bwd_indexed")
     return (dm, ds, dc, do, ws) if want_ws else (dm, ds, dc, do)
 
 
@@ -579,20 +625,47 @@ def gather_view_native(st: RenderState, ws, sums=None):
     return sums
 
 
+def backward_fit_gather_native(st: RenderState, target, mask, w_sil: float, depth_target, w_depth: float,
+                               g_scale: float, loss_out):
+    """gr_bwd_fit_gather on the current stream: the depth-loss backward of a view rendered with depth_grad=True up to
+    its per-Gaussian sums; returns (sums (n, 8), depth sums (n,)) for reduce_sums_native (the view's geom, bins and
+    saved sums are free after it)."""
+    L = _native.lib()
+    dev = st.saved.device
+    _check_operand(target, (st.gv.height, st.gv.width, 3), "target", dev)
+    _check_operand(mask, (st.gv.height, st.gv.width), "mask", dev)
+    _check_operand(depth_target, (st.gv.height, st.gv.width), "depth_target", dev)
+    ws = torch.empty((_ws_round(L.gr_bwd_bytes(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan))),), dtype=torch.uint8,
+                     device=dev)
+    sums = torch.empty((st.n, 8), dtype=torch.float32, device=dev)
+    sums3 = torch.empty((st.n,), dtype=torch.float32, device=dev)
+    _native.check(L.gr_bwd_fit_gather(ctypes.byref(st.gv), st.n, ctypes.byref(st.plan), _native.ptr(st.geom),
+                                      _native.ptr(st.bins), _native.ptr(st.saved), _native.ptr(target), _native.ptr(mask),
+                                      ctypes.c_float(w_sil), _native.ptr(depth_target), ctypes.c_float(w_depth),
+                                      ctypes.c_float(g_scale), _native.ptr(loss_out), _native.ptr(ws), ws.numel(),
+                                      _native.ptr(sums), _native.ptr(sums3), _stream(dev)), "gr_bwd_fit_gather")
+    return sums, sums3
+
+
 def reduce_sums_native(means, scales, colors, opacities, batch, grads, accumulate: bool) -> None:
-    """gr_reduce_sums on the current stream: ``batch`` = [(gr_view, sums from gather_view_native), ...] (at
-    most _native.REDUCE_MAX_VIEWS); the views' chain rules summed, written (accumulate=False) or added to
-    ``grads`` = (d_means, d_scales, d_colors, d_opacities)."""
+    """gr_reduce_sums on the current stream: ``batch`` = [(gr_view, sums from gather_view_native), ...] or
+    [(gr_view, sums, depth sums from backward_fit_gather_native), ...] (at most _native.REDUCE_MAX_VIEWS); the views'
+    chain rules summed, written (accumulate=False) or added to ``grads`` = (d_means, d_scales, d_colors,
+    d_opacities)."""
     L = _native.lib()
     if len(batch) > _native.REDUCE_MAX_VIEWS:
         raise ValueError(f"at most {_native.REDUCE_MAX_VIEWS} views per gr_reduce_sums batch")
     _check_params(means, scales, colors, opacities)
     n = int(means.shape[0])
     arr = (_native.GrSumsView * max(1, len(batch)))()
-    for k, (gv, sums) in enumerate(batch):
+    for k, item in enumerate(batch):
+        gv, sums = item[0], item[1]
+        sums3 = item[2] if len(item) > 2 else None
         _check_operand(sums, (n, 8), "sums", means.device)
+        _check_operand(sums3, (n,), "sums3", means.device)
         arr[k].view = gv
         arr[k].sums = sums.data_ptr()
+        arr[k].sums3 = sums3.data_ptr() if sums3 is not None else None
     for g, p, nm in zip(grads, (means, scales, colors, opacities), ("d_means", "d_scales", "d_colors", "d_opacities")):
         _check_operand(g, tuple(p.shape), nm, means.device)
     dm, ds, dc, do = grads
@@ -615,10 +688,14 @@ def _grad_background(st: RenderState, background: torch.Tensor, g_out: torch.Ten
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means, scales, colors, opacities, background, view, proj, gv, prepared, gv_depth=None,
-                bin_stream=None):
+                bin_stream=None, layout=None):
         """view / proj: the camera tensors (their gradients, gr_bwd_camera) or None; the render itself uses gv's
         host copy of them.  gv_depth: the f32-grade view a lazily rendered gv (two-piece mode) re-renders with
-        when a depth gradient arrives (LAZY_DEPTH), else None.  bin_stream: see forward_native."""
+        when a depth gradient arrives (LAZY_DEPTH), else None.  bin_stream: see forward_native.  layout: a
+        _Layout of the inputs (their Morton-ordered copy, rendered instead; the gradients return in the inputs'
+        order), or None."""
+        if layout is not None:
+            means, scales, colors, opacities = layout.tensors
         out, alpha, depth, st = forward_native(means, scales, colors, opacities, gv, prepared, bin_stream=bin_stream)
         # an output the loss does not use gets a None gradient instead of zeros, so an unused depth
         # output lets the backward skip the tail pairs (gr_bwd with g_depth = NULL)
@@ -627,12 +704,13 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.gv_depth = gv_depth
         # the render state's device buffers are saved tensors: autograd releases them after this node's backward
         # unless the graph is retained (a second backward through it then finds them)
-        ctx.save_for_backward(means, scales, colors, opacities, background, view, proj, st.geom, st.bins, st.saved)
+        ctx.save_for_backward(means, scales, colors, opacities, background, view, proj, st.geom, st.bins, st.saved,
+                              layout.index if layout is not None else None)
         return out, alpha, depth
 
     @staticmethod
     def backward(ctx, g_out, g_alpha, g_depth):
-        means, scales, colors, opacities, background, view, proj, geom, bins, saved = ctx.saved_tensors
+        means, scales, colors, opacities, background, view, proj, geom, bins, saved, index = ctx.saved_tensors
         st = RenderState(*ctx.meta, geom, bins, saved)
         if g_out is None:
             g_out = torch.zeros((st.gv.height, st.gv.width, 3), dtype=torch.float32, device=means.device)
@@ -647,13 +725,14 @@ class _RasterizeGaussians(torch.autograd.Function):
             # depth-gradient footprint and differentiate that render
             _, _, _, st = forward_native(means, scales, colors, opacities, ctx.gv_depth, images=False)
         need_view, need_proj = ctx.needs_input_grad[5], ctx.needs_input_grad[6]
-        dm, ds, dc, do, ws = backward_native(means, scales, colors, opacities, st, g_out, g_alpha, g_depth, want_ws=True)
+        dm, ds, dc, do, ws = backward_native(means, scales, colors, opacities, st, g_out, g_alpha, g_depth, want_ws=True,
+                                             index=index)
         dbg = _grad_background(st, background, g_out) if ctx.needs_input_grad[4] else None
         dview = dproj = None
         if need_view or need_proj:
             d = camera_grad_native(means, scales, colors, opacities, st, ws, g_depth is not None)
             dview, dproj = _camera_grads(d, view, proj, need_view, need_proj, colors.dim() == 3)
-        return dm, ds, dc, do, dbg, dview, dproj, None, None, None, None
+        return dm, ds, dc, do, dbg, dview, dproj, None, None, None, None, None
 
 
 def _device_inputs(means, scales, colors, opacities):
@@ -694,7 +773,13 @@ def prepare_view(means, scales, colors, opacities, view, proj, width, height, ba
 # ------------------------------------------------------------------------------------------------
 SPECULATE = os.environ.get("GR_SPECULATE", "1") != "0"
 SPEC_BIN = os.environ.get("GR_SPEC_BIN", "1") != "0"
-SPEC_DEPTH = 2
+# the camera after the one being rendered is also splatted ahead (gr_fwd_render_saved), so its call only composes
+# the outputs with the background it passes (gr_fwd_compose): the splats of consecutive calls run back to back on the
+# speculation stream while the host runs the caller's per-view code
+SPEC_RENDER = os.environ.get("GR_SPEC_RENDER", "1") != "0"
+# cameras prepared ahead: with the render-ahead, the one after the next is prepared before the next one's splat is
+# enqueued, so taking its plan never waits behind a splat
+SPEC_DEPTH = 3 if SPEC_RENDER else 2
 
 
 class _Speculation:
@@ -731,10 +816,13 @@ def _spec_take(key, tensors) -> Optional[Prepared]:
         return None
     _SPEC["hits"] += 1
     _SPEC["cold"].discard((sp.src, key))
-    if SPEC_BIN and pipe and pipe[0].prepared.binned is None:
+    if pipe and pipe[0].prepared.rendered is None and (SPEC_RENDER or (SPEC_BIN and pipe[0].prepared.binned is None)):
         nx = pipe[0].prepared
-        nx.binned = _bin_launch(_native.lib(), nx.gv, nx.n, nx.plan(), nx, _spec_stream(tensors[0].device),
-                                tensors[0].device)
+        dev = tensors[0].device
+        if SPEC_RENDER:  # the next camera's binning and splat, beside this view's compose, losses and host work
+            _render_launch(_native.lib(), nx, _spec_stream(dev), dev)
+        else:
+            nx.binned = _bin_launch(_native.lib(), nx.gv, nx.n, nx.plan(), nx, _spec_stream(dev), dev)
     return sp.prepared
 
 
@@ -774,6 +862,52 @@ def _spec_after(key, gv, tensors, inputs_ready) -> None:
         pipe.append(_Speculation(nxt, tensors, pv, src))
 
 
+# ------------------------------------------------------------------------------------------------
+# Spatial layout of the drop-in op.  A caller's Gaussians come in its own order (the reference fit loop's are in
+# random order, fit_multiview_stub.py:114-137); the tile sort, the splats' record gathers and the per-Gaussian
+# gathers all run several times faster on Morton-ordered Gaussians (spatial.py).  The op renders a Morton-ordered
+# copy of its inputs - made once per set of input tensors (the same live tensors at the same versions: a fit
+# loop's activations, shared by all the views of an iteration) - and gr_bwd_indexed writes each Gaussian's
+# gradients back to the caller's row, so nothing outside sees the copy (results differ from an unpermuted render
+# only in float summation order).  The permutation itself is kept per means tensor (a fit's parameter, updated in
+# place) and recomputed every LAYOUT_EVERY input sets.  GR_DROPIN_LAYOUT=0 turns this off.
+# ------------------------------------------------------------------------------------------------
+LAYOUT = os.environ.get("GR_DROPIN_LAYOUT", "1") != "0"
+LAYOUT_MIN = 32768  # Gaussians from which the copy pays for itself
+LAYOUT_EVERY = 16   # input sets rendered with one permutation before it is recomputed
+
+
+class _Layout:
+    __slots__ = ("refs", "versions", "tensors", "index")
+
+    def __init__(self, inputs, tensors, index):
+        self.refs = tuple(weakref.ref(t) for t in inputs)
+        self.versions = tuple(t._version for t in inputs)
+        self.tensors, self.index = tensors, index
+
+    def matches(self, inputs) -> bool:
+        return all(r() is t and t._version == v for r, t, v in zip(self.refs, inputs, self.versions))
+
+
+_LAYOUT: dict = {"entry": None, "perm": None}
+
+
+def _layout_of(m, s, c, o) -> _Layout:
+    """The Morton-ordered copy of these input tensors (cached: one entry)."""
+    e = _LAYOUT["entry"]
+    if e is not None and e.matches((m, s, c, o)):
+        return e
+    pc = _LAYOUT["perm"]  # [weakref(means), n, perm int64, perm int32, uses]
+    if pc is None or pc[0]() is not m or pc[1] != m.shape[0] or pc[4] >= LAYOUT_EVERY:
+        perm = spatial.morton_order(m)
+        pc = _LAYOUT["perm"] = [weakref.ref(m), m.shape[0], perm, perm.to(torch.int32), 0]
+    pc[4] += 1
+    with torch.no_grad():
+        tensors = tuple(t.detach().index_select(0, pc[2]).contiguous() for t in (m, s, c, o))
+    e = _LAYOUT["entry"] = _Layout((m, s, c, o), tensors, pc[3])
+    return e
+
+
 def rasterize(means, scales, colors, opacities, view, proj, width, height, background=None, cutoff=None,
               prepared: Optional[Prepared] = None, core_cutoff=DEFAULT_CORE_CUTOFF, depth_grad=True):
     """Differentiable render of one view on the HIP device: returns (rgb (H,W,3), alpha (H,W), depth (H,W)).
@@ -805,18 +939,23 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
     # the camera tensors enter the autograd op only when a gradient is wanted for them (gr_bwd_camera)
     cam_v = view if isinstance(view, torch.Tensor) and view.requires_grad else None
     cam_p = proj if isinstance(proj, torch.Tensor) and proj.requires_grad else None
-    if prepared is not None or not SPECULATE:
+    if prepared is not None:  # a preparation made by prepare_view is of the caller's own order: render that
         return _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, prepared, gv_depth)
+    # the rendered tensors: the Morton-ordered copy of the inputs
+    layout = _layout_of(m, s, c, o) if LAYOUT and m.shape[0] >= LAYOUT_MIN else None
+    if not SPECULATE:
+        return _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, None, gv_depth, None, layout)
+    rt = layout.tensors if layout is not None else (m, s, c, o)
     key = _view_key(gv)
-    pv = _spec_take(key, (m, s, c, o))
+    pv = _spec_take(key, rt)
     stream = torch.cuda.current_stream(dev)
     if pv is not None:
         stream.wait_event(pv.event)
         pv.geom.record_stream(stream)
     ready = torch.cuda.Event()
     ready.record(stream)
-    res = _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, pv, gv_depth)
-    _spec_after(key, gv, (m, s, c, o), ready)
+    res = _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, pv, gv_depth, None, layout)
+    _spec_after(key, gv, rt, ready)
     return res
 
 
@@ -868,6 +1007,6 @@ def render_gaussians_torch(
 
 __all__ = ["Camera", "get_default_device", "perspective", "look_at", "render_gaussians_torch", "rasterize",
            "make_view", "prepare_view", "prepare_native", "Prepared", "forward_native", "backward_native",
-           "backward_l1_native", "backward_fit_native", "forward_l1_native", "backward_splat_native", "reduce_views_native",
+           "backward_l1_native", "backward_fit_native", "backward_fit_gather_native", "forward_l1_native", "backward_splat_native", "reduce_views_native",
            "gather_view_native", "reduce_sums_native",
            "DEFAULT_CUTOFF", "DEPTH_GRAD_CUTOFF", "DEFAULT_CORE_CUTOFF", "FIT_CUTOFF", "default_cutoff"]

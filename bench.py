@@ -247,15 +247,17 @@ def pmc_of(pmc: dict, prefix: str) -> dict:
     return {}
 
 
-def dropin_op(n: int, V: int, R: int, steps: int, warmup: int, device) -> dict:
+def dropin_op(n: int, V: int, R: int, steps: int, warmup: int, device, depth_loss: bool = False) -> dict:
     """fit_multiview_stub.py:265-311 as written, on the drop-in module: the unchanged reference loop's use of
     the op (render_gaussians_torch per view with a fresh device background, torch losses, autograd, Adam,
-    float(loss) per iteration).  Mpx/s over ``steps`` iterations after ``warmup``."""
+    float(loss) per iteration).  Mpx/s over ``steps`` iterations after ``warmup``.  depth_loss: the loop with its
+    --depth_dir term, w_depth mean|depth / (depth.max() + 1e-6) - d_gt| (fit_multiview_stub.py:299-303)."""
     params = synthetic_params(n, device)
     cams = fm.orbit_cameras(V, R, R, device)
     g = torch.Generator(device=device).manual_seed(1)
     targets = [torch.rand((R, R, 3), generator=g, device=device) for _ in range(V)]
     masks = [(t.mean(dim=2) > 0.5).to(torch.float32) for t in targets]
+    depths = [torch.rand((R, R), generator=g, device=device) for _ in range(V)] if depth_loss else None
     opt = torch.optim.Adam(list(params.values()), lr=0.02)
 
     def iteration():
@@ -270,6 +272,9 @@ def dropin_op(n: int, V: int, R: int, steps: int, warmup: int, device) -> dict:
                                                            height=R, background=torch.tensor([0.0, 0.0, 0.0], device=device),
                                                            max_gaussians=max(3000, means.shape[0]), return_aux=True)
             loss_i = torch.mean(torch.abs(pred - tgt)) + 0.2 * torch.mean(torch.abs(alpha - masks[i]))
+            if depths is not None:
+                d_pred = depth / (depth.max() + 1e-6)
+                loss_i = loss_i + 0.05 * torch.mean(torch.abs(d_pred - depths[i]))
             total = total + loss_i
         reg = 1e-3 * opacities.mean() + 1e-3 * scales.mean()
         loss = total / len(targets) + reg
@@ -291,7 +296,8 @@ def dropin_op(n: int, V: int, R: int, steps: int, warmup: int, device) -> dict:
             "speculative_preparations": {"hits": tr._SPEC["hits"] - spec0["hits"],
                                          "misses": tr._SPEC["misses"] - spec0["misses"]},
             "path": "render_gaussians_torch (autograd op, default precision mode: depth_grad=True, 8/5.5-sigma "
-                    "footprint) as fit_multiview_stub.py:277-311 calls it, unchanged loop"}
+                    "footprint) as fit_multiview_stub.py:277-311 calls it, unchanged loop"
+                    + (", with the --depth_dir depth term (:299-303)" if depth_loss else "")}
 
 
 def psnr_vs_ref(fitter, cams, R: int, device, npix: int = 2048) -> dict:
@@ -450,11 +456,13 @@ def main():
     clk1 = sclk_mhz() if rank == 0 else None
     psnr = psnr_vs_ref(fitter, cams, R, device) if (rank == 0 and not args.no_psnr) else None
     my_views_n = max(len(fitter.my_views), 1)
-    drop = None
+    drop = drop_depth = None
     if rank == 0 and world == 1 and not args.no_dropin:
         del fitter
         torch.cuda.empty_cache()
-        drop = dropin_op(n, V, R, steps=2, warmup=1, device=device)
+        drop = dropin_op(n, V, R, steps=3, warmup=1, device=device)
+        torch.cuda.empty_cache()
+        drop_depth = dropin_op(n, V, R, steps=2, warmup=1, device=device, depth_loss=True)
 
     if rank == 0:
         bwd_ms, bwd_n = prof["raster_bwd"]
@@ -550,6 +558,7 @@ def main():
             "default_precision_mode": extra or None,
             "f32_grade_fit": f32g,
             "dropin_op": drop,
+            "dropin_depth_loss": drop_depth,
             "psnr_vs_ref": psnr,
             "pmc": {k: v for k, v in pmc.items() if k != "kernels"},
             "sclk_mhz": {"before": clk0, "after": clk1},

@@ -157,6 +157,15 @@ gr_status gr_fwd_render(const gr_view* v, int n, const gr_plan* plan, const void
                         size_t bins_bytes, void* scratch, size_t scratch_bytes, float* out_rgb,
                         float* out_alpha, float* out_depth, float* saved, void* stream);
 
+/* gr_fwd_render without output images but with every saved sum (the depth channel's too): the splat of a view
+ * whose background is not known yet (the drop-in op renders the next camera ahead of its call); gr_fwd_compose then
+ * writes the outputs from `saved` with the view's background (gr_view.background / background_dev), exactly as
+ * gr_fwd_render would have written them. */
+gr_status gr_fwd_render_saved(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins,
+                              size_t bins_bytes, void* scratch, size_t scratch_bytes, float* saved, void* stream);
+gr_status gr_fwd_compose(const gr_view* v, const float* saved, float* out_rgb, float* out_alpha, float* out_depth,
+                         void* stream);
+
 /* The binning half of gr_fwd_render (pair emission, tile sort, work items) on its own, so a caller can
  * run it on another stream (e.g. a high-priority one) and then render with gr_view.binned = 1 on the
  * same plan, geom, bins and scratch. */
@@ -174,6 +183,15 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
                  const void* geom, const void* bins, const float* saved, const float* g_rgb,
                  const float* g_alpha, const float* g_depth, float* d_means, float* d_scales,
                  float* d_colors, float* d_opacities, void* ws, size_t ws_bytes, void* stream);
+
+/* gr_bwd with the gradients of rendered Gaussian i written to row index[i] of d_* (index: device int[n], a
+ * permutation): a caller that renders a spatially re-ordered copy of its Gaussians (the drop-in op's Morton layout,
+ * 3dgaussian_amd/torch_renderer.py) gets its gradients back in its own order without a separate pass. */
+gr_status gr_bwd_indexed(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
+                         const float* colors, int color_dim, const float* opacities, const void* geom, const void* bins,
+                         const float* saved, const float* g_rgb, const float* g_alpha, const float* g_depth,
+                         const int* index, float* d_means, float* d_scales, float* d_colors, float* d_opacities, void* ws,
+                         size_t ws_bytes, void* stream);
 
 /* Camera gradient of a view after gr_bwd (its workspace ws still holds the per-Gaussian sums gr_bwd formed).
  * Replaces the autograd path of the reference's camera operands: python/torch_renderer.py:140-150 moves
@@ -264,12 +282,21 @@ gr_status gr_reduce_views(int num_views, const gr_reduce_view* views, int n, con
  * sum in f32, gr_reduce_views in f64).  Deterministic.  Replaces the same reference code as
  * gr_reduce_views (fit_multiview_stub.py:310, the autograd sums over the views). */
 typedef struct gr_sums_view {
-  gr_view view;      /* the view as rendered (its camera: the chain rule)      */
-  const float* sums; /* its gr_gather_view output                              */
+  gr_view view;       /* the view as rendered (its camera: the chain rule)                        */
+  const float* sums;  /* its gr_gather_view / gr_bwd_fit_gather output                           */
+  const float* sums3; /* its per-Gaussian depth sums (gr_bwd_fit_gather; n floats), or NULL (none) */
 } gr_sums_view;
 size_t gr_view_sums_floats(int n);
 gr_status gr_gather_view(const gr_view* v, int n, const gr_plan* plan, const void* geom, const void* bins,
                          const void* ws, float* sums, void* stream);
+/* gr_bwd_fit up to the reduction (its depth-loss kernels, the backward splat with the depth-coupled tail pairs and
+ * the gather), the per-Gaussian sums going to `sums` (gr_view_sums_floats(n)) and the depth sums to `sums3` (n
+ * floats): a depth-loss fit reduces a batch of such views with one gr_reduce_sums (their sums3 set), as the fit path
+ * without a depth term does.  The view's geom, bins, saved sums and ws may be released once this has run. */
+gr_status gr_bwd_fit_gather(const gr_view* v, int n, const gr_plan* plan, const void* geom, const void* bins,
+                            const float* saved, const float* target_rgb, const float* target_mask, float w_sil,
+                            const float* target_depth, float w_depth, float g_scale, float* loss_out, void* ws,
+                            size_t ws_bytes, float* sums, float* sums3, void* stream);
 gr_status gr_reduce_sums(int num_views, const gr_sums_view* views, int n, const float* means,
                          const float* scales, const float* colors, int color_dim,
                          const float* opacities, float* d_means, float* d_scales, float* d_colors,
@@ -281,7 +308,8 @@ gr_status gr_reduce_sums(int num_views, const gr_sums_view* views, int n, const 
  * stream (groups of prep_group views, the first of prep_first), then on render stream j % num_streams
  * (stream 0 = `stream`, the caller's) without a depth target gr_fwd_render_l1 + gr_bwd_splat +
  * gr_gather_view, every batch of a stream's views (reduce_batch at most, its last reduce_tail views)
- * gr_reduce_sums into that stream's accumulators; with depth targets gr_fwd_render + gr_bwd_fit.
+ * gr_reduce_sums into that stream's accumulators; with depth targets gr_fwd_render + gr_bwd_fit_gather per view and the
+ * same batched gr_reduce_sums (with the depth sums).
  * losses[j] (device) receives view j's loss; acc[4k + 0..3] are stream k's d_means, d_scales, d_colors,
  * d_opacities accumulators (written by its first batch, then added to), for k < min(num_streams,
  * num_views): the caller sums them in stream order.  Workspaces are the executor's own, reused in

@@ -7,8 +7,8 @@
   mean|out - t| + w_sil mean|alpha - m| (fit_multiview_stub.py:292-299) and its upstream
   sign(out - t) / (3HW), w_sil sign(alpha - m) / HW (torch's abs' with sign(0) = 0) scaled by 1/V, the
   oracle backward, gradients summed over the views.  Bars: loss relative 1e-5, every gradient relL2 1e-4.
-* test_long_fit_with_densify_vs_dense: the bench's fit after 50 Adam steps with one densify/prune in the
-  middle (device rule, C4 -> ~1.15M Gaussians), the fit path's render vs the exact dense float64 render
+* test_long_fit_with_densify_vs_dense: the bench's fit after the stub's default 300 Adam steps with densify/prune
+  every 80 (device rule, C4 -> ~1.5M Gaussians), the fit path's render vs the exact dense float64 render
   on a sample (1000 pixels, 1000 Gaussians' whole-image gradients), relL2 <= 1e-4.
 * test_dropin_loop_speculation_is_exact: the reference loop's calls (fresh device background per view,
   render_gaussians_torch, torch losses, autograd) give bit-identical losses and gradients with and
@@ -100,16 +100,19 @@ def fit_cutoff():
     return importlib.import_module("3dgaussian_amd.torch_renderer").FIT_CUTOFF
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 def test_long_fit_with_densify_vs_dense(cuda):
+    """The stub's default schedule (fit_multiview_stub.py:201-229, 318-325): 300 iterations, densify (ratio 0.15) and
+    prune (opacity 0.05) every 80, at C4: the fit footprint's cutoff margin on a fitted state whose
+    opacity and scale spread has grown for 300 steps and three densifications."""
     fm = importlib.import_module("3dgaussian_amd.fit_multiview")
     tr = importlib.import_module("3dgaussian_amd.torch_renderer")
     bench = importlib.import_module("bench")
     fit, _, _ = _fitter(fm, bench, cuda, 50)
-    for it in range(50):
+    for it in range(300):
         fit.step()
-        if it == 24:
-            fit.densify_and_prune(1_200_000, 0.15, 0.05)
+        if (it + 1) % 80 == 0:
+            fit.densify_and_prune(1_500_000, 0.15, 0.05)
     n = int(fit.params["means"].shape[0])
     assert n > N_C4
     with torch.no_grad():
@@ -132,8 +135,8 @@ def test_long_fit_with_densify_vs_dense(cuda):
     for k, x, gd in zip(("d_means", "d_scales", "d_colors", "d_opac"), grads, dense_g):
         errs[k] = orc.rel_l2(x.cpu().numpy()[sel], gd)
     op = acts[3].cpu().numpy()
-    print(f"C4 after 50 steps + densify (N={n}, opacity {op.min():.3g}..{op.max():.3g}), fit path vs dense sample:",
-          {k: f"{e:.2e}" for k, e in errs.items()})
+    print(f"C4 after 300 steps + 3 densify/prune (N={n}, opacity {op.min():.3g}..{op.max():.3g}), fit path vs dense "
+          f"sample:", {k: f"{e:.2e}" for k, e in errs.items()})
     for k, e in errs.items():
         assert e <= 1e-4, (k, e)
 
@@ -254,3 +257,65 @@ def test_gather_then_reduce_sums_matches_reduce_views(cuda):
         assert torch.equal(p1[k], p2[k]), k
         # one Adam step from the same start: parameter differences are the gradient differences scaled by lr
         torch.testing.assert_close(p1[k], p0[k], rtol=0, atol=1e-6)
+
+
+def test_dropin_layout_and_render_ahead(cuda):
+    """The drop-in op renders a Morton-ordered copy of a caller's Gaussians (torch_renderer._layout_of, from
+    LAYOUT_MIN Gaussians) and, from the second iteration of a loop, splats the next camera ahead of its call
+    (gr_fwd_render_saved + gr_fwd_compose).  Against the op without either (GR_DROPIN_LAYOUT=0, GR_SPECULATE=0): the
+    stub loop's losses and parameters agree within float summation order; with the layout, speculation on and off
+    are bit-identical (the same rendered tensors and kernels)."""
+    tr = importlib.import_module("3dgaussian_amd.torch_renderer")
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    bench = importlib.import_module("bench")
+    R, V, N = 160, 5, 2 * tr.LAYOUT_MIN
+    cams = fm.orbit_cameras(V, R, R, cuda)
+    g = torch.Generator(device=cuda).manual_seed(5)
+    targets = [torch.rand((R, R, 3), generator=g, device=cuda) for _ in range(V)]
+    masks = [(t.mean(dim=2) > 0.5).to(torch.float32) for t in targets]
+    res = {}
+    saved = tr.LAYOUT, tr.SPECULATE
+    try:
+        for layout, spec in ((False, False), (True, False), (True, True)):
+            tr.LAYOUT, tr.SPECULATE = layout, spec
+            h0 = tr._SPEC["hits"]
+            res[(layout, spec)] = _stub_loop(tr, bench.synthetic_params(N, cuda), cams, targets, masks, R, 3, cuda)
+            if spec:
+                assert tr._SPEC["hits"] - h0 >= 2 * (V - 1)
+    finally:
+        tr.LAYOUT, tr.SPECULATE = saved
+    base, lay, spec = res[(False, False)], res[(True, False)], res[(True, True)]
+    assert spec[0] == lay[0]
+    for k in lay[1]:
+        assert torch.equal(spec[1][k], lay[1][k]), k
+    np.testing.assert_allclose(lay[0], base[0], rtol=1e-5)
+    for k in base[1]:
+        err = orc.rel_l2(lay[1][k].cpu().numpy(), base[1][k].cpu().numpy())
+        assert err <= 1e-5, (k, err)
+
+
+def test_dropin_layout_gradients_vs_oracle(cuda):
+    """One view through the drop-in op with the Morton layout: outputs and gradients (returned in the caller's
+    order by gr_bwd_indexed) against the float64 binned oracle on the caller's order."""
+    tr = importlib.import_module("3dgaussian_amd.torch_renderer")
+    n, R = 2 * tr.LAYOUT_MIN, 192
+    sc = orc.synthetic_scene(n, seed=12, scale=0.05)
+    view, proj = orc.orbit_cameras(6, R, R)[4]
+    rng = np.random.default_rng(13)
+    g_rgb = rng.standard_normal((R, R, 3)).astype(np.float32)
+    g_a = rng.standard_normal((R, R)).astype(np.float32)
+    t = [torch.from_numpy(a).to(cuda).requires_grad_(True) for a in sc.arrays()]
+    assert tr.LAYOUT
+    out, alpha, depth = tr.render_gaussians_torch(*t, tr.Camera(torch.from_numpy(view).to(cuda), torch.from_numpy(proj).to(cuda)),
+                                                  R, R, max_gaussians=n, return_aux=True)
+    ((out * torch.from_numpy(g_rgb).to(cuda)).sum() + (alpha * torch.from_numpy(g_a).to(cuda)).sum()).backward()
+    v = orc.make_view(view, proj, R, R, None, cutoff=tr.default_cutoff(False), core_cutoff=tr.DEFAULT_CORE_CUTOFF)
+    o_out, o_a, o_d = orc.forward(v, sc, binned=True)
+    o_g = orc.backward(v, sc, g_rgb, g_a, None, binned=True)
+    errs = {"out": orc.rel_l2(out.detach().cpu().numpy(), o_out), "alpha": orc.rel_l2(alpha.detach().cpu().numpy(), o_a),
+            "depth": orc.rel_l2(depth.detach().cpu().numpy(), o_d)}
+    for k, x, og in zip(("d_means", "d_scales", "d_colors", "d_opac"), t, o_g):
+        errs[k] = orc.rel_l2(x.grad.cpu().numpy(), og)
+    print("drop-in layout vs binned oracle:", {k: f"{e:.2e}" for k, e in errs.items()})
+    for k, e in errs.items():
+        assert e <= 1e-4, (k, e)

@@ -263,8 +263,8 @@ def test_fused_param_step_matches_torch_adam(cuda):
 @pytest.mark.parametrize("sh", [False, True])
 def test_grouped_prepare_matches_single_view_prepare(cuda, sh):
     """gr_fwd_prepare_views_async (parameters read once for up to 4 views) writes, per view, exactly the geom
-    workspace (records, depths, rectangles, counts, offsets, plan) and the pinned-host plan that
-    gr_fwd_prepare_async writes for that view alone."""
+    workspace (records, depths, rectangles, counts, the pair totals, plan) and the pinned-host plan that
+    gr_fwd_prepare_async writes for that view alone (the Gaussians' offsets are the binning's: k_emit_cols)."""
     import torch
 
     fm = importlib.import_module("3dgaussian_amd.fit_multiview")
@@ -291,8 +291,8 @@ def test_grouped_prepare_matches_single_view_prepare(cuda, sh):
             assert pa.num_pairs > 0
             n = acts[0].shape[0]
             off = tr._native.geom_layout(n)
-            parts = [(off[0], (n + 1) * 36), (off[1], n * 16), (off[2], (n + 1) * 8), (off[3], (n + 1) * 8),
-                     (off[4], 24 + ((n + 256) // 256) * 8)]  # records + depths, rects, counts, offsets, plan + totals
+            parts = [(off[0], (n + 1) * 36), (off[1], n * 16), (off[2], (n + 1) * 8), (off[3] + 8 * n, 8),
+                     (off[4], 24 + ((n + 256) // 256) * 8)]  # records + depths, rects, counts, totals, plan + block scan
             for o, nb in parts:
                 assert torch.equal(a.geom[o:o + nb], b.geom[o:o + nb]), (k, q, o)
 
