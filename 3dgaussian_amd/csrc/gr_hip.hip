@@ -1478,7 +1478,7 @@ __device__ __forceinline__ void split3_frag2(const f32x2_t (&v)[4], s16x8 (&f)[3
 #define GR_F16_SB 12
 #endif
 // The A pre-scale of a view: 2^GR_F16_SA while the largest o max(1, z) of its kept Gaussians is below 2^11,
-// lowered by one per binade above, so o * c * ex * 2^sa and the depth channel's o * z * ex * 2^sa stay <= 2^15
+// lowered by one per binade above, so o * c * ex * 2^sa stays <= 2^15 (the z factor is a margin kept from an f16 depth channel)
 // (no inf, whatever the opacities and depths; k_plan computes it from k_preprocess's per-block maxima).  Views with
 // o z below 2048 - every fit, whose opacities are sigmoid outputs, at any sane camera distance - get exactly
 // GR_F16_SA.  The A operands are o c ex with o = max(op, 0)
@@ -1577,9 +1577,11 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
   int idn = stage_id(k0 + TP + tid, k1, pairs);
   int buf = 0;
   const f32x2_t X = {xc, xc}, Y = {yc, yc};
-  // core items outside f32 grade take f16 pieces (W, the colours and D); tail items (their small weights would be
-  // f16 subnormals) two bf16 pieces
-  constexpr bool F16 = GR_FWD_F16 && !PRECISE && !TAIL;
+  // core items of renders without a depth output take f16 pieces (W and the colours).  A depth output
+  // D / (W + 1e-6) divides by W: where W is small the pieces of its smallest terms are f16 subnormals
+  // (relL2 1.8e-3 on the drop-in's 65k-Gaussian view, tests/test_chain_gpu.py), so W and D stay on bf16
+  // pieces, whose exponent range is f32's; tail items (small weights) too
+  constexpr bool F16 = GR_FWD_F16 && !PRECISE && !TAIL && !ZCH;
   const f32x2_t SA = {sa, sa}, SB = {(float)GR_F16_SB, (float)GR_F16_SB};
   (void)SA;
   (void)SB;
@@ -1638,10 +1640,6 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
         split2h_frag2(bv, fb2h);
         split2h_frag2(aW, f2);
         cW = mfma16h_split2(f2, fb2h, cW);
-        if constexpr (ZCH) {  // o z ex 2^sa: f16_sa_of sized sa by the view's largest o max(1, z)
-          split2h_frag2(aD, f2);
-          cD = mfma16h_split2(f2, fb2h, cD);
-        }
       } else {  // no depth gradient will follow: W and D need only what the colours need
         s16x8 f2b[2], f2[2];
         split2_frag2(bv, f2b);
@@ -1763,7 +1761,7 @@ struct L1Args {
   const float* dscal = nullptr;    // device scalars: [0] max(depth), [1] the max's gradient per arg-max pixel
   int pieces = 2;                  // bf16 pieces of the upstream fragments (gr_fwd_render_l1: 3 at f32 grade)
   // gr_fwd_render_l1: the view loss, written by the forward's last finished tile (photometric / silhouette element
-  // counts n1 / n2, as k_tile_loss_final)
+  // counts n1 / n2, tile_loss_total)
   float* loss_out = nullptr;
   int64_t n1 = 0, n2 = 0;
 };
@@ -1888,35 +1886,43 @@ __device__ __forceinline__ float saved_depth(const float4* __restrict__ saved4, 
   return d < 0.0f ? 0.0f : d;
 }
 
+// Per tile the depth maximum; the last tile to finish (arrival ticket, the bins' ticket[tiles]) takes the image's.
 __global__ __launch_bounds__(256) void k_depth_tile_max(ViewK v, const float4* __restrict__ saved4,
-                                                        const float* __restrict__ savedD, float* __restrict__ tile_aux) {
-  const int tile = blockIdx.x, tid = threadIdx.x;
+                                                        const float* __restrict__ savedD, float* __restrict__ tile_aux,
+                                                        float* __restrict__ dscal, int* __restrict__ ticket) {
+  const int tile = blockIdx.x, tid = threadIdx.x, tiles = v.tiles_x * v.tiles_y;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
   float m = (x < v.W && y < v.H) ? saved_depth(saved4, savedD, y * v.W + x) : 0.0f;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   __shared__ float sm[4];
+  __shared__ int last;
   if ((tid & 63) == 0) sm[tid >> 6] = m;
   __syncthreads();
-  if (tid == 0) tile_aux[2 * tile] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
-}
-
-__global__ __launch_bounds__(256) void k_depth_max(const float* __restrict__ tile_aux, int tiles, float* __restrict__ dscal) {
-  float m = 0.0f;
-  for (int t = threadIdx.x; t < tiles; t += 256) m = fmaxf(m, tile_aux[2 * t]);
+  if (tid == 0) st_through(&tile_aux[2 * tile], fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3])));
+  if (!arrive_last(&ticket[tiles], tiles, &last)) return;
+  m = 0.0f;
+  for (int t = tid; t < tiles; t += 256) m = fmaxf(m, ld_through(&tile_aux[2 * t]));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  __shared__ float sm[4];
-  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+  if ((tid & 63) == 0) sm[tid >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0) dscal[0] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+  if (tid == 0) {
+    dscal[0] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+    ticket[tiles] = 0;
+  }
 }
 
+__device__ void depth_final(const float* __restrict__ tile_loss, const float* __restrict__ tile_aux, int tiles, int64_t HW,
+                            float w_depth, float g_scale, float* __restrict__ dscal, double (*r)[256]);
+// Per tile the depth loss's sums; the last tile to finish (the bins' ticket[tiles]) turns them into the max's
+// gradient per arg-max pixel (depth_final).
 __global__ __launch_bounds__(256) void k_depth_tile_sums(ViewK v, const float4* __restrict__ saved4,
                                                          const float* __restrict__ savedD, const float* __restrict__ t_depth,
-                                                         const float* __restrict__ dscal, float* __restrict__ tile_loss,
-                                                         float* __restrict__ tile_aux) {
+                                                         float* __restrict__ dscal, float* __restrict__ tile_loss,
+                                                         float* __restrict__ tile_aux, int64_t HW, float w_depth,
+                                                         float g_scale, int* __restrict__ ticket) {
   const int tile = blockIdx.x, tid = threadIdx.x;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
@@ -1943,36 +1949,41 @@ __global__ __launch_bounds__(256) void k_depth_tile_sums(ViewK v, const float4* 
   }
   __syncthreads();
   if (tid == 0) {
-    tile_loss[4 * tile + 2] = ((sm[0][0] + sm[0][1]) + sm[0][2]) + sm[0][3];
-    tile_loss[4 * tile + 3] = ((sm[1][0] + sm[1][1]) + sm[1][2]) + sm[1][3];
-    tile_aux[2 * tile + 1] = ((sm[2][0] + sm[2][1]) + sm[2][2]) + sm[2][3];
+    st_through(&tile_loss[4 * tile + 2], ((sm[0][0] + sm[0][1]) + sm[0][2]) + sm[0][3]);
+    st_through(&tile_loss[4 * tile + 3], ((sm[1][0] + sm[1][1]) + sm[1][2]) + sm[1][3]);
+    st_through(&tile_aux[2 * tile + 1], ((sm[2][0] + sm[2][1]) + sm[2][2]) + sm[2][3]);
   }
+  __shared__ int last;
+  __shared__ double r[3][256];
+  const int tiles = v.tiles_x * v.tiles_y;
+  if (!arrive_last(&ticket[tiles], tiles, &last)) return;
+  depth_final(tile_loss, tile_aux, tiles, HW, w_depth, g_scale, dscal, r);
+  if (tid == 0) ticket[tiles] = 0;
 }
 
-// dscal[1] = -(w_depth g_scale / HW) sum_p sign(.) (d_p / dm) / dm / (number of arg-max pixels)
-__global__ __launch_bounds__(256) void k_depth_final(const float* __restrict__ tile_loss, const float* __restrict__ tile_aux,
-                                                     int tiles, int64_t HW, float w_depth, float g_scale,
-                                                     float* __restrict__ dscal) {
-  __shared__ double r1[256], r2[256];
+// dscal[1] = -(w_depth g_scale / HW) sum_p sign(.) (d_p / dm) / dm / (number of arg-max pixels), from the tiles'
+// write-through sums (the last tile of k_depth_tile_sums)
+__device__ void depth_final(const float* __restrict__ tile_loss, const float* __restrict__ tile_aux, int tiles, int64_t HW,
+                            float w_depth, float g_scale, float* __restrict__ dscal, double (*r)[256]) {
   const int t = threadIdx.x;
   double s1 = 0.0, s2 = 0.0;
   for (int i = t; i < tiles; i += 256) {
-    s1 += (double)tile_loss[4 * i + 3];
-    s2 += (double)tile_aux[2 * i + 1];
+    s1 += (double)ld_through(&tile_loss[4 * i + 3]);
+    s2 += (double)ld_through(&tile_aux[2 * i + 1]);
   }
-  r1[t] = s1;
-  r2[t] = s2;
+  r[0][t] = s1;
+  r[1][t] = s2;
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
     if (t < w) {
-      r1[t] += r1[t + w];
-      r2[t] += r2[t + w];
+      r[0][t] += r[0][t + w];
+      r[1][t] += r[1][t + w];
     }
     __syncthreads();
   }
   if (t != 0) return;
-  const float gM = -((w_depth * g_scale) / (float)HW) * (float)r1[0];
-  dscal[1] = r2[0] > 0.0 ? gM / (float)r2[0] : 0.0f;
+  const float gM = -((w_depth * g_scale) / (float)HW) * (float)r[0][0];
+  dscal[1] = r[1][0] > 0.0 ? gM / (float)r[1][0] : 0.0f;
 }
 
 // The tile's L1 sums (block of 256 threads, one pixel each): waves, then the 4 wave sums in a fixed order.
@@ -2033,10 +2044,12 @@ __device__ __forceinline__ void tile_fragments(const float (*sU)[TP], uint4* __r
   }
 }
 
+// With the fit loss (l1.t_rgb) the last tile to finish (the bins' ticket[tiles]) also writes the view loss.
 __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __restrict__ saved4,
                                                      const float* __restrict__ savedD, const float* __restrict__ g_rgb,
                                                      const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
-                                                     uint4* __restrict__ UF, int pieces, L1Args l1, bool depth) {
+                                                     uint4* __restrict__ UF, int pieces, L1Args l1, bool depth,
+                                                     int* __restrict__ ticket) {
   const int tile = blockIdx.x, tid = threadIdx.x;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
@@ -2052,6 +2065,15 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
   for (int k = 0; k < 5; ++k) sU[k][tid] = u[k];
   __syncthreads();
   tile_fragments(sU, reinterpret_cast<uint4*>(UF) + (size_t)tile * UF_FRAGS, tid, pieces, depth);
+  if (l1.tile_loss && l1.loss_out) {  // (tile_loss_sums' stores are write-through)
+    __shared__ int last;
+    const int tiles = v.tiles_x * v.tiles_y;
+    if (arrive_last(&ticket[tiles], tiles, &last)) {
+      tile_loss_total<true>(l1.tile_loss, tiles, l1.n1, l1.n2, l1.w_sil, l1.t_depth ? l1.n1 / 3 : 0, l1.w_depth,
+                            l1.loss_out, reinterpret_cast<double (*)[256]>(&sU[0][0]));
+      if (tid == 0) ticket[tiles] = 0;
+    }
+  }
 }
 
 // gr_fwd_render_l1: a finished tile's pixel sums -> the fit loss's upstream fragments (the backward's
@@ -2112,7 +2134,7 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
   const float xc = (float)(tx * T + li) + 0.5f;  // A row = x
   const float yc = (float)(ty * T + li) + 0.5f;  // B col = y
   f32x4 cW = {0.f, 0.f, 0.f, 0.f}, cR = cW, cG = cW, cB = cW, cD = cW;
-  constexpr bool PREC = MODE == 1 || MODE == 5, ZCHK = MODE < 3, F16K = GR_FWD_F16 && MODE >= 2 && MODE <= 4;
+  constexpr bool PREC = MODE == 1 || MODE == 5, ZCHK = MODE < 3, F16K = GR_FWD_F16 && (MODE == 3 || MODE == 4);
   const int sa = F16K && f16_sa ? *f16_sa : GR_F16_SA;  // the view's A pre-scale (f16_sa_of; none: no pair to scale)
   if (k1 > k0) {  // (an empty tile's one item has no pair)
     if (it.x & 1)  // tail items: W and D only, two-piece splits (GR_TAIL2)
@@ -2165,7 +2187,7 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
   if constexpr (MODE == 4 || MODE == 5) {
     // an empty tile has no backward work item: only its loss terms are needed, not its fragments
     l1_tile_epilogue(v, tile, tid, acc, inside, y * v.W + x, l1, UF, smem, nch > 0);
-    // the view loss: the last tile to finish sums the tiles' L1 sums (k_tile_loss_final's order)
+    // the view loss: the last tile to finish sums the tiles' L1 sums (tile_loss_total, a fixed order)
     const int tiles = v.tiles_x * v.tiles_y;
     if (arrive_last(&ticket[tiles], tiles, &last_flag)) {
       tile_loss_total<true>(l1.tile_loss, tiles, l1.n1, l1.n2, l1.w_sil, 0, 0.0f, l1.loss_out,
@@ -3404,13 +3426,6 @@ __global__ __launch_bounds__(256) void k_l1_final(const float* __restrict__ part
 // w_sil mean|alpha - m|, the value k_l1_final gives for the same images.
 // The view loss from the per-tile sums (fixed order, double): mean|out - t| + w_sil mean|alpha - m|
 // (n2 = HW with a mask, else 0) + w_depth mean|d_pred - t_d| (n3 = HW with a depth target, else 0).
-__global__ __launch_bounds__(256) void k_tile_loss_final(const float* __restrict__ tile_loss, int tiles, int64_t n1,
-                                                         int64_t n2, float w_sil, int64_t n3, float w_depth,
-                                                         float* __restrict__ loss) {
-  __shared__ double r[3][256];
-  tile_loss_total<false>(tile_loss, tiles, n1, n2, w_sil, n3, w_depth, loss, r);
-}
-
 // d/da = g sign(a - b) / n1, d/dc = (w2 g) sign(c - d) / n2 (torch: abs' = sign, sign(0) = 0).
 __global__ __launch_bounds__(256) void k_l1_grad(const float* __restrict__ a, const float* __restrict__ b, int64_t n1,
                                                  const float* __restrict__ c, const float* __restrict__ d, int64_t n2,
@@ -4088,18 +4103,23 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
   float* tile_loss = w.tile_loss;
   const bool dfit = t_rgb && t_depth;  // fused depth loss (gr_bwd_fit)
   L1Args l1{t_rgb, t_mask, w_sil, g_scale, t_rgb ? tile_loss : nullptr};
+  if (t_rgb) {  // the view loss: written by k_pixel_grads' last tile
+    l1.loss_out = loss_out;
+    l1.n1 = (int64_t)(3 * HW);
+    l1.n2 = (int64_t)(t_mask ? HW : 0);
+  }
+  // the arrival tickets of the one-launch reductions below: the bins' (zeroed by the work-item builder, left zero
+  // by every kernel that takes one)
+  int* ticket = b.ticket;
   if (dfit) {
     l1.t_depth = t_depth;
     l1.w_depth = w_depth;
     l1.dscal = w.dscal;
     const float4* s4 = (const float4*)saved;
     const float* sD = saved + 4 * HW;
-    hipLaunchKernelGGL(k_depth_tile_max, dim3(tiles), dim3(256), 0, s, vk, s4, sD, w.tile_aux);
-    hipLaunchKernelGGL(k_depth_max, dim3(1), dim3(256), 0, s, (const float*)w.tile_aux, tiles, w.dscal);
-    hipLaunchKernelGGL(k_depth_tile_sums, dim3(tiles), dim3(256), 0, s, vk, s4, sD, t_depth, (const float*)w.dscal,
-                       tile_loss, w.tile_aux);
-    hipLaunchKernelGGL(k_depth_final, dim3(1), dim3(256), 0, s, (const float*)tile_loss, (const float*)w.tile_aux, tiles,
-                       (int64_t)HW, w_depth, g_scale, w.dscal);
+    hipLaunchKernelGGL(k_depth_tile_max, dim3(tiles), dim3(256), 0, s, vk, s4, sD, w.tile_aux, w.dscal, ticket);
+    hipLaunchKernelGGL(k_depth_tile_sums, dim3(tiles), dim3(256), 0, s, vk, s4, sD, t_depth, w.dscal, tile_loss, w.tile_aux,
+                       (int64_t)HW, w_depth, g_scale, ticket);
     GR_HIP_TRY(hipGetLastError());
   }
   const bool depth = g_depth != nullptr || dfit;  // an upstream depth gradient reaches the splat
@@ -4109,12 +4129,7 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
   const int pieces = (v->no_depth_grad == 2 || depth) ? 3 : 2;
   if (num_pairs > 0 || t_rgb) {
     hipLaunchKernelGGL(k_pixel_grads, dim3(tiles), dim3(256), 0, s, vk, (const float4*)saved, saved + 4 * HW, g_rgb,
-                       g_alpha, g_depth, UF, pieces, l1, depth);
-    GR_HIP_TRY(hipGetLastError());
-  }
-  if (t_rgb) {
-    hipLaunchKernelGGL(k_tile_loss_final, dim3(1), dim3(256), 0, s, (const float*)tile_loss, tiles, (int64_t)(3 * HW),
-                       (int64_t)(t_mask ? HW : 0), w_sil, (int64_t)(dfit ? HW : 0), w_depth, loss_out);
+                       g_alpha, g_depth, UF, pieces, l1, depth, ticket);
     GR_HIP_TRY(hipGetLastError());
   }
   if (num_pairs > 0) {
