@@ -470,8 +470,18 @@ size_t scratch_fixed(int vtiles, int64_t K, size_t off[5]) {
 // histogram + two scatter passes over keys and values.  Larger images use the hipcub radix sort on
 // 32-bit keys.
 
-// Waves per column block: the per-wave tile counters (tiles ints per wave) stay within 64 KB LDS.
-inline int tsort_waves(int tiles) { return tiles <= 4096 ? 4 : tiles <= 8192 ? 2 : 1; }
+// Waves per k_tile_place block: the per-wave tile cursors (tiles ints per wave) within 80 KB of LDS (two blocks per
+// CU); beyond 10240 tiles one wave, whose cursors take up to 128 KB.
+// GR_TUNE_PLACE_WAVES / GR_TUNE_COL_TARGET (environment, read once): tuning overrides for tools/bin_bench.py.
+static int64_t tune_env(const char* name) {
+  const char* e = std::getenv(name);
+  return e ? std::atoll(e) : 0;
+}
+inline int tsort_waves(int tiles) {
+  static const int64_t force = tune_env("GR_TUNE_PLACE_WAVES");
+  const int w = tiles <= 2560 ? 8 : tiles <= 5120 ? 4 : tiles <= 10240 ? 2 : 1;
+  return force == 1 || force == 2 || force == 4 || force == 8 ? std::min<int>(w, (int)force) : w;
+}
 
 #ifndef GR_TS_SEG
 #define GR_TS_SEG 24
@@ -479,26 +489,25 @@ inline int tsort_waves(int tiles) { return tiles <= 4096 ? 4 : tiles <= 8192 ? 2
 constexpr int TS_SEG = GR_TS_SEG;  // 64-pair steps per register-resident segment (1536 pairs per wave;
                                    // 16 and 32 (2048) were slower, two segments per wave much slower)
 
-// Columns of the counting sort: column c = the pairs of the G = 256 J consecutive Gaussians [c G, c G + G), one
-// k_emit_cols block each (which counts them per tile as it emits them), so the per-column tile counts need no pass
-// of their own.  J is chosen from the view's plan so that a column holds about one register segment per place
-// wave (64 TS_SEG pairs), and wider while the count matrix (tiles x columns ints, written, scanned and read) would
-// outweigh half the keys (many tiles: 1080p).  Columns follow the Gaussians, so their pair counts vary with the
-// scene (Morton order: near and far parts of the cloud); k_tile_place walks a long column in several segments.
+// Columns of the counting sort: runs of whole 256-Gaussian blocks (k_preprocess's, whose pair offsets k_plan scans)
+// cut by pair count: block b belongs to column floor(start(b) / target), start(b) = its first pair (core + tail
+// index), so a column holds at most target + one block's pairs whatever the scene (a Morton-ordered cloud seen in
+// perspective has near cells of many more pairs per Gaussian than far ones: columns of a fixed Gaussian count are
+// several times out of balance).  One k_emit_cols block per column (which counts its pairs per tile as it emits
+// them, so the per-column tile counts need no pass of their own).  The target fills 2/3 of one register segment per
+// place wave (64 TS_SEG pairs), and is raised while the count matrix (tiles x columns ints, written, scanned and
+// read) would outweigh half the keys (many tiles: 1080p).  A column may be empty (a block of more than `target`
+// pairs spans several targets).
 struct ColPlan {
-  int J, G, cols;
+  int64_t target;
+  int cols;
 };
-constexpr int COL_MAX_J = 64;
-inline ColPlan col_plan(int n, int64_t K, int tiles) {
+inline ColPlan col_plan(int64_t K, int tiles) {
   ColPlan p;
-  const int64_t nn = n > 0 ? n : 1, kk = K > 0 ? K : 1;
-  const int64_t pt = 64ll * TS_SEG * tsort_waves(tiles);  // pairs per column aimed at
-  int64_t J = (pt * nn + 128 * kk) / (256 * kk);           // round(pt n / (256 K))
-  const int64_t Jc = (2 * (int64_t)tiles * nn + 256 * kk - 1) / (256 * kk);  // tiles x cols <= K / 2
-  J = std::max<int64_t>(1, std::min<int64_t>(COL_MAX_J, std::max(J, std::min<int64_t>(Jc, COL_MAX_J))));
-  p.J = (int)J;
-  p.G = 256 * p.J;
-  p.cols = (int)((nn + p.G - 1) / p.G);
+  const int64_t kk = K > 0 ? K : 1;
+  static const int64_t force = tune_env("GR_TUNE_COL_TARGET");
+  p.target = force > 0 ? force : std::max<int64_t>(64ll * TS_SEG * tsort_waves(tiles) * 2 / 3, 2ll * tiles);
+  p.cols = (int)((kk + p.target - 1) / p.target);
   return p;
 }
 
@@ -507,8 +516,10 @@ inline ColPlan col_plan(int n, int64_t K, int tiles) {
 size_t tile_sort_tmp_bytes(int n, int64_t K, int tiles) {
   if (short_keys(tiles)) {
     const int st = tiles / 2;
-    const size_t cells = (size_t)st * col_plan(n, K, st).cols;
-    return 4 * align_up(cells * sizeof(int)) + 2 * align_up((size_t)st * sizeof(int));
+    const int cols = col_plan(K, st).cols;
+    const size_t cells = (size_t)st * cols;
+    return 4 * align_up(cells * sizeof(int)) + 2 * align_up((size_t)st * sizeof(int)) +
+           align_up((size_t)(cols + 1) * sizeof(int));
   }
   size_t tmp = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const int2*)nullptr,
@@ -821,22 +832,51 @@ __global__ __launch_bounds__(256) void k_emit_zones(ViewK v, int n, const int4* 
   }
 }
 
-// Differentiable path, counting-sort views: one block per column of the sort (ColPlan: Gaussians [c G, c G + G),
-// G = 256 J, thread t taking Gaussians c G + t J .. c G + t J + J - 1).  The block
-//   - scans its Gaussians' packed pair counts (core | tail << 32) on top of the column's offset (k_plan's exclusive
+// First block b in [0, nb) whose first pair start(b) (core + tail index, k_plan's scan) is >= x, or nb: a
+// block-wide search, 256 samples per level (two levels up to 16.7M Gaussians).  Block-uniform result.
+__device__ __forceinline__ int blk_first_at(const unsigned long long* __restrict__ bsum, int nb, int64_t x) {
+  int lo = 0, cnt = nb;  // the answer is in [lo, lo + cnt]; start(b) < x below lo
+  while (cnt > 0) {
+    const int S = (cnt + 255) / 256;
+    const int q = (int)threadIdx.x * S;
+    bool p = false;
+    if (q < cnt) {
+      const unsigned long long t = bsum[lo + q];
+      p = (int64_t)((t & 0xffffffffull) + (t >> 32)) < x;
+    }
+    const int k = __syncthreads_count(p);  // the samples below x are a prefix
+    if (k == 0) break;
+    const int a = lo + (k - 1) * S;  // start(a) < x
+    if (S == 1) {
+      lo = a + 1;
+      break;
+    }
+    lo = a + 1;
+    cnt = min(S - 1, nb - lo);
+  }
+  return lo;
+}
+
+// Differentiable path, counting-sort views: one block per column of the sort (ColPlan: 256-Gaussian blocks
+// [colb[c], colb[c + 1]), which it finds itself and records for k_tile_place), walked in rounds of 256 consecutive
+// Gaussians (one per thread: coalesced loads).  Per round the block
+//   - scans its Gaussians' packed pair counts (core | tail << 32) on top of the round's offset (k_plan's exclusive
 //     scan of the 256-Gaussian block totals) and writes every Gaussian's offsets (the gather and the reductions
 //     read them): no separate offsets pass;
-//   - emits its pairs, core pairs at [0, Kc) and tail pairs at [Kc, K), each in Gaussian order with the tiles in
-//     raster order (a pair's index is its partial-sum slot), staged in LDS and written with coalesced stores (direct
-//     scattered stores when the column overflows the window);
-//   - counts them per tile and zone in LDS and writes its row of each zone's count matrix M: no counting pass.
-constexpr int EWIN_COL = 6144;  // pairs staged in LDS per column block
+//   - emits the round's pairs, core pairs at [0, Kc) and tail pairs at [Kc, K), each in Gaussian order with the
+//     tiles in raster order (a pair's index is its partial-sum slot), staged in an LDS window and written with
+//     coalesced stores (direct scattered stores when a round overflows the window: about 8 pairs per Gaussian at
+//     C4, 2k per round);
+// and counts its pairs per tile and zone in LDS over the rounds, then writes its row of each zone's count matrix M:
+// no counting pass.
+constexpr int EWIN_COL = 4096;  // pairs staged in LDS per round
 inline size_t emit_cols_lds(int tiles, bool tail) { return (size_t)tiles * (tail ? 2 : 1) * sizeof(int) + EWIN_COL * 6; }
-__global__ __launch_bounds__(256) void k_emit_cols(ViewK v, int n, int J, int tiles, const int4* __restrict__ rect,
-                                                   const Cnt2* __restrict__ counts, const unsigned long long* __restrict__ bsum,
-                                                   Cnt2* __restrict__ offsets, const float4* __restrict__ rec,
-                                                   uint16_t* __restrict__ keys, int* __restrict__ ids, int* __restrict__ Mc,
-                                                   int* __restrict__ Mt) {
+__global__ __launch_bounds__(256) void k_emit_cols(ViewK v, int n, int nb, int64_t target, int cols, int tiles,
+                                                   const int4* __restrict__ rect, const Cnt2* __restrict__ counts,
+                                                   const unsigned long long* __restrict__ bsum, Cnt2* __restrict__ offsets,
+                                                   const float4* __restrict__ rec, uint16_t* __restrict__ keys,
+                                                   int* __restrict__ ids, int* __restrict__ Mc, int* __restrict__ Mt,
+                                                   int* __restrict__ colb) {
   extern __shared__ __attribute__((aligned(16))) int esm[];
   int* hc = esm;                              // [tiles] core pairs per tile
   int* ht = hc + tiles;                       // [tiles] tail pairs per tile (Mt != null)
@@ -844,33 +884,55 @@ __global__ __launch_bounds__(256) void k_emit_cols(ViewK v, int n, int J, int ti
   uint16_t* sK = (uint16_t*)(sI + EWIN_COL);  // [EWIN_COL] staged tile keys
   __shared__ unsigned long long wsum[4];
   const int c = blockIdx.x, tid = threadIdx.x;
-  const int i0 = c * 256 * J + tid * J, i1 = min(n, i0 + J);
   for (int t = tid; t < (Mt ? 2 : 1) * tiles; t += 256) hc[t] = 0;
-  unsigned long long own = 0;
-  for (int i = i0; i < i1; ++i) own += counts[i].v;
-  unsigned long long tot;
-  const unsigned long long ex = block_exclusive_scan<4>(own, wsum, tot);  // its barriers publish the zeroed counters
-  const Cnt2 cb{bsum[(size_t)c * J]};
   const int Kc = (int)offsets[n].c();
-  const int c0 = (int)cb.c(), t0 = (int)cb.t();         // the column's first core pair, first tail pair (after Kc)
-  const int nc = (int)(tot & 0xffffffffull), nt = (int)(tot >> 32);
-  const bool staged = nc + nt <= EWIN_COL;              // uniform per block
-  unsigned long long run = cb.v + ex;
-  for (int i = i0; i < i1; ++i) {
-    const Cnt2 cn = counts[i];
-    offsets[i].v = run;
+  const float thr_cut = radius_thr(v.cutoff), thr_core = radius_thr(v.core);
+  const int b0 = blk_first_at(bsum, nb, (int64_t)c * target);
+  const int b1 = c + 1 == cols ? nb : blk_first_at(bsum, nb, (int64_t)(c + 1) * target);
+  if (tid == 0) {
+    colb[c] = b0;
+    if (c + 1 == cols) colb[cols] = nb;
+  }
+  // a round's Gaussian (count, rectangle, record) and block offset are loaded one round ahead: the loads of round
+  // r + 1 are in flight while round r scans and emits
+  unsigned long long nx_cnt = 0, nx_b = 0;
+  int4 nx_rc = make_int4(0, 0, -1, -1);
+  float4 nx_a = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto fetch = [&](int blk) {
+    const int i = blk * 256 + tid;
+    nx_b = bsum[blk];
+    if (i < n) {
+      nx_cnt = counts[i].v;
+      nx_rc = rect[i];
+      nx_a = rec[(size_t)REC4 * i];
+    } else {
+      nx_cnt = 0;
+    }
+  };
+  if (b0 < b1) fetch(b0);
+  for (int blk = b0; blk < b1; ++blk) {
+    const int i = blk * 256 + tid;
+    const Cnt2 cn{nx_cnt}, cb{nx_b};
+    const int4 rc = nx_rc;
+    const float4 a = nx_a;
+    if (blk + 1 < b1) fetch(blk + 1);
+    unsigned long long tot;
+    // its first barrier publishes the zeroed counters and ends the previous round's window reads
+    const unsigned long long ex = block_exclusive_scan<4>(cn.v, wsum, tot);
+    const int c0 = (int)cb.c(), t0 = (int)cb.t();  // the round's first core pair, first tail pair (after Kc)
+    const int nc = (int)(tot & 0xffffffffull), nt = (int)(tot >> 32);
+    const bool staged = nc + nt <= EWIN_COL;       // uniform per block
+    const unsigned long long run = cb.v + ex;
+    if (i < n) offsets[i].v = run;
     if (cn.v != 0) {
-      const int4 r = rect[i];
-      const float4 a = rec[(size_t)REC4 * i];
       int kc = (int)(run & 0xffffffffull), kt = (int)(run >> 32);
-      const float thr_cut = radius_thr(v.cutoff), thr_core = radius_thr(v.core);
-      for (int ty = r.y; ty <= r.w; ++ty) {
+      for (int ty = rc.y; ty <= rc.w; ++ty) {
         const float ey = tile_ey(v, a.y, a.w, ty);
-        for (int tx = r.x; tx <= r.z; ++tx) {
+        for (int tx = rc.x; tx <= rc.z; ++tx) {
           const int cls = tile_class_e(tile_ex(v, a.x, a.z, tx) + ey, thr_cut, thr_core);
           if (cls == 0) continue;
           const int t = ty * v.tiles_x + tx;
-          const int e = cls == 2 ? kc++ - c0 : nc + (kt++ - t0);  // index in the column's window
+          const int e = cls == 2 ? kc++ - c0 : nc + (kt++ - t0);  // index in the round's window
           atomicAdd(cls == 2 ? &hc[t] : &ht[t], 1);
           if (staged) {
             sK[e] = (uint16_t)t;
@@ -883,15 +945,16 @@ __global__ __launch_bounds__(256) void k_emit_cols(ViewK v, int n, int J, int ti
         }
       }
     }
-    run += cn.v;
+    if (staged) {
+      __syncthreads();
+      for (int e = tid; e < nc + nt; e += 256) {
+        const int k = e < nc ? c0 + e : Kc + t0 + (e - nc);
+        keys[k] = sK[e];
+        ids[k] = sI[e];
+      }
+    }
   }
   __syncthreads();
-  if (staged)
-    for (int e = tid; e < nc + nt; e += 256) {
-      const int k = e < nc ? c0 + e : Kc + t0 + (e - nc);
-      keys[k] = sK[e];
-      ids[k] = sI[e];
-    }
   for (int t = tid; t < tiles; t += 256) {
     Mc[(size_t)c * tiles + t] = hc[t];
     if (Mt) Mt[(size_t)c * tiles + t] = ht[t];
@@ -1052,7 +1115,7 @@ __device__ __forceinline__ int xcd_item(int b, int nwg) {
 
 // ---- Stable counting sort of the pairs by tile -------------------------------------------------
 // The emitted pairs of each region (zone 0: core pairs [0, Kc), zone 1: tail pairs [Kc, K)) are cut into columns:
-// column c = the region's pairs of the Gaussians [c G, c G + G) (ColPlan), three dependent launches:
+// column c = the region's pairs of the 256-Gaussian blocks [colb[c], colb[c + 1]) (ColPlan), three dependent launches:
 //   k_emit_cols     emits the pairs and counts each column's pairs per tile into M[column][tile] (and writes the
 //                   Gaussians' offsets);
 //   k_tile_colscan  scans M over the columns of each tile (S = start of (column, tile) within the tile) and
@@ -1079,8 +1142,10 @@ struct TZone {
 };
 struct TZones {
   TZone z[2];
-  const Cnt2* offsets;  // the Gaussians' packed offsets (k_emit_cols; offsets[n] = the region totals)
-  int n, G;             // Gaussians, Gaussians per column
+  const Cnt2* offsets;             // the Gaussians' packed offsets (offsets[n] = the region totals)
+  const unsigned long long* bsum;  // the 256-Gaussian blocks' packed first pairs (k_plan)
+  const int* colb;                 // [cols + 1] the columns' first blocks (k_emit_cols)
+  int n, nb;                       // Gaussians, blocks
 };
 // Column block b of the combined grid -> (zone, column), XCD-aware within the grid.
 __device__ __forceinline__ int tzone_of(const TZones& Z, int b, int& c) {
@@ -1090,8 +1155,9 @@ __device__ __forceinline__ int tzone_of(const TZones& Z, int b, int& c) {
   return zone;
 }
 // Pairs [k0, k1) of column c in region `zone`, relative to the region's first pair.
+__device__ __forceinline__ Cnt2 blk_start(const TZones& Z, int b) { return b < Z.nb ? Cnt2{Z.bsum[b]} : Z.offsets[Z.n]; }
 __device__ __forceinline__ void column_range(const TZones& Z, int zone, int c, int64_t& k0, int64_t& k1) {
-  const Cnt2 a = Z.offsets[min(Z.n, c * Z.G)], b = Z.offsets[min(Z.n, (c + 1) * Z.G)];
+  const Cnt2 a = blk_start(Z, Z.colb[c]), b = blk_start(Z, Z.colb[c + 1]);
   k0 = zone ? a.t() : a.c();
   k1 = zone ? b.t() : b.c();
 }
@@ -1307,11 +1373,30 @@ __global__ __launch_bounds__(64 * WAVES, GR_PLACE_WAVES) void k_tile_place(TZone
   int d[TS_SEG], id[TS_SEG];
   ts_load(k0, k1, K - 1, lane, keys, ids_in, d, id);  // in flight while the tile starts are scanned
   for (int t = lane; t < tiles; t += 64) my[t] = 0;
-  // tile starts: thread i owns the contiguous tiles [i per, i per + per); their totals' exclusive scan over the block
+  // tile starts: thread i owns the contiguous tiles [i per, i per + per); their totals' exclusive scan over the block.
+  // The totals and this column's starts within the tiles are loaded PQ at a time, together (one memory latency per
+  // PQ tiles, not one per tile), and kept in registers for the cursor pass when the run fits (per <= PQ: up to
+  // 64 PQ WAVES tiles).
+  constexpr int PQ = 8;
   const int per = (tiles + NT - 1) / NT;
   const int tb = min(tiles, (int)threadIdx.x * per), te = min(tiles, tb + per);
+  const int* __restrict__ Sc = S + (size_t)c * tiles;
+  int tv[PQ], sv[PQ];
+  auto load_run = [&](int t0) {
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) {
+      const int t = min(t0 + q, tiles - 1);
+      tv[q] = T[t];
+      sv[q] = Sc[t];
+    }
+  };
+  load_run(tb);
   int own = 0;
-  for (int t = tb; t < te; ++t) own += T[t];
+  for (int t0 = tb; t0 < te; t0 += PQ) {
+    if (t0 != tb) load_run(t0);
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) own += t0 + q < te ? tv[q] : 0;
+  }
   int incl = own;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -1332,14 +1417,20 @@ __global__ __launch_bounds__(64 * WAVES, GR_PLACE_WAVES) void k_tile_place(TZone
   // cursor of (tile, wave) = region start + tile start + column start within the tile + lower waves' counts
   int run = zbase + incl - own;
   for (int u = 0; u < w; ++u) run += wsc[u];
-  for (int t = tb; t < te; ++t) {
-    int r = run + S[(size_t)c * tiles + t];
-    run += T[t];
+  for (int t0 = tb; t0 < te; t0 += PQ) {
+    if (te - tb > PQ) load_run(t0);  // (a run of at most PQ tiles is still in registers)
 #pragma unroll
-    for (int u = 0; u < WAVES; ++u) {
-      const int m = cur[(size_t)u * tiles + t];
-      cur[(size_t)u * tiles + t] = r;
-      r += m;
+    for (int q = 0; q < PQ; ++q) {
+      const int t = t0 + q;
+      if (t >= te) break;
+      int r = run + sv[q];
+      run += tv[q];
+#pragma unroll
+      for (int u = 0; u < WAVES; ++u) {
+        const int m = cur[(size_t)u * tiles + t];
+        cur[(size_t)u * tiles + t] = r;
+        r += m;
+      }
     }
   }
   __syncthreads();
@@ -2588,8 +2679,7 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
                                                     const Cnt2* __restrict__ offsets, const int* __restrict__ pos_of,
                                                     const float* __restrict__ partials, float* __restrict__ d_means,
                                                     float* __restrict__ d_scales, float* __restrict__ d_colors,
-                                                    float* __restrict__ d_opac, int depth, int acc,
-                                                    const int* __restrict__ out_index) {
+                                                    float* __restrict__ d_opac, int depth, int acc) {
   const int g0 = blockIdx.x * RG;
   const int tid = threadIdx.x, q4 = tid & 3;
   const int i = g0 + (tid >> 2);
@@ -2671,8 +2761,7 @@ __global__ __launch_bounds__(4 * RG) void k_reduce_bwd(ViewK v, int n, const flo
 #pragma unroll
   for (int q = 0; q < NPART; ++q) Sf[q] = sS[tid][q];
   const int gi = g0 + tid;
-  const size_t go = out_index ? (size_t)out_index[gi] : (size_t)gi;  // the row of Gaussian gi in the gradients
-  GradOut out{d_means + 3 * go, d_scales + 3 * go, d_colors + (size_t)CD * go, d_opac + go, acc != 0};
+  GradOut out{d_means + 3 * (size_t)gi, d_scales + 3 * (size_t)gi, d_colors + (size_t)CD * gi, d_opac + gi, acc != 0};
   chain_rule<CD, float>(v, gi, Sf, sS[tid][NPART] != 0.0f ? 1u : 0u, means, scales, colors, opac, out);
 }
 
@@ -2941,7 +3030,9 @@ __global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const floa
                                                      const float* __restrict__ scales, const float* __restrict__ colors,
                                                      const float* __restrict__ opac, float* __restrict__ d_means,
                                                      float* __restrict__ d_scales, float* __restrict__ d_colors,
-                                                     float* __restrict__ d_opac, int acc, const int* __restrict__ out_index) {
+                                                     float* __restrict__ d_opac, int acc, const int* __restrict__ sum_index) {
+  // sum_index (gr_bwd_indexed): Gaussian gi's sums are row sum_index[gi] of the views' sums (a render of a permuted
+  // copy); its parameters and gradients stay row gi
   constexpr int NG = 6 + CD;
   __shared__ float sG[CD == 48 ? 1 : 4][64][NG + 1];
   const int crw = reduce_sums_crw(B.nv, CD);
@@ -2950,10 +3041,11 @@ __global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const floa
   const int gi = (blockIdx.x * (4 / crw) + gw) * 64 + lane;
   GradRegs<CD> gr;
   if (gi < n) {
+    const size_t si = sum_index ? (size_t)sum_index[gi] : (size_t)gi;
     for (int vi = u; vi < B.nv; vi += crw) {
-      const float4 a = B.r[vi].sums[2 * (size_t)gi], b = B.r[vi].sums[2 * (size_t)gi + 1];
+      const float4 a = B.r[vi].sums[2 * si], b = B.r[vi].sums[2 * si + 1];
       // [o S0, o S2, S4, S6 | o S1, S8, S5, S7] -> S0..S8 (S3, the depth sum, is 0 without a depth gradient)
-      const float s3 = B.r[vi].sums3 ? B.r[vi].sums3[gi] : 0.0f;
+      const float s3 = B.r[vi].sums3 ? B.r[vi].sums3[si] : 0.0f;
       const float Sf[NPART] = {a.x, b.x, a.y, s3, a.z, b.z, a.w, b.w, b.y};
       const unsigned on = (a.x != 0.f || a.y != 0.f || a.z != 0.f || a.w != 0.f || b.x != 0.f || b.y != 0.f ||
                            b.z != 0.f || b.w != 0.f || s3 != 0.f) ? 1u : 0u;
@@ -2989,8 +3081,7 @@ __global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const floa
     }
   }
   if (u != 0 || gi >= n) return;
-  const size_t go = out_index ? (size_t)out_index[gi] : (size_t)gi;  // the row of Gaussian gi in the gradients
-  GradOut out{d_means + 3 * go, d_scales + 3 * go, d_colors + (size_t)CD * go, d_opac + go, acc != 0};
+  GradOut out{d_means + 3 * (size_t)gi, d_scales + 3 * (size_t)gi, d_colors + (size_t)CD * gi, d_opac + gi, acc != 0};
 #pragma unroll
   for (int q = 0; q < 3; ++q) out.mean(q, gr.m[q]);
   out.scale(0, gr.s[0]);
@@ -3865,13 +3956,15 @@ static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const vo
       // counting sort of each region (core pairs [0, Kc), tail pairs [Kc, K)) on 16-bit tile keys, columns of G
       // Gaussians: emission + per-column counts + offsets, the column scan, the placement + work items
       const int64_t Kc = plan->num_core_pairs, Kr[2] = {Kc, num_pairs - Kc};
-      const ColPlan cp = col_plan(n, num_pairs, tiles);
+      const ColPlan cp = col_plan(num_pairs, tiles);
+      const int nb = blocks_for(n + 1);
       const size_t cells = (size_t)tiles * cp.cols;
       const int waves = tsort_waves(tiles);
       TZones Z;
       Z.offsets = offs;
       Z.n = n;
-      Z.G = cp.G;
+      Z.nb = nb;
+      Z.bsum = (const unsigned long long*)g.total;
       char* q = (char*)sc.sort_tmp;
       for (int z = 0; z < 2; ++z) {
         TZone& zz = Z.z[z];
@@ -3887,17 +3980,23 @@ static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const vo
         zz.T = (int*)q;
         q += align_up((size_t)tiles * sizeof(int));
       }
+      int* colb = (int*)q;
+      Z.colb = colb;
       const bool tail = Kr[1] > 0;
-      hipLaunchKernelGGL(k_emit_cols, dim3(cp.cols), dim3(256), emit_cols_lds(tiles, tail), s, vk, n, cp.J, tiles,
-                         (const int4*)g.rect, cnt, (const unsigned long long*)g.total, (Cnt2*)g.offsets, (const float4*)g.rec,
-                         (uint16_t*)sc.keys_in, sc.ids_in, Z.z[0].M, tail ? Z.z[1].M : (int*)nullptr);
+      hipLaunchKernelGGL(k_emit_cols, dim3(cp.cols), dim3(256), emit_cols_lds(tiles, tail), s, vk, n, nb, cp.target, cp.cols,
+                         tiles, (const int4*)g.rect, cnt, (const unsigned long long*)g.total, (Cnt2*)g.offsets,
+                         (const float4*)g.rec, (uint16_t*)sc.keys_in, sc.ids_in, Z.z[0].M, tail ? Z.z[1].M : (int*)nullptr,
+                         colb);
       GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_tile_colscan, dim3((tiles + CS_T - 1) / CS_T, 2), dim3(CS_T * CS_G), 0, s, Z, tiles);
       GR_HIP_TRY(hipGetLastError());
       const int blocks = 1 + Z.z[0].cols + Z.z[1].cols;  // block 0: the work items
       const size_t lds = (size_t)tiles * sizeof(int) * waves;
       const int bits = bits_for((uint32_t)tiles);
-      if (waves == 4)
+      if (waves == 8)
+        hipLaunchKernelGGL(k_tile_place<8>, dim3(blocks), dim3(512), lds, s, Z, tiles, bits, b.ranges, b.items, b.num_items,
+                           b.tile_item0, b.ticket, b.pairs, b.pos_of);
+      else if (waves == 4)
         hipLaunchKernelGGL(k_tile_place<4>, dim3(blocks), dim3(256), lds, s, Z, tiles, bits, b.ranges, b.items, b.num_items,
                            b.tile_item0, b.ticket, b.pairs, b.pos_of);
       else if (waves == 2)
@@ -4073,7 +4172,7 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
                           const float* t_rgb, const float* t_mask, float w_sil, float g_scale, float* loss_out,
                           float* d_means, float* d_scales, float* d_colors, float* d_opacities, int accumulate, void* ws,
                           size_t ws_bytes, void* stream, const float* t_depth = nullptr, float w_depth = 0.0f,
-                          const int* out_index = nullptr, float* g_sums = nullptr, float* g_sums3 = nullptr) {
+                          const int* sum_index = nullptr, float* g_sums = nullptr, float* g_sums3 = nullptr) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
   if ((g_depth || (t_rgb && t_depth)) && v->no_depth_grad)
@@ -4172,23 +4271,25 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
     const dim3 grid((n + gpb - 1) / gpb), block(256);
     if (color_dim == 3)
       hipLaunchKernelGGL(k_reduce_sums<3>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
-                         d_colors, d_opacities, accumulate, out_index);
+                         d_colors, d_opacities, accumulate, sum_index);
     else if (color_dim == 12)
       hipLaunchKernelGGL(k_reduce_sums<12>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
-                         d_colors, d_opacities, accumulate, out_index);
+                         d_colors, d_opacities, accumulate, sum_index);
     else
       hipLaunchKernelGGL(k_reduce_sums<48>, grid, block, 0, s, B, n, means, scales, colors, opacities, d_means, d_scales,
-                         d_colors, d_opacities, accumulate, out_index);
+                         d_colors, d_opacities, accumulate, sum_index);
   } else if (gather_only) {  // no pair: every sum is zero
     GR_HIP_TRY(hipMemsetAsync(g_sums, 0, gr_view_sums_floats(n) * sizeof(float), s));
     if (g_sums3) GR_HIP_TRY(hipMemsetAsync(g_sums3, 0, (size_t)n * sizeof(float), s));
   } else {
-    // the backward without a depth gradient writes 8-float rows (bwd_item_bf16)
+    // the backward without a depth gradient writes 8-float rows (bwd_item_bf16).  No pair: every sum is zero, so
+    // the one-pass kernel's rows are the parameters' own (the gradients are zero or the accumulator unchanged in any
+    // order: sum_index needs no mapping here)
     const bool row8 = !depth;
     auto launch = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3((n + RG - 1) / RG), dim3(4 * RG), 0, s, vk, n, means, scales, colors, opacities,
                          (const Cnt2*)g.counts, (const Cnt2*)g.offsets, (const int*)b.pos_of, (const float*)partials,
-                         d_means, d_scales, d_colors, d_opacities, depth ? 1 : 0, accumulate, out_index);
+                         d_means, d_scales, d_colors, d_opacities, depth ? 1 : 0, accumulate);
     };
     if (color_dim == 3)
       row8 ? launch(k_reduce_bwd<3, true>) : launch(k_reduce_bwd<3, false>);

@@ -422,7 +422,8 @@ def backward_native(means, scales, colors, opacities, st: RenderState, g_out, g_
                     index=None):
     """Run gr_bwd.  Returns (d_means, d_scales, d_colors, d_opacities) (+ the backward workspace with
     ``want_ws``: it holds the per-Gaussian sums camera_grad_native reads).  ``index`` (int32 device, n): the
-    rendered Gaussians are a permuted copy, Gaussian i's gradients go to row index[i] (gr_bwd_indexed)."""
+    render was of a permuted copy; means .. opacities and the gradients are in the caller's order and index[r] is
+    the rendered position of the caller's row r (gr_bwd_indexed)."""
     L = _native.lib()
     dev = means.device
     cd = _color_dim(colors)
@@ -694,6 +695,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         when a depth gradient arrives (LAZY_DEPTH), else None.  bin_stream: see forward_native.  layout: a
         _Layout of the inputs (their Morton-ordered copy, rendered instead; the gradients return in the inputs'
         order), or None."""
+        caller = (means, scales, colors, opacities) if layout is not None else (None,) * 4
         if layout is not None:
             means, scales, colors, opacities = layout.tensors
         out, alpha, depth, st = forward_native(means, scales, colors, opacities, gv, prepared, bin_stream=bin_stream)
@@ -705,12 +707,12 @@ class _RasterizeGaussians(torch.autograd.Function):
         # the render state's device buffers are saved tensors: autograd releases them after this node's backward
         # unless the graph is retained (a second backward through it then finds them)
         ctx.save_for_backward(means, scales, colors, opacities, background, view, proj, st.geom, st.bins, st.saved,
-                              layout.index if layout is not None else None)
+                              layout.index if layout is not None else None, *caller)
         return out, alpha, depth
 
     @staticmethod
     def backward(ctx, g_out, g_alpha, g_depth):
-        means, scales, colors, opacities, background, view, proj, geom, bins, saved, index = ctx.saved_tensors
+        means, scales, colors, opacities, background, view, proj, geom, bins, saved, index, *caller = ctx.saved_tensors
         st = RenderState(*ctx.meta, geom, bins, saved)
         if g_out is None:
             g_out = torch.zeros((st.gv.height, st.gv.width, 3), dtype=torch.float32, device=means.device)
@@ -725,8 +727,9 @@ class _RasterizeGaussians(torch.autograd.Function):
             # depth-gradient footprint and differentiate that render
             _, _, _, st = forward_native(means, scales, colors, opacities, ctx.gv_depth, images=False)
         need_view, need_proj = ctx.needs_input_grad[5], ctx.needs_input_grad[6]
-        dm, ds, dc, do, ws = backward_native(means, scales, colors, opacities, st, g_out, g_alpha, g_depth, want_ws=True,
-                                             index=index)
+        # with a layout: the chain rule in the caller's order (its tensors; the rendered copy's sums gathered by index)
+        dm, ds, dc, do, ws = backward_native(*(caller if index is not None else (means, scales, colors, opacities)), st,
+                                             g_out, g_alpha, g_depth, want_ws=True, index=index)
         dbg = _grad_background(st, background, g_out) if ctx.needs_input_grad[4] else None
         dview = dproj = None
         if need_view or need_proj:
@@ -878,6 +881,7 @@ LAYOUT_EVERY = 16   # input sets rendered with one permutation before it is reco
 
 
 class _Layout:
+    """tensors: the rendered (Morton-ordered) copy; index: int32, the rendered position of each caller row."""
     __slots__ = ("refs", "versions", "tensors", "index")
 
     def __init__(self, inputs, tensors, index):
@@ -897,10 +901,12 @@ def _layout_of(m, s, c, o) -> _Layout:
     e = _LAYOUT["entry"]
     if e is not None and e.matches((m, s, c, o)):
         return e
-    pc = _LAYOUT["perm"]  # [weakref(means), n, perm int64, perm int32, uses]
+    pc = _LAYOUT["perm"]  # [weakref(means), n, perm int64, inverse int32, uses]
     if pc is None or pc[0]() is not m or pc[1] != m.shape[0] or pc[4] >= LAYOUT_EVERY:
         perm = spatial.morton_order(m)
-        pc = _LAYOUT["perm"] = [weakref.ref(m), m.shape[0], perm, perm.to(torch.int32), 0]
+        inv = torch.empty_like(perm, dtype=torch.int32)
+        inv[perm] = torch.arange(perm.numel(), dtype=torch.int32, device=perm.device)
+        pc = _LAYOUT["perm"] = [weakref.ref(m), m.shape[0], perm, inv, 0]
     pc[4] += 1
     with torch.no_grad():
         tensors = tuple(t.detach().index_select(0, pc[2]).contiguous() for t in (m, s, c, o))

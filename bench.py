@@ -18,7 +18,9 @@ Also reported on rank 0:
                 (48 B per pair forward, 84 B per core pair backward, + 40 B per pixel) x the units of one
                 launch / its average launch time (HIP events on its launch stream, gr_profile_begin/end,
                 over one single-stream step after the timed region: the timed steps overlap views on 4
-                streams and run uninstrumented), vs 8 TB/s; its PMC HBM traffic from profiles/pmc_traffic.json
+                streams and run uninstrumented; the events bracket the launch and so include its dispatch
+                gap, yet agree with rocprofv3's kernel-trace average of the same kernel within 2%: r04e
+                backward 189.5 us by events vs 192.2 us by rocprofv3 in the same gpurun call), vs 8 TB/s; its PMC HBM traffic from profiles/pmc_traffic.json
                 (tools/pmc_traffic.py); the executed bf16 MFMA rate beside it
   hbm_model     the north_star's framing: SURVEY.md 8(d)'s byte model of the tile-binned path per view at
                 this run's pair count (the fit path bins the survey's 5-sigma footprint), the bench value
@@ -32,6 +34,9 @@ Also reported on rank 0:
                 (fit_multiview_stub.py:265-311): per view render_gaussians_torch(..., return_aux=True) with
                 a fresh device background tensor, torch L1 + silhouette losses, loss.backward(),
                 torch.optim.Adam, float(loss) per iteration; same C4 workload
+  dropin_depth_loss
+                the same loop with the stub's --depth_dir term (fit_multiview_stub.py:299-303): the depth
+                output is differentiated, so the op renders at f32 grade with the depth footprint
   psnr_vs_ref   the checker leg (outside every timed region): one view of the final fitted state, the
                 bench's render path and the drop-in default path vs the exact float64 dense render
                 (oracle/gr_oracle.c, every Gaussian at every pixel) at 2048 random pixels

@@ -184,9 +184,11 @@ gr_status gr_bwd(const gr_view* v, int n, const gr_plan* plan, const float* mean
                  const float* g_alpha, const float* g_depth, float* d_means, float* d_scales,
                  float* d_colors, float* d_opacities, void* ws, size_t ws_bytes, void* stream);
 
-/* gr_bwd with the gradients of rendered Gaussian i written to row index[i] of d_* (index: device int[n], a
- * permutation): a caller that renders a spatially re-ordered copy of its Gaussians (the drop-in op's Morton layout,
- * 3dgaussian_amd/torch_renderer.py) gets its gradients back in its own order without a separate pass. */
+/* gr_bwd for a caller that rendered a spatially re-ordered copy of its Gaussians (the drop-in op's Morton layout,
+ * 3dgaussian_amd/torch_renderer.py): geom / bins / saved are the copy's render, means .. opacities and d_* are in the
+ * CALLER's order, and index[r] (device int[n], a permutation) is the rendered position of the caller's row r.  The
+ * chain rule runs in the caller's order (coalesced parameter reads and gradient writes; one gathered 32-byte sums
+ * row per Gaussian), so the gradients come back in the caller's order without a separate pass. */
 gr_status gr_bwd_indexed(const gr_view* v, int n, const gr_plan* plan, const float* means, const float* scales,
                          const float* colors, int color_dim, const float* opacities, const void* geom, const void* bins,
                          const float* saved, const float* g_rgb, const float* g_alpha, const float* g_depth,
