@@ -412,11 +412,11 @@ struct Bins {
   int* pairs;          // [K] Gaussian id of each sorted pair (its emission index: pos_of's inverse)
   int2* ranges;        // [vtiles] pair range of each virtual tile
   int4* items;         // [cap] work items (tile, k0, k1, chunk)
-  int* num_items;      // [1]
+  int* num_items;      // [2]: all work items, the non-empty ones (listed first; an empty tile's item comes after them)
   int* tile_item0;     // [tiles] first work item of each tile
   int* pos_of;         // [K] sorted position of each pair, by emission index (k_reduce_bwd's map)
-  int* ticket;         // [tiles + 1] arrivals of a split tile's items, then of finished tiles (k_raster_fwd_mfma);
-                       // zeroed by the work-item builder, left zero by the forward
+  int* ticket;         // [tiles] arrivals of a split tile's items (k_raster_fwd_mfma), then the finished-tile fan-in's
+                       // counters (arrive_last_tile); zeroed by the work-item builder, left zero by every user
 };
 
 // Forward-only scratch (freed by the caller after gr_fwd_render).
@@ -432,6 +432,11 @@ struct Scratch {
 inline int64_t item_cap(int tiles, int64_t K) { return (K + CH - 1) / CH + tiles; }
 
 // `vtiles` = 2 x tiles (core and tail lists of each tile) on the differentiable path.
+// The finished-tile fan-in's counters behind the per-tile tickets (arrive_last_tile): eight shards and a top counter,
+// each on a 128-byte line of its own.
+constexpr int FAN_STRIDE = 32;
+__host__ __device__ inline size_t fan_offset(int tiles) { return ((size_t)tiles + 1 + FAN_STRIDE - 1) / FAN_STRIDE * FAN_STRIDE; }
+
 size_t bins_fixed(int vtiles, int64_t K, size_t off[8]) {
   const int tiles = vtiles;
   const size_t kk = (size_t)(K > 0 ? K : 1);
@@ -441,10 +446,10 @@ size_t bins_fixed(int vtiles, int64_t K, size_t off[8]) {
   off[1] = o; o = align_up(o + kk * sizeof(int));
   off[2] = o; o = align_up(o + (size_t)tiles * sizeof(int2));
   off[3] = o; o = align_up(o + cap * sizeof(int4));
-  off[4] = o; o = align_up(o + sizeof(int));
+  off[4] = o; o = align_up(o + 2 * sizeof(int));
   off[5] = o; o = align_up(o + (size_t)tiles * sizeof(int));
   off[6] = o; o = align_up(o + kk * sizeof(int));
-  off[7] = o; o = align_up(o + ((size_t)tiles / 2 + 1) * sizeof(int));
+  off[7] = o; o = align_up(o + (fan_offset(tiles / 2) + 9 * FAN_STRIDE) * sizeof(int));
   return o;
 }
 
@@ -465,13 +470,15 @@ size_t scratch_fixed(int vtiles, int64_t K, size_t off[5]) {
 
 // Pair order by tile.  Pairs leave the emission in Gaussian order; the forward and backward need them
 // grouped by tile with ascending Gaussian ids inside a tile (a stable sort by tile).  Up to
-// TSORT_MAX_TILES tiles this is a stable counting sort over 16-bit tile keys (k_emit_cols, k_tile_colscan,
+// TSORT_MAX_TILES tiles this is a stable counting sort over 16-bit tile keys (k_emit_count, k_tile_colscan,
 // k_tile_place below): the keys are read twice and the ids once, instead of a radix sort's
 // histogram + two scatter passes over keys and values.  Larger images use the hipcub radix sort on
 // 32-bit keys.
 
-// Waves per k_tile_place block: the per-wave tile cursors (tiles ints per wave) within 80 KB of LDS (two blocks per
-// CU); beyond 10240 tiles one wave, whose cursors take up to 128 KB.
+// Waves per k_tile_place block: the per-wave tile cursors (tiles ints per wave) and the block's static LDS within
+// 64 KiB (four waves up to 4,000 tiles: an 800x800 view's 2,500 take 40 KB, so three to four blocks share a CU with
+// the other render streams' splat blocks; a block of 8 waves and 80 KB waited behind them up to 3x its standalone
+// time, profiles/r04p_*); beyond 16,256 tiles one wave, whose cursors take up to 128 KiB.
 // GR_TUNE_PLACE_WAVES / GR_TUNE_COL_TARGET (environment, read once): tuning overrides for tools/bin_bench.py.
 static int64_t tune_env(const char* name) {
   const char* e = std::getenv(name);
@@ -479,8 +486,10 @@ static int64_t tune_env(const char* name) {
 }
 inline int tsort_waves(int tiles) {
   static const int64_t force = tune_env("GR_TUNE_PLACE_WAVES");
-  const int w = tiles <= 2560 ? 8 : tiles <= 5120 ? 4 : tiles <= 10240 ? 2 : 1;
-  return force == 1 || force == 2 || force == 4 || force == 8 ? std::min<int>(w, (int)force) : w;
+  const int64_t per_wave = 4ll * tiles, budget = 65536 - 512;
+  const int w = 4 * per_wave <= budget ? 4 : 2 * per_wave <= budget ? 2 : 1;
+  if (force == 8 && 8 * per_wave <= 81920 - 512) return 8;
+  return force == 1 || force == 2 || force == 4 ? std::min<int>(w, (int)force) : w;
 }
 
 #ifndef GR_TS_SEG
@@ -489,37 +498,33 @@ inline int tsort_waves(int tiles) {
 constexpr int TS_SEG = GR_TS_SEG;  // 64-pair steps per register-resident segment (1536 pairs per wave;
                                    // 16 and 32 (2048) were slower, two segments per wave much slower)
 
-// Columns of the counting sort: runs of whole 256-Gaussian blocks (k_preprocess's, whose pair offsets k_plan scans)
-// cut by pair count: block b belongs to column floor(start(b) / target), start(b) = its first pair (core + tail
-// index), so a column holds at most target + one block's pairs whatever the scene (a Morton-ordered cloud seen in
-// perspective has near cells of many more pairs per Gaussian than far ones: columns of a fixed Gaussian count are
-// several times out of balance).  One k_emit_cols block per column (which counts its pairs per tile as it emits
-// them, so the per-column tile counts need no pass of their own).  The target fills 2/3 of one register segment per
-// place wave (64 TS_SEG pairs), and is raised while the count matrix (tiles x columns ints, written, scanned and
-// read) would outweigh half the keys (many tiles: 1080p).  A column may be empty (a block of more than `target`
-// pairs spans several targets).
-struct ColPlan {
-  int64_t target;
-  int cols;
-};
-inline ColPlan col_plan(int64_t K, int tiles) {
-  ColPlan p;
-  const int64_t kk = K > 0 ? K : 1;
+// Columns of the counting sort: each region's pairs (emission order) cut into columns of cw consecutive pairs, one
+// k_tile_place block per column and one register segment (64 TS_SEG pairs) per wave: every block and wave gets the
+// same work whatever the scene.  cw doubles (several segments per wave) while the count matrix (tiles x columns
+// ints, zeroed, counted into, scanned and read) would outweigh half the keys and columns remain to spare (many
+// tiles: 1080p).  The per-column tile counts come from the emission (k_emit_count), not from a pass of their own.
+inline int col_width(int64_t K, int tiles) {
   static const int64_t force = tune_env("GR_TUNE_COL_TARGET");
-  p.target = force > 0 ? force : std::max<int64_t>(64ll * TS_SEG * tsort_waves(tiles) * 2 / 3, 2ll * tiles);
-  p.cols = (int)((kk + p.target - 1) / p.target);
-  return p;
+  const int waves = tsort_waves(tiles);
+  if (force > 0) return (int)((force + 64 * waves - 1) / (64 * waves) * (64 * waves));
+  const int64_t kk = K > 0 ? K : 1;
+  int64_t pw = 64ll * TS_SEG;
+  auto cols_of = [&](int64_t w) { return (kk + w * waves - 1) / (w * waves); };
+  while ((int64_t)tiles * cols_of(pw) > (1ll << 28) || ((int64_t)tiles * cols_of(pw) > kk / 2 && cols_of(2 * pw) >= 1024))
+    pw *= 2;
+  return (int)(pw * waves);
 }
+inline int cols_of(int64_t Kz, int cw) { return (int)((Kz + cw - 1) / cw); }
 
 // Scratch behind the fixed part: counting sort = per region its count matrix M, its column scan S and its tile
 // totals T (`tiles` = virtual tiles, 2 x screen tiles); radix sort = its temp storage.
 size_t tile_sort_tmp_bytes(int n, int64_t K, int tiles) {
   if (short_keys(tiles)) {
+    // per region its M, S (columns x tiles) and T (tiles); each region has at most K pairs
     const int st = tiles / 2;
-    const int cols = col_plan(K, st).cols;
-    const size_t cells = (size_t)st * cols;
-    return 4 * align_up(cells * sizeof(int)) + 2 * align_up((size_t)st * sizeof(int)) +
-           align_up((size_t)(cols + 1) * sizeof(int));
+    const size_t cells = (size_t)st * cols_of(K > 0 ? K : 1, col_width(K, st));
+    (void)n;
+    return 4 * align_up(cells * sizeof(int)) + 2 * align_up((size_t)st * sizeof(int));
   }
   size_t tmp = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const int2*)nullptr,
@@ -832,132 +837,67 @@ __global__ __launch_bounds__(256) void k_emit_zones(ViewK v, int n, const int4* 
   }
 }
 
-// First block b in [0, nb) whose first pair start(b) (core + tail index, k_plan's scan) is >= x, or nb: a
-// block-wide search, 256 samples per level (two levels up to 16.7M Gaussians).  Block-uniform result.
-__device__ __forceinline__ int blk_first_at(const unsigned long long* __restrict__ bsum, int nb, int64_t x) {
-  int lo = 0, cnt = nb;  // the answer is in [lo, lo + cnt]; start(b) < x below lo
-  while (cnt > 0) {
-    const int S = (cnt + 255) / 256;
-    const int q = (int)threadIdx.x * S;
-    bool p = false;
-    if (q < cnt) {
-      const unsigned long long t = bsum[lo + q];
-      p = (int64_t)((t & 0xffffffffull) + (t >> 32)) < x;
-    }
-    const int k = __syncthreads_count(p);  // the samples below x are a prefix
-    if (k == 0) break;
-    const int a = lo + (k - 1) * S;  // start(a) < x
-    if (S == 1) {
-      lo = a + 1;
-      break;
-    }
-    lo = a + 1;
-    cnt = min(S - 1, nb - lo);
-  }
-  return lo;
-}
-
-// Differentiable path, counting-sort views: one block per column of the sort (ColPlan: 256-Gaussian blocks
-// [colb[c], colb[c + 1]), which it finds itself and records for k_tile_place), walked in rounds of 256 consecutive
-// Gaussians (one per thread: coalesced loads).  Per round the block
-//   - scans its Gaussians' packed pair counts (core | tail << 32) on top of the round's offset (k_plan's exclusive
-//     scan of the 256-Gaussian block totals) and writes every Gaussian's offsets (the gather and the reductions
-//     read them): no separate offsets pass;
-//   - emits the round's pairs, core pairs at [0, Kc) and tail pairs at [Kc, K), each in Gaussian order with the
-//     tiles in raster order (a pair's index is its partial-sum slot), staged in an LDS window and written with
-//     coalesced stores (direct scattered stores when a round overflows the window: about 8 pairs per Gaussian at
-//     C4, 2k per round);
-// and counts its pairs per tile and zone in LDS over the rounds, then writes its row of each zone's count matrix M:
-// no counting pass.
-constexpr int EWIN_COL = 4096;  // pairs staged in LDS per round
-inline size_t emit_cols_lds(int tiles, bool tail) { return (size_t)tiles * (tail ? 2 : 1) * sizeof(int) + EWIN_COL * 6; }
-__global__ __launch_bounds__(256) void k_emit_cols(ViewK v, int n, int nb, int64_t target, int cols, int tiles,
-                                                   const int4* __restrict__ rect, const Cnt2* __restrict__ counts,
-                                                   const unsigned long long* __restrict__ bsum, Cnt2* __restrict__ offsets,
-                                                   const float4* __restrict__ rec, uint16_t* __restrict__ keys,
-                                                   int* __restrict__ ids, int* __restrict__ Mc, int* __restrict__ Mt,
-                                                   int* __restrict__ colb) {
-  extern __shared__ __attribute__((aligned(16))) int esm[];
-  int* hc = esm;                              // [tiles] core pairs per tile
-  int* ht = hc + tiles;                       // [tiles] tail pairs per tile (Mt != null)
-  int* sI = ht + (Mt ? tiles : 0);            // [EWIN_COL] staged Gaussian ids
-  uint16_t* sK = (uint16_t*)(sI + EWIN_COL);  // [EWIN_COL] staged tile keys
+// Differentiable path, counting-sort views: one block per 256 consecutive Gaussians (k_preprocess's blocks, one per
+// thread).  The block
+//   - scans its Gaussians' packed pair counts (core | tail << 32) on top of the block's offset (k_plan's exclusive
+//     scan of the block totals) and writes every Gaussian's offsets (the gather and the reductions read them): no
+//     separate offsets pass;
+//   - emits its pairs, core pairs at [0, Kc) and tail pairs at [Kc, K), each in Gaussian order with the tiles in
+//     raster order (a pair's index is its partial-sum slot), staged in an LDS window and written with coalesced
+//     stores (direct scattered stores when the block overflows the window: about 8 pairs per Gaussian at C4, 2k per
+//     block).
+// (Counting the pairs per column here as well, in an LDS histogram flushed with atomics, doubled the kernel's VALU
+// work and bank conflicts and cost more than the counting pass it saved: profiles/r04r_pmc_bin.txt.)
+// Block 0 also zeroes the finished-tile fan-in's counters (`fan`), which the column scan's fan-in uses first.
+constexpr int EWIN_BLK = 4096;  // pairs staged in LDS per block
+__global__ __launch_bounds__(256) void k_emit_offsets(ViewK v, int n, const int4* __restrict__ rect, const Cnt2* __restrict__ counts,
+                                                      const unsigned long long* __restrict__ bsum, Cnt2* __restrict__ offsets,
+                                                      const float4* __restrict__ rec, uint16_t* __restrict__ keys,
+                                                      int* __restrict__ ids, int* __restrict__ fan) {
+  __shared__ int sI[EWIN_BLK];
+  __shared__ uint16_t sK[EWIN_BLK];
   __shared__ unsigned long long wsum[4];
-  const int c = blockIdx.x, tid = threadIdx.x;
-  for (int t = tid; t < (Mt ? 2 : 1) * tiles; t += 256) hc[t] = 0;
+  const int tid = threadIdx.x, b = blockIdx.x, i = b * 256 + tid;
+  if (b == 0 && tid < 9) fan[FAN_STRIDE * tid] = 0;
+  const Cnt2 cn{i < n ? counts[i].v : 0ull};
+  unsigned long long tot;
+  const unsigned long long ex = block_exclusive_scan<4>(cn.v, wsum, tot);
+  const Cnt2 cb{bsum[b]};
   const int Kc = (int)offsets[n].c();
-  const float thr_cut = radius_thr(v.cutoff), thr_core = radius_thr(v.core);
-  const int b0 = blk_first_at(bsum, nb, (int64_t)c * target);
-  const int b1 = c + 1 == cols ? nb : blk_first_at(bsum, nb, (int64_t)(c + 1) * target);
-  if (tid == 0) {
-    colb[c] = b0;
-    if (c + 1 == cols) colb[cols] = nb;
-  }
-  // a round's Gaussian (count, rectangle, record) and block offset are loaded one round ahead: the loads of round
-  // r + 1 are in flight while round r scans and emits
-  unsigned long long nx_cnt = 0, nx_b = 0;
-  int4 nx_rc = make_int4(0, 0, -1, -1);
-  float4 nx_a = make_float4(0.f, 0.f, 0.f, 0.f);
-  auto fetch = [&](int blk) {
-    const int i = blk * 256 + tid;
-    nx_b = bsum[blk];
-    if (i < n) {
-      nx_cnt = counts[i].v;
-      nx_rc = rect[i];
-      nx_a = rec[(size_t)REC4 * i];
-    } else {
-      nx_cnt = 0;
-    }
-  };
-  if (b0 < b1) fetch(b0);
-  for (int blk = b0; blk < b1; ++blk) {
-    const int i = blk * 256 + tid;
-    const Cnt2 cn{nx_cnt}, cb{nx_b};
-    const int4 rc = nx_rc;
-    const float4 a = nx_a;
-    if (blk + 1 < b1) fetch(blk + 1);
-    unsigned long long tot;
-    // its first barrier publishes the zeroed counters and ends the previous round's window reads
-    const unsigned long long ex = block_exclusive_scan<4>(cn.v, wsum, tot);
-    const int c0 = (int)cb.c(), t0 = (int)cb.t();  // the round's first core pair, first tail pair (after Kc)
-    const int nc = (int)(tot & 0xffffffffull), nt = (int)(tot >> 32);
-    const bool staged = nc + nt <= EWIN_COL;       // uniform per block
-    const unsigned long long run = cb.v + ex;
-    if (i < n) offsets[i].v = run;
-    if (cn.v != 0) {
-      int kc = (int)(run & 0xffffffffull), kt = (int)(run >> 32);
-      for (int ty = rc.y; ty <= rc.w; ++ty) {
-        const float ey = tile_ey(v, a.y, a.w, ty);
-        for (int tx = rc.x; tx <= rc.z; ++tx) {
-          const int cls = tile_class_e(tile_ex(v, a.x, a.z, tx) + ey, thr_cut, thr_core);
-          if (cls == 0) continue;
-          const int t = ty * v.tiles_x + tx;
-          const int e = cls == 2 ? kc++ - c0 : nc + (kt++ - t0);  // index in the round's window
-          atomicAdd(cls == 2 ? &hc[t] : &ht[t], 1);
-          if (staged) {
-            sK[e] = (uint16_t)t;
-            sI[e] = i;
-          } else {
-            const int k = e < nc ? c0 + e : Kc + t0 + (e - nc);
-            keys[k] = (uint16_t)t;
-            ids[k] = i;
-          }
+  const int c0 = (int)cb.c(), t0 = (int)cb.t();  // the block's first core pair, first tail pair (after Kc)
+  const int nc = (int)(tot & 0xffffffffull), nt = (int)(tot >> 32);
+  const bool staged = nc + nt <= EWIN_BLK;       // uniform per block
+  const unsigned long long run = cb.v + ex;
+  if (i < n) offsets[i].v = run;
+  if (cn.v != 0) {
+    const int4 rc = rect[i];
+    const float4 a = rec[(size_t)REC4 * i];
+    int kc = (int)(run & 0xffffffffull), kt = (int)(run >> 32);
+    const float thr_cut = radius_thr(v.cutoff), thr_core = radius_thr(v.core);
+    for (int ty = rc.y; ty <= rc.w; ++ty) {
+      const float ey = tile_ey(v, a.y, a.w, ty);
+      for (int tx = rc.x; tx <= rc.z; ++tx) {
+        const int cls = tile_class_e(tile_ex(v, a.x, a.z, tx) + ey, thr_cut, thr_core);
+        if (cls == 0) continue;
+        const int t = ty * v.tiles_x + tx;
+        const int e = cls == 2 ? kc++ - c0 : nc + (kt++ - t0);  // index in the block's window
+        if (staged) {
+          sK[e] = (uint16_t)t;
+          sI[e] = i;
+        } else {
+          const int k = e < nc ? c0 + e : Kc + t0 + (e - nc);
+          keys[k] = (uint16_t)t;
+          ids[k] = i;
         }
       }
     }
-    if (staged) {
-      __syncthreads();
-      for (int e = tid; e < nc + nt; e += 256) {
-        const int k = e < nc ? c0 + e : Kc + t0 + (e - nc);
-        keys[k] = sK[e];
-        ids[k] = sI[e];
-      }
-    }
   }
+  if (!staged) return;  // uniform per block
   __syncthreads();
-  for (int t = tid; t < tiles; t += 256) {
-    Mc[(size_t)c * tiles + t] = hc[t];
-    if (Mt) Mt[(size_t)c * tiles + t] = ht[t];
+  for (int e = tid; e < nc + nt; e += 256) {
+    const int k = e < nc ? c0 + e : Kc + t0 + (e - nc);
+    keys[k] = sK[e];
+    ids[k] = sI[e];
   }
 }
 
@@ -1019,33 +959,36 @@ __global__ __launch_bounds__(WI_THREADS) void k_work_items(int vtiles, const int
   __shared__ typename Scan::TempStorage tmp;
   __shared__ int carry;
   const int tiles = vtiles / 2;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int base = 0; base < tiles; base += WI_THREADS) {
-    const int t = base + (int)threadIdx.x;
-    const int2 rc = t < tiles ? ranges[2 * t] : make_int2(0, 0), rt = t < tiles ? ranges[2 * t + 1] : make_int2(0, 0);
-    const int chc = chunks_of(rc.y - rc.x), cht = chunks_of(rt.y - rt.x);
-    const int nch = t < tiles ? max(1, chc + cht) : 0;  // an empty tile: one empty item
-    int excl, total;
-    Scan(tmp).ExclusiveSum(nch, excl, total);
-    const int first = carry + excl;
-    if (t < tiles) {
-      ticket[t] = 0;
-      tile_item0[2 * t] = first;
-      tile_item0[2 * t + 1] = first + chc;
-      for (int c = 0; c < chc; ++c) items[first + c] = make_int4(2 * t, rc.x + c * CH, min(rc.y, rc.x + (c + 1) * CH), c);
-      for (int c = 0; c < cht; ++c)
-        items[first + chc + c] = make_int4(2 * t + 1, rt.x + c * CH, min(rt.y, rt.x + (c + 1) * CH), c);
-      if (chc + cht == 0) items[first] = make_int4(2 * t, 0, 0, 0);
+  // pass 0: the non-empty tiles' items, in tile order; pass 1: one empty item per empty tile, after all of them
+  for (int pass = 0; pass < 2; ++pass) {
+    if (threadIdx.x == 0 && pass == 0) carry = 0;
+    __syncthreads();
+    for (int base = 0; base < tiles; base += WI_THREADS) {
+      const int t = base + (int)threadIdx.x;
+      const int2 rc = t < tiles ? ranges[2 * t] : make_int2(0, 0), rt = t < tiles ? ranges[2 * t + 1] : make_int2(0, 0);
+      const int chc = chunks_of(rc.y - rc.x), cht = chunks_of(rt.y - rt.x);
+      const int nch = t >= tiles ? 0 : pass == 0 ? chc + cht : (chc + cht == 0 ? 1 : 0);
+      int excl, total;
+      Scan(tmp).ExclusiveSum(nch, excl, total);
+      const int first = carry + excl;
+      if (t < tiles && pass == 0) {
+        ticket[t] = 0;
+        tile_item0[2 * t] = first;
+        tile_item0[2 * t + 1] = first + chc;
+        for (int c = 0; c < chc; ++c) items[first + c] = make_int4(2 * t, rc.x + c * CH, min(rc.y, rc.x + (c + 1) * CH), c);
+        for (int c = 0; c < cht; ++c)
+          items[first + chc + c] = make_int4(2 * t + 1, rt.x + c * CH, min(rt.y, rt.x + (c + 1) * CH), c);
+      } else if (nch) {
+        tile_item0[2 * t] = tile_item0[2 * t + 1] = first;
+        items[first] = make_int4(2 * t, 0, 0, 0);
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) carry += total;
+      __syncthreads();
     }
-    __syncthreads();
-    if (threadIdx.x == 0) carry += total;
-    __syncthreads();
+    if (threadIdx.x == 0) num_items[1 - pass] = carry;  // (pass 0: the non-empty count; pass 1: all)
   }
-  if (threadIdx.x == 0) {
-    *num_items = carry;
-    ticket[tiles] = 0;
-  }
+  if (threadIdx.x < 9) ticket[fan_offset(tiles) + FAN_STRIDE * threadIdx.x] = 0;
 }
 
 // Staging pipeline for the 256-wide Gaussian batches of a work item: the records of batch b+1 are
@@ -1113,11 +1056,57 @@ __device__ __forceinline__ int xcd_item(int b, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
+// Write-through (sc1) stores and loads of data handed from one workgroup to another inside a launch, with an
+// arrival ticket (MI355X_MICROARCH.md, Valid forms, first row of the hand-off table: every store and load of the
+// handed-off bytes sc1; each storing wave drained, a barrier, then one lane's agent-scope atomic add; the workgroup
+// whose add returns count - 1 reads after its add has returned and a barrier).
+template <typename V>
+__device__ __forceinline__ void st_through(V* p, V x) { __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename V>
+__device__ __forceinline__ V ld_through(const V* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Every thread of the block calls this after its write-through stores: true in the block that arrives last of
+// `count` (uniform per block).  `flag`: one LDS word.
+__device__ __forceinline__ bool arrive_last(int* ticket, int count, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have completed
+  __syncthreads();                                   // ... and every wave's
+  if (threadIdx.x == 0) *flag = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == count - 1;
+  __syncthreads();
+  return *flag != 0;
+}
+
+// arrive_last for one arrival of each of `count` indices of a launch (a per-tile kernel's block, the block that
+// finishes a split tile, a column-scan block): index i arrives on shard i & 7 of `fan` (fan_offset: eight shards and a
+// top counter, each on a 128-byte line), the last arrival of each shard on the top counter.  One counter for all of
+// them would serialise the ~2,500 returning atomics of an 800^2 view (one word saturates at ~88 per us,
+// MI355X_MICROARCH.md fanin / dequeue: ~28 us at the end of the launch).  The counters are left zero.
+__device__ __forceinline__ bool arrive_last_of(int* fan, int count, int idx, int* flag) {
+  const int sh = idx & 7, nsh = count < 8 ? count : 8;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have completed
+  __syncthreads();                                   // ... and every wave's
+  if (threadIdx.x == 0) {
+    int last = 0;
+    if (__hip_atomic_fetch_add(&fan[FAN_STRIDE * sh], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ((count - sh + 7) >> 3) - 1) {
+      __hip_atomic_store(&fan[FAN_STRIDE * sh], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = __hip_atomic_fetch_add(&fan[FAN_STRIDE * 8], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
+      if (last) __hip_atomic_store(&fan[FAN_STRIDE * 8], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+__device__ __forceinline__ bool arrive_last_tile(int* ticket, int tiles, int tile, int* flag) {
+  return arrive_last_of(ticket + fan_offset(tiles), tiles, tile, flag);
+}
+
 // ---- Stable counting sort of the pairs by tile -------------------------------------------------
 // The emitted pairs of each region (zone 0: core pairs [0, Kc), zone 1: tail pairs [Kc, K)) are cut into columns:
-// column c = the region's pairs of the 256-Gaussian blocks [colb[c], colb[c + 1]) (ColPlan), three dependent launches:
-//   k_emit_cols     emits the pairs and counts each column's pairs per tile into M[column][tile] (and writes the
-//                   Gaussians' offsets);
+// column c = the region's pairs [c cw, c cw + cw) (col_width), a memset of M and three dependent launches:
+//   k_emit_count    emits the pairs and counts each column's pairs per tile into M[column][tile] (zeroed before;
+//                   it also writes the Gaussians' offsets);
 //   k_tile_colscan  scans M over the columns of each tile (S = start of (column, tile) within the tile) and
 //                   writes the tile's total T[tile];
 //   k_tile_place    one block per (region, column): scans T into the tile starts itself, re-counts per wave,
@@ -1142,10 +1131,7 @@ struct TZone {
 };
 struct TZones {
   TZone z[2];
-  const Cnt2* offsets;             // the Gaussians' packed offsets (offsets[n] = the region totals)
-  const unsigned long long* bsum;  // the 256-Gaussian blocks' packed first pairs (k_plan)
-  const int* colb;                 // [cols + 1] the columns' first blocks (k_emit_cols)
-  int n, nb;                       // Gaussians, blocks
+  int cw;  // pairs per column (col_width)
 };
 // Column block b of the combined grid -> (zone, column), XCD-aware within the grid.
 __device__ __forceinline__ int tzone_of(const TZones& Z, int b, int& c) {
@@ -1155,11 +1141,33 @@ __device__ __forceinline__ int tzone_of(const TZones& Z, int b, int& c) {
   return zone;
 }
 // Pairs [k0, k1) of column c in region `zone`, relative to the region's first pair.
-__device__ __forceinline__ Cnt2 blk_start(const TZones& Z, int b) { return b < Z.nb ? Cnt2{Z.bsum[b]} : Z.offsets[Z.n]; }
 __device__ __forceinline__ void column_range(const TZones& Z, int zone, int c, int64_t& k0, int64_t& k1) {
-  const Cnt2 a = blk_start(Z, Z.colb[c]), b = blk_start(Z, Z.colb[c + 1]);
-  k0 = zone ? a.t() : a.c();
-  k1 = zone ? b.t() : b.c();
+  k0 = (int64_t)c * Z.cw;
+  k1 = min(Z.z[zone].K, k0 + Z.cw);
+}
+
+// Per-column tile counts M[c][t]: one block per (region, column), the column's keys read once (coalesced, eight
+// loads in flight per thread) into an LDS histogram.
+__global__ __launch_bounds__(256) void k_tile_count(TZones Z, int tiles) {
+  extern __shared__ int hist[];
+  int c;
+  const int zone = tzone_of(Z, (int)blockIdx.x, c);
+  const TZone& zz = Z.z[zone];
+  const uint16_t* __restrict__ keys = zz.keys;
+  for (int t = threadIdx.x; t < tiles; t += 256) hist[t] = 0;
+  __syncthreads();
+  int64_t k0, k1;
+  column_range(Z, zone, c, k0, k1);
+  for (int64_t kb = k0 + threadIdx.x; kb < k1; kb += 256 * 8) {
+    int d[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = kb + j * 256 < k1 ? (int)keys[kb + j * 256] : -1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (d[j] >= 0) atomicAdd(&hist[d[j]], 1);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < tiles; t += 256) zz.M[(size_t)c * tiles + t] = hist[t];
 }
 
 // Column scan of M: S[c][t] = sum of M[c'][t] over c' < c, T[t] = the tile's total.  A block takes
@@ -1179,9 +1187,7 @@ __device__ __forceinline__ void column_range(const TZones& Z, int zone, int c, i
 #endif
 constexpr int CS_T = GR_CS_T, CS_G = GR_CS_THREADS / GR_CS_T, CS_R = GR_CS_R;
 
-__global__ __launch_bounds__(GR_CS_THREADS) void k_tile_colscan(TZones Z, int tiles) {
-  const TZone& zz = Z.z[blockIdx.y];
-  if (zz.K == 0) return;  // an empty region: no counts, and the work items get no totals for it
+__device__ __forceinline__ void tile_colscan_block(const TZone& zz, int tiles) {
   const int cols = zz.cols;
   const int* __restrict__ M = zz.M;
   int* __restrict__ S = zz.S;
@@ -1214,7 +1220,7 @@ __global__ __launch_bounds__(GR_CS_THREADS) void k_tile_colscan(TZones Z, int ti
       part[u][tl] = run;
       run += v;
     }
-    if (t < tiles) T[t] = run;
+    if (t < tiles) st_through(&T[t], run);  // read by this launch's last block (work_items_zones<true>)
   }
   __syncthreads();
   if (t < tiles) {
@@ -1237,9 +1243,30 @@ __global__ __launch_bounds__(GR_CS_THREADS) void k_tile_colscan(TZones Z, int ti
   }
 }
 
+
+template <bool THROUGH, int NT>
+__device__ void work_items_zones(int tiles, int Kc, const int* __restrict__ Tc, const int* __restrict__ Tt,
+                                 int2* __restrict__ ranges, int4* __restrict__ items, int* __restrict__ num_items,
+                                 int* __restrict__ tile_item0, int* __restrict__ ticket);
+// ... and the block that finishes last (arrive_last_of over the grid) scans the tile totals into the per-virtual-tile
+// ranges and cuts the work items (work_items_zones): no launch of its own between the scan and the placement.
+__global__ __launch_bounds__(GR_CS_THREADS) void k_tile_colscan(TZones Z, int tiles, int2* __restrict__ ranges,
+                                                             int4* __restrict__ items, int* __restrict__ num_items,
+                                                             int* __restrict__ tile_item0, int* __restrict__ ticket) {
+  __shared__ int last;
+  const TZone& zz = Z.z[blockIdx.y];
+  if (zz.K > 0) tile_colscan_block(zz, tiles);  // (an empty region: no counts, and the work items get no totals for it)
+  const int nb = (int)(gridDim.x * gridDim.y);
+  if (!arrive_last_of(ticket + fan_offset(tiles), nb, (int)(blockIdx.y * gridDim.x + blockIdx.x), &last)) return;
+  work_items_zones<true, GR_CS_THREADS>(tiles, Z.z[1].zbase, Z.z[0].K > 0 ? Z.z[0].T : nullptr, Z.z[1].K > 0 ? Z.z[1].T : nullptr,
+                                  ranges, items, num_items, tile_item0, ticket);
+}
+
+
 __device__ __forceinline__ void ts_load(int64_t kb, int64_t k1, int64_t klast, int lane, const uint16_t* __restrict__ keys,
                                         const int* __restrict__ ids_in, int (&d)[TS_SEG], int (&id)[TS_SEG]) {
-  // branch-free: out-of-range lanes load the last pair (K >= 1) and are marked d = -1
+  // branch-free: out-of-range lanes load the last pair (K >= 1) and are marked d = -1 (every column but a region's
+  // last is whole)
 #pragma unroll
   for (int j = 0; j < TS_SEG; ++j) {
     const int64_t k = kb + j * 64 + lane;
@@ -1288,80 +1315,103 @@ __device__ __forceinline__ void ts_place(int lane, int bits, int* my, const int 
 // Counting-sort views: the per-tile totals of the core region (Tc) and of the tail region (Tt, starting at Kc)
 // scanned into the virtual-tile ranges (2t: core, 2t+1: tail), then cut into work items of <= CH pairs.  Thread i
 // owns a contiguous run of tiles: its run's totals are scanned across the block once (three block scans instead of
-// three per NT tiles), then the run is walked again with running offsets.  Block 0 of k_tile_place.
-template <int NT>
-__device__ __forceinline__ void work_items_zones(int tiles, int Kc, const int* __restrict__ Tc, const int* __restrict__ Tt,
-                                                 int2* __restrict__ ranges, int4* __restrict__ items,
-                                                 int* __restrict__ num_items, int* __restrict__ tile_item0,
-                                                 int* __restrict__ ticket) {
-  typedef hipcub::BlockScan<int, NT> Scan;
-  __shared__ typename Scan::TempStorage tmp;
+// three per NT tiles), then the run is walked again with running offsets.  The last block of k_tile_colscan
+// (THROUGH: the totals were written in that launch, write-through).  A run's totals are loaded RUNQ at a time,
+// together, and kept in registers for the second walk when the run fits (<= RUNQ tiles: 2,560 tiles at NT = 256).
+constexpr int RUNQ = 10;
+template <bool THROUGH, int NT>
+__device__ void work_items_zones(int tiles, int Kc, const int* __restrict__ Tc, const int* __restrict__ Tt,
+                                 int2* __restrict__ ranges, int4* __restrict__ items, int* __restrict__ num_items,
+                                 int* __restrict__ tile_item0, int* __restrict__ ticket) {
+  __shared__ unsigned long long sh[NT / 64];  // two packed 64-bit block scans
   const int per = (tiles + NT - 1) / NT;
   const int t0 = min(tiles, (int)threadIdx.x * per), t1 = min(tiles, t0 + per);
-  int sc = 0, st = 0, sch = 0;
-  for (int t = t0; t < t1; ++t) {
-    const int nc = Tc ? Tc[t] : 0, nt = Tt ? Tt[t] : 0;  // null: an empty zone
-    sc += nc;
-    st += nt;
-    sch += max(1, chunks_of(nc) + chunks_of(nt));  // an empty tile: one empty item
+  int rc_[RUNQ], rt_[RUNQ];
+  auto ld = [&](const int* T, int t) { return !T || t >= t1 ? 0 : THROUGH ? ld_through(T + t) : T[t]; };
+  auto load_run = [&](int b) {
+#pragma unroll
+    for (int q = 0; q < RUNQ; ++q) {
+      rc_[q] = ld(Tc, b + q);
+      rt_[q] = ld(Tt, b + q);
+    }
+  };
+  int sc = 0, st = 0, sch = 0, se = 0;
+  for (int b = t0; b < t1; b += RUNQ) {
+    load_run(b);
+#pragma unroll
+    for (int q = 0; q < RUNQ; ++q) {
+      const int nc = rc_[q], nt = rt_[q];  // (0 past the run, and for an empty zone)
+      sc += nc;
+      st += nt;
+      const int ch = chunks_of(nc) + chunks_of(nt);
+      sch += ch;
+      se += ch == 0 && b + q < t1;  // an empty tile: one empty item, after every non-empty one
+    }
   }
-  int total;
-  Scan(tmp).ExclusiveSum(sc, sc);
-  __syncthreads();
-  Scan(tmp).ExclusiveSum(st, st);
-  __syncthreads();
-  Scan(tmp).ExclusiveSum(sch, sch, total);
-  for (int t = t0; t < t1; ++t) {
-    const int nc = Tc ? Tc[t] : 0, nt = Tt ? Tt[t] : 0;
-    const int2 rc = nc > 0 ? make_int2(sc, sc + nc) : make_int2(0, 0);
-    const int2 rt = nt > 0 ? make_int2(Kc + st, Kc + st + nt) : make_int2(0, 0);
-    const int chc = chunks_of(nc), cht = chunks_of(nt);
-    ranges[2 * t] = rc;
-    ranges[2 * t + 1] = rt;
-    tile_item0[2 * t] = sch;
-    tile_item0[2 * t + 1] = sch + chc;
-    ticket[t] = 0;
-    for (int c = 0; c < chc; ++c) items[sch + c] = make_int4(2 * t, rc.x + c * CH, min(rc.y, rc.x + (c + 1) * CH), c);
-    for (int c = 0; c < cht; ++c)
-      items[sch + chc + c] = make_int4(2 * t + 1, rt.x + c * CH, min(rt.y, rt.x + (c + 1) * CH), c);
-    if (chc + cht == 0) items[sch] = make_int4(2 * t, 0, 0, 0);
-    sc += nc;
-    st += nt;
-    sch += max(1, chc + cht);
+  // (pair counts < 2^31 and item counts: no carry between the packed halves)
+  unsigned long long t1v, t2v;
+  const unsigned long long e1 = block_exclusive_scan<NT / 64>((unsigned long long)sc | ((unsigned long long)st << 32), sh, t1v);
+  const unsigned long long e2 = block_exclusive_scan<NT / 64>((unsigned long long)sch | ((unsigned long long)se << 32), sh, t2v);
+  sc = (int)(e1 & 0xffffffffull);
+  st = (int)(e1 >> 32);
+  sch = (int)(e2 & 0xffffffffull);
+  se = (int)(e2 >> 32);
+  const int total = (int)(t2v & 0xffffffffull), empties = (int)(t2v >> 32);
+  se += total;
+  for (int b = t0; b < t1; b += RUNQ) {
+    if (t1 - t0 > RUNQ) load_run(b);  // (a run of at most RUNQ tiles is still in registers)
+#pragma unroll
+    for (int q = 0; q < RUNQ; ++q) {
+      const int t = b + q;
+      if (t < t1) {
+        const int nc = rc_[q], nt = rt_[q];
+        const int2 rc = nc > 0 ? make_int2(sc, sc + nc) : make_int2(0, 0);
+        const int2 rt = nt > 0 ? make_int2(Kc + st, Kc + st + nt) : make_int2(0, 0);
+        const int chc = chunks_of(nc), cht = chunks_of(nt);
+        ranges[2 * t] = rc;
+        ranges[2 * t + 1] = rt;
+        tile_item0[2 * t] = sch;
+        tile_item0[2 * t + 1] = sch + chc;
+        ticket[t] = 0;
+        for (int c = 0; c < chc; ++c) items[sch + c] = make_int4(2 * t, rc.x + c * CH, min(rc.y, rc.x + (c + 1) * CH), c);
+        for (int c = 0; c < cht; ++c)
+          items[sch + chc + c] = make_int4(2 * t + 1, rt.x + c * CH, min(rt.y, rt.x + (c + 1) * CH), c);
+        if (chc + cht == 0) {
+          tile_item0[2 * t] = tile_item0[2 * t + 1] = se;
+          items[se++] = make_int4(2 * t, 0, 0, 0);
+        }
+        sc += nc;
+        st += nt;
+        sch += chc + cht;
+      }
+    }
   }
   if (threadIdx.x == 0) {
-    *num_items = total;
-    ticket[tiles] = 0;
+    num_items[0] = total + empties;
+    num_items[1] = total;
   }
+  if (threadIdx.x < 9) ticket[fan_offset(tiles) + FAN_STRIDE * threadIdx.x] = 0;
 }
 
-// Grid: 1 + the columns of both regions (block 0: the work items).  LDS: the per-wave cursors [waves][tiles].
+// Grid: the columns of both regions.  LDS: the per-wave cursors [waves][tiles].
 #ifndef GR_PLACE_WAVES
 #define GR_PLACE_WAVES 3
 #endif
+constexpr int TS_CQ = 8;  // tiles per thread per round of k_tile_place's cursor pass
 template <int WAVES>
 __global__ __launch_bounds__(64 * WAVES, GR_PLACE_WAVES) void k_tile_place(TZones Z, int tiles, int bits,
-                                                                    int2* __restrict__ ranges, int4* __restrict__ items,
-                                                                    int* __restrict__ num_items, int* __restrict__ tile_item0,
-                                                                    int* __restrict__ ticket, int* __restrict__ pairs_out,
-                                                                    int* __restrict__ pos_of) {
-  if (blockIdx.x == 0) {
-    work_items_zones<64 * WAVES>(tiles, Z.z[1].zbase, Z.z[0].K > 0 ? Z.z[0].T : nullptr, Z.z[1].K > 0 ? Z.z[1].T : nullptr,
-                                 ranges, items, num_items, tile_item0, ticket);
-    return;
-  }
+                                                                    const int2* __restrict__ ranges,
+                                                                    int* __restrict__ pairs_out, int* __restrict__ pos_of) {
   extern __shared__ int cur[];  // [WAVES][tiles]
-  __shared__ int wsc[WAVES];
+  constexpr int NT = 64 * WAVES;
   int c;
-  const int zone = tzone_of(Z, (int)blockIdx.x - 1, c);
+  const int zone = tzone_of(Z, (int)blockIdx.x, c);
   const TZone& zz = Z.z[zone];
   const int64_t K = zz.K;
   const int zbase = zz.zbase;
   const uint16_t* __restrict__ keys = zz.keys;
   const int* __restrict__ ids_in = zz.ids;
-  const int* __restrict__ S = zz.S;
-  const int* __restrict__ T = zz.T;
-  constexpr int NT = 64 * WAVES;
+  const int* __restrict__ S = zz.S + (size_t)c * tiles;
   const int w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
   int* my = cur + (size_t)w * tiles;
   int64_t kc0, kc1;
@@ -1371,39 +1421,20 @@ __global__ __launch_bounds__(64 * WAVES, GR_PLACE_WAVES) void k_tile_place(TZone
   const int64_t k0 = min(kc1, kc0 + (int64_t)w * wsteps * 64), k1 = min(kc1, k0 + wsteps * 64);
   const int nseg = (int)((wsteps + TS_SEG - 1) / TS_SEG);
   int d[TS_SEG], id[TS_SEG];
-  ts_load(k0, k1, K - 1, lane, keys, ids_in, d, id);  // in flight while the tile starts are scanned
-  for (int t = lane; t < tiles; t += 64) my[t] = 0;
-  // tile starts: thread i owns the contiguous tiles [i per, i per + per); their totals' exclusive scan over the block.
-  // The totals and this column's starts within the tiles are loaded PQ at a time, together (one memory latency per
-  // PQ tiles, not one per tile), and kept in registers for the cursor pass when the run fits (per <= PQ: up to
-  // 64 PQ WAVES tiles).
-  constexpr int PQ = 8;
-  const int per = (tiles + NT - 1) / NT;
-  const int tb = min(tiles, (int)threadIdx.x * per), te = min(tiles, tb + per);
-  const int* __restrict__ Sc = S + (size_t)c * tiles;
-  int tv[PQ], sv[PQ];
-  auto load_run = [&](int t0) {
+  ts_load(k0, k1, K - 1, lane, keys, ids_in, d, id);  // in flight while the counters are cleared
+  // tile bases of the cursor pass (the tile's range start + this column's start within the tile), TS_CQ tiles per
+  // thread per round, strided over the block (coalesced) and loaded together; the first round under the count pass
+  int rx[TS_CQ], sx[TS_CQ];
+  auto load_bases = [&](int t0) {
 #pragma unroll
-    for (int q = 0; q < PQ; ++q) {
-      const int t = min(t0 + q, tiles - 1);
-      tv[q] = T[t];
-      sv[q] = Sc[t];
+    for (int q = 0; q < TS_CQ; ++q) {
+      const int t = min(t0 + q * NT, tiles - 1);
+      rx[q] = ranges[2 * t + zone].x;
+      sx[q] = S[t];
     }
   };
-  load_run(tb);
-  int own = 0;
-  for (int t0 = tb; t0 < te; t0 += PQ) {
-    if (t0 != tb) load_run(t0);
-#pragma unroll
-    for (int q = 0; q < PQ; ++q) own += t0 + q < te ? tv[q] : 0;
-  }
-  int incl = own;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(incl, o);
-    if (lane >= o) incl += y;
-  }
-  if (lane == 63) wsc[w] = incl;
+  load_bases((int)threadIdx.x);
+  for (int t = lane; t < tiles; t += 64) my[t] = 0;
   __builtin_amdgcn_wave_barrier();
   for (int seg = 0; seg < nseg; ++seg) {  // this wave's count per tile
     if (seg > 0) ts_load(k0 + (int64_t)seg * 64 * TS_SEG, k1, K - 1, lane, keys, ids_in, d, id);
@@ -1414,17 +1445,14 @@ __global__ __launch_bounds__(64 * WAVES, GR_PLACE_WAVES) void k_tile_place(TZone
     for (int j = 0; j < TS_SEG; ++j) atomicAdd(&my[d[j] < 0 ? 0 : d[j]], (d[j] < 0 ? 0 : 1) + (id[j] >> 31));
   }
   __syncthreads();
-  // cursor of (tile, wave) = region start + tile start + column start within the tile + lower waves' counts
-  int run = zbase + incl - own;
-  for (int u = 0; u < w; ++u) run += wsc[u];
-  for (int t0 = tb; t0 < te; t0 += PQ) {
-    if (te - tb > PQ) load_run(t0);  // (a run of at most PQ tiles is still in registers)
+  // cursor of (tile, wave) = tile start + column start within the tile + lower waves' counts
+  for (int t0 = threadIdx.x; t0 < tiles; t0 += TS_CQ * NT) {
+    if (t0 != (int)threadIdx.x) load_bases(t0);
 #pragma unroll
-    for (int q = 0; q < PQ; ++q) {
-      const int t = t0 + q;
-      if (t >= te) break;
-      int r = run + sv[q];
-      run += tv[q];
+    for (int q = 0; q < TS_CQ; ++q) {
+      const int t = t0 + q * NT;
+      if (t >= tiles) break;
+      int r = rx[q] + sx[q];
 #pragma unroll
       for (int u = 0; u < WAVES; ++u) {
         const int m = cur[(size_t)u * tiles + t];
@@ -1857,24 +1885,6 @@ struct L1Args {
   int64_t n1 = 0, n2 = 0;
 };
 
-// Write-through (sc1) stores and loads of data handed from one workgroup to another inside a launch, with an
-// arrival ticket (MI355X_MICROARCH.md, Valid forms, first row of the hand-off table: every store and load of the
-// handed-off bytes sc1; each storing wave drained, a barrier, then one lane's agent-scope atomic add; the workgroup
-// whose add returns count - 1 reads after its add has returned and a barrier).
-__device__ __forceinline__ void st_through(float* p, float x) { __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ float ld_through(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Every thread of the block calls this after its write-through stores: true in the block that arrives last of
-// `count` (uniform per block).  `flag`: one LDS word.
-__device__ __forceinline__ bool arrive_last(int* ticket, int count, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have completed
-  __syncthreads();                                   // ... and every wave's
-  if (threadIdx.x == 0) *flag = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == count - 1;
-  __syncthreads();
-  return *flag != 0;
-}
-
 // The view loss from the per-tile L1 sums (one block of 256 threads; double sums in a fixed order):
 // mean |out - t| + w_sil mean |alpha - m| (+ w_depth mean |d_pred - t_d| with n3 > 0).  THROUGH: the sums were
 // written in the same launch (write-through, arrive_last).
@@ -1977,7 +1987,7 @@ __device__ __forceinline__ float saved_depth(const float4* __restrict__ saved4, 
   return d < 0.0f ? 0.0f : d;
 }
 
-// Per tile the depth maximum; the last tile to finish (arrival ticket, the bins' ticket[tiles]) takes the image's.
+// Per tile the depth maximum; the last tile to finish (arrive_last_tile) takes the image's.
 __global__ __launch_bounds__(256) void k_depth_tile_max(ViewK v, const float4* __restrict__ saved4,
                                                         const float* __restrict__ savedD, float* __restrict__ tile_aux,
                                                         float* __restrict__ dscal, int* __restrict__ ticket) {
@@ -1992,22 +2002,19 @@ __global__ __launch_bounds__(256) void k_depth_tile_max(ViewK v, const float4* _
   if ((tid & 63) == 0) sm[tid >> 6] = m;
   __syncthreads();
   if (tid == 0) st_through(&tile_aux[2 * tile], fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3])));
-  if (!arrive_last(&ticket[tiles], tiles, &last)) return;
+  if (!arrive_last_tile(ticket, tiles, tile, &last)) return;
   m = 0.0f;
   for (int t = tid; t < tiles; t += 256) m = fmaxf(m, ld_through(&tile_aux[2 * t]));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if ((tid & 63) == 0) sm[tid >> 6] = m;
   __syncthreads();
-  if (tid == 0) {
-    dscal[0] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
-    ticket[tiles] = 0;
-  }
+  if (tid == 0) dscal[0] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
 }
 
 __device__ void depth_final(const float* __restrict__ tile_loss, const float* __restrict__ tile_aux, int tiles, int64_t HW,
                             float w_depth, float g_scale, float* __restrict__ dscal, double (*r)[256]);
-// Per tile the depth loss's sums; the last tile to finish (the bins' ticket[tiles]) turns them into the max's
+// Per tile the depth loss's sums; the last tile to finish (arrive_last_tile) turns them into the max's
 // gradient per arg-max pixel (depth_final).
 __global__ __launch_bounds__(256) void k_depth_tile_sums(ViewK v, const float4* __restrict__ saved4,
                                                          const float* __restrict__ savedD, const float* __restrict__ t_depth,
@@ -2047,9 +2054,8 @@ __global__ __launch_bounds__(256) void k_depth_tile_sums(ViewK v, const float4* 
   __shared__ int last;
   __shared__ double r[3][256];
   const int tiles = v.tiles_x * v.tiles_y;
-  if (!arrive_last(&ticket[tiles], tiles, &last)) return;
+  if (!arrive_last_tile(ticket, tiles, tile, &last)) return;
   depth_final(tile_loss, tile_aux, tiles, HW, w_depth, g_scale, dscal, r);
-  if (tid == 0) ticket[tiles] = 0;
 }
 
 // dscal[1] = -(w_depth g_scale / HW) sum_p sign(.) (d_p / dm) / dm / (number of arg-max pixels), from the tiles'
@@ -2135,7 +2141,7 @@ __device__ __forceinline__ void tile_fragments(const float (*sU)[TP], uint4* __r
   }
 }
 
-// With the fit loss (l1.t_rgb) the last tile to finish (the bins' ticket[tiles]) also writes the view loss.
+// With the fit loss (l1.t_rgb) the last tile to finish (arrive_last_tile) also writes the view loss.
 __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __restrict__ saved4,
                                                      const float* __restrict__ savedD, const float* __restrict__ g_rgb,
                                                      const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
@@ -2159,11 +2165,9 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
   if (l1.tile_loss && l1.loss_out) {  // (tile_loss_sums' stores are write-through)
     __shared__ int last;
     const int tiles = v.tiles_x * v.tiles_y;
-    if (arrive_last(&ticket[tiles], tiles, &last)) {
+    if (arrive_last_tile(ticket, tiles, tile, &last))
       tile_loss_total<true>(l1.tile_loss, tiles, l1.n1, l1.n2, l1.w_sil, l1.t_depth ? l1.n1 / 3 : 0, l1.w_depth,
                             l1.loss_out, reinterpret_cast<double (*)[256]>(&sU[0][0]));
-      if (tid == 0) ticket[tiles] = 0;
-    }
   }
 }
 
@@ -2214,9 +2218,10 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
   // LDS: two staged record buffers (2 x 9 KiB) during the loop, then the 4-wave reduction (20 KiB).
   __shared__ __attribute__((aligned(16))) float smem[4 * 5 * TP];
   __shared__ int last_flag;
-  const int nitems = *num_items;
+  // the non-empty items spread over the XCDs (xcd_item), then the empty tiles' items (background and loss terms)
+  const int nitems = num_items[0], nfull = num_items[1];
   if ((int)blockIdx.x >= nitems) return;
-  const int item = xcd_item(blockIdx.x, nitems);
+  const int item = (int)blockIdx.x < nfull ? xcd_item(blockIdx.x, nfull) : (int)blockIdx.x;
   const int4 it = items[item];
   const int tile = it.x >> 1, k0 = it.y, k1 = it.z;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
@@ -2280,11 +2285,9 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
     l1_tile_epilogue(v, tile, tid, acc, inside, y * v.W + x, l1, UF, smem, nch > 0);
     // the view loss: the last tile to finish sums the tiles' L1 sums (tile_loss_total, a fixed order)
     const int tiles = v.tiles_x * v.tiles_y;
-    if (arrive_last(&ticket[tiles], tiles, &last_flag)) {
+    if (arrive_last_tile(ticket, tiles, tile, &last_flag))
       tile_loss_total<true>(l1.tile_loss, tiles, l1.n1, l1.n2, l1.w_sil, 0, 0.0f, l1.loss_out,
                             reinterpret_cast<double (*)[256]>(smem));
-      if (tid == 0) ticket[tiles] = 0;
-    }
   }
 }
 
@@ -2591,7 +2594,7 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
   __shared__ __attribute__((aligned(16))) float4 sB[2][TP];
   __shared__ float sZ[2][DEPTH ? TP : 1];
   __shared__ __attribute__((aligned(16))) uint4 sUF[UL::CHUNKS * 64];
-  const int nitems = *num_items;
+  const int nitems = num_items[1];  // the non-empty items (listed first): an empty tile has nothing to differentiate
   if ((int)blockIdx.x >= nitems) return;
   const int item = xcd_item(blockIdx.x, nitems);
   const int4 it = items[item];
@@ -3834,7 +3837,7 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
     mapped = (gr_plan*)attr.devicePointer;
   (void)hipGetLastError();  // a pageable pointer leaves an error code behind
   // exclusive scan of the packed counts over the 256-Gaussian blocks (k_plan); the Gaussian level of the scan is
-  // the binning's (k_emit_cols writes the offsets as it emits)
+  // the binning's (k_emit_count writes the offsets as it emits)
   hipLaunchKernelGGL(k_plan, dim3(1), dim3(PLAN_THREADS), 0, s, g.total, blocks_for(n + 1), g.offsets + n, g.plan, mapped,
                      (const float*)g.omax, g.f16_sa);
   GR_HIP_TRY(hipGetLastError());
@@ -3956,20 +3959,16 @@ static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const vo
       // counting sort of each region (core pairs [0, Kc), tail pairs [Kc, K)) on 16-bit tile keys, columns of G
       // Gaussians: emission + per-column counts + offsets, the column scan, the placement + work items
       const int64_t Kc = plan->num_core_pairs, Kr[2] = {Kc, num_pairs - Kc};
-      const ColPlan cp = col_plan(num_pairs, tiles);
-      const int nb = blocks_for(n + 1);
-      const size_t cells = (size_t)tiles * cp.cols;
+      const int cw = col_width(num_pairs, tiles);
+      const size_t cells = (size_t)tiles * cols_of(num_pairs, cw);
       const int waves = tsort_waves(tiles);
       TZones Z;
-      Z.offsets = offs;
-      Z.n = n;
-      Z.nb = nb;
-      Z.bsum = (const unsigned long long*)g.total;
+      Z.cw = cw;
       char* q = (char*)sc.sort_tmp;
       for (int z = 0; z < 2; ++z) {
         TZone& zz = Z.z[z];
         zz.K = Kr[z];
-        zz.cols = Kr[z] > 0 ? cp.cols : 0;
+        zz.cols = cols_of(Kr[z], cw);
         zz.zbase = z == 0 ? 0 : (int)Kc;
         zz.keys = (const uint16_t*)sc.keys_in + (z == 0 ? 0 : Kc);
         zz.ids = sc.ids_in + (z == 0 ? 0 : Kc);
@@ -3980,31 +3979,31 @@ static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const vo
         zz.T = (int*)q;
         q += align_up((size_t)tiles * sizeof(int));
       }
-      int* colb = (int*)q;
-      Z.colb = colb;
-      const bool tail = Kr[1] > 0;
-      hipLaunchKernelGGL(k_emit_cols, dim3(cp.cols), dim3(256), emit_cols_lds(tiles, tail), s, vk, n, nb, cp.target, cp.cols,
-                         tiles, (const int4*)g.rect, cnt, (const unsigned long long*)g.total, (Cnt2*)g.offsets,
-                         (const float4*)g.rec, (uint16_t*)sc.keys_in, sc.ids_in, Z.z[0].M, tail ? Z.z[1].M : (int*)nullptr,
-                         colb);
+      int* fan = b.ticket + fan_offset(tiles);
+      hipLaunchKernelGGL(k_emit_offsets, dim3(blocks_for(n)), dim3(256), 0, s, vk, n, (const int4*)g.rect, cnt,
+                         (const unsigned long long*)g.total, (Cnt2*)g.offsets, (const float4*)g.rec,
+                         (uint16_t*)sc.keys_in, sc.ids_in, fan);
       GR_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_tile_colscan, dim3((tiles + CS_T - 1) / CS_T, 2), dim3(CS_T * CS_G), 0, s, Z, tiles);
+      const int blocks = Z.z[0].cols + Z.z[1].cols;
+      hipLaunchKernelGGL(k_tile_count, dim3(blocks), dim3(256), (size_t)tiles * sizeof(int), s, Z, tiles);
       GR_HIP_TRY(hipGetLastError());
-      const int blocks = 1 + Z.z[0].cols + Z.z[1].cols;  // block 0: the work items
+      hipLaunchKernelGGL(k_tile_colscan, dim3((tiles + CS_T - 1) / CS_T, 2), dim3(CS_T * CS_G), 0, s, Z, tiles, b.ranges,
+                         b.items, b.num_items, b.tile_item0, b.ticket);
+      GR_HIP_TRY(hipGetLastError());
       const size_t lds = (size_t)tiles * sizeof(int) * waves;
       const int bits = bits_for((uint32_t)tiles);
       if (waves == 8)
-        hipLaunchKernelGGL(k_tile_place<8>, dim3(blocks), dim3(512), lds, s, Z, tiles, bits, b.ranges, b.items, b.num_items,
-                           b.tile_item0, b.ticket, b.pairs, b.pos_of);
+        hipLaunchKernelGGL(k_tile_place<8>, dim3(blocks), dim3(512), lds, s, Z, tiles, bits, (const int2*)b.ranges, b.pairs,
+                           b.pos_of);
       else if (waves == 4)
-        hipLaunchKernelGGL(k_tile_place<4>, dim3(blocks), dim3(256), lds, s, Z, tiles, bits, b.ranges, b.items, b.num_items,
-                           b.tile_item0, b.ticket, b.pairs, b.pos_of);
+        hipLaunchKernelGGL(k_tile_place<4>, dim3(blocks), dim3(256), lds, s, Z, tiles, bits, (const int2*)b.ranges, b.pairs,
+                           b.pos_of);
       else if (waves == 2)
-        hipLaunchKernelGGL(k_tile_place<2>, dim3(blocks), dim3(128), lds, s, Z, tiles, bits, b.ranges, b.items, b.num_items,
-                           b.tile_item0, b.ticket, b.pairs, b.pos_of);
+        hipLaunchKernelGGL(k_tile_place<2>, dim3(blocks), dim3(128), lds, s, Z, tiles, bits, (const int2*)b.ranges, b.pairs,
+                           b.pos_of);
       else
-        hipLaunchKernelGGL(k_tile_place<1>, dim3(blocks), dim3(64), lds, s, Z, tiles, bits, b.ranges, b.items, b.num_items,
-                           b.tile_item0, b.ticket, b.pairs, b.pos_of);
+        hipLaunchKernelGGL(k_tile_place<1>, dim3(blocks), dim3(64), lds, s, Z, tiles, bits, (const int2*)b.ranges, b.pairs,
+                           b.pos_of);
       GR_HIP_TRY(hipGetLastError());
     } else {
       // radix sort of the whole pair array on virtual-tile keys (> TSORT_MAX_TILES tiles); the Gaussians' offsets

@@ -15,5 +15,5 @@ for cfg in "$@"; do
   (cd /tmp && GR_TUNE_PLACE_WAVES=$W GR_TUNE_COL_TARGET=$T timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/bin_${W}_${T} \
     -o run --output-format csv -- python3 $R/tools/bin_bench.py 30 > $O/bin_${W}_${T}.log 2>&1)
   grep us_per_binning $O/bin_${W}_${T}.log
-  (cd $R && python tools/kstats.py $O/bin_${W}_${T} | head -6)
+  (cd $R && python tools/kstats.py $O/bin_${W}_${T} > $O/bin_${W}_${T}.txt && sed -n 2,6p $O/bin_${W}_${T}.txt)
 done
