@@ -3733,13 +3733,28 @@ __device__ __forceinline__ void plan_scan(unsigned long long* __restrict__ bsum,
   __shared__ float shm[PLAN_THREADS / 64];
   const int tid = (int)threadIdx.x, per = (blocks + PLAN_THREADS - 1) / PLAN_THREADS;
   const int b0 = min(blocks, tid * per), b1 = min(blocks, b0 + per);
+  // a thread's run of block sums is loaded PLAN_Q at a time, together (one memory latency per PLAN_Q blocks, not one
+  // per block: 1M Gaussians are 3,907 blocks, 16 per thread), and kept in registers for the write-back when it fits
+  constexpr int PLAN_Q = 16;
+  unsigned long long v[PLAN_Q];
+  float m[PLAN_Q];
+  auto load_run = [&](int b) {
+#pragma unroll
+    for (int q = 0; q < PLAN_Q; ++q) {
+      v[q] = b + q < b1 ? bsum[b + q] : 0ull;
+      m[q] = b + q < b1 ? omax[b + q] : 0.0f;
+    }
+  };
   unsigned long long acc = 0, ex = 0;
   float om = 0.0f;
-  for (int b = b0; b < b1; ++b) {
-    const unsigned long long t = bsum[b];
-    acc += t;
-    ex += (t & 0xffffffffull) + (t >> 32);
-    om = fmaxf(om, omax[b]);
+  for (int b = b0; b < b1; b += PLAN_Q) {
+    load_run(b);
+#pragma unroll
+    for (int q = 0; q < PLAN_Q; ++q) {
+      acc += v[q];
+      ex += (v[q] & 0xffffffffull) + (v[q] >> 32);
+      om = fmaxf(om, m[q]);
+    }
   }
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) om = fmaxf(om, __shfl_xor(om, m));
@@ -3748,10 +3763,14 @@ __device__ __forceinline__ void plan_scan(unsigned long long* __restrict__ bsum,
   const unsigned long long base = block_exclusive_scan<PLAN_THREADS / 64>(acc, sh, grand);
   (void)block_exclusive_scan<PLAN_THREADS / 64>(ex, sh, exact);
   unsigned long long run = base;
-  for (int b = b0; b < b1; ++b) {
-    const unsigned long long t = bsum[b];
-    bsum[b] = run;
-    run += t;
+  for (int b = b0; b < b1; b += PLAN_Q) {
+    if (b1 - b0 > PLAN_Q) load_run(b);  // (a run of at most PLAN_Q blocks is still in registers)
+#pragma unroll
+    for (int q = 0; q < PLAN_Q; ++q)
+      if (b + q < b1) {
+        bsum[b + q] = run;
+        run += v[q];
+      }
   }
   if (tid != 0) return;
 #pragma unroll
