@@ -33,6 +33,11 @@ def test_library_exports_every_declared_symbol(pkg):
     assert not missing, missing
 
 
+def test_every_declared_symbol_has_a_ctypes_signature(pkg):
+    """_native binds exactly the header's entry points (argument and result types set before any call)."""
+    assert sorted(pkg._native._SIG) == declared_functions()
+
+
 def test_version_and_error_string(pkg):
     assert "gfx950" in pkg._native.version()
     assert isinstance(pkg._native.lib().gr_last_error(), bytes)
