@@ -79,6 +79,9 @@ L_MAX_ACC = 8  # GR_FIT_MAX_ACC: stream accumulators gr_fit_param_step sums
 # views prepared together (gr_fwd_prepare_views_async: the parameters read once for the group)
 PREP_GROUP = max(1, min(4, int(os.environ.get("GR_PREP_GROUP", "4"))))
 PREP_FIRST = max(1, min(PREP_GROUP, int(os.environ.get("GR_PREP_FIRST", "1"))))
+# groups prepared before the step's first render is enqueued: 2 (the first view's group and the next one), or 1
+# (only the first view's: the next group is enqueued after the first render)
+PREP_INITIAL = max(1, min(2, int(os.environ.get("GR_PREP_INITIAL", "2"))))
 # the fused path's reduction in two stages: each view's pair partials gathered into per-Gaussian sums right
 # after its backward splat (gr_gather_view: a lean kernel that runs beside the other streams' splats; the view's
 # workspaces are released at once), the chain rules of a stream's batch of views from those sums
@@ -374,7 +377,7 @@ class ViewShardedFitter:
                     ahead.update(zip(js, prepare_views(js)))
                 nxt[0] = js.stop
 
-        prepare_upto(min(PREP_FIRST, PREP_AHEAD - 1))
+        prepare_upto(min(PREP_FIRST, PREP_AHEAD - 1) if PREP_INITIAL > 1 else 0)
         return prepare_upto
 
     def _fit_view(self, i: int, device) -> "tr._native.GrView":
