@@ -101,6 +101,19 @@ class GrFitConfig(ctypes.Structure):
                 ("render_streams", ctypes.POINTER(ctypes.c_void_p)), ("prep_stream", ctypes.c_void_p)]
 
 
+FIT_MAX_ACC = 8      # GR_FIT_MAX_ACC
+FIT_MAX_PARAMS = 8   # GR_FIT_MAX_PARAMS
+
+
+class GrParamStep(ctypes.Structure):
+    """gr_param_step (include/gr_hip.h): one parameter tensor of a gr_fit_param_steps launch."""
+
+    _fields_ = [("count", ctypes.c_int64), ("act", ctypes.c_int), ("num_accs", ctypes.c_int), ("param", ctypes.c_void_p),
+                ("grad", ctypes.c_void_p), ("accs", ctypes.c_void_p * FIT_MAX_ACC), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("reg", ctypes.c_float), ("neg_step_size", ctypes.c_float),
+                ("bias_correction2_sqrt", ctypes.c_float)]
+
+
 class NativeLibraryError(ImportError):
     pass
 
@@ -143,6 +156,8 @@ _SIG = {
                                          _P]),
     "gr_adam_step": (ctypes.c_int, [ctypes.c_int64, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float, ctypes.c_double,
                                     ctypes.c_double, ctypes.c_float, _P]),
+    "gr_fit_param_steps": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(GrParamStep), ctypes.c_double, ctypes.c_double,
+                                          ctypes.c_float, _P]),
     "gr_fwd_render_l1": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P, _P,
                                         ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, ctypes.c_size_t, _P]),
     "gr_bwd_splat": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_size_t, _P]),

@@ -3578,6 +3578,45 @@ __global__ __launch_bounds__(256) void k_fit_param_step(int64_t count, int act, 
   }
 }
 
+// k_fit_param_step over several parameter tensors (gr_fit_param_steps): block b belongs to the tensor whose block
+// range [first[t], first[t + 1]) holds it and grid-strides over that tensor alone.
+struct ParamSteps {
+  gr_param_step s[GR_FIT_MAX_PARAMS];
+  int first[GR_FIT_MAX_PARAMS + 1];
+  int num;
+};
+__global__ __launch_bounds__(256) void k_fit_param_steps(ParamSteps P, float b1, float b2, float b2_c, float eps) {
+  int t = 0;
+  while (t + 1 < P.num && (int)blockIdx.x >= P.first[t + 1]) ++t;
+  const gr_param_step& q = P.s[t];
+  const int nb = P.first[t + 1] - P.first[t];
+  float* __restrict__ p = q.param;
+  float* __restrict__ m = q.exp_avg;
+  float* __restrict__ v = q.exp_avg_sq;
+  for (int64_t e = (int64_t)(blockIdx.x - P.first[t]) * 256 + threadIdx.x; e < q.count; e += (int64_t)nb * 256) {
+    float gact = q.num_accs > 0 ? q.accs[0][e] : 0.0f;
+    for (int a = 1; a < q.num_accs; ++a) gact = gact + q.accs[a][e];  // in stream order
+    gact = gact + q.reg;
+    const float x = p[e];
+    float g;
+    if (q.act == 1) {
+      const float z = expf(x);
+      g = x > 20.0f ? gact : gact * z / (z + 1.0f);
+    } else if (q.act == 2) {
+      const float y = 1.0f / (1.0f + expf(-x));
+      g = gact * (1.0f - y) * y;
+    } else {
+      g = gact;
+    }
+    if (q.grad) q.grad[e] = g;
+    const float mm = fmaf(b1, g - m[e], m[e]);
+    const float vv = fmaf(b2_c, g * g, v[e] * b2);
+    m[e] = mm;
+    v[e] = vv;
+    p[e] = fmaf(q.neg_step_size, mm / (sqrtf(vv) / q.bias_correction2_sqrt + eps), x);
+  }
+}
+
 // Adam alone on an assembled (e.g. all-reduced) gradient.
 __global__ __launch_bounds__(256) void k_adam_step(int64_t count, float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, float neg_step,
@@ -4722,6 +4761,32 @@ gr_status gr_fit_param_step(int64_t count, int act, float* param, float* grad, c
   const float w1 = (float)(1.0 - beta1), w2 = (float)(1.0 - beta2);
   if (GR_DEBUG_SKIP & 16) return GR_OK;
   hipLaunchKernelGGL(k_fit_param_step, dim3(blocks), dim3(256), 0, (hipStream_t)stream, count, act, param, grad, acc, reg, adam, exp_avg, exp_avg_sq, neg_step_size, bias_correction2_sqrt, w1, (float)beta2, w2, eps);
+  GR_HIP_TRY(hipGetLastError());
+  return GR_OK;
+}
+
+gr_status gr_fit_param_steps(int num, const gr_param_step* steps, double beta1, double beta2, float eps, void* stream) {
+  if (num < 0 || num > GR_FIT_MAX_PARAMS || (num > 0 && !steps))
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_param_steps: bad arguments");
+  ParamSteps P;
+  P.num = 0;
+  P.first[0] = 0;
+  for (int t = 0; t < num; ++t) {
+    const gr_param_step& q = steps[t];
+    if (q.count < 0 || q.act < 0 || q.act > 2 || !q.param || !q.exp_avg || !q.exp_avg_sq || q.num_accs < 0 ||
+        q.num_accs > GR_FIT_MAX_ACC)
+      return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_param_steps: bad parameter entry");
+    for (int a = 0; a < q.num_accs; ++a)
+      if (!q.accs[a]) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_param_steps: null accumulator");
+    if (q.count == 0) continue;
+    P.s[P.num] = q;
+    P.first[P.num + 1] = P.first[P.num] + (int)std::min<int64_t>((q.count + 255) / 256, 1024);
+    ++P.num;
+  }
+  if (P.num == 0) return GR_OK;
+  if (GR_DEBUG_SKIP & 16) return GR_OK;
+  hipLaunchKernelGGL(k_fit_param_steps, dim3(P.first[P.num]), dim3(256), 0, (hipStream_t)stream, P, (float)(1.0 - beta1),
+                     (float)beta2, (float)(1.0 - beta2), eps);
   GR_HIP_TRY(hipGetLastError());
   return GR_OK;
 }

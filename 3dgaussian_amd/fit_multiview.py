@@ -859,8 +859,25 @@ class ViewShardedFitter:
                                                      ctypes.c_double(b2), ctypes.c_float(eps), stream), "gr_fit_param_step")
             assembly.append(step_call)
         if flat is None:
-            for call in assembly:
-                call()
+            if len(plist) <= tr._native.FIT_MAX_PARAMS and all(len(pp) <= tr._native.FIT_MAX_ACC for pp in parts):
+                # world size 1: every parameter's gradient and Adam update in one launch (gr_fit_param_steps)
+                arr = (tr._native.GrParamStep * len(plist))()
+                for q, (k, p) in enumerate(zip(names, plist)):
+                    st, (neg_step, bc2s) = self.opt.state[p], steps[q]
+                    a = [pp[slot[k]] for pp in parts]
+                    e = arr[q]
+                    e.count, e.act, e.num_accs = p.numel(), act[k], len(a)
+                    e.param, e.grad = p.data.data_ptr(), p.grad.data_ptr()
+                    for j, x in enumerate(a):
+                        e.accs[j] = x.data_ptr()
+                    e.exp_avg, e.exp_avg_sq = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
+                    e.reg = reg.get(k, 0.0) if self.rank == 0 else 0.0
+                    e.neg_step_size, e.bias_correction2_sqrt = neg_step, bc2s
+                tr._native.check(L.gr_fit_param_steps(len(plist), arr, ctypes.c_double(b1), ctypes.c_double(b2),
+                                                      ctypes.c_float(eps), stream), "gr_fit_param_steps")
+            else:
+                for call in assembly:
+                    call()
             return loss.detach()
         bounds, o0 = [], 0
         for p in plist:

@@ -388,6 +388,24 @@ gr_status gr_fit_param_step(int64_t count, int act, float* param, float* grad, c
 gr_status gr_adam_step(int64_t count, float* param, const float* grad, float* exp_avg,
                        float* exp_avg_sq, float neg_step_size, float bias_correction2_sqrt,
                        double beta1, double beta2, float eps, void* stream);
+/* gr_fit_param_steps: gr_fit_param_step (adam != 0) for up to GR_FIT_MAX_PARAMS parameter tensors in one launch
+ * (world size 1: no all-reduce between the gradient and the update), each with its own count, activation, arrays,
+ * regulariser weight and bias corrections; the same results as one gr_fit_param_step per tensor. */
+#define GR_FIT_MAX_PARAMS 8
+typedef struct gr_param_step {
+  int64_t count;
+  int act;
+  int num_accs;
+  float* param;
+  float* grad;                           /* may be NULL: the gradient is not stored */
+  const float* accs[GR_FIT_MAX_ACC];
+  float* exp_avg;
+  float* exp_avg_sq;
+  float reg;
+  float neg_step_size;
+  float bias_correction2_sqrt;
+} gr_param_step;
+gr_status gr_fit_param_steps(int num, const gr_param_step* steps, double beta1, double beta2, float eps, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Introspection (host-only, no GPU needed).                                                  */

@@ -61,6 +61,8 @@ def test_struct_sizes_match_header(pkg):
     assert ctypes.sizeof(pkg._native.GrView) == 4 * (2 + 16 + 16 + 3 + 3 + 2 + 1) + 4 + 8 + 8  # binned + padding
     assert [f[0] for f in pkg._native.GrView._fields_] == [f[0] for f in orc.GrView._fields_]
     assert ctypes.sizeof(pkg._native.GrRenderParams) == 4 * (2 + 16 + 16 + 3 + 3)
+    # gr_param_step: int64, 2 ints, 2 pointers, GR_FIT_MAX_ACC pointers, 2 pointers, 3 floats (+ tail padding)
+    assert ctypes.sizeof(pkg._native.GrParamStep) == 8 + 8 + 16 + 8 * 8 + 16 + 16
 
 
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):

@@ -1,0 +1,52 @@
+"""GPU: gr_fit_param_steps (every parameter tensor's gradient and Adam update in one launch) gives exactly what one
+gr_fit_param_step per tensor gives, for each activation and with one to three stream accumulators."""
+from __future__ import annotations
+
+import ctypes
+
+import pytest
+import torch
+
+
+@pytest.mark.gpu
+def test_param_steps_equal_per_tensor_steps(pkg, cuda):
+    nat = pkg._native
+    L = nat.lib()
+    # (count, activation, accumulators, regulariser): identity / softplus / sigmoid, sizes across block boundaries
+    specs = [(3 * 1000, 0, 3, 0.0), (3 * 777, 1, 2, 1e-4), (1_000_003, 2, 1, 2e-6), (255, 2, 0, 0.0)]
+    b1, b2, eps = 0.9, 0.999, 1e-15
+    runs = []
+    for fused in (False, True):
+        state = []
+        for q, (n, act, na, reg) in enumerate(specs):
+            gg = torch.Generator(device=cuda).manual_seed(10 + q)
+            p = torch.randn(n, generator=gg, device=cuda) * 3.0
+            m = torch.randn(n, generator=gg, device=cuda) * 1e-3
+            v = torch.rand(n, generator=gg, device=cuda) * 1e-6
+            accs = [torch.randn(n, generator=gg, device=cuda) for _ in range(na)]
+            state.append((p, torch.empty_like(p), accs, m, v, act, reg, -(1e-3 / (1 - b1 ** (q + 2))),
+                          (1 - b2 ** (q + 2)) ** 0.5))
+        stream = ctypes.c_void_p(torch.cuda.current_stream(cuda).cuda_stream)
+        if fused:
+            arr = (nat.GrParamStep * len(state))()
+            for e, (p, gr, accs, m, v, act, reg, ns, bc) in zip(arr, state):
+                e.count, e.act, e.num_accs = p.numel(), act, len(accs)
+                e.param, e.grad = p.data_ptr(), gr.data_ptr()
+                for j, x in enumerate(accs):
+                    e.accs[j] = x.data_ptr()
+                e.exp_avg, e.exp_avg_sq = m.data_ptr(), v.data_ptr()
+                e.reg, e.neg_step_size, e.bias_correction2_sqrt = reg, ns, bc
+            nat.check(L.gr_fit_param_steps(len(state), arr, ctypes.c_double(b1), ctypes.c_double(b2), ctypes.c_float(eps),
+                                           stream), "gr_fit_param_steps")
+        else:
+            for p, gr, accs, m, v, act, reg, ns, bc in state:
+                ptrs = (ctypes.c_void_p * max(1, len(accs)))(*[x.data_ptr() for x in accs])
+                nat.check(L.gr_fit_param_step(p.numel(), act, nat.ptr(p), nat.ptr(gr), ptrs, len(accs), ctypes.c_float(reg),
+                                              1, nat.ptr(m), nat.ptr(v), ctypes.c_float(ns), ctypes.c_float(bc),
+                                              ctypes.c_double(b1), ctypes.c_double(b2), ctypes.c_float(eps), stream),
+                          "gr_fit_param_step")
+        torch.cuda.synchronize()
+        runs.append([(p, gr, m, v) for p, gr, _, m, v, *_ in state])
+    for a, b in zip(*runs):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
