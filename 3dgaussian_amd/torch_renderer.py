@@ -60,6 +60,18 @@ FIT_CUTOFF = float(os.environ.get("GR_FIT_CUTOFF", "5.0"))
 # knows it will differentiate the depth passes depth_grad="eager" (one f32-grade render).  GR_LAZY_DEPTH=0
 # makes True eager.
 LAZY_DEPTH = os.environ.get("GR_LAZY_DEPTH", "1") != "0"
+# Adaptive laziness: a caller whose loss does differentiate the depth (the reference loop with --depth_dir) would
+# pay for every view twice (the lazy render, then the f32-grade re-render in its backward).  After LAZY_ADAPT
+# such re-renders in a row, depth_grad=True renders at f32 grade up front (as "eager"); the first backward of such
+# a render that receives no depth gradient switches back to lazy.  Results are the eager mode's (within the parity
+# bar of the lazy ones).  GR_LAZY_ADAPT=0 never adapts.
+LAZY_ADAPT = max(0, int(os.environ.get("GR_LAZY_ADAPT", "2")))
+_LAZY = {"rerenders": 0, "eager": False}
+
+
+def reset_lazy_depth() -> None:
+    """Forget what adaptive laziness learned (a new loop / loss)."""
+    _LAZY["rerenders"], _LAZY["eager"] = 0, False
 
 
 def default_cutoff(depth_grad: bool = True) -> float:
@@ -689,7 +701,7 @@ def _grad_background(st: RenderState, background: torch.Tensor, g_out: torch.Ten
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means, scales, colors, opacities, background, view, proj, gv, prepared, gv_depth=None,
-                bin_stream=None, layout=None):
+                bin_stream=None, layout=None, adapted=False):
         """view / proj: the camera tensors (their gradients, gr_bwd_camera) or None; the render itself uses gv's
         host copy of them.  gv_depth: the f32-grade view a lazily rendered gv (two-piece mode) re-renders with
         when a depth gradient arrives (LAZY_DEPTH), else None.  bin_stream: see forward_native.  layout: a
@@ -704,6 +716,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.set_materialize_grads(False)
         ctx.meta = (st.gv, st.n, st.plan)
         ctx.gv_depth = gv_depth
+        ctx.adapted = adapted  # rendered at f32 grade because earlier backwards all differentiated the depth
         # the render state's device buffers are saved tensors: autograd releases them after this node's backward
         # unless the graph is retained (a second backward through it then finds them)
         ctx.save_for_backward(means, scales, colors, opacities, background, view, proj, st.geom, st.bins, st.saved,
@@ -726,6 +739,11 @@ class _RasterizeGaussians(torch.autograd.Function):
             # lazy default: the depth is differentiated after all - re-render at f32 grade with the
             # depth-gradient footprint and differentiate that render
             _, _, _, st = forward_native(means, scales, colors, opacities, ctx.gv_depth, images=False)
+            _LAZY["rerenders"] += 1
+            if LAZY_ADAPT and _LAZY["rerenders"] >= LAZY_ADAPT:
+                _LAZY["eager"] = True
+        elif g_depth is None and (ctx.gv_depth is not None or ctx.adapted):
+            _LAZY["rerenders"], _LAZY["eager"] = 0, False  # this loss has no depth term (any more)
         need_view, need_proj = ctx.needs_input_grad[5], ctx.needs_input_grad[6]
         # with a layout: the chain rule in the caller's order (its tensors; the rendered copy's sums gathered by index)
         dm, ds, dc, do, ws = backward_native(*(caller if index is not None else (means, scales, colors, opacities)), st,
@@ -735,7 +753,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         if need_view or need_proj:
             d = camera_grad_native(means, scales, colors, opacities, st, ws, g_depth is not None)
             dview, dproj = _camera_grads(d, view, proj, need_view, need_proj, colors.dim() == 3)
-        return dm, ds, dc, do, dbg, dview, dproj, None, None, None, None, None
+        return dm, ds, dc, do, dbg, dview, dproj, None, None, None, None, None, None
 
 
 def _device_inputs(means, scales, colors, opacities):
@@ -933,24 +951,27 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
         background = _default_background(dev)
     background = background.to(dtype=torch.float32, device=dev).reshape(3).contiguous()
     gv_depth = None
-    if depth_grad is True and not _eager(depth_grad) and cutoff is None:
+    adapted = depth_grad is True and not _eager(depth_grad) and cutoff is None and _LAZY["eager"]
+    if depth_grad is True and not _eager(depth_grad) and cutoff is None and not adapted:
         # lazy default: two-piece render with the no-depth-gradient footprint now, f32 grade only if needed
         gv_depth = make_view(view, proj, width, height, background, None, core_cutoff, True)
         gv = make_view(view, proj, width, height, background, None, core_cutoff, False)
     else:
         gv = make_view(view, proj, width, height, background, cutoff, core_cutoff, bool(depth_grad))
     if prepared is not None and (prepared.gv.cutoff != gv.cutoff or prepared.gv.no_depth_grad != gv.no_depth_grad):
-        # a preparation made for the eager view (prepare_view(depth_grad="eager"), or GR_LAZY_DEPTH=0)
+        # a preparation made for the other mode (prepare_view(depth_grad="eager"), GR_LAZY_DEPTH=0, or adaptive
+        # laziness switched since): render the prepared view
         gv, gv_depth = prepared.gv, None
+        adapted = False
     # the camera tensors enter the autograd op only when a gradient is wanted for them (gr_bwd_camera)
     cam_v = view if isinstance(view, torch.Tensor) and view.requires_grad else None
     cam_p = proj if isinstance(proj, torch.Tensor) and proj.requires_grad else None
     if prepared is not None:  # a preparation made by prepare_view is of the caller's own order: render that
-        return _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, prepared, gv_depth)
+        return _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, prepared, gv_depth, None, None, adapted)
     # the rendered tensors: the Morton-ordered copy of the inputs
     layout = _layout_of(m, s, c, o) if LAYOUT and m.shape[0] >= LAYOUT_MIN else None
     if not SPECULATE:
-        return _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, None, gv_depth, None, layout)
+        return _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, None, gv_depth, None, layout, adapted)
     rt = layout.tensors if layout is not None else (m, s, c, o)
     key = _view_key(gv)
     pv = _spec_take(key, rt)
@@ -960,7 +981,7 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
         pv.geom.record_stream(stream)
     ready = torch.cuda.Event()
     ready.record(stream)
-    res = _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, pv, gv_depth, None, layout)
+    res = _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, pv, gv_depth, None, layout, adapted)
     _spec_after(key, gv, rt, ready)
     return res
 

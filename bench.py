@@ -257,6 +257,7 @@ def dropin_op(n: int, V: int, R: int, steps: int, warmup: int, device, depth_los
     the op (render_gaussians_torch per view with a fresh device background, torch losses, autograd, Adam,
     float(loss) per iteration).  Mpx/s over ``steps`` iterations after ``warmup``.  depth_loss: the loop with its
     --depth_dir term, w_depth mean|depth / (depth.max() + 1e-6) - d_gt| (fit_multiview_stub.py:299-303)."""
+    tr.reset_lazy_depth()  # a fresh loop: the op has not yet seen whether this loss differentiates the depth
     params = synthetic_params(n, device)
     cams = fm.orbit_cameras(V, R, R, device)
     g = torch.Generator(device=device).manual_seed(1)

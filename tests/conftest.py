@@ -45,3 +45,12 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True)
+def _fresh_lazy_depth():
+    """Every test starts with the drop-in op's adaptive laziness unlearned (torch_renderer.reset_lazy_depth)."""
+    mod = sys.modules.get("3dgaussian_amd.torch_renderer")
+    if mod is not None:
+        mod.reset_lazy_depth()
+    yield

@@ -319,3 +319,65 @@ def test_dropin_layout_gradients_vs_oracle(cuda):
     print("drop-in layout vs binned oracle:", {k: f"{e:.2e}" for k, e in errs.items()})
     for k, e in errs.items():
         assert e <= 1e-4, (k, e)
+
+
+def test_dropin_adaptive_lazy_depth(cuda):
+    """A stub loop whose loss differentiates the depth (--depth_dir, fit_multiview_stub.py:299-303): the first
+    iteration's views are rendered lazily and re-rendered at f32 grade in the backward; from the second the op
+    renders them at f32 grade up front (LAZY_ADAPT).  Losses and parameters agree with the never-adapting op within
+    the parity bar; a loop without the depth term switches the op back."""
+    tr = importlib.import_module("3dgaussian_amd.torch_renderer")
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    bench = importlib.import_module("bench")
+    R, V, N = 96, 4, 3000
+    cams = fm.orbit_cameras(V, R, R, cuda)
+    g = torch.Generator(device=cuda).manual_seed(8)
+    targets = [torch.rand((R, R, 3), generator=g, device=cuda) for _ in range(V)]
+    depths = [torch.rand((R, R), generator=g, device=cuda) for _ in range(V)]
+
+    def loop(iters):
+        params = bench.synthetic_params(N, cuda)
+        opt = torch.optim.Adam(list(params.values()), lr=0.02)
+        losses = []
+        for _ in range(iters):
+            opt.zero_grad(set_to_none=True)
+            scales = torch.nn.functional.softplus(params["scales_raw"]) + 1e-3
+            opacities = torch.sigmoid(params["opacities_raw"])
+            colors = torch.sigmoid(params["colors_raw"])
+            total = torch.tensor(0.0, device=cuda)
+            for i in range(V):
+                pred, alpha, depth = tr.render_gaussians_torch(params["means"], scales, colors, opacities, cams[i],
+                                                               width=R, height=R, return_aux=True)
+                d_pred = depth / (depth.max() + 1e-6)
+                total = total + torch.mean(torch.abs(pred - targets[i])) + 0.05 * torch.mean(torch.abs(d_pred - depths[i]))
+            loss = total / V
+            loss.backward()
+            opt.step()
+            losses.append(float(loss.detach().cpu()))
+        return losses, {k: v.detach().clone() for k, v in params.items()}
+
+    saved = tr.LAZY_ADAPT
+    try:
+        tr.LAZY_ADAPT = 0
+        tr.reset_lazy_depth()
+        ref = loop(3)
+        assert not tr._LAZY["eager"]
+        tr.LAZY_ADAPT = 2
+        tr.reset_lazy_depth()
+        got = loop(3)
+        assert tr._LAZY["eager"]
+    finally:
+        tr.LAZY_ADAPT = saved
+    np.testing.assert_allclose(got[0], ref[0], rtol=1e-4)
+    for k in ref[1]:
+        err = orc.rel_l2(got[1][k].cpu().numpy(), ref[1][k].cpu().numpy())
+        assert err <= 1e-4, (k, err)
+    # a backward without a depth gradient switches the op back to lazy rendering
+    params = bench.synthetic_params(N, cuda)
+    pred, alpha, depth = tr.render_gaussians_torch(params["means"], torch.nn.functional.softplus(params["scales_raw"]),
+                                                   torch.sigmoid(params["colors_raw"]),
+                                                   torch.sigmoid(params["opacities_raw"]), cams[0], width=R, height=R,
+                                                   return_aux=True)
+    pred.sum().backward()
+    assert not tr._LAZY["eager"]
+
