@@ -36,7 +36,8 @@ Also reported on rank 0:
                 torch.optim.Adam, float(loss) per iteration; same C4 workload
   dropin_depth_loss
                 the same loop with the stub's --depth_dir term (fit_multiview_stub.py:299-303): the depth
-                output is differentiated, so the op renders at f32 grade with the depth footprint
+                output is differentiated, so the op renders at f32 grade with the depth footprint (after the
+                first iteration up front: torch_renderer.LAZY_ADAPT); two warmup iterations
   psnr_vs_ref   the checker leg (outside every timed region): one view of the final fitted state, the
                 bench's render path and the drop-in default path vs the exact float64 dense render
                 (oracle/gr_oracle.c, every Gaussian at every pixel) at 2048 random pixels
@@ -468,7 +469,9 @@ def main():
         torch.cuda.empty_cache()
         drop = dropin_op(n, V, R, steps=3, warmup=1, device=device)
         torch.cuda.empty_cache()
-        drop_depth = dropin_op(n, V, R, steps=2, warmup=1, device=device, depth_loss=True)
+        # two warmup iterations: the first teaches the op that this loss differentiates the depth (adaptive
+        # laziness), the second its camera order in that mode (speculation)
+        drop_depth = dropin_op(n, V, R, steps=2, warmup=2, device=device, depth_loss=True)
 
     if rank == 0:
         bwd_ms, bwd_n = prof["raster_bwd"]
