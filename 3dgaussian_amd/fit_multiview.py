@@ -449,8 +449,18 @@ class ViewShardedFitter:
                           if self.rank == 0 else None)
                 reg = None
                 if self._native_exec() and GATHER:
-                    reg = reg_fn() if reg_fn else None
                     total = self._views_native(means, scales, colors, opacities, self._depth_grad())
+                    # the regulariser's small kernels after the executor's call (the host starts the views'
+                    # preparations first), on the preparation stream behind the last preparation when the executor
+                    # runs on this driver's streams (as the Python schedule does; no extra hardware queue)
+                    rs = getattr(self, "_prep", None) if EXEC_STREAMS else None
+                    if reg_fn and rs is not None:
+                        main = torch.cuda.current_stream(device)
+                        with torch.cuda.stream(rs):
+                            reg = reg_fn()
+                        main.wait_stream(rs)
+                    elif reg_fn:
+                        reg = reg_fn()
                 elif self._depth_grad():
                     reg = reg_fn() if reg_fn else None
                     total = self._views_direct_depth(means, scales, colors, opacities)
