@@ -606,8 +606,15 @@ class ViewShardedFitter:
             cfg.render_streams = rs
             cfg.prep_stream = prep.cuda_stream
         losses_v = torch.empty(len(views), dtype=torch.float32, device=device)
-        acc = [tuple(torch.empty_like(t) for t in (m, s, c, o)) for _ in range(ns)]
-        ptrs = (ctypes.c_void_p * (4 * ns))(*[t.data_ptr() for a in acc for t in a])
+        # the streams' accumulators (and their pointer array) are kept across steps while the shapes hold: the
+        # executor writes them (accumulate = 0 first) only after the caller's stream, so after the previous step's
+        # parameter update read them; 4 x streams allocations per step were host time before the first launch
+        shapes = (ns,) + tuple(tuple(t.shape) for t in (m, s, c, o))
+        cached = getattr(self, "_native_acc", None)
+        if cached is None or cached[0] != shapes or cached[1][0][0].device != device:
+            acc = [tuple(torch.empty_like(t) for t in (m, s, c, o)) for _ in range(ns)]
+            self._native_acc = cached = (shapes, acc, (ctypes.c_void_p * (4 * ns))(*[t.data_ptr() for a in acc for t in a]))
+        acc, ptrs = cached[1], cached[2]
         L = tr._native.lib()
         tr._native.check(L.gr_fit_views(tr._native.executor(device.index or 0), ctypes.byref(cfg), len(views), cache[1],
                                         int(m.shape[0]), tr._native.ptr(m), tr._native.ptr(s), tr._native.ptr(c),
