@@ -864,7 +864,14 @@ class ViewShardedFitter:
                 grad = flat[off:off + p.numel()].view_as(p)
                 off += p.numel()
             else:
-                grad = torch.empty_like(p)
+                # the gradient tensor is kept across steps (zero_grad(set_to_none) drops p.grad each step; the
+                # kernel overwrites every element, in stream order after the previous step's readers)
+                kept = self._grad_keep.get(k) if hasattr(self, "_grad_keep") else None
+                if kept is None or kept.shape != p.shape or kept.device != p.device:
+                    if not hasattr(self, "_grad_keep"):
+                        self._grad_keep = {}
+                    self._grad_keep[k] = kept = torch.empty_like(p)
+                grad = kept
             p.grad = grad
             r = reg.get(k, 0.0) if self.rank == 0 else 0.0
 
