@@ -646,7 +646,14 @@ class ViewShardedFitter:
         # made on the main stream before the side streams wait for it: every stream's use is ordered
         # after its allocation, and main waits for every stream before they are read or freed
         losses_v = torch.empty(max(1, len(views)), dtype=torch.float32, device=device)
-        acc = [tuple(torch.empty_like(t) for t in (m, s, c, o)) for _ in streams]
+        # the streams' accumulators are kept across steps while the shapes hold (written only after the side
+        # streams wait for main below, i.e. after the previous step's parameter update read them): 4 x streams
+        # allocations per step were host time before the first preparation
+        shapes = (len(streams),) + tuple(tuple(t.shape) for t in (m, s, c, o))
+        cached = getattr(self, "_direct_acc", None)
+        if cached is None or cached[0] != shapes or cached[1][0][0].device != device:
+            self._direct_acc = cached = (shapes, [tuple(torch.empty_like(t) for t in (m, s, c, o)) for _ in streams])
+        acc = cached[1]
         for st in streams[1:]:
             st.wait_stream(main)
         w_sil = self.w_sil if (self.masks is not None and self.w_sil > 0.0) else 0.0
@@ -738,7 +745,11 @@ class ViewShardedFitter:
             self._side = side = [torch.cuda.Stream(device) for _ in range(ns - 1)]
         streams = [main] + (side[:ns - 1] if ns > 1 else [])
         losses_v = torch.empty(max(1, len(views)), dtype=torch.float32, device=device)
-        acc = [tuple(torch.empty_like(t) for t in (m, s, c, o)) for _ in streams]
+        shapes = (len(streams),) + tuple(tuple(t.shape) for t in (m, s, c, o))  # kept across steps (_views_direct)
+        cached = getattr(self, "_direct_acc", None)
+        if cached is None or cached[0] != shapes or cached[1][0][0].device != device:
+            self._direct_acc = cached = (shapes, [tuple(torch.empty_like(t) for t in (m, s, c, o)) for _ in streams])
+        acc = cached[1]
         for st in streams[1:]:
             st.wait_stream(main)
         w_sil = self.w_sil if (self.masks is not None and self.w_sil > 0.0) else 0.0
