@@ -2157,7 +2157,9 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
     pixel_upstream(v, p, saved4[p], savedD[p], g_rgb, g_alpha, g_depth, l1, u, l_rgb, l_sil);
   }
   if (l1.tile_loss) tile_loss_sums(tile, tid, l_rgb, l_sil, l1.tile_loss);
-  __shared__ float sU[5][TP];
+  // six rows, not five: the last tile reuses the buffer as tile_loss_total's double[3][256] (6 KiB)
+  __shared__ __attribute__((aligned(16))) float sU[6][TP];
+  static_assert(sizeof(sU) >= 3 * 256 * sizeof(double), "tile_loss_total scratch");
 #pragma unroll
   for (int k = 0; k < 5; ++k) sU[k][tid] = u[k];
   __syncthreads();

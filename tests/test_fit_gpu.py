@@ -229,6 +229,45 @@ def test_direct_depth_path_matches_autograd_path(cuda, sh):
         assert err <= 1e-5, (k, err)
 
 
+@pytest.mark.parametrize("path", ["python", "native", "autograd"])
+@pytest.mark.parametrize("with_depth", [False, True])
+def test_fit_loss_value_vs_torch_loss_many_tiles(cuda, path, with_depth):
+    """The fit step's loss value (the fused paths' device loss: gr_fwd_render_l1 / gr_bwd_fit_gather's
+    tile sums finished by the last tile, k_pixel_grads with a depth target) against the stub's torch loss
+    (fit_multiview_stub.py:293-308) on the drop-in op's images, at 320x320 = 400 tiles: more than the 256
+    threads of the last tile's reduction (its scratch was 1 KiB short past 128 tiles)."""
+    import torch
+
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    bench = importlib.import_module("bench")
+    W = H = 320
+    cams = fm.orbit_cameras(3, W, H, cuda)
+    g = torch.Generator(device=cuda).manual_seed(11)
+    targets = [torch.rand((H, W, 3), generator=g, device=cuda) for _ in cams]
+    masks = [(t.mean(dim=2) > 0.5).float() for t in targets]
+    depths = [torch.rand((H, W), generator=g, device=cuda) for _ in cams] if with_depth else None
+    saved = (fm.DIRECT_BACKWARD, fm.NATIVE_EXEC)
+    fm.DIRECT_BACKWARD = path != "autograd"
+    fm.NATIVE_EXEC = "1" if path == "native" else "0"
+    try:
+        f = fm.ViewShardedFitter(bench.synthetic_params(40_000, cuda), cams, targets, W, H, masks=masks, depths=depths)
+        with torch.no_grad():
+            m, s, c, o = fm.activations(f.params)
+            ref = 0.0
+            for i, cam in enumerate(cams):
+                pred, alpha, depth = fm.hip_render(m, s, c, o, cam, W, H, f._background(cuda))
+                li = torch.mean(torch.abs(pred - targets[i])) + f.w_sil * torch.mean(torch.abs(alpha - masks[i]))
+                if with_depth:
+                    li = li + f.w_depth * torch.mean(torch.abs(depth / (depth.max() + 1e-6) - depths[i]))
+                ref += float(li)
+            ref = ref / len(cams) + float(f.reg_opacity * o.mean() + f.reg_scale * s.mean())
+        loss = float(f.step())
+    finally:
+        fm.DIRECT_BACKWARD, fm.NATIVE_EXEC = saved
+    print(f"loss {loss:.8f} torch {ref:.8f} rel {abs(loss - ref) / ref:.2e}")
+    assert abs(loss - ref) <= 1e-5 * abs(ref), (loss, ref)
+
+
 def test_fused_param_step_matches_torch_adam(cuda):
     """gr_fit_param_step (gradients through the activations + regulariser, Adam's update) against torch's
     autograd + torch.optim.Adam on the same views, over three steps (Adam's bias corrections move)."""

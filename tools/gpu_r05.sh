@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-4 GPU passes on the box (each step under its own time limit; the first failure ends the call).
-#   bash tools/gpu_r04.sh <tag> <step>...
+# Round-5 GPU passes on the box (each step under its own time limit; the first failure ends the call).
+#   bash tools/gpu_r05.sh <tag> <step>...
 # steps: bench (20-step driver command), stats1 / stats4 (rocprofv3 kernel stats of the bench, 1 / 4 streams),
 #        dropin (rocprofv3 kernel stats of the drop-in loop), tests (pytest -m gpu), smoke, configs (C2 C3),
 #        pmc (stamped PMC passes -> profiles/pmc_traffic.json)
@@ -38,6 +38,11 @@ for step in "$@"; do
       (cd $R && timeout -k 10 300 python tools/bench_configs.py C2 C3 > $O/configs.txt 2>$O/configs.err) ;;
     pmc)
       (cd $R && bash tools/pmc_profile.sh gpurun_out/$TAG/pmc && cp $O/pmc/pmc.json $R/profiles/pmc_traffic.json) ;;
+    ab:*)  # ab:<rounds>:<dir>,<dir>... same-box bench A/B of tree copies (tools/ab_bench.sh)
+      IFS=: read -r _ n dirs <<< "$step"
+      (cd $R && bash tools/ab_bench.sh $TAG $n ${dirs//,/ } > $O/ab.txt 2>&1) ;;
+    testk:*)  # testk:<pytest -k expression> a subset of the GPU tests
+      (cd $R && timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -s -k "${step#testk:}" > $O/pytest_gpu_k.log 2>&1) ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
