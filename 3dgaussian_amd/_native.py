@@ -43,6 +43,7 @@ class GrView(ctypes.Structure):
         ("no_depth_grad", ctypes.c_int),
         ("background_dev", ctypes.c_void_p),  # optional device pointer to the 3 background floats
         ("binned", ctypes.c_int),  # 1: gr_fwd_bin already built the bins; the render launches only the splat
+        ("tile", ctypes.c_int),  # screen tile edge: 0/16 (default) or 32 (fused fit path)
     ]
 
 

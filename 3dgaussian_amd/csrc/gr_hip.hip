@@ -93,11 +93,15 @@ constexpr float LOG2E = 1.4426950408889634f;
 
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
-inline int tiles_x_of(int w) { return (w + T - 1) / T; }
-inline int tiles_y_of(int h) { return (h + T - 1) / T; }
+// Tile edge of a view (gr_view.tile): GR_TILE (16) or 32 (the fused fit path's 32-pixel tiles, T32).
+constexpr int T32 = 32, TP32 = T32 * T32;
+inline int tile_of(const gr_view* v) { return v->tile == T32 ? T32 : T; }
+inline int tiles_x_of(int w, int t = T) { return (w + t - 1) / t; }
+inline int tiles_y_of(int h, int t = T) { return (h + t - 1) / t; }
+inline int tiles_of(const gr_view* v) { return tiles_x_of(v->width, tile_of(v)) * tiles_y_of(v->height, tile_of(v)); }
 // Binning unit of the differentiable path: virtual tile 2t holds tile t's core pairs, 2t+1 its tail
 // pairs (two-zone footprint), so the pair lists, ranges and work items are per virtual tile.
-inline int vtiles_of(const gr_view* v) { return 2 * tiles_x_of(v->width) * tiles_y_of(v->height); }
+inline int vtiles_of(const gr_view* v) { return 2 * tiles_of(v); }
 
 int bits_for(uint32_t maxval) {
   int b = 1;
@@ -108,6 +112,7 @@ int bits_for(uint32_t maxval) {
 // Kernel parameter block (by value): matrices etc.
 struct ViewK {
   int W, H, tiles_x, tiles_y;
+  int T, ts;          // tile edge and its log2 (the preparation and binning; the splat kernels are per tile size)
   float V[16], P[16];
   float bg[3];
   float cam[3];
@@ -123,8 +128,11 @@ ViewK make_viewk(const gr_view* v) {
   ViewK k;
   k.W = v->width;
   k.H = v->height;
-  k.tiles_x = tiles_x_of(v->width);
-  k.tiles_y = tiles_y_of(v->height);
+  k.T = tile_of(v);
+  k.ts = k.T == T32 ? 5 : 4;
+  static_assert(T == 16, "ViewK::ts");
+  k.tiles_x = tiles_x_of(v->width, k.T);
+  k.tiles_y = tiles_y_of(v->height, k.T);
   std::memcpy(k.V, v->view, sizeof(k.V));
   std::memcpy(k.P, v->proj, sizeof(k.P));
   std::memcpy(k.bg, v->background, sizeof(k.bg));
@@ -256,7 +264,7 @@ __device__ __forceinline__ int tile_rect(const ViewK& v, const Proj& p, float op
   const int x1 = (hix >= wm1) ? (v.W - 1) : (int)ceilf(hix);
   const int y0 = (loy <= 0.0f) ? 0 : (int)floorf(loy);
   const int y1 = (hiy >= hm1) ? (v.H - 1) : (int)ceilf(hiy);
-  r = make_int4(x0 / T, y0 / T, x1 / T, y1 / T);
+  r = make_int4(x0 >> v.ts, y0 >> v.ts, x1 >> v.ts, y1 >> v.ts);  // (x0, y0 >= 0: the oracle's x0 / T)
   return (r.z - r.x + 1) * (r.w - r.y + 1);
 }
 
@@ -264,9 +272,9 @@ __device__ __forceinline__ int tile_rect(const ViewK& v, const Proj& p, float op
 // exponent e = log2(w/o); q = -0.5 log2(e) / sigma^2 as stored in record word A
 // (oracle/gr_oracle.c tile_emax, bit-exact).
 __device__ __forceinline__ float tile_emax(const ViewK& v, float px, float py, float qx, float qy, int tx, int ty) {
-  const int xe = min(tx * T + T - 1, v.W - 1), ye = min(ty * T + T - 1, v.H - 1);
-  const float lox = (float)(tx * T) + 0.5f, hix = (float)xe + 0.5f;
-  const float loy = (float)(ty * T) + 0.5f, hiy = (float)ye + 0.5f;
+  const int xe = min(tx * v.T + v.T - 1, v.W - 1), ye = min(ty * v.T + v.T - 1, v.H - 1);
+  const float lox = (float)(tx * v.T) + 0.5f, hix = (float)xe + 0.5f;
+  const float loy = (float)(ty * v.T) + 0.5f, hiy = (float)ye + 0.5f;
   const float cx = px < lox ? lox : (px > hix ? hix : px);
   const float cy = py < loy ? loy : (py > hiy ? hiy : py);
   const float dx = cx - px, dy = cy - py;
@@ -278,15 +286,15 @@ __device__ __forceinline__ float radius_thr(float R) { return (-0.5f * LOG2E) * 
 // tile_emax in its column and row terms, ex(tx) + ey(ty) (the same float operations, so the same value bit for bit):
 // the tile loops of the preparation and of the emission evaluate the row term once per row.
 __device__ __forceinline__ float tile_ex(const ViewK& v, float px, float qx, int tx) {
-  const int xe = min(tx * T + T - 1, v.W - 1);
-  const float lox = (float)(tx * T) + 0.5f, hix = (float)xe + 0.5f;
+  const int xe = min(tx * v.T + v.T - 1, v.W - 1);
+  const float lox = (float)(tx * v.T) + 0.5f, hix = (float)xe + 0.5f;
   const float cx = px < lox ? lox : (px > hix ? hix : px);
   const float dx = cx - px;
   return (dx * dx) * qx;
 }
 __device__ __forceinline__ float tile_ey(const ViewK& v, float py, float qy, int ty) {
-  const int ye = min(ty * T + T - 1, v.H - 1);
-  const float loy = (float)(ty * T) + 0.5f, hiy = (float)ye + 0.5f;
+  const int ye = min(ty * v.T + v.T - 1, v.H - 1);
+  const float loy = (float)(ty * v.T) + 0.5f, hiy = (float)ye + 0.5f;
   const float cy = py < loy ? loy : (py > hiy ? hiy : py);
   const float dy = cy - py;
   return (dy * dy) * qy;
@@ -398,6 +406,12 @@ Geom geom_view(void* base, int n) {
 #define GR_CH 2048
 #endif
 constexpr int CH = GR_CH;  // Gaussians per raster work item (one chunk of one tile's list)
+// 32-pixel tiles (gr_view.tile = 32): four times the pixels per pair, so a quarter... of the pairs per item would keep
+// the item's work; fewer, longer items keep the split tiles' partial sums (4 x 1024 floats per item) small.
+#ifndef GR_CH32
+#define GR_CH32 1024
+#endif
+constexpr int CH32 = GR_CH32;
 constexpr int NPART = 9;  // backward partial sums per (Gaussian, tile) pair
 
 // Virtual tiles up to which the pairs are grouped by the stable counting sort (16-bit keys; see
@@ -429,7 +443,18 @@ struct Scratch {
   void* sort_tmp;
 };
 
-inline int64_t item_cap(int tiles, int64_t K) { return (K + CH - 1) / CH + tiles; }
+inline int64_t item_cap(int tiles, int64_t K, int ch = CH) { return (K + ch - 1) / ch + tiles; }
+// Per tile size: the work-item length, the split-tile partial sums per item (forward channels x pixels) and the
+// backward's upstream fragments per tile.
+constexpr int UF32_FRAGS = 2 * 4 * 2 * 2 * 64;  // uint4 per 32-pixel tile: (side, channel, K-step, piece) x 64 lanes
+struct TileCfg {
+  int T, ch;
+  size_t part_floats, uf_frags;
+};
+constexpr int UF_FRAGS16 = 2 * 3 * 3 * 64;  // (= UF_FRAGS below)
+inline TileCfg tile_cfg(const gr_view* v) {
+  return tile_of(v) == T32 ? TileCfg{T32, CH32, (size_t)4 * TP32, (size_t)UF32_FRAGS} : TileCfg{T, CH, (size_t)5 * TP, (size_t)UF_FRAGS16};
+}
 
 // `vtiles` = 2 x tiles (core and tail lists of each tile) on the differentiable path.
 // The finished-tile fan-in's counters behind the per-tile tickets (arrive_last_tile): eight shards and a top counter,
@@ -437,10 +462,10 @@ inline int64_t item_cap(int tiles, int64_t K) { return (K + CH - 1) / CH + tiles
 constexpr int FAN_STRIDE = 32;
 __host__ __device__ inline size_t fan_offset(int tiles) { return ((size_t)tiles + 1 + FAN_STRIDE - 1) / FAN_STRIDE * FAN_STRIDE; }
 
-size_t bins_fixed(int vtiles, int64_t K, size_t off[8]) {
+size_t bins_fixed(int vtiles, int64_t K, size_t off[8], int ch = CH) {
   const int tiles = vtiles;
   const size_t kk = (size_t)(K > 0 ? K : 1);
-  const size_t cap = (size_t)item_cap(tiles, K);
+  const size_t cap = (size_t)item_cap(tiles, K, ch);
   size_t o = 0;
   off[0] = o; o = align_up(o + (short_keys(tiles) ? 1 : kk) * sizeof(uint32_t));
   off[1] = o; o = align_up(o + kk * sizeof(int));
@@ -455,14 +480,14 @@ size_t bins_fixed(int vtiles, int64_t K, size_t off[8]) {
 
 // off: [0] emitted keys, [1] emitted ids, [2] split-tile partials, [3] / [4] (radix path) unsorted /
 // sorted pairs
-size_t scratch_fixed(int vtiles, int64_t K, size_t off[5]) {
+size_t scratch_fixed(int vtiles, int64_t K, size_t off[5], int ch = CH, size_t part_floats = (size_t)5 * TP) {
   const int tiles = vtiles;
   const size_t kk = (size_t)(K > 0 ? K : 1);
-  const size_t cap = (size_t)item_cap(tiles, K);
+  const size_t cap = (size_t)item_cap(tiles, K, ch);
   size_t o = 0;
   off[0] = o; o = align_up(o + kk * sizeof(uint32_t));
   off[1] = o; o = align_up(o + kk * sizeof(int));
-  off[2] = o; o = align_up(o + cap * 5 * TP * sizeof(float));
+  off[2] = o; o = align_up(o + cap * part_floats * sizeof(float));
   off[3] = o; o = align_up(o + (short_keys(tiles) ? 1 : kk) * sizeof(int2));
   off[4] = o; o = align_up(o + (short_keys(tiles) ? 1 : kk) * sizeof(int2));
   return o;
@@ -541,9 +566,9 @@ size_t sort_tmp_bytes(int64_t K, int bits) {
   return tmp;
 }
 
-Bins bins_view(void* base, int tiles, int64_t K) {
+Bins bins_view(void* base, int tiles, int64_t K, int ch = CH) {
   size_t off[8];
-  bins_fixed(tiles, K, off);
+  bins_fixed(tiles, K, off, ch);
   char* b = (char*)base;
   Bins r;
   r.keys = (uint32_t*)(b + off[0]);
@@ -557,9 +582,9 @@ Bins bins_view(void* base, int tiles, int64_t K) {
   return r;
 }
 
-Scratch scratch_view(void* base, int tiles, int64_t K) {
+Scratch scratch_view(void* base, int tiles, int64_t K, int ch = CH, size_t part_floats = (size_t)5 * TP) {
   size_t off[5];
-  const size_t fixed = scratch_fixed(tiles, K, off);
+  const size_t fixed = scratch_fixed(tiles, K, off, ch, part_floats);
   char* b = (char*)base;
   Scratch r;
   r.keys_in = (uint32_t*)(b + off[0]);
@@ -951,10 +976,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define GR_WI_THREADS 256
 #endif
 constexpr int WI_THREADS = GR_WI_THREADS;
-__device__ __forceinline__ int chunks_of(int len) { return (len + CH - 1) / CH; }
+__device__ __forceinline__ int chunks_of(int len, int ch) { return (len + ch - 1) / ch; }
 __global__ __launch_bounds__(WI_THREADS) void k_work_items(int vtiles, const int2* __restrict__ ranges, int4* __restrict__ items,
                                                      int* __restrict__ num_items, int* __restrict__ tile_item0,
-                                                     int* __restrict__ ticket) {
+                                                     int* __restrict__ ticket, int ch) {
   typedef hipcub::BlockScan<int, WI_THREADS> Scan;
   __shared__ typename Scan::TempStorage tmp;
   __shared__ int carry;
@@ -966,7 +991,7 @@ __global__ __launch_bounds__(WI_THREADS) void k_work_items(int vtiles, const int
     for (int base = 0; base < tiles; base += WI_THREADS) {
       const int t = base + (int)threadIdx.x;
       const int2 rc = t < tiles ? ranges[2 * t] : make_int2(0, 0), rt = t < tiles ? ranges[2 * t + 1] : make_int2(0, 0);
-      const int chc = chunks_of(rc.y - rc.x), cht = chunks_of(rt.y - rt.x);
+      const int chc = chunks_of(rc.y - rc.x, ch), cht = chunks_of(rt.y - rt.x, ch);
       const int nch = t >= tiles ? 0 : pass == 0 ? chc + cht : (chc + cht == 0 ? 1 : 0);
       int excl, total;
       Scan(tmp).ExclusiveSum(nch, excl, total);
@@ -975,9 +1000,9 @@ __global__ __launch_bounds__(WI_THREADS) void k_work_items(int vtiles, const int
         ticket[t] = 0;
         tile_item0[2 * t] = first;
         tile_item0[2 * t + 1] = first + chc;
-        for (int c = 0; c < chc; ++c) items[first + c] = make_int4(2 * t, rc.x + c * CH, min(rc.y, rc.x + (c + 1) * CH), c);
+        for (int c = 0; c < chc; ++c) items[first + c] = make_int4(2 * t, rc.x + c * ch, min(rc.y, rc.x + (c + 1) * ch), c);
         for (int c = 0; c < cht; ++c)
-          items[first + chc + c] = make_int4(2 * t + 1, rt.x + c * CH, min(rt.y, rt.x + (c + 1) * CH), c);
+          items[first + chc + c] = make_int4(2 * t + 1, rt.x + c * ch, min(rt.y, rt.x + (c + 1) * ch), c);
       } else if (nch) {
         tile_item0[2 * t] = tile_item0[2 * t + 1] = first;
         items[first] = make_int4(2 * t, 0, 0, 0);
@@ -1130,6 +1155,7 @@ struct TZone {
   int* T;
 };
 struct TZones {
+  int ch;  // work-item length (pairs): CH, or CH32 for 32-pixel tiles
   TZone z[2];
   int cw;  // pairs per column (col_width)
 };
@@ -1247,7 +1273,7 @@ __device__ __forceinline__ void tile_colscan_block(const TZone& zz, int tiles) {
 template <bool THROUGH, int NT>
 __device__ void work_items_zones(int tiles, int Kc, const int* __restrict__ Tc, const int* __restrict__ Tt,
                                  int2* __restrict__ ranges, int4* __restrict__ items, int* __restrict__ num_items,
-                                 int* __restrict__ tile_item0, int* __restrict__ ticket);
+                                 int* __restrict__ tile_item0, int* __restrict__ ticket, int ch);
 // ... and the block that finishes last (arrive_last_of over the grid) scans the tile totals into the per-virtual-tile
 // ranges and cuts the work items (work_items_zones): no launch of its own between the scan and the placement.
 __global__ __launch_bounds__(GR_CS_THREADS) void k_tile_colscan(TZones Z, int tiles, int2* __restrict__ ranges,
@@ -1259,7 +1285,7 @@ __global__ __launch_bounds__(GR_CS_THREADS) void k_tile_colscan(TZones Z, int ti
   const int nb = (int)(gridDim.x * gridDim.y);
   if (!arrive_last_of(ticket + fan_offset(tiles), nb, (int)(blockIdx.y * gridDim.x + blockIdx.x), &last)) return;
   work_items_zones<true, GR_CS_THREADS>(tiles, Z.z[1].zbase, Z.z[0].K > 0 ? Z.z[0].T : nullptr, Z.z[1].K > 0 ? Z.z[1].T : nullptr,
-                                  ranges, items, num_items, tile_item0, ticket);
+                                  ranges, items, num_items, tile_item0, ticket, Z.ch);
 }
 
 
@@ -1322,7 +1348,7 @@ constexpr int RUNQ = 10;
 template <bool THROUGH, int NT>
 __device__ void work_items_zones(int tiles, int Kc, const int* __restrict__ Tc, const int* __restrict__ Tt,
                                  int2* __restrict__ ranges, int4* __restrict__ items, int* __restrict__ num_items,
-                                 int* __restrict__ tile_item0, int* __restrict__ ticket) {
+                                 int* __restrict__ tile_item0, int* __restrict__ ticket, int ch) {
   __shared__ unsigned long long sh[NT / 64];  // two packed 64-bit block scans
   const int per = (tiles + NT - 1) / NT;
   const int t0 = min(tiles, (int)threadIdx.x * per), t1 = min(tiles, t0 + per);
@@ -1343,9 +1369,9 @@ __device__ void work_items_zones(int tiles, int Kc, const int* __restrict__ Tc, 
       const int nc = rc_[q], nt = rt_[q];  // (0 past the run, and for an empty zone)
       sc += nc;
       st += nt;
-      const int ch = chunks_of(nc) + chunks_of(nt);
-      sch += ch;
-      se += ch == 0 && b + q < t1;  // an empty tile: one empty item, after every non-empty one
+      const int nch = chunks_of(nc, ch) + chunks_of(nt, ch);
+      sch += nch;
+      se += nch == 0 && b + q < t1;  // an empty tile: one empty item, after every non-empty one
     }
   }
   // (pair counts < 2^31 and item counts: no carry between the packed halves)
@@ -1367,15 +1393,15 @@ __device__ void work_items_zones(int tiles, int Kc, const int* __restrict__ Tc, 
         const int nc = rc_[q], nt = rt_[q];
         const int2 rc = nc > 0 ? make_int2(sc, sc + nc) : make_int2(0, 0);
         const int2 rt = nt > 0 ? make_int2(Kc + st, Kc + st + nt) : make_int2(0, 0);
-        const int chc = chunks_of(nc), cht = chunks_of(nt);
+        const int chc = chunks_of(nc, ch), cht = chunks_of(nt, ch);
         ranges[2 * t] = rc;
         ranges[2 * t + 1] = rt;
         tile_item0[2 * t] = sch;
         tile_item0[2 * t + 1] = sch + chc;
         ticket[t] = 0;
-        for (int c = 0; c < chc; ++c) items[sch + c] = make_int4(2 * t, rc.x + c * CH, min(rc.y, rc.x + (c + 1) * CH), c);
+        for (int c = 0; c < chc; ++c) items[sch + c] = make_int4(2 * t, rc.x + c * ch, min(rc.y, rc.x + (c + 1) * ch), c);
         for (int c = 0; c < cht; ++c)
-          items[sch + chc + c] = make_int4(2 * t + 1, rt.x + c * CH, min(rt.y, rt.x + (c + 1) * CH), c);
+          items[sch + chc + c] = make_int4(2 * t + 1, rt.x + c * ch, min(rt.y, rt.x + (c + 1) * ch), c);
         if (chc + cht == 0) {
           tile_item0[2 * t] = tile_item0[2 * t + 1] = se;
           items[se++] = make_int4(2 * t, 0, 0, 0);
@@ -1813,7 +1839,7 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
 }
 
 // Items of a tile (virtual tiles 2t: core, 2t+1: tail; contiguous in the item list).
-__device__ __forceinline__ int tile_chunks(int2 r) { return (r.y - r.x + CH - 1) / CH; }
+__device__ __forceinline__ int tile_chunks(int2 r, int ch = CH) { return (r.y - r.x + ch - 1) / ch; }
 
 __device__ __forceinline__ void write_pixel(const ViewK& v, int p, const float* acc, float* __restrict__ out_rgb,
                                             float* __restrict__ out_alpha, float* __restrict__ out_depth,
@@ -1849,6 +1875,7 @@ __global__ __launch_bounds__(256) void k_compose(ViewK v, int hw, const float4* 
 // bf16 split-precision backward (k_raster_bwd_bf16): per tile, A fragments of v_mfma_f32_32x32x16_bf16
 // for 2 sides (T: contraction over x, R: over y) x 3 channel pairs x 3 bf16 pieces x 64 lanes, 16 B each.
 constexpr int UF_FRAGS = 2 * 3 * 3 * 64;  // uint4 per tile
+static_assert(UF_FRAGS == UF_FRAGS16, "TileCfg");
 // channel pairs on the 32 MFMA rows (16 per channel): (dC_r, dC_g), (dC_b, -), (dW, dD); tail items
 // (depth-coupled terms only) need just the last pair
 // Without an upstream depth gradient dD is identically zero, so the four live channels fill two pairs:
@@ -2623,6 +2650,394 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
     bwd_item_bf16<true, true, GR_TAIL2 ? 2 : PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF, depth3);
   else
     bwd_item_bf16<false, true, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF, depth3);
+}
+
+#ifndef GR_FWD32_WAVES
+#define GR_FWD32_WAVES 4
+#endif
+#ifndef GR_BWD32_WAVES
+#define GR_BWD32_WAVES 3
+#endif
+#ifndef GR_BWD32_BATCH
+#define GR_BWD32_BATCH 256
+#endif
+// ================================================================================================
+// 32-pixel tiles (gr_view.tile = 32): the fused fit path's forward (gr_fwd_render_l1, no_depth_grad = 1) and
+// backward splat (gr_bwd_splat).  With a ~3-pixel sigma the 5-sigma footprint spans ~32 pixels: 16-pixel tiles
+// give 7.8 (Gaussian, tile) pairs per Gaussian at C4, 32-pixel tiles 3.7, so the binning, the per-pair gradient
+// rows and their gather halve, while the separable splat's per-Gaussian slot work (exponentials, operand splits,
+// epilogue) stays the same: ~32 x and ~32 y slots per Gaussian either way.  The contractions move
+// to v_mfma_f32_32x32x16 with M = 32 pixels of ONE channel (the 16-pixel kernels pack two channels of 16).
+// Operand layout of v_mfma_f32_32x32x16_{f16,bf16} (gfx950): lane l (r = l & 31, h = l >> 5) supplies
+// A[m = r][k = kslot_pixel(h, j)] and B[k = kslot_pixel(h, j)][n = r], j = 0..7, and holds D[m][n = r] for
+// m = 16 (i >> 3) + kslot_pixel(h, i & 7), i = 0..15 — so with K = 16 pixels per step s (pixel 16 s + k) the
+// rows a lane holds are exactly the pixels whose exponentials it computed for its own B operands.
+// ================================================================================================
+constexpr int F32_PLANES = 8;  // staged record fields (px py qx qy o r g b): no depth channel on the fit path
+constexpr int F32_BUF = F32_PLANES * TP;  // floats per staging buffer (256 Gaussians)
+constexpr int F32_LD = T32 + 1;            // padded row of the forward's reduction / upstream tiles in LDS
+__device__ __forceinline__ f32x16 mfma32h(const s16x8& a, const s16x8& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma32b(const s16x8& a, const s16x8& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// offset of kslot j from the lane's first slot (kslot_pixel(h, j) - 4 h)
+__device__ __forceinline__ constexpr int kslot_off(int j) { return j < 4 ? j : j + 4; }
+
+// Forward of one work item of a 32-pixel tile: every wave contracts its 64 Gaussians of each 256-Gaussian batch
+// over the whole tile (4 K-steps of 16 per batch), C_k[x][y] += sum_g A_k[x][g] B[g][y] with A = o v_k ex * 2^sa
+// (v = 1, r, g, b) and B = ey * 2^SB on f16 two-piece operands (split2h_frag2, MODE 4's precision), four f32x16
+// accumulators per lane.  The four waves' sums meet in LDS (fixed wave order), a split tile's items through the
+// write-through partials of the last item to arrive (item order), then the L1 epilogue per pixel (four pixels per
+// thread), the backward's upstream fragments (UF32) and the view loss by the last tile (as k_raster_fwd_mfma<4>).
+__global__ __launch_bounds__(256, GR_FWD32_WAVES) void k_fwd32_l1(ViewK v, int n, const int4* __restrict__ items,
+                                                                 const int* __restrict__ num_items,
+                                                                 const int2* __restrict__ ranges, const int* __restrict__ pairs,
+                                                                 const float4* __restrict__ rec, float* __restrict__ fwd_part,
+                                                                 float* __restrict__ out_rgb, float* __restrict__ out_alpha,
+                                                                 L1Args l1, uint4* __restrict__ UF, const int* __restrict__ f16_sa,
+                                                                 const int* __restrict__ tile_item0, int* __restrict__ ticket,
+                                                                 int ch) {
+  // LDS: the staged batches (2 x 8 planes x 256 floats) during the loop; then the waves' sums of two channels
+  // (4 waves x 2 x 32 x 33); then the tile's upstream vectors (4 x 32 x 33); then the view loss's double[3][256]
+  __shared__ __attribute__((aligned(16))) float smem[4 * 2 * T32 * F32_LD];
+  static_assert(sizeof(smem) >= 2 * F32_BUF * sizeof(float) && sizeof(smem) >= 3 * 256 * sizeof(double), "k_fwd32_l1 LDS");
+  __shared__ int last_flag;
+  const int nitems = num_items[0], nfull = num_items[1];
+  if ((int)blockIdx.x >= nitems) return;
+  const int item = (int)blockIdx.x < nfull ? xcd_item(blockIdx.x, nfull) : (int)blockIdx.x;
+  const int4 it = items[item];
+  const int tile = it.x >> 1, k0 = it.y, k1 = it.z;
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int sa = f16_sa ? *f16_sa : GR_F16_SA;
+  f32x16 cW = {}, cR = {}, cG = {}, cB = {};
+  if (k1 > k0) {
+    auto stage = [&](int g, int b) { glds4_planes<false, false>(rec_of(g, n, rec), nullptr, smem + b * F32_BUF + 64 * wave); };
+    stage(stage_pair(stage_id(k0 + tid, k1, pairs), k0 + tid, k1), 0);
+    int idn = stage_id(k0 + TP + tid, k1, pairs);
+    int buf = 0;
+    const float xc = (float)(tx * T32 + r) + 0.5f, yc = (float)(ty * T32 + r) + 0.5f;  // A row x, B column y
+    const f32x2_t X = {xc, xc}, Y = {yc, yc}, SA = {(float)sa, (float)sa}, SB = {(float)GR_F16_SB, (float)GR_F16_SB};
+    for (int base = k0; base < k1; base += TP, buf ^= 1) {
+      stage_wait();
+      if (base + TP < k1) stage(stage_pair(idn, base + TP + tid, k1), buf ^ 1);
+      idn = stage_id(base + 2 * TP + tid, k1, pairs);
+      const int cnt = min(TP, k1 - base) - wave * 64;
+      const int nks = cnt <= 0 ? 0 : min(4, (cnt + 15) >> 4);  // K-steps of 16 (padding records are zero)
+      for (int ks = 0; ks < nks; ++ks) {
+        // this lane's 8 Gaussians of the K-step: kslot_pixel(h, 0..7) = 4h + {0..3} and 8 + 4h + {0..3}
+        const float* s = smem + buf * F32_BUF + wave * 64 + ks * 16 + 4 * h;
+        auto ld = [&](int f, f32x2_t (&q)[4]) {
+          const float4 u0 = *reinterpret_cast<const float4*>(s + f * TP);
+          const float4 u1 = *reinterpret_cast<const float4*>(s + f * TP + 8);
+          q[0] = f32x2_t{u0.x, u0.y};
+          q[1] = f32x2_t{u0.z, u0.w};
+          q[2] = f32x2_t{u1.x, u1.y};
+          q[3] = f32x2_t{u1.z, u1.w};
+        };
+        f32x2_t px[4], py[4], qx[4], qy[4], o[4];
+        ld(0, px);
+        ld(1, py);
+        ld(2, qx);
+        ld(3, qy);
+        ld(4, o);
+        f32x2_t oe[4], bv[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const f32x2_t dx = X - px[p], dy = Y - py[p];
+          const f32x2_t ax = __builtin_elementwise_fma(dx * qx[p], dx, SA);
+          const f32x2_t ay = __builtin_elementwise_fma(dy * qy[p], dy, SB);
+          const f32x2_t ex = {__builtin_amdgcn_exp2f(ax.x), __builtin_amdgcn_exp2f(ax.y)};
+          bv[p] = f32x2_t{__builtin_amdgcn_exp2f(ay.x), __builtin_amdgcn_exp2f(ay.y)};
+          oe[p] = o[p] * ex;
+        }
+        s16x8 fb[2], fa[2];
+        split2h_frag2(bv, fb);
+        split2h_frag2(oe, fa);
+        cW = mfma32h(fa[1], fb[0], cW);
+        cW = mfma32h(fa[0], fb[1], cW);
+        cW = mfma32h(fa[0], fb[0], cW);
+        f32x2_t c[4], a[4];
+#define GR_FWD32_CH(F, ACC)                                   \
+  ld(F, c);                                                   \
+  _Pragma("unroll") for (int p = 0; p < 4; ++p) a[p] = oe[p] * c[p]; \
+  split2h_frag2(a, fa);                                       \
+  ACC = mfma32h(fa[1], fb[0], ACC);                           \
+  ACC = mfma32h(fa[0], fb[1], ACC);                           \
+  ACC = mfma32h(fa[0], fb[0], ACC);
+        GR_FWD32_CH(5, cR)
+        GR_FWD32_CH(6, cG)
+        GR_FWD32_CH(7, cB)
+#undef GR_FWD32_CH
+      }
+    }
+    const float sc = __builtin_ldexpf(1.0f, -(sa + GR_F16_SB));  // the operands carried 2^sa and 2^SB (exact)
+    cW *= sc;
+    cR *= sc;
+    cG *= sc;
+    cB *= sc;
+  }
+  // the four waves' sums, two channels per round: wave w's rows x = 16 (i >> 3) + kslot_pixel(h, i & 7) of column y = r
+  const int px0 = tid & 31, py0 = tid >> 5;  // this thread's pixels (px0, py0 + 8 q), q = 0..3
+  float acc[4][4];                           // [pixel q][W, R, G, B]
+#pragma unroll
+  for (int round = 0; round < 2; ++round) {
+    __syncthreads();  // the staging buffers (round 0) / the previous round's reads (round 1) are done
+    const f32x16& c0 = round == 0 ? cW : cG;
+    const f32x16& c1 = round == 0 ? cR : cB;
+    float* w0 = smem + (wave * 2) * T32 * F32_LD;
+    float* w1 = w0 + T32 * F32_LD;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int x = 16 * (i >> 3) + kslot_pixel(h, i & 7);
+      w0[x * F32_LD + r] = c0[i];
+      w1[x * F32_LD + r] = c1[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int a = px0 * F32_LD + py0 + 8 * q;
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        const float* b = smem + cc * T32 * F32_LD + a;
+        acc[q][2 * round + cc] = ((b[0] + b[2 * T32 * F32_LD]) + b[4 * T32 * F32_LD]) + b[6 * T32 * F32_LD];
+      }
+    }
+  }
+  const int nch = tile_chunks(ranges[2 * tile], ch) + tile_chunks(ranges[2 * tile + 1], ch);
+  if (nch > 1) {
+    // a tile split over several items: each leaves its partial sums (write-through) and takes the tile's ticket; the
+    // last to arrive sums every item's partials in item order (deterministic) and finishes the tile
+    float* dst = fwd_part + (size_t)item * 4 * TP32;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) st_through(dst + c * TP32 + (py0 + 8 * q) * T32 + px0, acc[q][c]);
+    if (!arrive_last(&ticket[tile], nch, &last_flag)) return;
+    const float* src = fwd_part + (size_t)tile_item0[2 * tile] * 4 * TP32;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[q][c] = 0.f;
+    for (int e = 0; e < nch; ++e)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[q][c] += ld_through(src + (size_t)e * 4 * TP32 + c * TP32 + (py0 + 8 * q) * T32 + px0);
+    if (tid == 0) ticket[tile] = 0;  // left zero for a later render of the same bins
+  }
+  // per pixel: outputs, the L1 terms and the upstream vector u = (dC_r, dC_g, dC_b, dW)
+  float u[4][5];
+  float l_rgb = 0.f, l_sil = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int x = tx * T32 + px0, y = ty * T32 + py0 + 8 * q;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) u[q][c] = 0.f;
+    if (x < v.W && y < v.H) {
+      const int p = y * v.W + x;
+      const float a5[5] = {acc[q][0], acc[q][1], acc[q][2], acc[q][3], 0.0f};
+      write_pixel(v, p, a5, out_rgb, out_alpha, nullptr, nullptr, nullptr);
+      float lr = 0.f, ls = 0.f;
+      pixel_upstream(v, p, make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]), 0.0f, nullptr, nullptr, nullptr, l1,
+                     u[q], lr, ls);
+      l_rgb += lr;
+      l_sil += ls;
+    }
+  }
+  tile_loss_sums(tile, tid, l_rgb, l_sil, l1.tile_loss);  // (its barrier ends every read of smem above)
+  if (nch > 0) {  // an empty tile has no backward work item: no fragments
+    float* sU = smem;  // [channel][x][y], rows of F32_LD
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) sU[c * T32 * F32_LD + px0 * F32_LD + py0 + 8 * q] = u[q][c];
+    __syncthreads();
+    // fragment set (side, channel, K-step s), lane l: side 0 (T, contraction over x) A[m = y][k] = U[x = 16 s + k][y],
+    // side 1 (R, over y) A[m = x][k] = U[x][y = 16 s + k], k = kslot_pixel(h, j); two round-to-nearest bf16 pieces
+    uint4* fr = UF + (size_t)tile * UF32_FRAGS;
+    for (int e = tid; e < 16 * 64; e += 256) {
+      const int set = e >> 6, l = e & 63, side = set >> 3, c = (set >> 1) & 3, s = set & 1;
+      const int m = l & 31, hh = l >> 5;
+      float val[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 16 * s + kslot_pixel(hh, j);
+        val[j] = side == 0 ? sU[c * T32 * F32_LD + k * F32_LD + m] : sU[c * T32 * F32_LD + m * F32_LD + k];
+      }
+      s16x8 f2[2];
+      split2_frag(val, f2);
+      __builtin_memcpy(&fr[(set * 2 + 0) * 64 + l], &f2[0], 16);
+      __builtin_memcpy(&fr[(set * 2 + 1) * 64 + l], &f2[1], 16);
+    }
+  }
+  // the view loss: the last tile to finish sums the tiles' L1 sums (tile_loss_total, a fixed order)
+  const int tiles = v.tiles_x * v.tiles_y;
+  if (arrive_last_tile(ticket, tiles, tile, &last_flag))
+    tile_loss_total<true>(l1.tile_loss, tiles, l1.n1, l1.n2, l1.w_sil, 0, 0.0f, l1.loss_out,
+                          reinterpret_cast<double (*)[256]>(smem));
+}
+
+// Backward of one work item of a 32-pixel tile (no upstream depth gradient, two-piece bf16 operands as
+// k_raster_bwd_bf16<false, 2>): per group of 32 Gaussians (lane r = l & 31 owns Gaussian r, half h = l >> 5 its
+// slots kslot_pixel(h, .) of each 16-pixel K-step s) the contractions
+//   T_c[y][g] = sum_x U_c[x][y] ex_g(x)   and   R_c[x][g] = sum_y U_c[x][y] ey_g(y),   c = dC_r, dC_g, dC_b, dW,
+// each 2 K-steps x 3 piece products on v_mfma_f32_32x32x16_bf16, then the per-Gaussian epilogue over the lane's 16
+// rows (the same sums as the 16-pixel kernel, moments about the first slot of each K-step) and the 8-float row
+// [o S0, o S2, S4, S6 | o S1, S8, S5, S7] at the pair's sorted position (the gather is unchanged).
+__global__ __launch_bounds__(256, GR_BWD32_WAVES) void k_bwd32(ViewK v, int n, const int4* __restrict__ items,
+                                                              const int* __restrict__ num_items, const int* __restrict__ pairs,
+                                                              const float4* __restrict__ rec, const uint4* __restrict__ UF,
+                                                              float* __restrict__ partials) {
+  constexpr int NB = GR_BWD32_BATCH;  // Gaussians staged per batch (NB / 4 per wave)
+  constexpr int WG = NB / 4;          // per wave: one or two groups of 32
+  __shared__ __attribute__((aligned(16))) float4 sA[2][NB];
+  __shared__ __attribute__((aligned(16))) float4 sB[2][NB];
+  __shared__ __attribute__((aligned(16))) uint4 sUF[2 * 4 * 2 * 2 * 64];  // (side, channel, s, piece) x 64 lanes
+  const int nitems = num_items[1];
+  if ((int)blockIdx.x >= nitems) return;
+  const int item = xcd_item(blockIdx.x, nitems);
+  const int4 it = items[item];
+  const int tile = it.x >> 1, k0 = it.y, k1 = it.z;
+  if (k1 <= k0) return;
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  {  // the tile's 32 fragment chunks -> LDS (DMA)
+    const uint4* src = UF + (size_t)tile * UF32_FRAGS;
+    for (int cc = wave; cc < 32; cc += 4) glds16(src + 64 * cc + lane, sUF + 64 * cc);
+  }
+  // pixel centres of the lane's first slot per K-step: base + kslot offsets (compile-time)
+  const float pxb[2] = {(float)(tx * T32 + 4 * h) + 0.5f, (float)(tx * T32 + 16 + 4 * h) + 0.5f};
+  const float pyb[2] = {(float)(ty * T32 + 4 * h) + 0.5f, (float)(ty * T32 + 16 + 4 * h) + 0.5f};
+  {  // the first batch (lanes < WG stage this wave's WG Gaussians)
+    const int k = k0 + wave * WG + (lane < WG ? lane : 0);
+    if (lane < WG) {
+      const int gid = stage_pair(stage_id(k, k1, pairs), k, k1);
+      glds16(rec_of(gid, n, rec), &sA[0][WG * wave]);
+      glds16(rec_of(gid, n, rec) + 1, &sB[0][WG * wave]);
+    }
+  }
+  int idn = stage_id(k0 + NB + wave * WG + (lane < WG ? lane : 0), k1, pairs);
+  int buf = 0;
+  for (int base = k0; base < k1; base += NB, buf ^= 1) {
+    stage_wait();
+    if (base == k0) __syncthreads();  // the fragment chunks (every wave's DMA) are in LDS
+    if (base + NB < k1 && lane < WG) {
+      const int gid = stage_pair(idn, base + NB + wave * WG + lane, k1);
+      glds16(rec_of(gid, n, rec), &sA[buf ^ 1][WG * wave]);
+      glds16(rec_of(gid, n, rec) + 1, &sB[buf ^ 1][WG * wave]);
+    }
+    idn = stage_id(base + 2 * NB + wave * WG + (lane < WG ? lane : 0), k1, pairs);
+    const int nb = min(NB, k1 - base);
+    for (int gi = 0; gi < WG / 32; ++gi) {
+      const int g0 = wave * WG + gi * 32;
+      if (g0 >= nb) break;  // wave-uniform
+      const int j = g0 + r;
+      const float4 a = sA[buf][j];
+      const float4 b = sB[buf][j];
+      const int myslot = j < nb ? base + j : -1;
+      // exponentials of the lane's 8 slots per K-step (moments about the first slot: two constant fmas per slot)
+      float ex[2][8], ey[2][8], d0x[2], d0y[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        d0x[s] = pxb[s] - a.x;
+        d0y[s] = pyb[s] - a.y;
+        const float tX = a.z * d0x[s], tY = a.w * d0y[s];
+        const float cX = tX * d0x[s], cY = tY * d0y[s];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float oq = (float)kslot_off(q);
+          ex[s][q] = __builtin_amdgcn_exp2f(q == 0 ? cX : fmaf(tX, 2.0f * oq, fmaf(a.z, oq * oq, cX)));
+          ey[s][q] = __builtin_amdgcn_exp2f(q == 0 ? cY : fmaf(tY, 2.0f * oq, fmaf(a.w, oq * oq, cY)));
+        }
+      }
+      float S[NPART] = {-0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f};
+      float S4s[2] = {-0.f, -0.f}, S6c[2] = {-0.f, -0.f}, S8c[2] = {-0.f, -0.f};
+      float U0[2] = {-0.f, -0.f}, S5c[2] = {-0.f, -0.f}, S7c[2] = {-0.f, -0.f};
+      {  // T: contraction over x (B = ex), rows y
+        s16x8 BT[2][2];
+        split2_frag(ex[0], BT[0]);
+        split2_frag(ex[1], BT[1]);
+        f32x16 D[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const uint4* A0 = sUF + ((0 * 4 + c) * 2 + 0) * 2 * 64;  // (side 0, c, s = 0, piece 0)
+          f32x16 d = {};
+#pragma unroll
+          for (int s = 0; s < 2; ++s) d = mfma32b(as_frag(A0[(s * 2 + 1) * 64 + lane]), BT[s][0], d);
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const s16x8 a0 = as_frag(A0[(s * 2) * 64 + lane]);
+            d = mfma32b(a0, BT[s][1], d);
+            d = mfma32b(a0, BT[s][0], d);
+          }
+          D[c] = d;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int s = i >> 3, q = i & 7;
+          const float e = ey[s][q], oq = (float)kslot_off(q);
+          const float T0 = D[0][i], T1 = D[1][i], T2 = D[2][i], T3 = D[3][i];
+          S[0] = fmaf(e, T0, S[0]);
+          S[1] = fmaf(e, T1, S[1]);
+          S[2] = fmaf(e, T2, S[2]);
+          const float t = e * fmaf(b.w, T2, fmaf(b.z, T1, fmaf(b.y, T0, T3)));
+          S4s[s] += t;
+          if (q != 0) {  // slot 0 of each K-step is the origin of its moments
+            S6c[s] = fmaf(t, oq, S6c[s]);
+            S8c[s] = fmaf(t, oq * oq, S8c[s]);
+          }
+        }
+      }
+      {  // R: contraction over y (B = ey), rows x
+        s16x8 BR[2][2];
+        split2_frag(ey[0], BR[0]);
+        split2_frag(ey[1], BR[1]);
+        f32x16 D[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const uint4* A0 = sUF + ((1 * 4 + c) * 2 + 0) * 2 * 64;  // (side 1, c, s = 0, piece 0)
+          f32x16 d = {};
+#pragma unroll
+          for (int s = 0; s < 2; ++s) d = mfma32b(as_frag(A0[(s * 2 + 1) * 64 + lane]), BR[s][0], d);
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const s16x8 a0 = as_frag(A0[(s * 2) * 64 + lane]);
+            d = mfma32b(a0, BR[s][1], d);
+            d = mfma32b(a0, BR[s][0], d);
+          }
+          D[c] = d;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int s = i >> 3, q = i & 7;
+          const float oq = (float)kslot_off(q);
+          const float u = ex[s][q] * fmaf(b.w, D[2][i], fmaf(b.z, D[1][i], fmaf(b.y, D[0][i], D[3][i])));
+          U0[s] += u;
+          if (q != 0) {
+            S5c[s] = fmaf(u, oq, S5c[s]);
+            S7c[s] = fmaf(u, oq * oq, S7c[s]);
+          }
+        }
+      }
+      S[4] = S4s[0] + S4s[1];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        S[6] += fmaf(d0y[s], S4s[s], S6c[s]);
+        S[8] += fmaf(d0y[s] * d0y[s], S4s[s], fmaf(2.0f * d0y[s], S6c[s], S8c[s]));
+        S[5] += fmaf(d0x[s], U0[s], S5c[s]);
+        S[7] += fmaf(d0x[s] * d0x[s], U0[s], fmaf(2.0f * d0x[s], S5c[s], S7c[s]));
+      }
+      // lanes r and r + 32 hold the two halves of Gaussian r's slots (pair32); row as k_raster_bwd_bf16<false, .>
+      const float Pa = pair32(S[0], S[1]), Pb = pair32(S[2], S[8]), Pc = pair32(S[4], S[5]);
+      const float Pd = pair32(S[6], S[7]);
+      if (myslot >= 0)
+        reinterpret_cast<float4*>(partials)[2 * (size_t)myslot + h] =
+            h == 0 ? make_float4(b.x * Pa, b.x * Pb, Pc, Pd) : make_float4(b.x * Pa, Pb, Pc, Pd);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3664,6 +4079,7 @@ gr_status check_view(const gr_view* v) {
   if (!v) return set_error(GR_ERR_INVALID_ARGUMENT, "view is null");
   if (v->width <= 0 || v->height <= 0) return set_error(GR_ERR_INVALID_ARGUMENT, "width/height must be positive");
   if ((int64_t)v->width * v->height > (1ll << 30)) return set_error(GR_ERR_INVALID_ARGUMENT, "image too large");
+  if (v->tile != 0 && v->tile != T && v->tile != T32) return set_error(GR_ERR_INVALID_ARGUMENT, "tile must be 0, 16 or 32");
   return GR_OK;
 }
 
@@ -3712,7 +4128,7 @@ void gr_geom_layout(int n, size_t offsets_out[GR_GEOM_PARTS]) { geom_fixed(n, of
 void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[4]) {
   (void)n;
   size_t off[8];
-  bins_fixed(vtiles_of(v), plan ? plan->num_pairs : 0, off);
+  bins_fixed(vtiles_of(v), plan ? plan->num_pairs : 0, off, tile_cfg(v).ch);
   offsets_out[0] = off[0];
   offsets_out[1] = off[1];
   offsets_out[2] = off[2];
@@ -3729,21 +4145,22 @@ size_t gr_saved_floats(const gr_view* v) { return (size_t)5 * v->width * v->heig
 size_t gr_bins_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
   size_t off[8];
-  return bins_fixed(vtiles_of(v), plan->num_pairs, off);
+  return bins_fixed(vtiles_of(v), plan->num_pairs, off, tile_cfg(v).ch);
 }
 
 size_t gr_fwd_scratch_bytes(const gr_view* v, int n, const gr_plan* plan) {
   const int vtiles = vtiles_of(v);
+  const TileCfg tc = tile_cfg(v);
   size_t off[5];
-  return scratch_fixed(vtiles, plan->num_pairs, off) + align_up(tile_sort_tmp_bytes(n, plan->num_pairs, vtiles));
+  return scratch_fixed(vtiles, plan->num_pairs, off, tc.ch, tc.part_floats) + align_up(tile_sort_tmp_bytes(n, plan->num_pairs, vtiles));
 }
 
 // Backward workspace: pair partials (one 9-float slot per rectangle tile) + per-pixel upstream
 // vectors (tiles x 5 x 256).
 size_t gr_bwd_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
-  const size_t tiles = (size_t)tiles_x_of(v->width) * tiles_y_of(v->height);
-  const size_t per_tile = UF_FRAGS * sizeof(uint4);
+  const size_t tiles = (size_t)tiles_of(v);
+  const size_t per_tile = tile_cfg(v).uf_frags * sizeof(uint4);
   return align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)) + align_up(tiles * per_tile) +
          align_up(tiles * 4 * sizeof(float)) + align_up(tiles * 2 * sizeof(float)) +
          align_up(4 * sizeof(float)) +  // per-tile loss sums, per-tile depth max / arg-max counts, depth scalars
@@ -3991,11 +4408,11 @@ struct BwdWs {
   double* cam_part;  // [blocks][CAM_GRADS]: per-block camera-gradient partials (gr_bwd_camera)
 };
 static BwdWs bwd_ws(const gr_view* v, int n, const gr_plan* plan, void* ws) {
-  const size_t tiles = (size_t)tiles_x_of(v->width) * tiles_y_of(v->height);
+  const size_t tiles = (size_t)tiles_of(v);
   BwdWs w;
   w.partials = (float*)ws;
   w.UF = (uint4*)((char*)ws + align_up((size_t)(plan->num_slots > 0 ? plan->num_slots : 1) * NPART * sizeof(float)));
-  w.tile_loss = (float*)((char*)w.UF + align_up(tiles * UF_FRAGS * sizeof(uint4)));
+  w.tile_loss = (float*)((char*)w.UF + align_up(tiles * tile_cfg(v).uf_frags * sizeof(uint4)));
   w.tile_aux = (float*)((char*)w.tile_loss + align_up(tiles * 4 * sizeof(float)));
   w.dscal = (float*)((char*)w.tile_aux + align_up(tiles * 2 * sizeof(float)));
   w.sums = (float*)((char*)w.dscal + align_up(4 * sizeof(float)));
@@ -4024,6 +4441,7 @@ static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const vo
       const int waves = tsort_waves(tiles);
       TZones Z;
       Z.cw = cw;
+      Z.ch = tile_cfg(v).ch;
       char* q = (char*)sc.sort_tmp;
       for (int z = 0; z < 2; ++z) {
         TZone& zz = Z.z[z];
@@ -4088,14 +4506,14 @@ static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const vo
                          b.pairs, b.pos_of);
       GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_work_items, dim3(1), dim3(WI_THREADS), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
-                         b.tile_item0, b.ticket);
+                         b.tile_item0, b.ticket, tile_cfg(v).ch);
     }
   } else {
     // no pair: the Gaussians' offsets (written by the emission otherwise) are all zero
     if (n > 0) GR_HIP_TRY(hipMemsetAsync(geom_view((void*)geom, n).offsets, 0, (size_t)n * sizeof(unsigned long long), s));
     GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * vtiles, s));
     hipLaunchKernelGGL(k_work_items, dim3(1), dim3(WI_THREADS), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
-                       b.tile_item0, b.ticket);
+                       b.tile_item0, b.ticket, tile_cfg(v).ch);
   }
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_BINNING, s);
@@ -4123,8 +4541,13 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
   hipStream_t s = (hipStream_t)stream;
   const ViewK vk = make_viewk(v);
   const int tiles = vk.tiles_x * vk.tiles_y, vtiles = 2 * tiles;
-  Bins b = bins_view(bins, vtiles, num_pairs);
-  Scratch sc = scratch_view(scratch, vtiles, num_pairs);
+  const TileCfg tc = tile_cfg(v);
+  if (tc.T == T32 && (!l1 || v->no_depth_grad != 1))
+    return set_error(GR_ERR_INVALID_ARGUMENT, "32-pixel tiles (gr_view.tile = 32): gr_fwd_render_l1 with no_depth_grad = 1 only");
+  if (tc.T == T32 && vk.core != vk.cutoff)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "32-pixel tiles (gr_view.tile = 32): one-zone footprint only (core_cutoff <= 0 or >= cutoff)");
+  Bins b = bins_view(bins, vtiles, num_pairs, tc.ch);
+  Scratch sc = scratch_view(scratch, vtiles, num_pairs, tc.ch, tc.part_floats);
   if (!v->binned) {
     for (int rep = 0; rep < GR_DEBUG_BIN_REPS; ++rep) {  // > 1: timing experiments only (idempotent repeats)
       st = bin_impl(v, n, plan, geom, b, sc, vk, s);
@@ -4133,7 +4556,7 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
   }
   Geom g = geom_view((void*)geom, n > 0 ? n : 1);
   const size_t HW = (size_t)v->width * v->height;
-  const int64_t cap = item_cap(vtiles, num_pairs);
+  const int64_t cap = item_cap(vtiles, num_pairs, tc.ch);
   L1Args la{nullptr, nullptr, 0.f, 0.f, nullptr};
   uint4* UF = nullptr;
   if (l1) {
@@ -4154,6 +4577,12 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
     prof_mark(PROF_RASTER_FWD, s);
     // no_depth_grad: 0 default (f32-grade W / D), 1 two-piece splits, 2 f32-grade without a depth gradient
     const bool f32g = v->no_depth_grad != 1;
+    if (tc.T == T32)
+      hipLaunchKernelGGL(k_fwd32_l1, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items,
+                         (const int2*)b.ranges, (const int*)b.pairs, (const float4*)g.rec, sc.fwd_part, out_rgb, out_alpha, la,
+                         UF, (const int*)(n > 0 && num_pairs > 0 ? g.f16_sa : nullptr), (const int*)b.tile_item0, b.ticket,
+                         tc.ch);
+    else
     hipLaunchKernelGGL(l1 ? (f32g ? k_raster_fwd_mfma<5> : k_raster_fwd_mfma<4>)
                           : (f32g ? k_raster_fwd_mfma<1>
                                   : (out_depth || depth_sums ? k_raster_fwd_mfma<2> : k_raster_fwd_mfma<3>)),
@@ -4206,8 +4635,9 @@ gr_status gr_fwd_bin(const gr_view* v, int n, const gr_plan* plan, const void* g
     return set_error(GR_ERR_WORKSPACE, "forward scratch workspace too small");
   const ViewK vk = make_viewk(v);
   const int vtiles = 2 * vk.tiles_x * vk.tiles_y;
-  return bin_impl(v, n, plan, geom, bins_view(bins, vtiles, plan->num_pairs), scratch_view(scratch, vtiles, plan->num_pairs),
-                  vk, (hipStream_t)stream);
+  const TileCfg tc = tile_cfg(v);
+  return bin_impl(v, n, plan, geom, bins_view(bins, vtiles, plan->num_pairs, tc.ch),
+                  scratch_view(scratch, vtiles, plan->num_pairs, tc.ch, tc.part_floats), vk, (hipStream_t)stream);
 }
 
 gr_status gr_fwd_render_l1(const gr_view* v, int n, const gr_plan* plan, const void* geom, void* bins, size_t bins_bytes,
@@ -4237,6 +4667,8 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
   if ((g_depth || (t_rgb && t_depth)) && v->no_depth_grad)
     return set_error(GR_ERR_INVALID_ARGUMENT,
                      "depth gradient for a view rendered with no_depth_grad (render it with depth_grad=True)");
+  if (tile_of(v) != T)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "32-pixel tiles (gr_view.tile = 32): the fused fit path only (gr_bwd_splat)");
   if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
   if (color_dim != 3 && color_dim != 12 && color_dim != 48)
     return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");
@@ -4431,11 +4863,18 @@ gr_status gr_bwd_splat(const gr_view* v, int n, const gr_plan* plan, const void*
   const ViewK vk = make_viewk(v);
   const int tiles = vk.tiles_x * vk.tiles_y;
   const Geom g = geom_view((void*)geom, n);
-  const Bins b = bins_view((void*)bins, 2 * tiles, plan->num_pairs);
+  const TileCfg tc = tile_cfg(v);
+  if (tc.T == T32 && v->no_depth_grad != 1)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "32-pixel tiles (gr_view.tile = 32): no_depth_grad = 1 only");
+  const Bins b = bins_view((void*)bins, 2 * tiles, plan->num_pairs, tc.ch);
   const BwdWs w = bwd_ws(v, n, plan, ws);
-  const int64_t cap = item_cap(2 * tiles, plan->num_pairs);
+  const int64_t cap = item_cap(2 * tiles, plan->num_pairs, tc.ch);
   if (GR_DEBUG_SKIP & 2) return GR_OK;
   prof_mark(PROF_RASTER_BWD, s);
+  if (tc.T == T32)
+    hipLaunchKernelGGL(k_bwd32, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items,
+                       (const int*)b.pairs, (const float4*)g.rec, (const uint4*)w.UF, w.partials);
+  else
   hipLaunchKernelGGL((v->no_depth_grad == 1 ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>), dim3((unsigned)cap),
                      dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items, (const int*)b.pairs,
                      (const float4*)g.rec, (const uint4*)w.UF, w.partials, (float*)nullptr);
@@ -4469,7 +4908,7 @@ gr_status gr_reduce_views(int num_views, const gr_reduce_view* views, int n, con
       return set_error(GR_ERR_INVALID_ARGUMENT, "gr_reduce_views: null workspace");
     const ViewK vk = make_viewk(&rv.view);
     const Geom g = geom_view((void*)rv.geom, n);
-    const Bins b = bins_view((void*)rv.bins, 2 * vk.tiles_x * vk.tiles_y, rv.plan.num_pairs);
+    const Bins b = bins_view((void*)rv.bins, 2 * vk.tiles_x * vk.tiles_y, rv.plan.num_pairs, tile_cfg(&rv.view).ch);
     B.r[k].v = vk;
     B.r[k].offsets = (const Cnt2*)g.offsets;
     B.r[k].pos_of = rv.plan.num_pairs > 0 ? (const int*)b.pos_of : nullptr;
@@ -4513,7 +4952,7 @@ gr_status gr_gather_view(const gr_view* v, int n, const gr_plan* plan, const voi
   }
   const ViewK vk = make_viewk(v);
   const Geom g = geom_view((void*)geom, n);
-  const Bins b = bins_view((void*)bins, 2 * vk.tiles_x * vk.tiles_y, plan->num_pairs);
+  const Bins b = bins_view((void*)bins, 2 * vk.tiles_x * vk.tiles_y, plan->num_pairs, tile_cfg(v).ch);
   if (GR_DEBUG_SKIP & 4) return GR_OK;
   prof_mark(PROF_REDUCE, s);
   hipLaunchKernelGGL(k_gather_view<false>, dim3((n + 63) / 64), dim3(256), 0, s, n, (const Cnt2*)g.offsets,

@@ -106,6 +106,10 @@ BIN_STREAM = os.environ.get("GR_BIN_STREAM", "")
 # the fused path at f32 grade (gr_view.no_depth_grad = 2: three-piece splits in both splats, as the default
 # precision mode) instead of its two-piece mode: the precision reference of the fit path (bench.py f32_grade_fit)
 F32_GRADE = os.environ.get("GR_F32_GRADE", "0") != "0"
+# screen tile edge of the fused path's views (gr_view.tile): 32-pixel tiles halve the (Gaussian, tile) pairs of the
+# ~3-pixel-sigma C4 scene (7.8 -> 3.7 per Gaussian), so the binning and the per-pair gradient rows and their gather
+# (DESIGN.md §5); 16 = the drop-in op's tiles.  The f32-grade reference mode (F32_GRADE) keeps 16.
+FIT_TILE = int(os.environ.get("GR_FIT_TILE", "32"))
 
 
 # ------------------------------------------------------------------------------------------------
@@ -387,12 +391,13 @@ class ViewShardedFitter:
         cache = getattr(self, "_gv_cache", None)
         if cache is None:
             self._gv_cache = cache = {}
-        gv = cache.get((i, F32_GRADE))
+        gv = cache.get((i, F32_GRADE, FIT_TILE))
         if gv is None:
             cam = self.cams[i]
-            gv = cache[(i, F32_GRADE)] = tr.make_view(cam.view, cam.proj, self.width, self.height,
+            gv = cache[(i, F32_GRADE, FIT_TILE)] = tr.make_view(cam.view, cam.proj, self.width, self.height,
                                                       self._background(device), cutoff=tr.FIT_CUTOFF,
-                                                      core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
+                                                      core_cutoff=tr.FIT_CUTOFF, depth_grad=False,
+                                                      tile=0 if F32_GRADE else FIT_TILE)
             if F32_GRADE:
                 gv.no_depth_grad = 2
         return gv

@@ -181,11 +181,11 @@ def _host_matrix(t: torch.Tensor) -> np.ndarray:
 
 
 def make_view(view, proj, width: int, height: int, background=None, cutoff: Optional[float] = None,
-              core_cutoff: float = DEFAULT_CORE_CUTOFF, depth_grad: bool = True) -> _native.GrView:
+              core_cutoff: float = DEFAULT_CORE_CUTOFF, depth_grad: bool = True, tile: int = 0) -> _native.GrView:
     """Build a gr_view from host (numpy / tensor) matrices.  ``depth_grad=False`` promises that the
     depth output will get no gradient (gr_view.no_depth_grad): W and D are then accumulated within
     2^-16 relative instead of f32-grade, and a depth gradient raises in the backward.
-    ``cutoff=None``: ``default_cutoff(depth_grad)``."""
+    ``cutoff=None``: ``default_cutoff(depth_grad)``.  ``tile``: gr_view.tile (0/16, or 32 on the fused fit path)."""
     if cutoff is None:
         cutoff = default_cutoff(depth_grad)
     V = view if isinstance(view, np.ndarray) else _host_matrix(view)
@@ -218,6 +218,7 @@ def make_view(view, proj, width: int, height: int, background=None, cutoff: Opti
     gv.cutoff = float(cutoff)
     gv.core_cutoff = float(core_cutoff)
     gv.no_depth_grad = 0 if depth_grad else 1
+    gv.tile = int(tile)
     return gv
 
 
@@ -563,20 +564,26 @@ def _binned(gv: _native.GrView) -> _native.GrView:
 
 
 def forward_l1_native(means, scales, colors, opacities, gv: _native.GrView, prepared: Prepared, target, mask,
-                      w_sil: float, g_scale: float, loss_out, bin_stream=None):
+                      w_sil: float, g_scale: float, loss_out, bin_stream=None, out=None, alpha=None):
     """gr_fwd_render_l1 on the current stream (the fused fit path; gv with no_depth_grad, no depth output):
     the forward of one view whose epilogue evaluates the fit loss ``mean|out - target| + w_sil
     mean|alpha - mask|`` (mask may be None) into ``loss_out`` and its upstream gradients (scaled by
     ``g_scale``) into the backward workspace.  No image is written.  Returns (RenderState, workspace):
     pass them to ``backward_splat_native`` and then ``reduce_views_native``.  ``bin_stream``: run the
     view's binning (gr_fwd_bin) on that stream (after the preparation's event) and only the splat on the
-    current one, which waits for it."""
+    current one, which waits for it.  ``out`` (H,W,3) / ``alpha`` (H,W): float32 device tensors the render also
+    writes its images into (tests; the fit path renders none)."""
     L = _native.lib()
     dev = means.device
     n = int(means.shape[0])
     if (prepared.n != n or prepared.gv.width != gv.width or prepared.gv.height != gv.height
-            or prepared.gv.cutoff != gv.cutoff or prepared.gv.core_cutoff != gv.core_cutoff):
-        raise ValueError("prepared view does not match this render (Gaussian count, image size or cutoffs)")
+            or prepared.gv.cutoff != gv.cutoff or prepared.gv.core_cutoff != gv.core_cutoff
+            or prepared.gv.tile != gv.tile):
+        raise ValueError("prepared view does not match this render (Gaussian count, image size, cutoffs or tile)")
+    if out is not None:
+        _check_operand(out, (gv.height, gv.width, 3), "out", dev)
+    if alpha is not None:
+        _check_operand(alpha, (gv.height, gv.width), "alpha", dev)
     _check_operand(target, (gv.height, gv.width, 3), "target", dev)
     _check_operand(mask, (gv.height, gv.width), "mask", dev)
     plan = prepared.plan()
@@ -585,7 +592,9 @@ def forward_l1_native(means, scales, colors, opacities, gv: _native.GrView, prep
     _native.check(L.gr_fwd_render_l1(ctypes.byref(rv), n, ctypes.byref(plan), _native.ptr(prepared.geom),
                                      _native.ptr(bins), bins.numel(), _native.ptr(scratch), scratch.numel(),
                                      _native.ptr(target), _native.ptr(mask), ctypes.c_float(w_sil), ctypes.c_float(g_scale),
-                                     _native.ptr(loss_out), None, None, _native.ptr(ws), ws.numel(), _stream(dev)),
+                                     _native.ptr(loss_out), _native.ptr(out) if out is not None else None,
+                                     _native.ptr(alpha) if alpha is not None else None, _native.ptr(ws), ws.numel(),
+                                     _stream(dev)),
                   "gr_fwd_render_l1")
     del scratch
     return RenderState(gv, n, plan, prepared.geom, bins, None), ws

@@ -92,6 +92,11 @@ typedef struct gr_view {
   int binned;          /* 1: gr_fwd_bin has already built this view's bins (same plan, geom, bins   */
                        /* and scratch, ordered before the render); gr_fwd_render(_l1) then launches */
                        /* only the splat.  0 (default): the render bins the view itself            */
+  int tile;            /* screen tile edge: 0 or 16 (default, GR_TILE) or 32.  32-pixel tiles halve the   */
+                       /* (Gaussian, tile) pairs of a ~3-pixel-sigma scene and with them the binning and  */
+                       /* the per-pair gradient rows; supported on the fused fit path only (preparation,  */
+                       /* gr_fwd_bin, gr_fwd_render_l1 with no_depth_grad = 1, gr_bwd_splat,               */
+                       /* gr_gather_view, gr_reduce_sums); the other entry points reject it.              */
 } gr_view;
 
 /* ------------------------------------------------------------------------------------------ */

@@ -40,6 +40,7 @@ class GrView(ctypes.Structure):
         ("no_depth_grad", ctypes.c_int),  # product precision mode; the oracle always computes in float64
         ("background_dev", ctypes.c_void_p),  # product only (device background); the oracle reads background
         ("binned", ctypes.c_int),  # product only (gr_fwd_bin ran); the oracle always bins
+        ("tile", ctypes.c_int),  # tile edge of the binned semantics: 0/16 or 32
     ]
 
 
@@ -109,8 +110,9 @@ def camera_position(view: np.ndarray) -> np.ndarray:
     return np.linalg.inv(np.asarray(view, dtype=np.float64))[:3, 3].astype(np.float32)
 
 
-def make_view(view, proj, width, height, background=None, cutoff=7.0, core_cutoff=0.0) -> GrView:
-    """core_cutoff <= 0 (default) = one zone; the product's default is DEFAULT_CORE_CUTOFF (5.5)."""
+def make_view(view, proj, width, height, background=None, cutoff=7.0, core_cutoff=0.0, tile=0) -> GrView:
+    """core_cutoff <= 0 (default) = one zone; the product's default is DEFAULT_CORE_CUTOFF (5.5).  tile: the binned
+    semantics' tile edge (0/16, or 32 as the fit path's gr_view.tile)."""
     v = GrView()
     v.width, v.height = int(width), int(height)
     v.view[:] = [float(x) for x in np.asarray(view, dtype=np.float32).reshape(16)]
@@ -120,6 +122,7 @@ def make_view(view, proj, width, height, background=None, cutoff=7.0, core_cutof
     v.cam_pos[:] = [float(x) for x in camera_position(view)]
     v.cutoff = float(cutoff)
     v.core_cutoff = float(core_cutoff)
+    v.tile = int(tile)
     return v
 
 
@@ -148,7 +151,8 @@ def bin_pairs(v: GrView, rec: np.ndarray, rect: np.ndarray, counts: np.ndarray):
     rec/rect/counts from preprocess().  ranges: (2*tiles, 2)."""
     n = counts.shape[0]
     rec = np.ascontiguousarray(rec, np.float32)
-    tiles = math.ceil(v.width / TILE) * math.ceil(v.height / TILE)
+    te = 32 if v.tile == 32 else TILE
+    tiles = math.ceil(v.width / te) * math.ceil(v.height / te)
     offsets = np.zeros((n + 1,), np.int32)
     rect = np.ascontiguousarray(rect, np.int32)
     counts = np.ascontiguousarray(counts, np.int32)

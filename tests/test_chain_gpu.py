@@ -66,7 +66,8 @@ def test_fit_chain_c4_batch_vs_oracle(cuda):
     ora = [np.zeros(a.shape, np.float64) for a in hip]
     ora_loss, out_err, flips = 0.0, 0.0, 0
     for i, (view, proj) in enumerate(cams):
-        v = orc.make_view(view, proj, W, H, None, cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF)
+        # the binned semantics at the fused path's tile size (gr_view.tile = fm.FIT_TILE)
+        v = orc.make_view(view, proj, W, H, None, cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF, tile=fm.FIT_TILE)
         out, alpha, _ = orc.forward(v, sc, binned=True)
         # the HIP forward's own images in the fused path's precision mode (the same f16 accumulation as
         # gr_fwd_render_l1): the L1 kink makes sign(out - t) at near-ties depend on the last float bit, so the
