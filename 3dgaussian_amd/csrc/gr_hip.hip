@@ -409,7 +409,7 @@ constexpr int CH = GR_CH;  // Gaussians per raster work item (one chunk of one t
 // 32-pixel tiles (gr_view.tile = 32): four times the pixels per pair, so a quarter... of the pairs per item would keep
 // the item's work; fewer, longer items keep the split tiles' partial sums (4 x 1024 floats per item) small.
 #ifndef GR_CH32
-#define GR_CH32 1024
+#define GR_CH32 2048
 #endif
 constexpr int CH32 = GR_CH32;
 constexpr int NPART = 9;  // backward partial sums per (Gaussian, tile) pair
@@ -2653,7 +2653,7 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
 }
 
 #ifndef GR_FWD32_WAVES
-#define GR_FWD32_WAVES 4
+#define GR_FWD32_WAVES 3
 #endif
 #ifndef GR_BWD32_WAVES
 #define GR_BWD32_WAVES 3

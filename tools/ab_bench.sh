@@ -14,6 +14,13 @@ for r in $(seq 1 $ROUNDS); do
     name=$(basename $(cd $R/$d && pwd))
     (cd $R/$d && timeout -k 10 240 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-psnr --no-dropin \
       --no-extra-modes > $O/ab_${name}_$r.log 2>&1)
-    echo "$name round $r: $(grep -o '"value": [0-9.]*' $O/ab_${name}_$r.log | head -1)"
+    echo "$name round $r: $(python3 -c "
+import json,sys
+for l in open(sys.argv[1]):
+    if l.startswith('{'):
+        d=json.loads(l); s=d.get('splats',{})
+        print(d['value'], 'fwd_us', s.get('fwd',{}).get('avg_launch_us'), 'bwd_us', s.get('bwd',{}).get('avg_launch_us'),
+              'red_us', d.get('reduce_us_per_view'), 'bin_us', d.get('binning_us_per_view'))
+" $O/ab_${name}_$r.log)"
   done
 done
