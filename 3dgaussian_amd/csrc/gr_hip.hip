@@ -2661,6 +2661,21 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
 #ifndef GR_BWD32_BATCH
 #define GR_BWD32_BATCH 256
 #endif
+// timing diagnostics only (results wrong): 1 = two piece products per K-step instead of three (32 MFMAs per group),
+// 2 = no exponentials (VALU), 4 = no T-side epilogue
+#ifndef GR_BWD32_DIAG
+#define GR_BWD32_DIAG 0
+#endif
+// phase fences of k_bwd32 (GR_BWD32_FENCE = 1): the compiler may not move instructions across them, so a pass's
+// MFMAs are not hoisted above the previous pass's epilogue (which would keep every accumulator live at once)
+#ifndef GR_BWD32_FENCE
+#define GR_BWD32_FENCE 1
+#endif
+#if GR_BWD32_FENCE
+#define GR_BWD32_PHASE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define GR_BWD32_PHASE() ((void)0)
+#endif
 // ================================================================================================
 // 32-pixel tiles (gr_view.tile = 32): the fused fit path's forward (gr_fwd_render_l1, no_depth_grad = 1) and
 // backward splat (gr_bwd_splat).  With a ~3-pixel sigma the 5-sigma footprint spans ~32 pixels: 16-pixel tiles
@@ -2949,41 +2964,58 @@ __global__ __launch_bounds__(256, GR_BWD32_WAVES) void k_bwd32(ViewK v, int n, c
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const float oq = (float)kslot_off(q);
+#if GR_BWD32_DIAG & 2
+          ex[s][q] = (q == 0 ? cX : fmaf(tX, 2.0f * oq, fmaf(a.z, oq * oq, cX)));
+          ey[s][q] = (q == 0 ? cY : fmaf(tY, 2.0f * oq, fmaf(a.w, oq * oq, cY)));
+#else
           ex[s][q] = __builtin_amdgcn_exp2f(q == 0 ? cX : fmaf(tX, 2.0f * oq, fmaf(a.z, oq * oq, cX)));
           ey[s][q] = __builtin_amdgcn_exp2f(q == 0 ? cY : fmaf(tY, 2.0f * oq, fmaf(a.w, oq * oq, cY)));
+#endif
         }
       }
       float S[NPART] = {-0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f};
       float S4s[2] = {-0.f, -0.f}, S6c[2] = {-0.f, -0.f}, S8c[2] = {-0.f, -0.f};
       float U0[2] = {-0.f, -0.f}, S5c[2] = {-0.f, -0.f}, S7c[2] = {-0.f, -0.f};
+      // one channel's contraction on one side (side 0: T over x with B = ex pieces, side 1: R over y with B = ey
+      // pieces): 2 K-steps x 3 piece products (a_lo b_hi, a_hi b_lo, a_hi b_hi)
+      auto contract = [&](int side, int c, const s16x8 (&B)[2][2]) {
+        const uint4* A0 = sUF + ((side * 4 + c) * 2 + 0) * 2 * 64;  // (side, c, s = 0, piece 0)
+        f32x16 d = {};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) d = mfma32b(as_frag(A0[(s * 2 + 1) * 64 + lane]), B[s][0], d);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const s16x8 a0 = as_frag(A0[(s * 2) * 64 + lane]);
+          if (!(GR_BWD32_DIAG & 1)) d = mfma32b(a0, B[s][1], d);
+          d = mfma32b(a0, B[s][0], d);
+        }
+        return d;
+      };
+      // Each side in two passes of two channels, (dC_r, dW) then (dC_g, dC_b): the first pass leaves
+      // p = b_r T_r + T_W per row (the same float operations as fmaf(b_b, T_b, fmaf(b_g, T_g, fmaf(b_r, T_r, T_W)))),
+      // so 32 accumulators and 16 partials are live instead of 64 accumulators.
       {  // T: contraction over x (B = ex), rows y
         s16x8 BT[2][2];
         split2_frag(ex[0], BT[0]);
         split2_frag(ex[1], BT[1]);
-        f32x16 D[4];
+        float p[16];
+        {
+          const f32x16 D0 = contract(0, 0, BT), D3 = contract(0, 3, BT);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const uint4* A0 = sUF + ((0 * 4 + c) * 2 + 0) * 2 * 64;  // (side 0, c, s = 0, piece 0)
-          f32x16 d = {};
-#pragma unroll
-          for (int s = 0; s < 2; ++s) d = mfma32b(as_frag(A0[(s * 2 + 1) * 64 + lane]), BT[s][0], d);
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const s16x8 a0 = as_frag(A0[(s * 2) * 64 + lane]);
-            d = mfma32b(a0, BT[s][1], d);
-            d = mfma32b(a0, BT[s][0], d);
+          for (int i = 0; i < 16; ++i) {
+            S[0] = fmaf(ey[i >> 3][i & 7], D0[i], S[0]);
+            p[i] = fmaf(b.y, D0[i], D3[i]);
           }
-          D[c] = d;
         }
+        GR_BWD32_PHASE();  // keeps the second pass's MFMAs (and their accumulators) after the first pass's epilogue
+        const f32x16 D1 = contract(0, 1, BT), D2 = contract(0, 2, BT);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int s = i >> 3, q = i & 7;
           const float e = ey[s][q], oq = (float)kslot_off(q);
-          const float T0 = D[0][i], T1 = D[1][i], T2 = D[2][i], T3 = D[3][i];
-          S[0] = fmaf(e, T0, S[0]);
-          S[1] = fmaf(e, T1, S[1]);
-          S[2] = fmaf(e, T2, S[2]);
-          const float t = e * fmaf(b.w, T2, fmaf(b.z, T1, fmaf(b.y, T0, T3)));
+          S[1] = fmaf(e, D1[i], S[1]);
+          S[2] = fmaf(e, D2[i], S[2]);
+          const float t = e * fmaf(b.w, D2[i], fmaf(b.z, D1[i], p[i]));
           S4s[s] += t;
           if (q != 0) {  // slot 0 of each K-step is the origin of its moments
             S6c[s] = fmaf(t, oq, S6c[s]);
@@ -2991,30 +3023,24 @@ __global__ __launch_bounds__(256, GR_BWD32_WAVES) void k_bwd32(ViewK v, int n, c
           }
         }
       }
+      GR_BWD32_PHASE();
       {  // R: contraction over y (B = ey), rows x
         s16x8 BR[2][2];
         split2_frag(ey[0], BR[0]);
         split2_frag(ey[1], BR[1]);
-        f32x16 D[4];
+        float p[16];
+        {
+          const f32x16 D0 = contract(1, 0, BR), D3 = contract(1, 3, BR);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const uint4* A0 = sUF + ((1 * 4 + c) * 2 + 0) * 2 * 64;  // (side 1, c, s = 0, piece 0)
-          f32x16 d = {};
-#pragma unroll
-          for (int s = 0; s < 2; ++s) d = mfma32b(as_frag(A0[(s * 2 + 1) * 64 + lane]), BR[s][0], d);
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const s16x8 a0 = as_frag(A0[(s * 2) * 64 + lane]);
-            d = mfma32b(a0, BR[s][1], d);
-            d = mfma32b(a0, BR[s][0], d);
-          }
-          D[c] = d;
+          for (int i = 0; i < 16; ++i) p[i] = fmaf(b.y, D0[i], D3[i]);
         }
+        GR_BWD32_PHASE();
+        const f32x16 D1 = contract(1, 1, BR), D2 = contract(1, 2, BR);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int s = i >> 3, q = i & 7;
           const float oq = (float)kslot_off(q);
-          const float u = ex[s][q] * fmaf(b.w, D[2][i], fmaf(b.z, D[1][i], fmaf(b.y, D[0][i], D[3][i])));
+          const float u = ex[s][q] * fmaf(b.w, D2[i], fmaf(b.z, D1[i], p[i]));
           U0[s] += u;
           if (q != 0) {
             S5c[s] = fmaf(u, oq, S5c[s]);

@@ -150,3 +150,37 @@ def test_tile32_rejected_outside_fit_path(pkg, cuda):
     gv.tile = 24
     with pytest.raises(ValueError, match="tile must be"):
         tr.prepare_native(*t, gv)
+
+
+@pytest.mark.parametrize("opac_range", [(1e-4, 1e-3), (100.0, 3000.0), (3000.0, 6000.0), (0.0, 1e5), "mixed_negative"])
+def test_tile32_f16_operand_range(pkg, cuda, opac_range):
+    """k_fwd32_l1 multiplies on f16 pieces pre-scaled like k_raster_fwd_mfma<4> (f16_sa_of): tiny, huge and mixed
+    large-negative / live opacities stay finite and within the parity bar vs the float64 binned oracle at tile 32."""
+    from test_scale_gpu import _opacities
+
+    tr = pkg.torch_renderer
+    rng = np.random.default_rng(7)
+    sc = orc.synthetic_scene(3000, seed=3, scale=0.05)
+    sc = orc.Scene(sc.means, sc.scales, sc.colors, _opacities(rng, opac_range, sc.opacities.shape))
+    view, proj = orc.orbit_cameras(4, 160, 120)[2]
+    W, H = 160, 120
+    t = [torch.from_numpy(a).to(cuda).contiguous() for a in sc.arrays()]
+    g = torch.Generator(device=cuda).manual_seed(14)
+    target = torch.rand((H, W, 3), generator=g, device=cuda)
+    loss, out, alpha, grads, _ = _fused_view(tr, t, view, proj, W, H, 32, target, None, 0.0, 1.0, cuda)
+    v = orc.make_view(view, proj, W, H, None, cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF, tile=32)
+    o_out, o_alpha, _ = orc.forward(v, sc, binned=True)
+    h_out = out.cpu().numpy().astype(np.float64)
+    g_rgb = (np.sign(h_out - target.cpu().numpy()) / (3 * H * W)).astype(np.float32)
+    ora = orc.backward(v, sc, g_rgb, np.zeros((H, W), np.float32), None, binned=True)
+    errs = {"out": orc.rel_l2(h_out, o_out), "alpha": orc.rel_l2(alpha.cpu().numpy(), o_alpha)}
+    for name, h, o in zip(("d_means", "d_scales", "d_colors", "d_opac"), grads, ora):
+        h = h.cpu().numpy()
+        if name == "d_scales":
+            h, o = h[:, :2], o[:, :2]
+        errs[name] = orc.rel_l2(h, o)
+    live = int((sc.opacities > 0).sum())
+    print(f"opacities {opac_range}: {live} live;", {k: f"{e:.2e}" for k, e in errs.items()})
+    assert live > 0 and np.isfinite(h_out).all() and float(np.abs(h_out).sum()) > 0.0
+    for k, e in errs.items():
+        assert e <= 1e-4, (k, e)
