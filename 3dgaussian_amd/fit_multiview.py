@@ -273,7 +273,10 @@ def hip_render(means, scales, colors, opacities, cam, width, height, background,
 
 
 class ViewShardedFitter:
-    """One fit iteration = render own views, backward, one gradient all-reduce, Adam."""
+    """One fit iteration = render own views, backward, one gradient all-reduce, Adam.
+
+    On the fused path every parameter's ``.grad`` after ``step()`` is a tensor the fitter keeps and overwrites in
+    place on the next step (no allocation per step): copy it to keep a step's gradient."""
 
     def __init__(self, params: dict, cams: list, targets: list, width: int, height: int, lr: float = 0.02,
                  masks: Optional[list] = None, depths: Optional[list] = None, silhouette_weight: float = 0.2,
@@ -463,6 +466,7 @@ class ViewShardedFitter:
                         main = torch.cuda.current_stream(device)
                         with torch.cuda.stream(rs):
                             reg = reg_fn()
+                        reg.record_stream(main)  # allocated on rs, read on main: not reused by rs early
                         main.wait_stream(rs)
                     elif reg_fn:
                         reg = reg_fn()
@@ -725,6 +729,8 @@ class ViewShardedFitter:
         if tail_fn is not None:
             with torch.cuda.stream(prep):
                 tail = tail_fn()
+                if isinstance(tail, torch.Tensor):
+                    tail.record_stream(main)  # allocated on the preparation stream, read on main
         for st in streams[1:]:
             main.wait_stream(st)
         main.wait_stream(prep)
@@ -888,6 +894,8 @@ class ViewShardedFitter:
                         self._grad_keep = {}
                     self._grad_keep[k] = kept = torch.empty_like(p)
                 grad = kept
+            # p.grad is this kept tensor, overwritten in place every step (an alias, not a fresh tensor): a caller that
+            # keeps a reference to p.grad across steps (logging, clipping history, EMA) must copy it
             p.grad = grad
             r = reg.get(k, 0.0) if self.rank == 0 else 0.0
 

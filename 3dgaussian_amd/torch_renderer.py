@@ -27,6 +27,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import os
+import threading
 import weakref
 from dataclasses import dataclass
 from typing import Optional
@@ -66,12 +67,51 @@ LAZY_DEPTH = os.environ.get("GR_LAZY_DEPTH", "1") != "0"
 # a render that receives no depth gradient switches back to lazy.  Results are the eager mode's (within the parity
 # bar of the lazy ones).  GR_LAZY_ADAPT=0 never adapts.
 LAZY_ADAPT = max(0, int(os.environ.get("GR_LAZY_ADAPT", "2")))
-_LAZY = {"rerenders": 0, "eager": False}
+# What the op adapts to is kept per CALLER, keyed by the caller's means tensor (a fit's parameter: the same object
+# across its iterations; the reference loop passes params["means"] itself, fit_multiview_stub.py:268): the adaptive
+# laziness above and the Morton layout's permutation (below).  Two fits interleaved on one process (one with a depth
+# loss, one without) therefore never change each other's renders: each gets exactly what it gets alone.  Within one
+# caller the rounding of depth_grad=True renders does depend on its own history (lazy for its first LAZY_ADAPT
+# iterations, f32 grade after), within the parity bar either way; GR_LAZY_ADAPT=0 makes it history-free.
+# Every piece of module state (callers, the speculation pipelines per device) is guarded by one lock.
+_LOCK = threading.RLock()
+
+
+class _Caller:
+    __slots__ = ("rerenders", "eager", "layout", "perm")
+
+    def __init__(self):
+        self.rerenders, self.eager, self.layout, self.perm = 0, False, None, None
+
+
+_CALLERS: dict = {}  # id(means) -> (weakref(means), _Caller)
+
+
+def _caller_of(means: torch.Tensor) -> _Caller:
+    with _LOCK:
+        e = _CALLERS.get(id(means))
+        if e is not None and e[0]() is means:
+            return e[1]
+        if len(_CALLERS) >= 256:  # forget callers whose tensors are gone
+            for k in [k for k, (r, _) in _CALLERS.items() if r() is None]:
+                del _CALLERS[k]
+        c = _Caller()
+        _CALLERS[id(means)] = (weakref.ref(means), c)
+        return c
+
+
+def lazy_eager(means: torch.Tensor) -> bool:
+    """Whether adaptive laziness renders this caller's depth_grad=True views at f32 grade up front."""
+    with _LOCK:
+        e = _CALLERS.get(id(means))
+        return bool(e is not None and e[0]() is means and e[1].eager)
 
 
 def reset_lazy_depth() -> None:
-    """Forget what adaptive laziness learned (a new loop / loss)."""
-    _LAZY["rerenders"], _LAZY["eager"] = 0, False
+    """Forget what adaptive laziness learned, for every caller (a new loop / loss)."""
+    with _LOCK:
+        for _, c in _CALLERS.values():
+            c.rerenders, c.eager = 0, False
 
 
 def default_cutoff(depth_grad: bool = True) -> float:
@@ -710,13 +750,14 @@ def _grad_background(st: RenderState, background: torch.Tensor, g_out: torch.Ten
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means, scales, colors, opacities, background, view, proj, gv, prepared, gv_depth=None,
-                bin_stream=None, layout=None, adapted=False):
+                bin_stream=None, layout=None, adapted=False, caller=None):
         """view / proj: the camera tensors (their gradients, gr_bwd_camera) or None; the render itself uses gv's
         host copy of them.  gv_depth: the f32-grade view a lazily rendered gv (two-piece mode) re-renders with
         when a depth gradient arrives (LAZY_DEPTH), else None.  bin_stream: see forward_native.  layout: a
         _Layout of the inputs (their Morton-ordered copy, rendered instead; the gradients return in the inputs'
         order), or None."""
-        caller = (means, scales, colors, opacities) if layout is not None else (None,) * 4
+        ctx.caller = caller  # the caller's adaptive state (_Caller) or None
+        callers_t = (means, scales, colors, opacities) if layout is not None else (None,) * 4
         if layout is not None:
             means, scales, colors, opacities = layout.tensors
         out, alpha, depth, st = forward_native(means, scales, colors, opacities, gv, prepared, bin_stream=bin_stream)
@@ -729,7 +770,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         # the render state's device buffers are saved tensors: autograd releases them after this node's backward
         # unless the graph is retained (a second backward through it then finds them)
         ctx.save_for_backward(means, scales, colors, opacities, background, view, proj, st.geom, st.bins, st.saved,
-                              layout.index if layout is not None else None, *caller)
+                              layout.index if layout is not None else None, *callers_t)
         return out, alpha, depth
 
     @staticmethod
@@ -748,11 +789,14 @@ class _RasterizeGaussians(torch.autograd.Function):
             # lazy default: the depth is differentiated after all - re-render at f32 grade with the
             # depth-gradient footprint and differentiate that render
             _, _, _, st = forward_native(means, scales, colors, opacities, ctx.gv_depth, images=False)
-            _LAZY["rerenders"] += 1
-            if LAZY_ADAPT and _LAZY["rerenders"] >= LAZY_ADAPT:
-                _LAZY["eager"] = True
-        elif g_depth is None and (ctx.gv_depth is not None or ctx.adapted):
-            _LAZY["rerenders"], _LAZY["eager"] = 0, False  # this loss has no depth term (any more)
+            if ctx.caller is not None:
+                with _LOCK:
+                    ctx.caller.rerenders += 1
+                    if LAZY_ADAPT and ctx.caller.rerenders >= LAZY_ADAPT:
+                        ctx.caller.eager = True
+        elif g_depth is None and (ctx.gv_depth is not None or ctx.adapted) and ctx.caller is not None:
+            with _LOCK:
+                ctx.caller.rerenders, ctx.caller.eager = 0, False  # this loss has no depth term (any more)
         need_view, need_proj = ctx.needs_input_grad[5], ctx.needs_input_grad[6]
         # with a layout: the chain rule in the caller's order (its tensors; the rendered copy's sums gathered by index)
         dm, ds, dc, do, ws = backward_native(*(caller if index is not None else (means, scales, colors, opacities)), st,
@@ -762,7 +806,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         if need_view or need_proj:
             d = camera_grad_native(means, scales, colors, opacities, st, ws, g_depth is not None)
             dview, dproj = _camera_grads(d, view, proj, need_view, need_proj, colors.dim() == 3)
-        return dm, ds, dc, do, dbg, dview, dproj, None, None, None, None, None, None
+        return dm, ds, dc, do, dbg, dview, dproj, None, None, None, None, None, None, None
 
 
 def _device_inputs(means, scales, colors, opacities):
@@ -825,7 +869,16 @@ class _Speculation:
                                        for r, t, v in zip(self.refs, tensors, self.versions))
 
 
-_SPEC: dict = {"last": None, "next": {}, "views": {}, "cold": set(), "pipe": [], "hits": 0, "misses": 0}
+# hit / miss counters over all devices; the learned camera order and the pipeline per device (_spec_of)
+_SPEC: dict = {"hits": 0, "misses": 0}
+
+
+def _spec_of(dev: torch.device) -> dict:
+    key = ("dev", str(dev))
+    d = _SPEC.get(key)
+    if d is None:
+        d = _SPEC[key] = {"last": None, "next": {}, "views": {}, "cold": set(), "pipe": [], "stream": None}
+    return d
 
 
 def _view_key(gv: _native.GrView) -> tuple:
@@ -835,17 +888,18 @@ def _view_key(gv: _native.GrView) -> tuple:
 def _spec_take(key, tensors) -> Optional[Prepared]:
     """The speculative preparation of this view, if the pipeline's head is exactly these inputs; then the
     next entry is binned on the speculation stream (before this view's kernels are enqueued)."""
-    pipe = _SPEC["pipe"]
+    D = _spec_of(tensors[0].device)
+    pipe = D["pipe"]
     if not pipe:
         return None
     sp = pipe.pop(0)
     if not sp.matches(key, tensors):
         _SPEC["misses"] += 1
-        _SPEC["cold"].add((sp.src, sp.key))
+        D["cold"].add((sp.src, sp.key))
         pipe.clear()
         return None
     _SPEC["hits"] += 1
-    _SPEC["cold"].discard((sp.src, key))
+    D["cold"].discard((sp.src, key))
     if pipe and pipe[0].prepared.rendered is None and (SPEC_RENDER or (SPEC_BIN and pipe[0].prepared.binned is None)):
         nx = pipe[0].prepared
         dev = tensors[0].device
@@ -857,30 +911,31 @@ def _spec_take(key, tensors) -> Optional[Prepared]:
 
 
 def _spec_stream(dev: torch.device) -> "torch.cuda.Stream":
-    st = _SPEC.get(("stream", str(dev)))
-    if st is None:
-        st = _SPEC[("stream", str(dev))] = torch.cuda.Stream(dev)
-    return st
+    D = _spec_of(dev)
+    if D["stream"] is None:
+        D["stream"] = torch.cuda.Stream(dev)
+    return D["stream"]
 
 
 def _spec_after(key, gv, tensors, inputs_ready) -> None:
     """Learn the camera order and fill the pipeline with the cameras expected next: their preparations on a
     stream of their own that waits only for the input tensors (``inputs_ready``, recorded before this
     view's kernels), so they run beside this view's render."""
-    last = _SPEC["last"]
+    D = _spec_of(tensors[0].device)
+    last = D["last"]
     if last is not None:
-        _SPEC["next"][last] = key
-    _SPEC["last"] = key
-    _SPEC["views"][key] = gv
-    if len(_SPEC["views"]) > 4096:
-        _SPEC["views"].clear()
-        _SPEC["next"].clear()
-    pipe = _SPEC["pipe"]
+        D["next"][last] = key
+    D["last"] = key
+    D["views"][key] = gv
+    if len(D["views"]) > 4096:
+        D["views"].clear()
+        D["next"].clear()
+    pipe = D["pipe"]
     ps = None
     while len(pipe) < SPEC_DEPTH:
         src = pipe[-1].key if pipe else key
-        nxt = _SPEC["next"].get(src)
-        if nxt is None or (src, nxt) in _SPEC["cold"] or nxt == key:
+        nxt = D["next"].get(src)
+        if nxt is None or (src, nxt) in D["cold"] or nxt == key:
             return
         if ps is None:
             ps = _spec_stream(tensors[0].device)
@@ -888,7 +943,7 @@ def _spec_after(key, gv, tensors, inputs_ready) -> None:
             for t in tensors:  # read on ps: not reused by the allocator before ps is done with them
                 t.record_stream(ps)
         with torch.cuda.stream(ps):
-            pv = prepare_native(*tensors, _SPEC["views"][nxt])
+            pv = prepare_native(*tensors, D["views"][nxt])
         pipe.append(_Speculation(nxt, tensors, pv, src))
 
 
@@ -920,24 +975,21 @@ class _Layout:
         return all(r() is t and t._version == v for r, t, v in zip(self.refs, inputs, self.versions))
 
 
-_LAYOUT: dict = {"entry": None, "perm": None}
-
-
-def _layout_of(m, s, c, o) -> _Layout:
-    """The Morton-ordered copy of these input tensors (cached: one entry)."""
-    e = _LAYOUT["entry"]
+def _layout_of(caller: _Caller, m, s, c, o) -> _Layout:
+    """The Morton-ordered copy of these input tensors (cached: one entry per caller)."""
+    e = caller.layout
     if e is not None and e.matches((m, s, c, o)):
         return e
-    pc = _LAYOUT["perm"]  # [weakref(means), n, perm int64, inverse int32, uses]
+    pc = caller.perm  # [weakref(means), n, perm int64, inverse int32, uses]
     if pc is None or pc[0]() is not m or pc[1] != m.shape[0] or pc[4] >= LAYOUT_EVERY:
         perm = spatial.morton_order(m)
         inv = torch.empty_like(perm, dtype=torch.int32)
         inv[perm] = torch.arange(perm.numel(), dtype=torch.int32, device=perm.device)
-        pc = _LAYOUT["perm"] = [weakref.ref(m), m.shape[0], perm, inv, 0]
+        pc = caller.perm = [weakref.ref(m), m.shape[0], perm, inv, 0]
     pc[4] += 1
     with torch.no_grad():
         tensors = tuple(t.detach().index_select(0, pc[2]).contiguous() for t in (m, s, c, o))
-    e = _LAYOUT["entry"] = _Layout((m, s, c, o), tensors, pc[3])
+    e = caller.layout = _Layout((m, s, c, o), tensors, pc[3])
     return e
 
 
@@ -955,12 +1007,21 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
             background = torch.zeros(3, dtype=torch.float32, device=dev)
         return cpu_renderer.render(means, scales, colors, opacities, view, proj, width, height,
                                    background.to(dtype=torch.float32, device=dev))
+    with _LOCK:  # the op's adaptive state (per caller) and speculation pipeline (per device)
+        return _rasterize_hip(means, scales, colors, opacities, view, proj, width, height, background, cutoff, prepared,
+                              core_cutoff, depth_grad)
+
+
+def _rasterize_hip(means, scales, colors, opacities, view, proj, width, height, background, cutoff, prepared,
+                   core_cutoff, depth_grad):
+    dev = means.device
+    caller = _caller_of(means)
     m, s, c, o = _device_inputs(means, scales, colors, opacities)
     if background is None:
         background = _default_background(dev)
     background = background.to(dtype=torch.float32, device=dev).reshape(3).contiguous()
     gv_depth = None
-    adapted = depth_grad is True and not _eager(depth_grad) and cutoff is None and _LAZY["eager"]
+    adapted = depth_grad is True and not _eager(depth_grad) and cutoff is None and caller.eager
     if depth_grad is True and not _eager(depth_grad) and cutoff is None and not adapted:
         # lazy default: two-piece render with the no-depth-gradient footprint now, f32 grade only if needed
         gv_depth = make_view(view, proj, width, height, background, None, core_cutoff, True)
@@ -976,11 +1037,13 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
     cam_v = view if isinstance(view, torch.Tensor) and view.requires_grad else None
     cam_p = proj if isinstance(proj, torch.Tensor) and proj.requires_grad else None
     if prepared is not None:  # a preparation made by prepare_view is of the caller's own order: render that
-        return _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, prepared, gv_depth, None, None, adapted)
+        return _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, prepared, gv_depth, None, None, adapted,
+                                         caller)
     # the rendered tensors: the Morton-ordered copy of the inputs
-    layout = _layout_of(m, s, c, o) if LAYOUT and m.shape[0] >= LAYOUT_MIN else None
+    layout = _layout_of(caller, m, s, c, o) if LAYOUT and m.shape[0] >= LAYOUT_MIN else None
     if not SPECULATE:
-        return _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, None, gv_depth, None, layout, adapted)
+        return _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, None, gv_depth, None, layout, adapted,
+                                         caller)
     rt = layout.tensors if layout is not None else (m, s, c, o)
     key = _view_key(gv)
     pv = _spec_take(key, rt)
@@ -990,7 +1053,7 @@ def rasterize(means, scales, colors, opacities, view, proj, width, height, backg
         pv.geom.record_stream(stream)
     ready = torch.cuda.Event()
     ready.record(stream)
-    res = _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, pv, gv_depth, None, layout, adapted)
+    res = _RasterizeGaussians.apply(m, s, c, o, background, cam_v, cam_p, gv, pv, gv_depth, None, layout, adapted, caller)
     _spec_after(key, gv, rt, ready)
     return res
 

@@ -57,6 +57,7 @@ N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr
 from __future__ import annotations
 
 import argparse
+import ctypes
 import importlib
 import json
 import math
@@ -97,6 +98,15 @@ BF16_FLOP_PER_CORE_PAIR_FWD = 4 * 3 * MFMA_16x16x32 / 32
 BF16_FLOP_PER_TAIL_PAIR_FWD = 1 * 3 * MFMA_16x16x32 / 32
 FWD_KERNEL = "k_raster_fwd_mfma"
 BWD_KERNEL = "k_raster_bwd_bf16"
+# The same at 32-pixel tiles (gr_view.tile = 32, the fit path's default: k_fwd32_l1 / k_bwd32): per pair
+#   backward f32-equivalent 2 sides x 4 channels x 32 rows x 32 (K) x 2 = 16,384; executed 48 v_mfma_f32_32x32x16_bf16
+#   per 32 pairs (2 sides x 4 channels x 2 K-steps x 3 piece products) = 49,152 FLOP per pair;
+#   forward f32-equivalent 4 channels x 32 x 32 x 2 = 8,192; executed 12 v_mfma_f32_32x32x16_f16 per 16 pairs
+#   (4 channels x 3 products) = 24,576 FLOP per pair.
+F32_FLOP_PER_PAIR_BWD32 = 2 * 4 * 32 * 32 * 2
+MFMA_FLOP_PER_PAIR_BWD32 = 48 * MFMA_32x32x16 / 32
+F32_FLOP_PER_PAIR_FWD32 = 4 * 32 * 32 * 2
+MFMA_FLOP_PER_PAIR_FWD32 = 12 * MFMA_32x32x16 / 16
 # SURVEY.md §8(d) HBM model of the tile-binned algorithm (the north_star's "fraction of the HBM
 # roofline" framing): bytes per view = N (3 B_in + 2 x 36) + K (2 x 12 + 2 x 36 + 2 x 36) + 60 H W
 # with B_in = 40 (RGB), K = pairs per view as binned here.
@@ -190,16 +200,38 @@ def _cpu_op_fwd_bwd(n: int, res: int, views: int, nviews: int, sample: int = 0) 
     return time.perf_counter() - t0
 
 
+def usable_cores() -> tuple:
+    """(cores this process may run on, how that was found): the CPU affinity mask, capped by the cgroup's CPU quota
+    when one is set (a GPU box's share of a many-core host shows there, not in os.cpu_count())."""
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    how = f"sched_getaffinity {cores}"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, math.ceil(int(quota) / int(period)))
+            how += f", cgroup cpu.max quota {q}"
+            cores = min(cores, q)
+    except (OSError, ValueError):
+        pass
+    return cores, how
+
+
 def cpu_baseline(n: int, res: int, views: int) -> dict:
     """The build's CPU op (cpu_renderer.py, torch on the host cores: the reference's dense semantics) on ONE
-    view of the workload (fwd + bwd), plus config C1 through the same op and the float64 oracle port."""
+    whole view of the workload (all n Gaussians, fwd + bwd, unscaled), torch and OpenMP on every usable core; plus
+    config C1 through the same op and the float64 oracle port."""
     from oracle import oracle as orc
 
-    threads = torch.get_num_threads()
-    sub = min(n, 250_000)  # a bounded sample (~15 s): a quarter of the Gaussians, scaled linearly to all n
-    dt = _cpu_op_fwd_bwd(n, res, views, 1, sub) * (n / sub)
-    c1 = _cpu_op_fwd_bwd(1200, 128, 4, 4)
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    cores, how = usable_cores()
+    saved = torch.get_num_threads()
+    torch.set_num_threads(cores)
+    try:
+        threads = torch.get_num_threads()
+        dt = _cpu_op_fwd_bwd(n, res, views, 1)
+        c1 = _cpu_op_fwd_bwd(1200, 128, 4, 4)
+    finally:
+        torch.set_num_threads(saved)
     scene = orc.synthetic_scene(n, seed=0)
     view, proj = orc.orbit_cameras(views, res, res)[0]
     v = orc.make_view(view, proj, res, res, cutoff=tr.default_cutoff(False), core_cutoff=tr.DEFAULT_CORE_CUTOFF)
@@ -209,16 +241,15 @@ def cpu_baseline(n: int, res: int, views: int) -> dict:
     orc.backward(v, scene, gr, None, None, binned=True)
     dto = time.perf_counter() - t0
     return {"value": round(res * res / dt / 1e6, 5), "unit": "Mpixels/sec fwd+bwd", "cores": threads, "kind": "port",
-            "host_cpu_count": os.cpu_count(), "torch_threads": threads,
-            "sample": f"1 view of the workload at {res}x{res} fwd+bwd through render_gaussians_torch on host tensors "
-                      f"(cpu_renderer.py, dense: every Gaussian at every pixel, as the reference), torch with {threads} "
-                      f"threads, timed on {sub} of the {n} Gaussians ({dt * sub / n:.1f} s) and scaled by {n / sub:g} "
-                      f"(the dense op's cost is linear in the Gaussian count)",
+            "host_cpu_count": os.cpu_count(), "usable_cores": cores, "usable_cores_from": how, "torch_threads": threads,
+            "sample": f"1 whole view of the workload ({n} Gaussians, {res}x{res}) fwd+bwd through render_gaussians_torch on "
+                      f"host tensors (cpu_renderer.py, dense: every Gaussian at every pixel, as the reference), torch with "
+                      f"{threads} threads, {dt:.1f} s, unscaled",
             "c1": {"value": round(4 * 128 * 128 / c1 / 1e6, 4), "unit": "Mpixels/sec fwd+bwd", "threads": threads,
                    "sample": f"config C1: 1200 Gaussians, 4 views 128x128, one fit step's fwd+bwd through the same op, "
                              f"{c1:.2f} s"},
-            "oracle": {"value": round(res * res / dto / 1e6, 5), "unit": "Mpixels/sec fwd+bwd", "cores": cores,
-                       "sample": f"1 view of the workload, oracle/gr_oracle.c binned float64 fwd+bwd, OpenMP {cores} "
+            "oracle": {"value": round(res * res / dto / 1e6, 5), "unit": "Mpixels/sec fwd+bwd", "cores": omp,
+                       "sample": f"1 view of the workload, oracle/gr_oracle.c binned float64 fwd+bwd, OpenMP {omp} "
                                  f"threads, {dto:.1f} s"}}
 
 
@@ -337,19 +368,64 @@ def psnr_vs_ref(fitter, cams, R: int, device, npix: int = 2048) -> dict:
     return res
 
 
-def pairs_per_view(fitter, cams, R, cutoff, core_cutoff):
-    """Mean (pairs, core pairs) per view of this rank's views at the given footprint (the same
-    binning kernels as the render; no splat)."""
-    pairs, core = [], []
+def splat_replay(fitter, device) -> dict:
+    """The fit path's two splat kernels timed on their own: every view of this rank prepared and binned first
+    (untimed), then its forward splat (gr_fwd_render_l1 on the binned view) launched once per view back to back on
+    one stream between two HIP events, then its backward splat (gr_bwd_splat) the same way.  One launch per view, in
+    view order, is what a single-stream step runs (GR_STREAMS=1), so the averages compare with a rocprofv3
+    kernel-trace summary of the bench run under GR_STREAMS=1 (profiles/); a splat launched before the first event keeps
+    the GPU busy while the timed launches are submitted, so no host gap lands inside the events."""
+    L = tr._native.lib()
+    nat = tr._native
     with torch.no_grad():
-        means, scales, colors, opac = fm.activations(fitter.params)
-        m, s, c, o = (t.contiguous() for t in (means, scales, colors, opac))
-        for i in fitter.my_views:
-            gv = tr.make_view(cams[i].view, cams[i].proj, R, R, None, cutoff, core_cutoff)
-            plan = tr.prepare_native(m, s, c, o, gv).plan()
-            pairs.append(int(plan.num_pairs))
-            core.append(int(plan.num_core_pairs))
-    return float(np.mean(pairs)), float(np.mean(core))
+        acts = [a.detach().float().contiguous() for a in fm.activations(fitter.params)]
+    n = int(acts[0].shape[0])
+    cur = torch.cuda.current_stream(device)
+    sp = ctypes.c_void_p(cur.cuda_stream)
+    V = max(len(fitter.targets), 1)
+    w_sil = fitter.w_sil if fitter.masks is not None else 0.0
+    views = []
+    for i in fitter.my_views:
+        gv = fitter._fit_view(i, device)
+        prep = tr.prepare_native(*acts, gv)
+        plan = prep.plan()
+        bins, scratch, bgv, done = tr._bin_launch(L, gv, n, plan, prep, cur, device)
+        ws = torch.empty((tr._ws_round(L.gr_bwd_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8,
+                         device=device)
+        loss = torch.zeros(1, device=device)
+        mask = fitter.masks[i] if fitter.masks is not None else None
+        views.append((gv, bgv, plan, prep.geom, bins, scratch, ws, loss, fitter.targets[i], mask))
+
+    def fwd(v):
+        gv, bgv, plan, geom, bins, scratch, ws, loss, tgt, mask = v
+        nat.check(L.gr_fwd_render_l1(ctypes.byref(bgv), n, ctypes.byref(plan), nat.ptr(geom), nat.ptr(bins), bins.numel(),
+                                     nat.ptr(scratch), scratch.numel(), nat.ptr(tgt), nat.ptr(mask), ctypes.c_float(w_sil),
+                                     ctypes.c_float(1.0 / V), nat.ptr(loss), None, None, nat.ptr(ws), ws.numel(), sp),
+                  "gr_fwd_render_l1")
+
+    def bwd(v):
+        gv, bgv, plan, geom, bins, scratch, ws = v[:7]
+        nat.check(L.gr_bwd_splat(ctypes.byref(gv), n, ctypes.byref(plan), nat.ptr(geom), nat.ptr(bins), nat.ptr(ws),
+                                 ws.numel(), sp), "gr_bwd_splat")
+
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    torch.cuda.synchronize()
+    fwd(views[0])
+    ev[0].record(cur)
+    for v in views:
+        fwd(v)
+    ev[1].record(cur)
+    for v in views:
+        bwd(v)
+    ev[2].record(cur)
+    torch.cuda.synchronize()
+    k = len(views)
+    pairs = [int(v[2].num_pairs) for v in views]
+    out = {"fwd_us": 1e3 * ev[0].elapsed_time(ev[1]) / k, "bwd_us": 1e3 * ev[1].elapsed_time(ev[2]) / k, "launches": k,
+           "pairs": float(np.mean(pairs)), "tile": int(views[0][0].tile) or 16}
+    del views
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -435,8 +511,11 @@ def main():
     sync()
     prof = pkg._native.profile_end()
     fm.NUM_STREAMS = streams_saved
-    # the fit step renders its views through the fused path: one zone at FIT_CUTOFF (fit_multiview._views_direct)
-    avg_pairs, avg_core = pairs_per_view(fitter, cams, R, tr.FIT_CUTOFF, tr.FIT_CUTOFF)
+    # the splat kernels' launch durations for the roofline: replayed once per view back to back (splat_replay)
+    replay = splat_replay(fitter, device) if rank == 0 else None
+    # the fit step renders its views through the fused path: one zone at FIT_CUTOFF (fit_multiview._views_direct), at
+    # the fit's tile size; the replay's plans are those views'
+    avg_pairs = avg_core = replay["pairs"] if replay else 0.0
 
     # the default precision mode: what a caller with a depth loss gets (f32-grade W / D, three-piece
     # backward with the tail pairs): the same fit with a depth term in the loss (C3's losses)
@@ -474,46 +553,58 @@ def main():
         drop_depth = dropin_op(n, V, R, steps=2, warmup=2, device=device, depth_loss=True)
 
     if rank == 0:
-        bwd_ms, bwd_n = prof["raster_bwd"]
-        fwd_ms, fwd_n = prof["raster_fwd"]
         bwd_conc_us = 1e3 * prof_concurrent["raster_bwd"][0] / max(prof_concurrent["raster_bwd"][1], 1)
         fwd_conc_us = 1e3 * prof_concurrent["raster_fwd"][0] / max(prof_concurrent["raster_fwd"][1], 1)
-        bwd_avg_s = bwd_ms / max(bwd_n, 1) / 1e3
-        fwd_avg_s = fwd_ms / max(fwd_n, 1) / 1e3
+        bwd_avg_s = replay["bwd_us"] / 1e6
+        fwd_avg_s = replay["fwd_us"] / 1e6
         pmc = pmc_table()
-        avg_tail = avg_pairs - avg_core
         px = R * R
+        t32 = replay["tile"] == 32
         # SURVEY.md 8(d) per-unit bytes: a pair = 12 B key/value + 36 B projected record read once per
         # splat pass; the backward also writes its 36 B of gradient partials; per pixel 20 B of outputs
         # + 20 B of saved state written (forward) / 20 B of upstream grads + 20 B saved read (backward)
         kernels = {
-            "fwd": dict(kernel=FWD_KERNEL, variant="k_raster_fwd_mfma<4>", t=fwd_avg_s, n=fwd_n, conc_us=fwd_conc_us, units=avg_pairs,
-                        unit_bytes=12 + 36, px_bytes=40,
-                        units_desc="pairs per launch",
-                        flop=BF16_FLOP_PER_CORE_PAIR_FWD * avg_core + BF16_FLOP_PER_TAIL_PAIR_FWD * avg_tail,
-                        f32=F32_FLOP_PER_CORE_PAIR_FWD * avg_core + F32_FLOP_PER_TAIL_PAIR_FWD * avg_tail),
-            "bwd": dict(kernel=BWD_KERNEL, variant="k_raster_bwd_bf16<false,2>", t=bwd_avg_s, n=bwd_n, conc_us=bwd_conc_us, units=avg_core,
-                        unit_bytes=12 + 36 + 36, px_bytes=40,
-                        units_desc="core pairs per launch (no upstream depth gradient: tail pairs skipped)",
-                        flop=BF16_FLOP_PER_CORE_PAIR_BWD * avg_core, f32=F32_FLOP_PER_CORE_PAIR_BWD * avg_core),
+            "fwd": dict(variant="k_fwd32_l1" if t32 else "k_raster_fwd_mfma<4>", t=fwd_avg_s, conc_us=fwd_conc_us,
+                        units=avg_pairs, unit_bytes=12 + 36, px_bytes=40, units_desc="pairs per launch",
+                        flop=(MFMA_FLOP_PER_PAIR_FWD32 if t32 else BF16_FLOP_PER_CORE_PAIR_FWD) * avg_pairs,
+                        f32=(F32_FLOP_PER_PAIR_FWD32 if t32 else F32_FLOP_PER_CORE_PAIR_FWD) * avg_pairs),
+            "bwd": dict(variant="k_bwd32" if t32 else "k_raster_bwd_bf16<false,2>", t=bwd_avg_s, conc_us=bwd_conc_us,
+                        units=avg_pairs, unit_bytes=12 + 36 + 36, px_bytes=40, units_desc="pairs per launch",
+                        flop=(MFMA_FLOP_PER_PAIR_BWD32 if t32 else BF16_FLOP_PER_CORE_PAIR_BWD) * avg_pairs,
+                        f32=(F32_FLOP_PER_PAIR_BWD32 if t32 else F32_FLOP_PER_CORE_PAIR_BWD) * avg_pairs),
         }
+        timing = (f"HIP events around {replay['launches']} launches (one per view, back to back on one stream, after the "
+                  f"timed region; splat_replay); compare the GR_STREAMS=1 rocprofv3 kernel-trace summary in profiles/")
 
         def roof(k):
+            """The kernel against the bound that binds it: the MFMA pipe (executed 16-bit MFMA FLOP/s vs the dense
+            bf16 peak; the split operands make it execute 3x the f32-equivalent contraction) - at 32-pixel tiles the
+            splats do 4x the pixel work per pair on half the pairs, so their HBM traffic per pixel halves and the
+            per-pair HBM model (under "hbm") no longer bounds them."""
             e = kernels[k]
             nbytes = e["unit_bytes"] * e["units"] + e["px_bytes"] * px
             t = e["t"] if e["t"] > 0 else float("inf")  # a launch left out (GR_DEBUG_SKIP variant builds)
             ach = nbytes / t / 1e9
             mf = e["flop"] / t / 1e12
             pk = pmc_of(pmc, e["variant"])
+            hbm = {"achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                   "algorithmic_bytes_per_launch": int(nbytes),
+                   "bytes_model": f"{e['unit_bytes']} B x {e['units_desc']} ({int(e['units'])}) + {e['px_bytes']} B x {px} px",
+                   "traffic": pk.get("hbm_bytes_per_launch")}
+            if t32:
+                return {"bound": "mfma", "kernel": e["variant"], "achieved": round(mf, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(mf / BF16_MFMA_PEAK_TFLOPS, 4), "traffic": pk.get("hbm_bytes_per_launch"),
+                        "valu_frac": pk.get("valu_frac"), "mfma_frac": pk.get("mfma_frac"),
+                        "executed_flop_per_launch": int(e["flop"]), "f32_equivalent_tflops": round(e["f32"] / t / 1e12, 1),
+                        "f32_peak": F32_MFMA_PEAK_TFLOPS, "hbm": hbm,
+                        "avg_launch_us": round(e["t"] * 1e6, 1), "launches": replay["launches"], "timing": timing,
+                        "avg_launch_us_multi_stream": round(e["conc_us"], 1), "streams_in_timed_region": streams_saved}
             return {"bound": "hbm", "kernel": e["variant"], "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": pk.get("hbm_bytes_per_launch"),
                     "valu_frac": pk.get("valu_frac"), "mfma_frac": pk.get("mfma_frac"),
-                    "valu_per_32_pair_step": pk.get("valu_per_12_mfma"),
-                    "algorithmic_bytes_per_launch": int(nbytes),
-                    "bytes_model": f"{e['unit_bytes']} B x {e['units_desc']} ({int(e['units'])}) + {e['px_bytes']} B x {px} px",
-                    "avg_launch_us": round(e["t"] * 1e6, 1), "launches": e["n"],
-                    "timing": "HIP events on the launch stream, one single-stream step after the timed region",
+                    "algorithmic_bytes_per_launch": int(nbytes), "bytes_model": hbm["bytes_model"],
+                    "avg_launch_us": round(e["t"] * 1e6, 1), "launches": replay["launches"], "timing": timing,
                     "avg_launch_us_multi_stream": round(e["conc_us"], 1), "streams_in_timed_region": streams_saved,
                     "mfma": {"executed_bf16_tflops": round(mf, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
                              "frac": round(mf / BF16_MFMA_PEAK_TFLOPS, 4),
@@ -543,6 +634,7 @@ def main():
             "data": "synthetic (seeded Gaussians per SURVEY.md 8(d), random targets)",
             "config": {"workload": f"C4: {n} Gaussians, {V} orbit views {R}x{R}, fwd+bwd+grad all-reduce+Adam per step",
                        "gaussians": n, "views": V, "width": R, "height": R, "cutoff_sigma": tr.FIT_CUTOFF, "core_cutoff_sigma": tr.FIT_CUTOFF,
+                       "tile": replay["tile"],
                        "render_path": "fused fit path: per view gr_fwd_render_l1 (forward, loss and upstream gradients) "
                                       "+ gr_bwd_splat + gr_gather_view (per-Gaussian sums), then gr_reduce_sums (chain rule) "
                                       "per batch of a stream's views (fit_multiview._views_direct, 4 HIP streams)",
