@@ -232,6 +232,7 @@ def cpu_baseline(n: int, res: int, views: int) -> dict:
         c1 = _cpu_op_fwd_bwd(1200, 128, 4, 4)
     finally:
         torch.set_num_threads(saved)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0")) or cores  # the oracle's OpenMP threads
     scene = orc.synthetic_scene(n, seed=0)
     view, proj = orc.orbit_cameras(views, res, res)[0]
     v = orc.make_view(view, proj, res, res, cutoff=tr.default_cutoff(False), core_cutoff=tr.DEFAULT_CORE_CUTOFF)

@@ -136,3 +136,16 @@ def test_fit_driver_on_cpu_reproduces_reference_curve(pkg, tmp_path):
              "--prune_interval", str(int(d["densify_interval"])), "--seed", str(int(d["seed"])), "--device", "cpu"])
     losses = np.array([float(x) for x in (tmp_path / "loss.txt").read_text().split()])
     np.testing.assert_allclose(losses, d["losses"], rtol=1e-4)
+
+
+def test_bench_cpu_baseline_small():
+    """bench.cpu_baseline on a small scene (the leg the GPU bench runs at C4 on every usable core): the keys the bench
+    line carries, the thread count equal to the usable cores."""
+    import importlib
+
+    bench = importlib.import_module("bench")
+    cores, how = bench.usable_cores()
+    out = bench.cpu_baseline(2000, 48, 2)
+    assert out["value"] > 0 and out["kind"] == "port" and out["oracle"]["value"] > 0 and out["c1"]["value"] > 0
+    assert out["usable_cores"] == cores and out["torch_threads"] == cores and out["cores"] == cores
+    assert "sched_getaffinity" in how and "unscaled" in out["sample"]
