@@ -370,12 +370,12 @@ def psnr_vs_ref(fitter, cams, R: int, device, npix: int = 2048) -> dict:
 
 
 def splat_replay(fitter, device) -> dict:
-    """The fit path's two splat kernels timed on their own: every view of this rank prepared and binned first
-    (untimed), then its forward splat (gr_fwd_render_l1 on the binned view) launched once per view back to back on
-    one stream between two HIP events, then its backward splat (gr_bwd_splat) the same way.  One launch per view, in
-    view order, is what a single-stream step runs (GR_STREAMS=1), so the averages compare with a rocprofv3
-    kernel-trace summary of the bench run under GR_STREAMS=1 (profiles/); a splat launched before the first event keeps
-    the GPU busy while the timed launches are submitted, so no host gap lands inside the events."""
+    """The fit path's two splat kernels timed on their own, in a single-stream schedule of this rank's views: per view
+    its binning (untimed), then its forward splat (gr_fwd_render_l1 on the binned view) and backward splat
+    (gr_bwd_splat), each between two HIP events on the stream.  Every preparation is enqueued first and the host never
+    waits inside the loop, so the GPU runs the launches back to back (no host gap inside an event pair) with the
+    caches as a single-stream step leaves them (binning -> forward -> backward of the same view): the averages compare
+    with a rocprofv3 kernel-trace summary of the bench under GR_STREAMS=1 (profiles/)."""
     L = tr._native.lib()
     nat = tr._native
     with torch.no_grad():
@@ -385,46 +385,41 @@ def splat_replay(fitter, device) -> dict:
     sp = ctypes.c_void_p(cur.cuda_stream)
     V = max(len(fitter.targets), 1)
     w_sil = fitter.w_sil if fitter.masks is not None else 0.0
-    views = []
+    preps = []
     for i in fitter.my_views:
         gv = fitter._fit_view(i, device)
-        prep = tr.prepare_native(*acts, gv)
+        preps.append((i, gv, tr.prepare_native(*acts, gv)))
+    torch.cuda.synchronize()
+    ev = []
+    pairs = []
+    for i, gv, prep in preps:
         plan = prep.plan()
+        pairs.append(int(plan.num_pairs))
         bins, scratch, bgv, done = tr._bin_launch(L, gv, n, plan, prep, cur, device)
         ws = torch.empty((tr._ws_round(L.gr_bwd_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8,
                          device=device)
         loss = torch.zeros(1, device=device)
         mask = fitter.masks[i] if fitter.masks is not None else None
-        views.append((gv, bgv, plan, prep.geom, bins, scratch, ws, loss, fitter.targets[i], mask))
-
-    def fwd(v):
-        gv, bgv, plan, geom, bins, scratch, ws, loss, tgt, mask = v
-        nat.check(L.gr_fwd_render_l1(ctypes.byref(bgv), n, ctypes.byref(plan), nat.ptr(geom), nat.ptr(bins), bins.numel(),
-                                     nat.ptr(scratch), scratch.numel(), nat.ptr(tgt), nat.ptr(mask), ctypes.c_float(w_sil),
-                                     ctypes.c_float(1.0 / V), nat.ptr(loss), None, None, nat.ptr(ws), ws.numel(), sp),
-                  "gr_fwd_render_l1")
-
-    def bwd(v):
-        gv, bgv, plan, geom, bins, scratch, ws = v[:7]
-        nat.check(L.gr_bwd_splat(ctypes.byref(gv), n, ctypes.byref(plan), nat.ptr(geom), nat.ptr(bins), nat.ptr(ws),
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        e[0].record(cur)
+        nat.check(L.gr_fwd_render_l1(ctypes.byref(bgv), n, ctypes.byref(plan), nat.ptr(prep.geom), nat.ptr(bins),
+                                     bins.numel(), nat.ptr(scratch), scratch.numel(), nat.ptr(fitter.targets[i]),
+                                     nat.ptr(mask), ctypes.c_float(w_sil), ctypes.c_float(1.0 / V), nat.ptr(loss), None,
+                                     None, nat.ptr(ws), ws.numel(), sp), "gr_fwd_render_l1")
+        e[1].record(cur)
+        nat.check(L.gr_bwd_splat(ctypes.byref(gv), n, ctypes.byref(plan), nat.ptr(prep.geom), nat.ptr(bins), nat.ptr(ws),
                                  ws.numel(), sp), "gr_bwd_splat")
-
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[2].record(cur)
+        e[3].record(cur)  # an empty event pair: the markers' own cost, subtracted below
+        ev.append(e)
     torch.cuda.synchronize()
-    fwd(views[0])
-    ev[0].record(cur)
-    for v in views:
-        fwd(v)
-    ev[1].record(cur)
-    for v in views:
-        bwd(v)
-    ev[2].record(cur)
-    torch.cuda.synchronize()
-    k = len(views)
-    pairs = [int(v[2].num_pairs) for v in views]
-    out = {"fwd_us": 1e3 * ev[0].elapsed_time(ev[1]) / k, "bwd_us": 1e3 * ev[1].elapsed_time(ev[2]) / k, "launches": k,
-           "pairs": float(np.mean(pairs)), "tile": int(views[0][0].tile) or 16}
-    del views
+    k = len(ev)
+    mark = 1e3 * sum(e[2].elapsed_time(e[3]) for e in ev) / k
+    fwd = 1e3 * sum(e[0].elapsed_time(e[1]) for e in ev) / k
+    bwd = 1e3 * sum(e[1].elapsed_time(e[2]) for e in ev) / k
+    out = {"fwd_us": fwd - mark, "bwd_us": bwd - mark, "fwd_us_events": fwd, "bwd_us_events": bwd, "marker_us": mark,
+           "launches": k, "pairs": float(np.mean(pairs)), "tile": int(preps[0][1].tile) or 16}
+    del preps, ev
     torch.cuda.empty_cache()
     return out
 
@@ -574,8 +569,9 @@ def main():
                         flop=(MFMA_FLOP_PER_PAIR_BWD32 if t32 else BF16_FLOP_PER_CORE_PAIR_BWD) * avg_pairs,
                         f32=(F32_FLOP_PER_PAIR_BWD32 if t32 else F32_FLOP_PER_CORE_PAIR_BWD) * avg_pairs),
         }
-        timing = (f"HIP events around {replay['launches']} launches (one per view, back to back on one stream, after the "
-                  f"timed region; splat_replay); compare the GR_STREAMS=1 rocprofv3 kernel-trace summary in profiles/")
+        timing = (f"HIP events around each of {replay['launches']} launches (one per view, a single-stream schedule after "
+                  f"the timed region: splat_replay), less the cost of an empty event pair measured beside them "
+                  f"(avg_launch_us_events keeps it); compare the GR_STREAMS=1 rocprofv3 kernel-trace summary in profiles/")
 
         def roof(k):
             """The kernel against the bound that binds it: the MFMA pipe (executed 16-bit MFMA FLOP/s vs the dense
@@ -592,13 +588,15 @@ def main():
                    "algorithmic_bytes_per_launch": int(nbytes),
                    "bytes_model": f"{e['unit_bytes']} B x {e['units_desc']} ({int(e['units'])}) + {e['px_bytes']} B x {px} px",
                    "traffic": pk.get("hbm_bytes_per_launch")}
+            ev_us = replay[k + "_us_events"]
             if t32:
                 return {"bound": "mfma", "kernel": e["variant"], "achieved": round(mf, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(mf / BF16_MFMA_PEAK_TFLOPS, 4), "traffic": pk.get("hbm_bytes_per_launch"),
                         "valu_frac": pk.get("valu_frac"), "mfma_frac": pk.get("mfma_frac"),
                         "executed_flop_per_launch": int(e["flop"]), "f32_equivalent_tflops": round(e["f32"] / t / 1e12, 1),
                         "f32_peak": F32_MFMA_PEAK_TFLOPS, "hbm": hbm,
-                        "avg_launch_us": round(e["t"] * 1e6, 1), "launches": replay["launches"], "timing": timing,
+                        "avg_launch_us": round(e["t"] * 1e6, 1), "avg_launch_us_events": round(ev_us, 1),
+                        "event_marker_us": round(replay["marker_us"], 2), "launches": replay["launches"], "timing": timing,
                         "avg_launch_us_multi_stream": round(e["conc_us"], 1), "streams_in_timed_region": streams_saved}
             return {"bound": "hbm", "kernel": e["variant"], "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
