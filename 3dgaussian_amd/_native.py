@@ -44,6 +44,8 @@ class GrView(ctypes.Structure):
         ("background_dev", ctypes.c_void_p),  # optional device pointer to the 3 background floats
         ("binned", ctypes.c_int),  # 1: gr_fwd_bin already built the bins; the render launches only the splat
         ("tile", ctypes.c_int),  # screen tile edge: 0/16 (default) or 32 (fused fit path)
+        ("device_counts", ctypes.c_int),  # 1: plans are capacities, the counts stay on the device (sized preparation)
+        ("chunk", ctypes.c_int),  # work-item length in pairs (0: the default 2048)
     ]
 
 
@@ -99,7 +101,8 @@ class GrFitConfig(ctypes.Structure):
 
     _fields_ = [("num_streams", ctypes.c_int), ("prep_ahead", ctypes.c_int), ("prep_group", ctypes.c_int),
                 ("prep_first", ctypes.c_int), ("reduce_batch", ctypes.c_int), ("reduce_tail", ctypes.c_int),
-                ("render_streams", ctypes.POINTER(ctypes.c_void_p)), ("prep_stream", ctypes.c_void_p)]
+                ("render_streams", ctypes.POINTER(ctypes.c_void_p)), ("prep_stream", ctypes.c_void_p),
+                ("caps", ctypes.POINTER(GrPlan)), ("observed", ctypes.c_void_p), ("overflow", ctypes.c_void_p)]
 
 
 FIT_MAX_ACC = 8      # GR_FIT_MAX_ACC
@@ -131,6 +134,9 @@ _SIG = {
     "gr_fwd_prepare_views_async": (ctypes.c_int, [ctypes.c_int, _VP, ctypes.c_int, _P, _P, _P, ctypes.c_int, _P,
                                                   ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t,
                                                   ctypes.POINTER(ctypes.c_void_p), _P]),
+    "gr_fwd_prepare_views_sized": (ctypes.c_int, [ctypes.c_int, _VP, ctypes.c_int, _P, _P, _P, ctypes.c_int, _P,
+                                                  ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, _PP,
+                                                  ctypes.POINTER(ctypes.c_void_p), _P, _P]),
     "gr_bins_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
     "gr_saved_floats": (ctypes.c_size_t, [_VP]),
     "gr_fwd_scratch_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
@@ -159,6 +165,8 @@ _SIG = {
                                     ctypes.c_double, ctypes.c_float, _P]),
     "gr_fit_param_steps": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(GrParamStep), ctypes.c_double, ctypes.c_double,
                                           ctypes.c_float, _P]),
+    "gr_fit_param_steps_sched": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(GrParamStep), ctypes.c_double, ctypes.c_double,
+                                                ctypes.c_float, _P, _P, _P, _P, _P]),
     "gr_fwd_render_l1": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P, _P,
                                         ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, ctypes.c_size_t, _P]),
     "gr_bwd_splat": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_size_t, _P]),

@@ -187,6 +187,7 @@ gr_status gr_fit_views(gr_executor* ex, const gr_fit_config* cfg, int num_views,
       cfg->reduce_batch > GR_REDUCE_MAX_VIEWS || cfg->reduce_tail < 0 || cfg->reduce_tail > cfg->reduce_batch)
     return gr_exec_set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views: configuration out of range");
   if (num_views == 0 || n <= 0) return GR_OK;
+  if (cfg->caps && !cfg->overflow) return gr_exec_set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views: caps without overflow");
   const bool depth = views[0].target_depth != nullptr;  // the depth-loss path (one form per call)
   for (int j = 0; j < num_views; ++j) {
     if ((views[j].target_depth != nullptr) != depth)
@@ -294,6 +295,7 @@ static gr_status enqueue_views(gr_executor* ex, const gr_fit_config* cfg, int nu
                                float* const* acc, const Sched& sc, const std::vector<hipStream_t>& st, hipStream_t prep,
                                bool depth, int nslots, int& ngroups) {
   const int ns = sc.ns;
+  const bool sized = cfg->caps != nullptr;  // device-side sizing: the plans are capacities, nothing to wait for
   const size_t geom_bytes = gr_geom_bytes(n);
   std::vector<void*> geom(num_views, nullptr);
   std::vector<int> slot_of(num_views, -1);
@@ -317,11 +319,15 @@ static gr_status enqueue_views(gr_executor* ex, const gr_fit_config* cfg, int nu
         slot_of[g0 + q] = sl;
         vs[q] = views[g0 + q].view;
         gs[q] = geom[g0 + q];
-        ps[q] = &ex->plans[g0 + q];
+        ps[q] = sized ? (cfg->observed ? &cfg->observed[g0 + q] : nullptr) : &ex->plans[g0 + q];
         group_of[g0 + q] = ngroups;
       }
-      GR_EXEC_CALL(gr_fwd_prepare_views_async(cnt, vs, n, means, scales, colors, color_dim, opacities, gs, geom_bytes, ps,
-                                              prep));
+      if (sized)
+        GR_EXEC_CALL(gr_fwd_prepare_views_sized(cnt, vs, n, means, scales, colors, color_dim, opacities, gs, geom_bytes,
+                                                cfg->caps + g0, ps, cfg->overflow, prep));
+      else
+        GR_EXEC_CALL(gr_fwd_prepare_views_async(cnt, vs, n, means, scales, colors, color_dim, opacities, gs, geom_bytes, ps,
+                                                prep));
       GR_EXEC_TRY(hipEventRecord(ex->groups[ngroups], prep));
       ++ngroups;
       next_prep = g0 + cnt;
@@ -366,8 +372,8 @@ static gr_status enqueue_views(gr_executor* ex, const gr_fit_config* cfg, int nu
     GR_EXEC_CALL(prepare_upto(j));
     const hipEvent_t ev = ex->groups[group_of[j]];
     GR_EXEC_TRY(hipStreamWaitEvent(s, ev, 0));
-    GR_EXEC_TRY(hipEventSynchronize(ev));  // the plan (pair count) sizes this view's workspaces
-    const gr_plan plan = ex->plans[j];
+    if (!sized) GR_EXEC_TRY(hipEventSynchronize(ev));  // the plan (pair count) sizes this view's workspaces
+    const gr_plan plan = sized ? cfg->caps[j] : ex->plans[j];
     if (plan.num_pairs < 0 || plan.num_slots < 0) return gr_exec_set_error(GR_ERR_OVERFLOW, "pair count overflows int32");
     const gr_view& v = views[j].view;
     const size_t bins_bytes = gr_bins_bytes(&v, n, &plan), scratch_bytes = gr_fwd_scratch_bytes(&v, n, &plan);

@@ -452,8 +452,30 @@ struct TileCfg {
   size_t part_floats, uf_frags;
 };
 constexpr int UF_FRAGS16 = 2 * 3 * 3 * 64;  // (= UF_FRAGS below)
-inline TileCfg tile_cfg(const gr_view* v) {
-  return tile_of(v) == T32 ? TileCfg{T32, CH32, (size_t)4 * TP32, (size_t)UF32_FRAGS} : TileCfg{T, CH, (size_t)5 * TP, (size_t)UF_FRAGS16};
+// Work-item length: gr_view.chunk when set (a view with few tiles gets more, shorter items to fill the CUs: one
+// workgroup per item), else the tile size's default; a multiple of 64 in [64, 8192].
+// Unset (0), a view with K pairs (host-sized plans) gets the largest power of two <= K / 1024 within [512, default]:
+// at least ~1024 items (four per CU) when the pairs allow (C2 / C3: 256 tiles of ~2k pairs each, 0.93 -> 0.89 ms per
+// step); large views keep the default.  (A device-sized view's plan holds capacities: its rule reads them, so it
+// matches the host-sized view's item length unless the two fall on either side of a power of two.)
+static int64_t tune_env(const char* name);
+inline int chunk_of(const gr_view* v, int base, int64_t K) {
+  static const int64_t force = tune_env("GR_TUNE_CHUNK");
+  int64_t c = base;
+  if (v->chunk > 0) {
+    c = v->chunk;
+  } else if (force > 0) {
+    c = force;
+  } else if (K >= 0) {
+    c = 512;
+    while (c < base && 2 * c * 1024 <= K) c *= 2;
+  }
+  return (int)std::min<int64_t>(8192, std::max<int64_t>(64, (c + 63) / 64 * 64));
+}
+// K: the plan's pair count (the work-item length follows it, chunk_of); -1 where only the tile geometry is needed
+inline TileCfg tile_cfg(const gr_view* v, int64_t K = -1) {
+  return tile_of(v) == T32 ? TileCfg{T32, chunk_of(v, CH32, K), (size_t)4 * TP32, (size_t)UF32_FRAGS}
+                           : TileCfg{T, chunk_of(v, CH, K), (size_t)5 * TP, (size_t)UF_FRAGS16};
 }
 
 // `vtiles` = 2 x tiles (core and tail lists of each tile) on the differentiable path.
@@ -884,6 +906,10 @@ __global__ __launch_bounds__(256) void k_emit_offsets(ViewK v, int n, const int4
   __shared__ unsigned long long wsum[4];
   const int tid = threadIdx.x, b = blockIdx.x, i = b * 256 + tid;
   if (b == 0 && tid < 9) fan[FAN_STRIDE * tid] = 0;
+  if (offsets[n].v == 0ull) {  // no pair (a view over its capacity, gr_fwd_prepare_views_sized): every offset is zero
+    if (i < n) offsets[i].v = 0ull;
+    return;
+  }
   const Cnt2 cn{i < n ? counts[i].v : 0ull};
   unsigned long long tot;
   const unsigned long long ex = block_exclusive_scan<4>(cn.v, wsum, tot);
@@ -1158,7 +1184,23 @@ struct TZones {
   int ch;  // work-item length (pairs): CH, or CH32 for 32-pixel tiles
   TZone z[2];
   int cw;  // pairs per column (col_width)
+  // device-side sizing (gr_view.device_counts): the packed true counts (core | tail << 32, the offsets' end) on the
+  // device; z[*].K and cols are then the capacities (the grid), and zone_at() gives each zone's true K, first pair and
+  // key / id pointers (z[0].keys / ids: the arrays' start)
+  const unsigned long long* kdev;
 };
+__device__ __forceinline__ TZone zone_at(const TZones& Z, int zone) {
+  TZone zz = Z.z[zone];
+  if (Z.kdev) {
+    const unsigned long long e = *Z.kdev;
+    const int Kc = (int)(e & 0xffffffffull);
+    zz.K = zone ? (int64_t)(e >> 32) : (int64_t)Kc;
+    zz.zbase = zone ? Kc : 0;
+    zz.keys = Z.z[0].keys + zz.zbase;
+    zz.ids = Z.z[0].ids + zz.zbase;
+  }
+  return zz;
+}
 // Column block b of the combined grid -> (zone, column), XCD-aware within the grid.
 __device__ __forceinline__ int tzone_of(const TZones& Z, int b, int& c) {
   b = xcd_item(b, Z.z[0].cols + Z.z[1].cols);
@@ -1166,10 +1208,11 @@ __device__ __forceinline__ int tzone_of(const TZones& Z, int b, int& c) {
   c = b - (zone ? Z.z[0].cols : 0);
   return zone;
 }
-// Pairs [k0, k1) of column c in region `zone`, relative to the region's first pair.
-__device__ __forceinline__ void column_range(const TZones& Z, int zone, int c, int64_t& k0, int64_t& k1) {
+// Pairs [k0, k1) of column c in a region of K pairs, relative to the region's first pair (k1 <= k0: a column past the
+// region's true end under device-side sizing).
+__device__ __forceinline__ void column_range(const TZones& Z, int64_t K, int c, int64_t& k0, int64_t& k1) {
   k0 = (int64_t)c * Z.cw;
-  k1 = min(Z.z[zone].K, k0 + Z.cw);
+  k1 = min(K, k0 + Z.cw);
 }
 
 // Per-column tile counts M[c][t]: one block per (region, column), the column's keys read once (coalesced, eight
@@ -1178,12 +1221,12 @@ __global__ __launch_bounds__(256) void k_tile_count(TZones Z, int tiles) {
   extern __shared__ int hist[];
   int c;
   const int zone = tzone_of(Z, (int)blockIdx.x, c);
-  const TZone& zz = Z.z[zone];
+  const TZone zz = zone_at(Z, zone);
   const uint16_t* __restrict__ keys = zz.keys;
   for (int t = threadIdx.x; t < tiles; t += 256) hist[t] = 0;
   __syncthreads();
   int64_t k0, k1;
-  column_range(Z, zone, c, k0, k1);
+  column_range(Z, zz.K, c, k0, k1);
   for (int64_t kb = k0 + threadIdx.x; kb < k1; kb += 256 * 8) {
     int d[8];
 #pragma unroll
@@ -1280,11 +1323,12 @@ __global__ __launch_bounds__(GR_CS_THREADS) void k_tile_colscan(TZones Z, int ti
                                                              int4* __restrict__ items, int* __restrict__ num_items,
                                                              int* __restrict__ tile_item0, int* __restrict__ ticket) {
   __shared__ int last;
-  const TZone& zz = Z.z[blockIdx.y];
+  const TZone zz = zone_at(Z, (int)blockIdx.y);
   if (zz.K > 0) tile_colscan_block(zz, tiles);  // (an empty region: no counts, and the work items get no totals for it)
   const int nb = (int)(gridDim.x * gridDim.y);
   if (!arrive_last_of(ticket + fan_offset(tiles), nb, (int)(blockIdx.y * gridDim.x + blockIdx.x), &last)) return;
-  work_items_zones<true, GR_CS_THREADS>(tiles, Z.z[1].zbase, Z.z[0].K > 0 ? Z.z[0].T : nullptr, Z.z[1].K > 0 ? Z.z[1].T : nullptr,
+  const TZone z0 = zone_at(Z, 0), z1 = zone_at(Z, 1);
+  work_items_zones<true, GR_CS_THREADS>(tiles, z1.zbase, z0.K > 0 ? z0.T : nullptr, z1.K > 0 ? z1.T : nullptr,
                                   ranges, items, num_items, tile_item0, ticket, Z.ch);
 }
 
@@ -1432,7 +1476,7 @@ __global__ __launch_bounds__(64 * WAVES, GR_PLACE_WAVES) void k_tile_place(TZone
   constexpr int NT = 64 * WAVES;
   int c;
   const int zone = tzone_of(Z, (int)blockIdx.x, c);
-  const TZone& zz = Z.z[zone];
+  const TZone zz = zone_at(Z, zone);
   const int64_t K = zz.K;
   const int zbase = zz.zbase;
   const uint16_t* __restrict__ keys = zz.keys;
@@ -1441,7 +1485,8 @@ __global__ __launch_bounds__(64 * WAVES, GR_PLACE_WAVES) void k_tile_place(TZone
   const int w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
   int* my = cur + (size_t)w * tiles;
   int64_t kc0, kc1;
-  column_range(Z, zone, c, kc0, kc1);
+  column_range(Z, K, c, kc0, kc1);
+  if (kc1 <= kc0) return;  // a column past the region's end (device-side sizing; uniform per block)
   // this wave's part of the column: whole 64-pair steps, the parts in wave order
   const int64_t steps = (kc1 - kc0 + 63) / 64, wsteps = (steps + WAVES - 1) / WAVES;
   const int64_t k0 = min(kc1, kc0 + (int64_t)w * wsteps * 64), k1 = min(kc1, k0 + wsteps * 64);
@@ -2243,7 +2288,8 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
                                                          float* __restrict__ out_alpha, float* __restrict__ out_depth,
                                                          float4* __restrict__ saved4, float* __restrict__ savedD,
                                                          L1Args l1, uint4* __restrict__ UF, const int* __restrict__ f16_sa,
-                                                         const int* __restrict__ tile_item0, int* __restrict__ ticket) {
+                                                         const int* __restrict__ tile_item0, int* __restrict__ ticket,
+                                                         int ch) {
   // LDS: two staged record buffers (2 x 9 KiB) during the loop, then the 4-wave reduction (20 KiB).
   __shared__ __attribute__((aligned(16))) float smem[4 * 5 * TP];
   __shared__ int last_flag;
@@ -2290,7 +2336,7 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
   for (int c = 0; c < 5; ++c)
     acc[c] = ((smem[0 * 5 * TP + c * TP + tid] + smem[1 * 5 * TP + c * TP + tid]) + smem[2 * 5 * TP + c * TP + tid]) +
              smem[3 * 5 * TP + c * TP + tid];
-  const int nch = tile_chunks(ranges[2 * tile]) + tile_chunks(ranges[2 * tile + 1]);
+  const int nch = tile_chunks(ranges[2 * tile], ch) + tile_chunks(ranges[2 * tile + 1], ch);
   if (nch > 1) {
     // a tile split over several items: each leaves its partial sums (write-through) and takes the tile's ticket;
     // the last to arrive sums every item's partials in item order (deterministic) and finishes the tile
@@ -4185,10 +4231,17 @@ struct ParamSteps {
   int first[GR_FIT_MAX_PARAMS + 1];
   int num;
 };
-__global__ __launch_bounds__(256) void k_fit_param_steps(ParamSteps P, float b1, float b2, float b2_c, float eps) {
+// sched (gr_fit_param_steps_sched): the step's (neg_step_size, bias_correction2_sqrt) are sched[2 *step_dev + 0/1], and a
+// step whose views overflowed their capacities (*ovf) updates nothing.
+__global__ __launch_bounds__(256) void k_fit_param_steps(ParamSteps P, float b1, float b2, float b2_c, float eps,
+                                                         const float* __restrict__ sched, const int* __restrict__ step_dev,
+                                                         const int* __restrict__ ovf) {
+  if (ovf && *ovf) return;  // (uniform)
   int t = 0;
   while (t + 1 < P.num && (int)blockIdx.x >= P.first[t + 1]) ++t;
   const gr_param_step& q = P.s[t];
+  const int ts = sched ? *step_dev : 0;
+  const float neg_step = sched ? sched[2 * ts] : q.neg_step_size, bc2s = sched ? sched[2 * ts + 1] : q.bias_correction2_sqrt;
   const int nb = P.first[t + 1] - P.first[t];
   float* __restrict__ p = q.param;
   float* __restrict__ m = q.exp_avg;
@@ -4213,8 +4266,21 @@ __global__ __launch_bounds__(256) void k_fit_param_steps(ParamSteps P, float b1,
     const float vv = fmaf(b2_c, g * g, v[e] * b2);
     m[e] = mm;
     v[e] = vv;
-    p[e] = fmaf(q.neg_step_size, mm / (sqrtf(vv) / q.bias_correction2_sqrt + eps), x);
+    p[e] = fmaf(neg_step, mm / (sqrtf(vv) / bc2s + eps), x);
   }
+}
+
+// After a gr_fit_param_steps_sched update: the step counter advances when the update ran; an overflow is reported
+// to the host (sticky flag in pinned memory) and cleared for the next step.
+__global__ void k_step_advance(int* __restrict__ step_dev, int* __restrict__ ovf, int* host_flags) {
+  if (threadIdx.x != 0) return;
+  const int o = *ovf;
+  const int t = *step_dev + (o ? 0 : 1);
+  *step_dev = t;
+  *ovf = 0;
+  if (o) host_flags[0] = 1;
+  host_flags[1] = t;
+  __threadfence_system();
 }
 
 // Adam alone on an assembled (e.g. all-reduced) gradient.
@@ -4311,7 +4377,7 @@ void gr_geom_layout(int n, size_t offsets_out[GR_GEOM_PARTS]) { geom_fixed(n, of
 void gr_bins_layout(const gr_view* v, int n, const gr_plan* plan, size_t offsets_out[4]) {
   (void)n;
   size_t off[8];
-  bins_fixed(vtiles_of(v), plan ? plan->num_pairs : 0, off, tile_cfg(v).ch);
+  bins_fixed(vtiles_of(v), plan ? plan->num_pairs : 0, off, tile_cfg(v, plan ? plan->num_pairs : 0).ch);
   offsets_out[0] = off[0];
   offsets_out[1] = off[1];
   offsets_out[2] = off[2];
@@ -4328,12 +4394,12 @@ size_t gr_saved_floats(const gr_view* v) { return (size_t)5 * v->width * v->heig
 size_t gr_bins_bytes(const gr_view* v, int n, const gr_plan* plan) {
   (void)n;
   size_t off[8];
-  return bins_fixed(vtiles_of(v), plan->num_pairs, off, tile_cfg(v).ch);
+  return bins_fixed(vtiles_of(v), plan->num_pairs, off, tile_cfg(v, plan->num_pairs).ch);
 }
 
 size_t gr_fwd_scratch_bytes(const gr_view* v, int n, const gr_plan* plan) {
   const int vtiles = vtiles_of(v);
-  const TileCfg tc = tile_cfg(v);
+  const TileCfg tc = tile_cfg(v, plan->num_pairs);
   size_t off[5];
   return scratch_fixed(vtiles, plan->num_pairs, off, tc.ch, tc.part_floats) + align_up(tile_sort_tmp_bytes(n, plan->num_pairs, vtiles));
 }
@@ -4367,9 +4433,12 @@ constexpr int PLAN_THREADS = GR_PLAN_THREADS;
 // block sums) is replaced by its exclusive scan, offsets[n] gets the packed grand total.  The packed
 // words cannot carry into each other as long as K < 2^31, which is checked against the exact total
 // (the sum of every block's two words) before the plan is trusted.
+// cap (device-side sizing, gr_fwd_prepare_views_sized): the view's capacities; counts beyond them leave the device
+// plan and the offsets' end at zero (the binning then emits nothing: a view without pairs) and raise *ovf.
 __device__ __forceinline__ void plan_scan(unsigned long long* __restrict__ bsum, int blocks,
                                           unsigned long long* __restrict__ off_end, gr_plan* plan, gr_plan* host_plan,
-                                          const float* __restrict__ omax, int* __restrict__ f16_sa) {
+                                          const float* __restrict__ omax, int* __restrict__ f16_sa,
+                                          const gr_plan* cap = nullptr, int* ovf = nullptr) {
   __shared__ unsigned long long sh[PLAN_THREADS / 64];
   __shared__ float shm[PLAN_THREADS / 64];
   const int tid = (int)threadIdx.x, per = (blocks + PLAN_THREADS - 1) / PLAN_THREADS;
@@ -4418,14 +4487,17 @@ __device__ __forceinline__ void plan_scan(unsigned long long* __restrict__ bsum,
   for (int w = 1; w < PLAN_THREADS / 64; ++w) om = fmaxf(om, shm[w]);  // published by the scans' barriers
   *f16_sa = f16_sa_of(om);
   const bool ok = exact < (1ull << 31);  // then neither packed word carried
-  *off_end = grand;
-  plan->num_pairs = ok ? (long long)exact : -1;
-  plan->num_slots = ok ? (long long)exact : -1;  // one partial-sum slot per pair
-  plan->num_core_pairs = ok ? (long long)(grand & 0xffffffffull) : -1;
-  if (host_plan) {  // pinned host memory (gr_fwd_prepare_async): no copy command behind the scan
-    host_plan->num_pairs = plan->num_pairs;
-    host_plan->num_slots = plan->num_slots;
-    host_plan->num_core_pairs = plan->num_core_pairs;
+  const long long np = ok ? (long long)exact : -1, nc = ok ? (long long)(grand & 0xffffffffull) : -1;
+  const bool fits = !cap || (ok && nc <= cap->num_core_pairs && np - nc <= cap->num_pairs - cap->num_core_pairs);
+  *off_end = fits ? grand : 0ull;
+  plan->num_pairs = fits ? np : 0;
+  plan->num_slots = fits ? np : 0;  // one partial-sum slot per pair
+  plan->num_core_pairs = fits ? nc : 0;
+  if (!fits) *ovf = 1;
+  if (host_plan) {  // pinned host memory (gr_fwd_prepare_async): no copy command behind the scan; the true counts
+    host_plan->num_pairs = np;
+    host_plan->num_slots = np;
+    host_plan->num_core_pairs = nc;
     __threadfence_system();
   }
 }
@@ -4457,10 +4529,13 @@ __global__ __launch_bounds__(256) void k_offsets(int n, const unsigned long long
 // The two scans for a batch of views (gr_fwd_prepare_views_async): block / row k = view k.
 struct HostPlans {
   gr_plan* p[PREP_MAX_VIEWS];
+  gr_plan cap[PREP_MAX_VIEWS];  // device-side sizing (ovf != null): the views' capacities
+  int* ovf;
 };
 __global__ __launch_bounds__(PLAN_THREADS) void k_plan_views(PrepBatch B, int n, HostPlans hp) {
   const Geom& g = B.g[blockIdx.x];
-  plan_scan(g.total, (n + 256) / 256, g.offsets + n, g.plan, hp.p[blockIdx.x], g.omax, g.f16_sa);
+  plan_scan(g.total, (n + 256) / 256, g.offsets + n, g.plan, hp.p[blockIdx.x], g.omax, g.f16_sa,
+            hp.ovf ? &hp.cap[blockIdx.x] : nullptr, hp.ovf);
 }
 
 gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, const float* scales, const float* colors,
@@ -4468,6 +4543,7 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
                                void* stream) {
   gr_status st = check_view(v);
   if (st != GR_OK) return st;
+  if (v->device_counts) return set_error(GR_ERR_INVALID_ARGUMENT, "device_counts views are prepared by gr_fwd_prepare_views_sized");
   if (n < 0) return set_error(GR_ERR_INVALID_ARGUMENT, "n must be >= 0");
   if (color_dim != 3 && color_dim != 12 && color_dim != 48)
     return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");
@@ -4505,25 +4581,40 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
   return GR_OK;
 }
 
-gr_status gr_fwd_prepare_views_async(int num_views, const gr_view* views, int n, const float* means,
-                                     const float* scales, const float* colors, int color_dim, const float* opacities,
-                                     void* const* geoms, size_t geom_bytes, gr_plan* const* plans, void* stream) {
+static gr_status prepare_views_impl(int num_views, const gr_view* views, int n, const float* means, const float* scales,
+                                    const float* colors, int color_dim, const float* opacities, void* const* geoms,
+                                    size_t geom_bytes, gr_plan* const* plans, const gr_plan* caps, int* ovf,
+                                    void* stream) {
   if (num_views < 1 || num_views > PREP_MAX_VIEWS)
     return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fwd_prepare_views_async: num_views must be in [1, GR_PREPARE_MAX_VIEWS]");
-  if (!views || !geoms || !plans) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
-  if (num_views == 1)
+  if (!views || !geoms || (!plans && !caps)) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+  if (num_views == 1 && !caps)
     return gr_fwd_prepare_async(&views[0], n, means, scales, colors, color_dim, opacities, geoms[0], geom_bytes, plans[0],
                                 stream);
   for (int k = 0; k < num_views; ++k) {
     gr_status st = check_view(&views[k]);
     if (st != GR_OK) return st;
-    if (!plans[k] || !geoms[k]) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+    if ((!caps && !plans[k]) || !geoms[k]) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
+    if (caps) {
+      if (!views[k].device_counts)
+        return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fwd_prepare_views_sized: the views must have device_counts = 1");
+      if (!short_keys(vtiles_of(&views[k])))
+        return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fwd_prepare_views_sized: more than 8,192 screen tiles");
+      if (caps[k].num_core_pairs < 0 || caps[k].num_pairs < caps[k].num_core_pairs || caps[k].num_pairs >= (1ll << 31) ||
+          caps[k].num_slots < caps[k].num_pairs)
+        return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fwd_prepare_views_sized: bad capacities");
+    } else if (views[k].device_counts) {
+      return set_error(GR_ERR_INVALID_ARGUMENT, "device_counts views are prepared by gr_fwd_prepare_views_sized");
+    }
   }
+  if (caps && !ovf) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fwd_prepare_views_sized: overflow is null");
   if (n < 0) return set_error(GR_ERR_INVALID_ARGUMENT, "n must be >= 0");
   if (color_dim != 3 && color_dim != 12 && color_dim != 48)
     return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");
   if (n == 0) {
-    for (int k = 0; k < num_views; ++k) *plans[k] = gr_plan{0, 0, 0};
+    if (plans)
+      for (int k = 0; k < num_views; ++k)
+        if (plans[k]) *plans[k] = gr_plan{0, 0, 0};
     return GR_OK;
   }
   if (!means || !scales || !colors || !opacities) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
@@ -4531,17 +4622,21 @@ gr_status gr_fwd_prepare_views_async(int num_views, const gr_view* views, int n,
   hipStream_t s = (hipStream_t)stream;
   PrepBatch B;
   HostPlans hp;
+  hp.ovf = caps ? ovf : nullptr;
   bool all_mapped = true;
   B.nv = num_views;
   for (int k = 0; k < num_views; ++k) {
     B.v[k] = make_viewk(&views[k]);
     B.g[k] = geom_view(geoms[k], n);
+    hp.cap[k] = caps ? caps[k] : gr_plan{0, 0, 0};
     hipPointerAttribute_t attr;
     hp.p[k] = nullptr;
-    if (hipPointerGetAttributes(&attr, plans[k]) == hipSuccess && attr.type == hipMemoryTypeHost && attr.devicePointer)
+    if (plans && plans[k] && hipPointerGetAttributes(&attr, plans[k]) == hipSuccess && attr.type == hipMemoryTypeHost &&
+        attr.devicePointer)
       hp.p[k] = (gr_plan*)attr.devicePointer;
     (void)hipGetLastError();
-    all_mapped = all_mapped && hp.p[k];
+    // (device-side sizing: an observed plan that is not mapped host memory is left unwritten; nothing waits for it)
+    all_mapped = all_mapped && (hp.p[k] || caps);
   }
   const int blocks = blocks_for(n + 1);
   for (int rep = 0; rep < GR_DEBUG_PREP_REPS; ++rep) {  // > 1: timing experiments only (idempotent repeats)
@@ -4559,6 +4654,22 @@ gr_status gr_fwd_prepare_views_async(int num_views, const gr_view* views, int n,
     for (int k = 0; k < num_views; ++k)
       if (!hp.p[k]) GR_HIP_TRY(hipMemcpyAsync(plans[k], B.g[k].plan, sizeof(gr_plan), hipMemcpyDeviceToHost, s));
   return GR_OK;
+}
+
+gr_status gr_fwd_prepare_views_async(int num_views, const gr_view* views, int n, const float* means,
+                                     const float* scales, const float* colors, int color_dim, const float* opacities,
+                                     void* const* geoms, size_t geom_bytes, gr_plan* const* plans, void* stream) {
+  return prepare_views_impl(num_views, views, n, means, scales, colors, color_dim, opacities, geoms, geom_bytes, plans,
+                            nullptr, nullptr, stream);
+}
+
+gr_status gr_fwd_prepare_views_sized(int num_views, const gr_view* views, int n, const float* means,
+                                     const float* scales, const float* colors, int color_dim, const float* opacities,
+                                     void* const* geoms, size_t geom_bytes, const gr_plan* caps, gr_plan* const* observed,
+                                     int* overflow, void* stream) {
+  if (!caps) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fwd_prepare_views_sized: caps is null");
+  return prepare_views_impl(num_views, views, n, means, scales, colors, color_dim, opacities, geoms, geom_bytes, observed,
+                            caps, overflow, stream);
 }
 
 gr_status gr_fwd_prepare(const gr_view* v, int n, const float* means, const float* scales, const float* colors,
@@ -4624,7 +4735,9 @@ static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const vo
       const int waves = tsort_waves(tiles);
       TZones Z;
       Z.cw = cw;
-      Z.ch = tile_cfg(v).ch;
+      Z.ch = tile_cfg(v, num_pairs).ch;
+      // device-side sizing: Kr are the regions' capacities (columns = grid); the true counts are read on the device
+      Z.kdev = v->device_counts ? (const unsigned long long*)(g.offsets + n) : nullptr;
       char* q = (char*)sc.sort_tmp;
       for (int z = 0; z < 2; ++z) {
         TZone& zz = Z.z[z];
@@ -4667,6 +4780,8 @@ static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const vo
                            b.pos_of);
       GR_HIP_TRY(hipGetLastError());
     } else {
+      if (v->device_counts)
+        return set_error(GR_ERR_INVALID_ARGUMENT, "device_counts views need the counting-sort binning (<= 8,192 tiles)");
       // radix sort of the whole pair array on virtual-tile keys (> TSORT_MAX_TILES tiles); the Gaussians' offsets
       // first (the counting-sort path's emission writes them itself)
       hipLaunchKernelGGL(k_offsets, dim3(blocks_for(n)), dim3(256), 0, s, n, (const unsigned long long*)g.counts,
@@ -4689,14 +4804,14 @@ static gr_status bin_impl(const gr_view* v, int n, const gr_plan* plan, const vo
                          b.pairs, b.pos_of);
       GR_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_work_items, dim3(1), dim3(WI_THREADS), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
-                         b.tile_item0, b.ticket, tile_cfg(v).ch);
+                         b.tile_item0, b.ticket, tile_cfg(v, num_pairs).ch);
     }
   } else {
     // no pair: the Gaussians' offsets (written by the emission otherwise) are all zero
     if (n > 0) GR_HIP_TRY(hipMemsetAsync(geom_view((void*)geom, n).offsets, 0, (size_t)n * sizeof(unsigned long long), s));
     GR_HIP_TRY(hipMemsetAsync(b.ranges, 0, sizeof(int2) * vtiles, s));
     hipLaunchKernelGGL(k_work_items, dim3(1), dim3(WI_THREADS), 0, s, vtiles, (const int2*)b.ranges, b.items, b.num_items,
-                       b.tile_item0, b.ticket, tile_cfg(v).ch);
+                       b.tile_item0, b.ticket, tile_cfg(v, num_pairs).ch);
   }
   GR_HIP_TRY(hipGetLastError());
   prof_mark(PROF_BINNING, s);
@@ -4724,7 +4839,7 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
   hipStream_t s = (hipStream_t)stream;
   const ViewK vk = make_viewk(v);
   const int tiles = vk.tiles_x * vk.tiles_y, vtiles = 2 * tiles;
-  const TileCfg tc = tile_cfg(v);
+  const TileCfg tc = tile_cfg(v, num_pairs);
   if (tc.T == T32 && (!l1 || v->no_depth_grad != 1))
     return set_error(GR_ERR_INVALID_ARGUMENT, "32-pixel tiles (gr_view.tile = 32): gr_fwd_render_l1 with no_depth_grad = 1 only");
   if (tc.T == T32 && vk.core != vk.cutoff)
@@ -4772,7 +4887,8 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
                        dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
                        (const int*)b.num_items, (const int2*)b.ranges, (const int*)b.pairs, (const float4*)g.rec,
                        sc.fwd_part, out_rgb, out_alpha, out_depth, saved4, savedD, la, UF,
-                       (const int*)(n > 0 && num_pairs > 0 ? g.f16_sa : nullptr), (const int*)b.tile_item0, b.ticket);
+                       (const int*)(n > 0 && num_pairs > 0 ? g.f16_sa : nullptr), (const int*)b.tile_item0, b.ticket,
+                       tc.ch);
     GR_HIP_TRY(hipGetLastError());
     prof_mark(PROF_RASTER_FWD, s);
   }
@@ -4818,7 +4934,7 @@ gr_status gr_fwd_bin(const gr_view* v, int n, const gr_plan* plan, const void* g
     return set_error(GR_ERR_WORKSPACE, "forward scratch workspace too small");
   const ViewK vk = make_viewk(v);
   const int vtiles = 2 * vk.tiles_x * vk.tiles_y;
-  const TileCfg tc = tile_cfg(v);
+  const TileCfg tc = tile_cfg(v, plan->num_pairs);
   return bin_impl(v, n, plan, geom, bins_view(bins, vtiles, plan->num_pairs, tc.ch),
                   scratch_view(scratch, vtiles, plan->num_pairs, tc.ch, tc.part_floats), vk, (hipStream_t)stream);
 }
@@ -4868,7 +4984,7 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
   const ViewK vk = make_viewk(v);
   const int tiles = vk.tiles_x * vk.tiles_y;
   Geom g = geom_view((void*)geom, n);
-  Bins b = bins_view((void*)bins, 2 * tiles, num_pairs);
+  Bins b = bins_view((void*)bins, 2 * tiles, num_pairs, tile_cfg(v, num_pairs).ch);
   const size_t HW = (size_t)v->width * v->height;
   const BwdWs w = bwd_ws(v, n, plan, ws);
   float* partials = w.partials;
@@ -4906,7 +5022,7 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
     GR_HIP_TRY(hipGetLastError());
   }
   if (num_pairs > 0) {
-    const int64_t cap = item_cap(2 * tiles, num_pairs);
+    const int64_t cap = item_cap(2 * tiles, num_pairs, tile_cfg(v, num_pairs).ch);
     prof_mark(PROF_RASTER_BWD, s);
     auto kern = depth ? k_raster_bwd_bf16<true, 3> : (pieces == 2 ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>);
     hipLaunchKernelGGL(kern, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items, (const int*)b.num_items,
@@ -5046,7 +5162,7 @@ gr_status gr_bwd_splat(const gr_view* v, int n, const gr_plan* plan, const void*
   const ViewK vk = make_viewk(v);
   const int tiles = vk.tiles_x * vk.tiles_y;
   const Geom g = geom_view((void*)geom, n);
-  const TileCfg tc = tile_cfg(v);
+  const TileCfg tc = tile_cfg(v, plan->num_pairs);
   if (tc.T == T32 && v->no_depth_grad != 1)
     return set_error(GR_ERR_INVALID_ARGUMENT, "32-pixel tiles (gr_view.tile = 32): no_depth_grad = 1 only");
   const Bins b = bins_view((void*)bins, 2 * tiles, plan->num_pairs, tc.ch);
@@ -5091,7 +5207,7 @@ gr_status gr_reduce_views(int num_views, const gr_reduce_view* views, int n, con
       return set_error(GR_ERR_INVALID_ARGUMENT, "gr_reduce_views: null workspace");
     const ViewK vk = make_viewk(&rv.view);
     const Geom g = geom_view((void*)rv.geom, n);
-    const Bins b = bins_view((void*)rv.bins, 2 * vk.tiles_x * vk.tiles_y, rv.plan.num_pairs, tile_cfg(&rv.view).ch);
+    const Bins b = bins_view((void*)rv.bins, 2 * vk.tiles_x * vk.tiles_y, rv.plan.num_pairs, tile_cfg(&rv.view, rv.plan.num_pairs).ch);
     B.r[k].v = vk;
     B.r[k].offsets = (const Cnt2*)g.offsets;
     B.r[k].pos_of = rv.plan.num_pairs > 0 ? (const int*)b.pos_of : nullptr;
@@ -5135,7 +5251,7 @@ gr_status gr_gather_view(const gr_view* v, int n, const gr_plan* plan, const voi
   }
   const ViewK vk = make_viewk(v);
   const Geom g = geom_view((void*)geom, n);
-  const Bins b = bins_view((void*)bins, 2 * vk.tiles_x * vk.tiles_y, plan->num_pairs, tile_cfg(v).ch);
+  const Bins b = bins_view((void*)bins, 2 * vk.tiles_x * vk.tiles_y, plan->num_pairs, tile_cfg(v, plan->num_pairs).ch);
   if (GR_DEBUG_SKIP & 4) return GR_OK;
   prof_mark(PROF_REDUCE, s);
   hipLaunchKernelGGL(k_gather_view<false>, dim3((n + 63) / 64), dim3(256), 0, s, n, (const Cnt2*)g.offsets,
@@ -5389,7 +5505,8 @@ gr_status gr_fit_param_step(int64_t count, int act, float* param, float* grad, c
   return GR_OK;
 }
 
-gr_status gr_fit_param_steps(int num, const gr_param_step* steps, double beta1, double beta2, float eps, void* stream) {
+static gr_status param_steps_impl(int num, const gr_param_step* steps, double beta1, double beta2, float eps,
+                                  const float* sched, int* step_dev, int* overflow, int* host_flags, void* stream) {
   if (num < 0 || num > GR_FIT_MAX_PARAMS || (num > 0 && !steps))
     return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_param_steps: bad arguments");
   ParamSteps P;
@@ -5407,12 +5524,35 @@ gr_status gr_fit_param_steps(int num, const gr_param_step* steps, double beta1, 
     P.first[P.num + 1] = P.first[P.num] + (int)std::min<int64_t>((q.count + 255) / 256, 1024);
     ++P.num;
   }
-  if (P.num == 0) return GR_OK;
+  if (P.num == 0 && !sched) return GR_OK;
   if (GR_DEBUG_SKIP & 16) return GR_OK;
-  hipLaunchKernelGGL(k_fit_param_steps, dim3(P.first[P.num]), dim3(256), 0, (hipStream_t)stream, P, (float)(1.0 - beta1),
-                     (float)beta2, (float)(1.0 - beta2), eps);
-  GR_HIP_TRY(hipGetLastError());
+  if (P.num > 0) {
+    hipLaunchKernelGGL(k_fit_param_steps, dim3(P.first[P.num]), dim3(256), 0, (hipStream_t)stream, P, (float)(1.0 - beta1),
+                       (float)beta2, (float)(1.0 - beta2), eps, sched, (const int*)step_dev, (const int*)overflow);
+    GR_HIP_TRY(hipGetLastError());
+  }
+  if (sched) {
+    int* mapped = nullptr;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, host_flags) == hipSuccess && attr.type == hipMemoryTypeHost && attr.devicePointer)
+      mapped = (int*)attr.devicePointer;
+    (void)hipGetLastError();
+    if (!mapped) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_param_steps_sched: host_flags must be pinned host memory");
+    hipLaunchKernelGGL(k_step_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, step_dev, overflow, mapped);
+    GR_HIP_TRY(hipGetLastError());
+  }
   return GR_OK;
+}
+
+gr_status gr_fit_param_steps(int num, const gr_param_step* steps, double beta1, double beta2, float eps, void* stream) {
+  return param_steps_impl(num, steps, beta1, beta2, eps, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+gr_status gr_fit_param_steps_sched(int num, const gr_param_step* steps, double beta1, double beta2, float eps,
+                                   const float* sched, int* step_dev, int* overflow, int* host_flags, void* stream) {
+  if (!sched || !step_dev || !overflow || !host_flags)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_param_steps_sched: null schedule, counter, overflow or flags");
+  return param_steps_impl(num, steps, beta1, beta2, eps, sched, step_dev, overflow, host_flags, stream);
 }
 
 gr_status gr_adam_step(int64_t count, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,

@@ -110,6 +110,16 @@ F32_GRADE = os.environ.get("GR_F32_GRADE", "0") != "0"
 # ~3-pixel-sigma C4 scene (7.8 -> 3.7 per Gaussian), so the binning and the per-pair gradient rows and their gather
 # (DESIGN.md §5); 16 = the drop-in op's tiles.  The f32-grade reference mode (F32_GRADE) keeps 16.
 FIT_TILE = int(os.environ.get("GR_FIT_TILE", "32"))
+# the fused step captured once as a HIP graph and replayed (world size 1; ViewShardedFitter._graph_step): the views are
+# prepared against per-view pair capacities (gr_fwd_prepare_views_sized: the counts stay on the device, nothing in
+# the step waits for the host), the Adam scalars come from a device table indexed by a device step counter, and a
+# step whose views exceed their capacities updates nothing and is redone with larger ones.  1 = on, 0 = eager steps.
+GRAPH_MODE = os.environ.get("GR_GRAPH", "0")
+GRAPH = GRAPH_MODE != "0"
+# "sized": the same device-sized step enqueued eagerly every step (no capture); "exec": likewise through the native
+# executor (gr_fit_views with capacities); "1": captured once and replayed
+GRAPH_CAPTURE = GRAPH_MODE not in ("sized", "exec")
+GRAPH_MARGIN = float(os.environ.get("GR_GRAPH_MARGIN", "1.25"))  # capacity over the counts seen (+ 4096 pairs)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -272,6 +282,30 @@ def hip_render(means, scales, colors, opacities, cam, width, height, background,
                                      prepared=prepared, depth_grad=depth_grad)
 
 
+class _EagerReplay:
+    """GR_GRAPH=sized: replay() enqueues the device-sized step again instead of launching a captured graph."""
+
+    def __init__(self, body, gs):
+        self.body, self.gs = body, gs
+
+    def replay(self):
+        self.gs.loss = self.body()
+
+
+class _GraphState:
+    """The captured fused step (ViewShardedFitter._graph_build) and its device-side sizing state."""
+
+    def __init__(self):
+        self.graph = None
+        self.key = None
+        self.sched = None
+        self.sched_len = 0
+        self.sched_key = None
+        self.overflows = 0  # steps redone with larger capacities (tests, bench)
+        self.builds = 0  # captures
+        self.inflight = []
+
+
 class ViewShardedFitter:
     """One fit iteration = render own views, backward, one gradient all-reduce, Adam.
 
@@ -320,6 +354,7 @@ class ViewShardedFitter:
 
     def canonical_params(self) -> dict:
         """The parameters in the stub's order (undoes the trainer's Morton permutation)."""
+        self.graph_sync()
         if self.perm is None:
             return self.params
         out = {}
@@ -448,8 +483,10 @@ class ViewShardedFitter:
         if RESORT_EVERY and self.steps_done and self.steps_done % RESORT_EVERY == 0:
             self.respatialize()
         self.steps_done += 1
-        self.opt.zero_grad(set_to_none=True)
         device = self.params["means"].device
+        if self._graph_ok(device):
+            return self._graph_step(device)
+        self.opt.zero_grad(set_to_none=True)
         if self._direct(device) and self.params["means"].shape[0] > 0 and self._fused_step_ok():
             with torch.no_grad():
                 means, scales, colors, opacities = activations(self.params)
@@ -568,7 +605,7 @@ class ViewShardedFitter:
             return self.width * self.height <= NATIVE_EXEC_MAX_PIXELS
         return str(NATIVE_EXEC) not in ("0", "False", "")
 
-    def _views_native(self, means, scales, colors, opacities, depth: bool) -> torch.Tensor:
+    def _views_native(self, means, scales, colors, opacities, depth: bool, sized=None) -> torch.Tensor:
         """_views_direct / _views_direct_depth through the native executor (gr_fit_views): one C call per
         step; returns the sum of the view losses and leaves the stream accumulators in self._acc_parts."""
         device = means.device
@@ -579,7 +616,7 @@ class ViewShardedFitter:
             return torch.zeros((), device=device)
         ns = max(1, min(NUM_STREAMS, len(views)))
         w_sil = self.w_sil if (self.masks is not None and self.w_sil > 0.0) else 0.0
-        key = (tuple(views), depth, F32_GRADE, w_sil > 0.0, str(device))
+        key = (tuple(views), depth, F32_GRADE, w_sil > 0.0, str(device), sized is not None)
         cache = getattr(self, "_native_targets", None)
         if cache is None or cache[0] != key:
             arr = (tr._native.GrFitTarget * len(views))()
@@ -592,15 +629,19 @@ class ViewShardedFitter:
                     if i not in gvd:
                         gvd[i] = tr.make_view(cam.view, cam.proj, self.width, self.height, self._background(device),
                                               depth_grad=True)
-                    arr[j].view = gvd[i]
+                    arr[j].view = gvd[i] if sized is None else tr.sized_view(gvd[i])
                     arr[j].target_depth = self.depths[i].data_ptr()
                 else:
-                    arr[j].view = self._fit_view(i, device)
+                    arr[j].view = self._fit_view(i, device) if sized is None else tr.sized_view(self._fit_view(i, device))
                     arr[j].target_depth = None
                 arr[j].target_rgb = self.targets[i].data_ptr()
                 arr[j].target_mask = self.masks[i].data_ptr() if w_sil > 0.0 else None
             self._native_targets = cache = (key, arr)
         cfg = tr._native.GrFitConfig(NUM_STREAMS, PREP_AHEAD, PREP_GROUP, PREP_FIRST, REDUCE_BATCH, min(REDUCE_TAIL, REDUCE_BATCH))
+        if sized is not None:  # device-side sizing: the capacities, the observed counts, the overflow word
+            cfg.caps = sized.caps_arr
+            cfg.observed = sized.observed.data_ptr()
+            cfg.overflow = sized.ovf.data_ptr()
         if EXEC_STREAMS:
             # the Python schedule's own torch streams: the same hardware-queue placement (stream creation
             # order decides it), so the two schedules differ only in their host code
@@ -634,7 +675,7 @@ class ViewShardedFitter:
         self._native_keep = (m, s, c, o)  # read by the executor's streams until the caller's stream passes them
         return losses_v.sum()
 
-    def _views_direct(self, means, scales, colors, opacities, tail_fn=None):
+    def _views_direct(self, means, scales, colors, opacities, tail_fn=None, sized=None):
         """This rank's views without autograd: per view, gr_fwd_render_l1 (the HIP forward whose epilogue
         evaluates the view's L1 + silhouette loss and its upstream gradients, fit_multiview_stub.py:292-299)
         and gr_bwd_splat (the backward splat, :310); every REDUCE_BATCH views of a HIP stream,
@@ -683,8 +724,13 @@ class ViewShardedFitter:
             bin_stream.wait_stream(main)
         pins = self._plan_pins(len(views))
         ahead: dict = {}
-        prepare_upto = self._prep_groups(views, ahead, lambda js: tr.prepare_views_native(
-            m, s, c, o, [self._fit_view(views[q], device) for q in js], [pins[q] for q in js]), prep)
+        if sized is None:
+            prepare_upto = self._prep_groups(views, ahead, lambda js: tr.prepare_views_native(
+                m, s, c, o, [self._fit_view(views[q], device) for q in js], [pins[q] for q in js]), prep)
+        else:  # device-side sizing (_graph_step): capacities in, true counts to the pinned `observed` rows
+            prepare_upto = self._prep_groups(views, ahead, lambda js: tr.prepare_views_sized(
+                m, s, c, o, [tr.sized_view(self._fit_view(views[q], device)) for q in js], [sized.caps[q] for q in js],
+                [sized.observed[q] for q in js], sized.ovf), prep)
         pending: list = [[] for _ in streams]  # per stream: (render state, partials) awaiting their reduction
         started = [False] * ns
         sizes = _batch_sizes(ns, len(views))
@@ -741,7 +787,7 @@ class ViewShardedFitter:
         self._acc_parts = acc[:used] if used > 0 else [tuple(torch.zeros_like(t) for t in (m, s, c, o))]
         return (losses_v[:len(views)].sum() if views else torch.zeros((), device=device)), tail
 
-    def _views_direct_depth(self, means, scales, colors, opacities) -> torch.Tensor:
+    def _views_direct_depth(self, means, scales, colors, opacities, sized=None) -> torch.Tensor:
         """The fused path with the depth term (fit_multiview_stub.py:301-305): per view the HIP forward in the
         default precision mode (depth output, f32-grade W and D, the depth-gradient footprint), then
         gr_bwd_fit (L1 + silhouette + depth loss gradients and the render backward) adding the gradient into
@@ -782,8 +828,13 @@ class ViewShardedFitter:
                                         depth_grad=True)
             return cache[i]
 
-        prepare_upto = self._prep_groups(views, ahead, lambda js: tr.prepare_views_native(
-            m, s, c, o, [gv_of(views[q]) for q in js], [pins[q] for q in js]), prep)
+        if sized is None:
+            prepare_upto = self._prep_groups(views, ahead, lambda js: tr.prepare_views_native(
+                m, s, c, o, [gv_of(views[q]) for q in js], [pins[q] for q in js]), prep)
+        else:  # device-side sizing (_graph_step)
+            prepare_upto = self._prep_groups(views, ahead, lambda js: tr.prepare_views_sized(
+                m, s, c, o, [tr.sized_view(gv_of(views[q])) for q in js], [sized.caps[q] for q in js],
+                [sized.observed[q] for q in js], sized.ovf), prep)
         # per view its render and the depth-loss backward up to the per-Gaussian sums (gr_bwd_fit_gather); per batch
         # of a stream's views one chain-rule pass (gr_reduce_sums with the depth sums), as _views_direct
         pending: list = [[] for _ in streams]
@@ -840,7 +891,7 @@ class ViewShardedFitter:
         return set(self.params) in ({"means", "scales_raw", "opacities_raw", "colors_raw"},
                                     {"means", "scales_raw", "opacities_raw", "sh_raw"})
 
-    def _fused_param_step(self, scales, opacities, loss) -> torch.Tensor:
+    def _fused_param_step(self, scales, opacities, loss, sized=None) -> torch.Tensor:
         """fit_multiview_stub.py:307-311 after the views: d loss / d raw parameters through the activations
         (softplus + 1e-3, sigmoid, identity) and the regulariser (rank 0), then torch.optim.Adam's update with
         its own state tensors, one gr_fit_param_step pass per parameter (world size 1), or gradient assembly
@@ -870,7 +921,8 @@ class ViewShardedFitter:
                 st["step"] = torch.tensor(0.0, dtype=torch.float32)
                 st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-            st["step"] += 1
+            if sized is None:  # (a captured step: the graph driver advances the host counts per replay)
+                st["step"] += 1
             t = float(st["step"])
             neg_step = -(lr / (1.0 - b1 ** t))
             bc2s = (1.0 - b2 ** t) ** 0.5
@@ -921,8 +973,16 @@ class ViewShardedFitter:
                     e.exp_avg, e.exp_avg_sq = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
                     e.reg = reg.get(k, 0.0) if self.rank == 0 else 0.0
                     e.neg_step_size, e.bias_correction2_sqrt = neg_step, bc2s
-                tr._native.check(L.gr_fit_param_steps(len(plist), arr, ctypes.c_double(b1), ctypes.c_double(b2),
-                                                      ctypes.c_float(eps), stream), "gr_fit_param_steps")
+                if sized is None:
+                    tr._native.check(L.gr_fit_param_steps(len(plist), arr, ctypes.c_double(b1), ctypes.c_double(b2),
+                                                          ctypes.c_float(eps), stream), "gr_fit_param_steps")
+                else:  # the step's scalars from the device table, skipped on overflow (gr_fit_param_steps_sched)
+                    tr._native.check(L.gr_fit_param_steps_sched(
+                        len(plist), arr, ctypes.c_double(b1), ctypes.c_double(b2), ctypes.c_float(eps),
+                        tr._native.ptr(sized.sched), tr._native.ptr(sized.step_dev), tr._native.ptr(sized.ovf),
+                        ctypes.c_void_p(sized.flags.data_ptr()), stream), "gr_fit_param_steps_sched")
+            elif sized is not None:
+                raise RuntimeError("graph step: more parameters or stream accumulators than one gr_fit_param_steps launch")
             else:
                 for call in assembly:
                     call()
@@ -974,10 +1034,195 @@ class ViewShardedFitter:
         self.opt.step()
         return loss_all
 
+    # ---- the fused step as one HIP graph (GR_GRAPH) -------------------------------------------------------------
+    def _graph_ok(self, device) -> bool:
+        """The graph applies: the fused path with its one-launch parameter update (world size 1), the Python
+        schedule without a separate binning stream, and the optimizer state made by an eager step."""
+        if not (GRAPH and self.world == 1 and device.type == "cuda" and BIN_STREAM == "" and self._direct(device)
+                and self.params["means"].shape[0] > 0 and self._fused_step_ok()):
+            return False
+        if min(NUM_STREAMS, len(self.my_views)) > tr._native.FIT_MAX_ACC or len(self.params) > tr._native.FIT_MAX_PARAMS:
+            return False
+        return all(bool(self.opt.state.get(p)) for p in self.params.values())
+
+    def _graph_key(self) -> tuple:
+        g = self.opt.param_groups[0]
+        plist = list(self.params.values())
+        return (tuple((p.data_ptr(), tuple(p.shape)) for p in plist),
+                tuple((self.opt.state[p]["exp_avg"].data_ptr(), self.opt.state[p]["exp_avg_sq"].data_ptr()) for p in plist),
+                float(g["lr"]), tuple(g["betas"]), float(g["eps"]), tuple(self.my_views), self._depth_grad(),
+                self.w_sil, self.w_depth, self.reg_opacity, self.reg_scale, F32_GRADE, FIT_TILE, NUM_STREAMS,
+                tuple(t.data_ptr() for t in self.targets))
+
+    def _probe_counts(self, device) -> list:
+        """Every view of this rank prepared once with host-read plans: [(pairs, slots, core pairs)] per view."""
+        with torch.no_grad():
+            m, s, c, o = (t.detach().float().contiguous() for t in activations(self.params))
+            views = self.my_views
+            pins = torch.zeros((max(1, len(views)), 3), dtype=torch.int64, pin_memory=True)
+            depth = self._depth_grad()
+            for j0 in range(0, len(views), tr._native.PREPARE_MAX_VIEWS):
+                js = range(j0, min(len(views), j0 + tr._native.PREPARE_MAX_VIEWS))
+                gvs = [tr.make_view(self.cams[views[q]].view, self.cams[views[q]].proj, self.width, self.height,
+                                    self._background(device), depth_grad=True) if depth else self._fit_view(views[q], device)
+                       for q in js]
+                tr.prepare_views_native(m, s, c, o, gvs, [pins[q] for q in js])
+            torch.cuda.synchronize(device)
+            return [tuple(int(x) for x in r) for r in pins[:len(views)].tolist()]
+
+    @staticmethod
+    def _caps_of(counts, old=None) -> list:
+        def grow(x):
+            return (int(x * GRAPH_MARGIN) + 4096 + 4095) // 4096 * 4096
+        caps = []
+        for j, (k, _, kc) in enumerate(counts):
+            cc, ct = grow(kc), grow(k - kc)
+            if old is not None:
+                cc, ct = max(cc, int(old[j].num_core_pairs)), max(ct, int(old[j].num_pairs - old[j].num_core_pairs))
+            caps.append(tr._native.GrPlan(cc + ct, cc + ct, cc))
+        return caps
+
+    def _graph_sched(self, device, t0: int):
+        """(neg_step_size, bias_correction2_sqrt) of updates t0+1 .. t0+65536 onward from update 1, as the eager step
+        computes them (same expressions, rounded to float32 as its ctypes arguments): index t = updates applied."""
+        g = self.opt.param_groups[0]
+        lr, (b1, b2) = float(g["lr"]), g["betas"]
+        T = max(1 << 16, 2 * (t0 + 1))
+        tab = np.empty((T, 2), dtype=np.float32)
+        for t in range(T):
+            u = float(t + 1)
+            tab[t, 0] = -(lr / (1.0 - b1 ** u))
+            tab[t, 1] = (1.0 - b2 ** u) ** 0.5
+        return torch.from_numpy(tab.reshape(-1)).to(device), T
+
+    def _graph_body(self, gs):
+        """The fused step (step()'s first branch, eager) on device-sized views, for capture."""
+        with torch.no_grad():
+            means, scales, colors, opacities = activations(self.params)
+            reg_fn = ((lambda: self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean())
+                      if self.rank == 0 else None)
+            if GRAPH_MODE == "exec":  # the native executor with capacities (as step()'s executor branch)
+                total = self._views_native(means, scales, colors, opacities, self._depth_grad(), sized=gs)
+                rs = getattr(self, "_prep", None) if EXEC_STREAMS else None
+                reg = None
+                if reg_fn and rs is not None:
+                    main = torch.cuda.current_stream(means.device)
+                    with torch.cuda.stream(rs):
+                        reg = reg_fn()
+                    reg.record_stream(main)
+                    main.wait_stream(rs)
+                elif reg_fn:
+                    reg = reg_fn()
+            elif self._depth_grad():
+                reg = reg_fn() if reg_fn else None
+                total = self._views_direct_depth(means, scales, colors, opacities, sized=gs)
+            else:
+                total, reg = self._views_direct(means, scales, colors, opacities, reg_fn, sized=gs)
+            loss = total / len(self.targets)
+            if reg is not None:
+                loss = loss + reg
+        return self._fused_param_step(scales, opacities, loss, sized=gs)
+
+    def _graph_build(self, device, counts=None, old_caps=None):
+        """(Re)capture the step: capacities from `counts` (or a probe), the device step counter at the updates applied
+        so far (the optimizer's step count), a fresh schedule table when it runs short."""
+        gs = getattr(self, "_gs", None)
+        if gs is None:
+            gs = self._gs = _GraphState()
+        gs.graph = None
+        n_views = max(1, len(self.my_views))
+        t0 = int(float(self.opt.state[next(iter(self.params.values()))]["step"]))
+        if counts is None:
+            counts = self._probe_counts(device)
+        gs.caps = self._caps_of(counts, old_caps)
+        gs.caps_arr = (tr._native.GrPlan * max(1, len(gs.caps)))(*gs.caps)
+        gs.observed = torch.zeros((n_views, 3), dtype=torch.int64, pin_memory=True)
+        gs.flags = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        gs.ovf = torch.zeros(1, dtype=torch.int32, device=device)
+        gs.step_dev = torch.tensor([t0], dtype=torch.int32, device=device)
+        if gs.sched is None or gs.sched_len < t0 + 1024 or gs.sched_key != self._graph_key()[2:5]:
+            gs.sched, gs.sched_len = self._graph_sched(device, t0)
+            gs.sched_key = self._graph_key()[2:5]
+        gs.done_host = t0
+        torch.cuda.synchronize(device)
+        if GRAPH_CAPTURE:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="relaxed"):
+                gs.loss = self._graph_body(gs)
+        else:  # (diagnostics: the device-sized step without the graph, enqueued by the host every step)
+            g = _EagerReplay(lambda: self._graph_body(gs), gs)
+        gs.graph = g
+        gs.builds += 1
+        gs.key = self._graph_key()
+        gs.n = int(self.params["means"].shape[0])
+        gs.inflight = []
+        return gs
+
+    def _graph_step(self, device) -> torch.Tensor:
+        gs = getattr(self, "_gs", None)
+        if gs is None or gs.graph is None or gs.key != self._graph_key():
+            self.graph_sync()
+            counts = None
+            if gs is not None and gs.graph is not None and gs.n == int(self.params["means"].shape[0]):
+                counts = [tuple(int(x) for x in r) for r in gs.observed[:len(self.my_views)].tolist()]
+            gs = self._graph_build(device, counts)
+        elif int(float(self.opt.state[next(iter(self.params.values()))]["step"])) + 2 >= gs.sched_len:
+            self.graph_sync()
+            gs = self._graph_build(device, [tuple(int(x) for x in r) for r in gs.observed[:len(self.my_views)].tolist()],
+                                   gs.caps)
+        gs.graph.replay()
+        out = gs.loss.detach().clone()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        for p in self.params.values():  # torch.optim.Adam's host step count, as the eager step advances it
+            self.opt.state[p]["step"] += 1
+        gs.inflight.append((out, ev))
+        if len(gs.inflight) > 2:
+            gs.inflight.pop(0)
+        if len(gs.inflight) == 2:  # the previous step (the GPU is busy with this one meanwhile)
+            gs.inflight[0][1].synchronize()
+            self._graph_check(device)
+        return out
+
+    def _graph_check(self, device) -> None:
+        """A replayed step whose views exceeded their capacities updated nothing (and neither did any later one: the
+        parameters did not change): grow the capacities from the true counts, recapture, and redo those steps, their
+        losses written into the tensors step() returned for them."""
+        gs = self._gs
+        while int(gs.flags[0]) != 0:
+            torch.cuda.synchronize(device)
+            done = int(gs.flags[1])
+            applied = int(float(self.opt.state[next(iter(self.params.values()))]["step"]))
+            lost = applied - done
+            redo = gs.inflight[len(gs.inflight) - lost:] if lost > 0 else []
+            counts = [tuple(int(x) for x in r) for r in gs.observed[:len(self.my_views)].tolist()]
+            for p in self.params.values():
+                self.opt.state[p]["step"] -= lost
+            gs.overflows += 1
+            inflight = gs.inflight
+            gs = self._graph_build(device, counts, gs.caps)
+            for out, _ in redo:  # (an overflowing redo updates nothing, nor do the ones after it: counted next round)
+                gs.graph.replay()
+                out.copy_(gs.loss)
+                for p in self.params.values():
+                    self.opt.state[p]["step"] += 1
+            torch.cuda.synchronize(device)
+            gs.inflight = inflight
+
+    def graph_sync(self) -> None:
+        """Wait for the replayed steps and redo any that overflowed (densify, the parameters' readers and the end of a
+        fit call this; a no-op without a graph)."""
+        gs = getattr(self, "_gs", None)
+        if gs is None or gs.graph is None:
+            return
+        torch.cuda.synchronize(self.params["means"].device)
+        self._graph_check(self.params["means"].device)
+
     def densify_and_prune(self, max_gaussians: int, densify_ratio: float, prune_opacity: float,
                           on_device: Optional[bool] = None) -> None:
         """on_device (default: N >= DEVICE_DENSIFY_MIN): the device-side rule with a device generator
         (densify_and_prune_device); otherwise the host rule with the stub's CPU random stream."""
+        self.graph_sync()
         n_now = int(self.params["means"].shape[0])
         if on_device is None:
             on_device = self.params["means"].device.type == "cuda" and n_now >= DEVICE_DENSIFY_MIN

@@ -303,14 +303,17 @@ class Prepared:
     the next view before rendering the current one keeps the device busy while the host reads the
     plan (ViewShardedFitter does this)."""
 
-    __slots__ = ("gv", "n", "geom", "plan_host", "event", "binned", "rendered")
+    __slots__ = ("gv", "n", "geom", "plan_host", "event", "binned", "rendered", "caps")
 
-    def __init__(self, gv, n, geom, plan_host, event):
+    def __init__(self, gv, n, geom, plan_host, event, caps=None):
         self.gv, self.n, self.geom, self.plan_host, self.event = gv, n, geom, plan_host, event
         self.binned = None  # (bins, scratch, binned gr_view, event) when the speculation binned it ahead
         self.rendered = None  # (saved sums, event) when the speculation also rendered it ahead (_render_launch)
+        self.caps = caps  # device-side sizing (prepare_views_sized): the view's capacities, its plan for every later call
 
     def plan(self) -> _native.GrPlan:
+        if self.caps is not None:  # no host read: the counts stay on the device (gr_view.device_counts)
+            return self.caps
         self.event.synchronize()
         pairs, slots, core = (int(x) for x in self.plan_host.tolist())
         if pairs < 0 or slots < 0:
@@ -359,6 +362,44 @@ def prepare_views_native(means, scales, colors, opacities, gvs, plan_hosts) -> l
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
     return [Prepared(gv, n, g, p, ev) for gv, g, p in zip(gvs, geoms, plan_hosts)]
+
+
+def sized_view(gv: _native.GrView) -> _native.GrView:
+    """gv with device_counts = 1 (made once per view structure and kept on it): the view of prepare_views_sized."""
+    b = getattr(gv, "_sized_copy", None)
+    if b is None:
+        b = _native.GrView.from_buffer_copy(gv)
+        b.device_counts = 1
+        gv._sized_copy = b
+    return b
+
+
+def prepare_views_sized(means, scales, colors, opacities, gvs, caps, observed, overflow) -> list:
+    """gr_fwd_prepare_views_sized on the current stream: as prepare_views_native for views with device_counts = 1
+    (sized_view) against per-view capacities ``caps`` (GrPlan each; num_pairs / num_core_pairs bound the view's pairs
+    / core pairs); ``observed``: one pinned int64 tensor of 3 elements per view (or None) receiving the true counts;
+    ``overflow``: a device int32 raised when a view exceeds its capacity (it then renders without pairs).  The
+    returned Prepared hand out their capacities as plans: no host wait anywhere after this call (the fit step can be
+    captured in a graph)."""
+    L = _native.lib()
+    k = len(gvs)
+    if not 1 <= k <= _native.PREPARE_MAX_VIEWS or len(caps) != k or len(observed) != k:
+        raise ValueError(f"1 to {_native.PREPARE_MAX_VIEWS} views, one capacity and one observed buffer each")
+    _check_params(means, scales, colors, opacities)
+    dev = means.device
+    n = int(means.shape[0])
+    nbytes = int(L.gr_geom_bytes(n))
+    geoms = [torch.empty((nbytes,), dtype=torch.uint8, device=dev) for _ in range(k)]
+    views = (_native.GrView * k)(*gvs)
+    capa = (_native.GrPlan * k)(*caps)
+    gptr = (ctypes.c_void_p * k)(*[g.data_ptr() for g in geoms])
+    optr = (ctypes.c_void_p * k)(*[o.data_ptr() if o is not None else None for o in observed])
+    _native.check(L.gr_fwd_prepare_views_sized(k, views, n, _native.ptr(means), _native.ptr(scales), _native.ptr(colors),
+                                               _color_dim(colors), _native.ptr(opacities), gptr, nbytes, capa, optr,
+                                               _native.ptr(overflow), _stream(dev)), "gr_fwd_prepare_views_sized")
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    return [Prepared(gv, n, g, o, ev, caps=c) for gv, g, o, c in zip(gvs, geoms, observed, caps)]
 
 
 def _bin_launch(L, gv, n, plan, prepared, bin_stream, dev):

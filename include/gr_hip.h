@@ -97,6 +97,15 @@ typedef struct gr_view {
                        /* the per-pair gradient rows; supported on the fused fit path only (preparation,  */
                        /* gr_fwd_bin, gr_fwd_render_l1 with no_depth_grad = 1, gr_bwd_splat,               */
                        /* gr_gather_view, gr_reduce_sums); the other entry points reject it.              */
+  int device_counts;   /* 1: the view was prepared by gr_fwd_prepare_views_sized, and every gr_plan passed  */
+                       /* with it holds CAPACITIES (buffer sizes and grids), not the view's counts: the     */
+                       /* kernels read the true pair counts from the device (the preparation's device plan), */
+                       /* so no host read of the counts sits between the preparation and the render (the   */
+                       /* fit step can be captured as one HIP graph).  0 (default): plans are the counts.   */
+  int chunk;           /* work-item length in pairs (a multiple of 64, <= 8192).  0 (default): the largest  */
+                       /* power of two <= num_pairs / 1024 within [512, 2048] (at least ~4 items per CU).    */
+                       /* Each item is one workgroup of the splats; the split tiles' partial sums are added */
+                       /* in item order, so the value changes float rounding, deterministically.            */
 } gr_view;
 
 /* ------------------------------------------------------------------------------------------ */
@@ -142,6 +151,19 @@ gr_status gr_fwd_prepare_views_async(int num_views, const gr_view* views, int n,
                                      const float* scales, const float* colors, int color_dim,
                                      const float* opacities, void* const* geoms, size_t geom_bytes,
                                      gr_plan* const* plans, void* stream);
+
+/* Device-side sizing: gr_fwd_prepare_views_async against per-view CAPACITIES caps[k] (num_pairs: all pairs,
+ * num_core_pairs: core pairs; the tail capacity is their difference), for views with device_counts = 1.  The true
+ * counts go to the device plan (read by the binning and the splats) and, when observed[k] is non-NULL (pinned host
+ * memory), to observed[k] (the caller's next capacities).  A view whose core or tail pairs exceed its capacity is
+ * rendered as a view without pairs (background, zero gradients: no kernel reads or writes past a capacity) and sets
+ * *overflow (device int) to 1: a caller redoes such a step with larger capacities (gr_fit_param_steps_sched skips
+ * its update).  The downstream calls (gr_fwd_bin, gr_fwd_render(_l1), gr_bwd*, gr_gather_view, ...) take caps[k]
+ * as their plan.  Needs the counting-sort binning (at most 8,192 screen tiles). */
+gr_status gr_fwd_prepare_views_sized(int num_views, const gr_view* views, int n, const float* means,
+                                     const float* scales, const float* colors, int color_dim,
+                                     const float* opacities, void* const* geoms, size_t geom_bytes,
+                                     const gr_plan* caps, gr_plan* const* observed, int* overflow, void* stream);
 
 /* Tile-sorted (tile, Gaussian) pair lists, per-tile ranges and work items. */
 size_t gr_bins_bytes(const gr_view* v, int n, const gr_plan* plan);
@@ -344,6 +366,13 @@ typedef struct gr_fit_config {
    * ones first. */
   void* const* render_streams;
   void* prep_stream;
+  /* Device-side sizing (optional; NULL: the host reads each view's plan before sizing its render): per view its
+   * capacities (gr_fwd_prepare_views_sized; the views must have device_counts = 1), the pinned rows receiving the
+   * true counts (may be NULL) and the device int raised when a view exceeds its capacities.  No host wait in the
+   * call then: the host enqueues the whole step while the device runs it. */
+  const gr_plan* caps;
+  gr_plan* observed;
+  int* overflow;
 } gr_fit_config;
 gr_status gr_executor_create(int device, gr_executor** executor);
 void gr_executor_destroy(gr_executor* executor);
@@ -411,6 +440,14 @@ typedef struct gr_param_step {
   float bias_correction2_sqrt;
 } gr_param_step;
 gr_status gr_fit_param_steps(int num, const gr_param_step* steps, double beta1, double beta2, float eps, void* stream);
+/* gr_fit_param_steps with the step's Adam scalars and its validity on the device, so that a step captured once (HIP
+ * graph) can be replayed: each entry's neg_step_size / bias_correction2_sqrt are replaced by sched[2t], sched[2t+1]
+ * with t = *step_dev (the updates applied so far; sched holds them for every step the caller may run), and nothing is
+ * updated when *overflow != 0 (a view of the step exceeded its capacity: gr_fwd_prepare_views_sized).  After the
+ * update one thread advances *step_dev (no overflow) or raises host_flags[0] (overflow, sticky: the caller clears
+ * it), mirrors *step_dev to host_flags[1] and clears *overflow for the next step.  host_flags: pinned host int[2]. */
+gr_status gr_fit_param_steps_sched(int num, const gr_param_step* steps, double beta1, double beta2, float eps,
+                                   const float* sched, int* step_dev, int* overflow, int* host_flags, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Introspection (host-only, no GPU needed).                                                  */

@@ -41,6 +41,8 @@ class GrView(ctypes.Structure):
         ("background_dev", ctypes.c_void_p),  # product only (device background); the oracle reads background
         ("binned", ctypes.c_int),  # product only (gr_fwd_bin ran); the oracle always bins
         ("tile", ctypes.c_int),  # tile edge of the binned semantics: 0/16 or 32
+        ("device_counts", ctypes.c_int),  # (the HIP path's device-side sizing; the oracle ignores it)
+        ("chunk", ctypes.c_int),  # (the HIP path's work-item length; the oracle ignores it)
     ]
 
 

@@ -199,9 +199,11 @@ def test_f32_grade_fit_mode(cuda):
     targets = [torch.rand((Ht, Wt, 3), generator=g, device=cuda) for _ in cams]
     masks = [(t.mean(dim=2) > 0.5).float() for t in targets]
     out = {}
+    # both modes at 16-pixel tiles (the f32-grade mode's): the two-piece splits are what differs, not the per-tile
+    # culling (the 32-pixel fit path is pinned against the oracle at its own tile size in test_tile32_gpu.py)
     for f32 in (False, True):
-        saved = fm.F32_GRADE
-        fm.F32_GRADE = f32
+        saved = fm.F32_GRADE, fm.FIT_TILE
+        fm.F32_GRADE, fm.FIT_TILE = f32, 16
         try:
             f = fm.ViewShardedFitter(bench.synthetic_params(40_000, cuda), cams, targets, Wt, Ht, masks=masks)
             with torch.no_grad():
@@ -211,7 +213,7 @@ def test_f32_grade_fit_mode(cuda):
                 acc = [sum(p[q] for p in parts[1:]) + parts[0][q] if len(parts) > 1 else parts[0][q] for q in range(4)]
             out[f32] = (total, [a.cpu().numpy() for a in acc], acts)
         finally:
-            fm.F32_GRADE = saved
+            fm.F32_GRADE, fm.FIT_TILE = saved
     sc = orc.Scene(*(a.cpu().numpy() for a in out[True][2]))
     ora = None
     for i, (view, proj) in enumerate(orc.orbit_cameras(6, Wt, Ht)):

@@ -39,7 +39,7 @@ def params_for(n, sh, dev):
     return p
 
 
-def run(name, steps):
+def run(name, steps, warmup=2):
     c = CONFIGS[name]
     dev = torch.device("cuda:0")
     params = params_for(c["n"], c["sh"], dev)
@@ -49,7 +49,8 @@ def run(name, steps):
     masks = [(t.mean(dim=2) > 0.5).float() for t in targets]
     depths = [torch.rand((c["h"], c["w"]), generator=g, device=dev) for _ in range(c["views"])] if c["depth"] else None
     fitter = fm.ViewShardedFitter(params, cams, targets, c["w"], c["h"], lr=0.02, masks=masks, depths=depths)
-    fitter.step()
+    for _ in range(warmup):  # as bench.py's default warmup (the first steps grow the allocator's pools)
+        fitter.step()
     torch.cuda.synchronize()
     dens = c.get("densify")
     n_dens = 0
@@ -63,7 +64,7 @@ def run(name, steps):
     dt = time.perf_counter() - t0
     px = c["views"] * c["w"] * c["h"] * steps
     print(json.dumps({"config": name, "gaussians": c["n"], "views": c["views"], "width": c["w"], "height": c["h"],
-                      "sh_degree": c["sh"] or None, "depth_loss": c["depth"], "steps": steps,
+                      "sh_degree": c["sh"] or None, "depth_loss": c["depth"], "steps": steps, "warmup": warmup,
                       "ms_per_step": round(1e3 * dt / steps, 2), "mpx_per_s": round(px / dt / 1e6, 1),
                       "loss": float(loss), "streams": fm.NUM_STREAMS, "densify_calls": n_dens,
                       "gaussians_at_end": int(fitter.params["means"].shape[0])}), flush=True)
@@ -72,6 +73,7 @@ def run(name, steps):
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 3
+    warmup = int(sys.argv[sys.argv.index("--warmup") + 1]) if "--warmup" in sys.argv else 2
     for name in (args or ["C2", "C3", "C5", "C5d"]):
         if name in CONFIGS:
-            run(name, steps)
+            run(name, steps, warmup)
