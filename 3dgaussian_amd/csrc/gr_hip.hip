@@ -2650,7 +2650,7 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
 }
 
 #ifndef GR_BF16_WAVES
-#define GR_BF16_WAVES 2
+#define GR_BF16_WAVES 3  // 168 VGPRs (one spilled) instead of 170 at 2 waves: default mode +3.5% (C4d 600 -> 619)
 #endif
 #ifndef GR_BF16_WAVES_ND
 #define GR_BF16_WAVES_ND 2

@@ -13,15 +13,14 @@ Synthetic data (no network): means ~ U(-0.6,0.6)^3, opacity sigmoid(-2.2), colou
 density-matched scale 0.1061*(1200/N)^(1/3); targets are seeded random images.
 
 Also reported on rank 0:
-  roofline      the dominant kernel (the splat kernel with the longer launches, forward or backward; both
-                under "splats") against the HBM roofline: SURVEY.md 8(d)'s algorithmic bytes per unit
-                (48 B per pair forward, 84 B per core pair backward, + 40 B per pixel) x the units of one
-                launch / its average launch time (HIP events on its launch stream, gr_profile_begin/end,
-                over one single-stream step after the timed region: the timed steps overlap views on 4
-                streams and run uninstrumented; the events bracket the launch and so include its dispatch
-                gap, yet agree with rocprofv3's kernel-trace average of the same kernel within 2%: r04e
-                backward 189.5 us by events vs 192.2 us by rocprofv3 in the same gpurun call), vs 8 TB/s; its PMC HBM traffic from profiles/pmc_traffic.json
-                (tools/pmc_traffic.py); the executed bf16 MFMA rate beside it
+  roofline      the dominant kernel (the backward splat; both splats under "splats"): at 32-pixel tiles its
+                executed 16-bit MFMA FLOP/s against the dense bf16 peak (48 v_mfma_f32_32x32x16 per 32 pairs),
+                with SURVEY.md 8(d)'s byte model beside it under "hbm" (48 B per pair forward, 84 B per pair
+                backward, + 40 B per pixel, vs 8 TB/s); the launch time from splat_replay (HIP events around each
+                launch in a single-stream schedule after the timed region, less an empty event pair's cost: the
+                timed steps overlap views on 4 streams and run uninstrumented), which agrees with the GR_STREAMS=1
+                rocprofv3 kernel-trace average in profiles/ (r05: 209.6 vs 206.0 us); PMC HBM traffic and
+                VALU / MFMA busy fractions from profiles/pmc_traffic.json when its source stamp matches
   hbm_model     the north_star's framing: SURVEY.md 8(d)'s byte model of the tile-binned path per view at
                 this run's pair count (the fit path bins the survey's 5-sigma footprint), the bench value
                 as a fraction of that 8 TB/s roofline and of the survey table's C4 roof (2,830 Mpx/s)
@@ -519,7 +518,8 @@ def main():
     if not args.no_extra_modes:
         gd = torch.Generator(device=device).manual_seed(2)
         fitter.depths = [torch.rand((R, R), generator=gd, device=device) for _ in range(V)]
-        fitter.step()
+        for _ in range(max(1, args.warmup)):  # the depth path's larger workspaces: warmed up as the headline's
+            fitter.step()
         k = max(1, min(args.steps, 5))
         dt, _ = timed(k)
         fitter.depths = None
@@ -528,7 +528,8 @@ def main():
                          "pairs; loss L1 + silhouette + 0.05 depth L1 (fit_multiview_stub.py:299-305)"}
         # the headline's own loss and footprint with every splat at f32 grade (no_depth_grad = 2)
         fm.F32_GRADE = True
-        fitter.step()
+        for _ in range(max(1, args.warmup)):
+            fitter.step()
         dt, _ = timed(k)
         fm.F32_GRADE = False
         f32g = {"value": round(V * R * R * k / dt / 1e6, 2), "steps": k, "ms_per_step": round(1e3 * dt / k, 3),

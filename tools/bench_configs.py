@@ -3,6 +3,7 @@
   C2  100k Gaussians, 8 orbit views, 512x512, L1 + silhouette
   C3  50k Gaussians, SH degree 3, 8 orbit views, 256x256, L1 + silhouette + depth losses
   C5  3M Gaussians, 100 orbit views, 1920x1080, L1 + silhouette (1-GPU share of the 8-GPU config)
+  C4d the C4 workload with the depth term (bench.py's default_precision_mode)
   C5d the C5 densify/prune loop: starts at 2.7M Gaussians and densifies (ratio 0.15, prune opacity 0.05,
       device rule, Morton re-layout, Adam reset; fit_multiview_stub.py:318-325) every 2 steps to 3M, the
       densify steps inside the timed region
@@ -22,6 +23,7 @@ CONFIGS = {
     "C2": dict(n=100_000, views=8, w=512, h=512, sh=0, depth=False),
     "C3": dict(n=50_000, views=8, w=256, h=256, sh=3, depth=True),
     "C5": dict(n=3_000_000, views=100, w=1920, h=1080, sh=0, depth=False),
+    "C4d": dict(n=1_000_000, views=50, w=800, h=800, sh=0, depth=True),  # bench.py's default_precision_mode workload
     "C5d": dict(n=2_700_000, views=100, w=1920, h=1080, sh=0, depth=False,
                 densify=dict(every=2, max_gaussians=3_000_000, ratio=0.15, prune=0.05)),
 }
