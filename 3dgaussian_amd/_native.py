@@ -73,7 +73,7 @@ class GrPlan(ctypes.Structure):
 
 CAMERA_GRADS = 35  # GR_CAMERA_GRADS: d view (16), d proj (16), d cam_pos (3)
 REDUCE_MAX_VIEWS = 16  # GR_REDUCE_MAX_VIEWS
-PREPARE_MAX_VIEWS = 4  # GR_PREPARE_MAX_VIEWS
+PREPARE_MAX_VIEWS = 8  # GR_PREPARE_MAX_VIEWS
 
 
 class GrReduceView(ctypes.Structure):
@@ -118,6 +118,19 @@ class GrParamStep(ctypes.Structure):
                 ("bias_correction2_sqrt", ctypes.c_float)]
 
 
+BATCH_MAX_VIEWS = 8  # GR_BATCH_MAX_VIEWS
+
+
+class GrBatchView(ctypes.Structure):
+    """gr_batch_view (include/gr_hip.h): one view of a gr_fit_views_batched call."""
+
+    _fields_ = [("view", GrView), ("plan", GrPlan), ("geom", ctypes.c_void_p), ("bins", ctypes.c_void_p),
+                ("bins_bytes", ctypes.c_size_t), ("scratch", ctypes.c_void_p), ("scratch_bytes", ctypes.c_size_t),
+                ("ws", ctypes.c_void_p), ("ws_bytes", ctypes.c_size_t), ("saved", ctypes.c_void_p),
+                ("target_rgb", ctypes.c_void_p), ("target_mask", ctypes.c_void_p), ("target_depth", ctypes.c_void_p),
+                ("sums", ctypes.c_void_p), ("sums3", ctypes.c_void_p), ("loss", ctypes.c_void_p)]
+
+
 class NativeLibraryError(ImportError):
     pass
 
@@ -137,6 +150,8 @@ _SIG = {
     "gr_fwd_prepare_views_sized": (ctypes.c_int, [ctypes.c_int, _VP, ctypes.c_int, _P, _P, _P, ctypes.c_int, _P,
                                                   ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, _PP,
                                                   ctypes.POINTER(ctypes.c_void_p), _P, _P]),
+    "gr_fit_views_batched": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(GrBatchView), ctypes.c_int, ctypes.c_float,
+                                            ctypes.c_float, ctypes.c_float, _P]),
     "gr_bins_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),
     "gr_saved_floats": (ctypes.c_size_t, [_VP]),
     "gr_fwd_scratch_bytes": (ctypes.c_size_t, [_VP, ctypes.c_int, _PP]),

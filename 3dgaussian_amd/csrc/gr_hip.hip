@@ -896,11 +896,35 @@ __global__ __launch_bounds__(256) void k_emit_zones(ViewK v, int n, const int4* 
 // (Counting the pairs per column here as well, in an LDS histogram flushed with atomics, doubled the kernel's VALU
 // work and bank conflicts and cost more than the counting pass it saved: profiles/r04r_pmc_bin.txt.)
 // Block 0 also zeroes the finished-tile fan-in's counters (`fan`), which the column scan's fan-in uses first.
+// ---- Batched launches (gr_fit_views_batched) -----------------------------------------------------------------------
+// A kernel's blocks for several views of the same image size in ONE launch: block b belongs to the view whose block
+// range [first[v], first[v + 1]) holds it and runs exactly as block b - first[v] of that view's own launch (a per-view
+// grid of gx x (count / gx) blocks), with that view's arguments.  Small views (C2, C3: ~300 work items per splat, a
+// few hundred blocks per binning kernel) leave most CUs idle per launch; eight views per launch fill them.  The kernel
+// bodies take blockIdx / gridDim as parameters (shadowing the builtins), so the single-view launch is the same code.
+constexpr int GR_BATCH_MAX = 8;
+struct BI {
+  int x, y;
+};
+template <class A>
+struct VBatch {
+  int nv;
+  int first[GR_BATCH_MAX + 1];
+  int gx[GR_BATCH_MAX];
+  A a[GR_BATCH_MAX];
+};
+template <class A>
+__device__ __forceinline__ int vbatch_view(const VBatch<A>& B, int b) {
+  int v = 0;
+  while (v + 1 < B.nv && b >= B.first[v + 1]) ++v;
+  return v;
+}
+
 constexpr int EWIN_BLK = 4096;  // pairs staged in LDS per block
-__global__ __launch_bounds__(256) void k_emit_offsets(ViewK v, int n, const int4* __restrict__ rect, const Cnt2* __restrict__ counts,
+__device__ __forceinline__ void k_emit_offsets_body(ViewK v, int n, const int4* __restrict__ rect, const Cnt2* __restrict__ counts,
                                                       const unsigned long long* __restrict__ bsum, Cnt2* __restrict__ offsets,
                                                       const float4* __restrict__ rec, uint16_t* __restrict__ keys,
-                                                      int* __restrict__ ids, int* __restrict__ fan) {
+                                                      int* __restrict__ ids, int* __restrict__ fan, const BI blockIdx, const BI gridDim) {
   __shared__ int sI[EWIN_BLK];
   __shared__ uint16_t sK[EWIN_BLK];
   __shared__ unsigned long long wsum[4];
@@ -951,6 +975,31 @@ __global__ __launch_bounds__(256) void k_emit_offsets(ViewK v, int n, const int4
     ids[k] = sI[e];
   }
 }
+__global__ __launch_bounds__(256) void k_emit_offsets(ViewK v, int n, const int4* __restrict__ rect, const Cnt2* __restrict__ counts,
+                                                      const unsigned long long* __restrict__ bsum, Cnt2* __restrict__ offsets,
+                                                      const float4* __restrict__ rec, uint16_t* __restrict__ keys,
+                                                      int* __restrict__ ids, int* __restrict__ fan) {
+  k_emit_offsets_body(v, n, rect, counts, bsum, offsets, rec, keys, ids, fan, BI{(int)blockIdx.x, (int)blockIdx.y}, BI{(int)gridDim.x, (int)gridDim.y});
+}
+struct k_emit_offsets_args {
+  ViewK v;
+  int n;
+  const int4* rect;
+  const Cnt2* counts;
+  const unsigned long long* bsum;
+  Cnt2* offsets;
+  const float4* rec;
+  uint16_t* keys;
+  int* ids;
+  int* fan;
+};
+__global__ __launch_bounds__(256) void k_emit_offsets_views(VBatch<k_emit_offsets_args> B) {
+  const int vb = vbatch_view(B, (int)blockIdx.x);
+  const k_emit_offsets_args& a = B.a[vb];
+  const int lb = (int)blockIdx.x - B.first[vb], gx = B.gx[vb];
+  k_emit_offsets_body(a.v, a.n, a.rect, a.counts, a.bsum, a.offsets, a.rec, a.keys, a.ids, a.fan, BI{lb % gx, lb / gx}, BI{gx, (B.first[vb + 1] - B.first[vb]) / gx});
+}
+
 
 // Radix-sort path: the sorted (id, emission index) values -> the Gaussian ids and the sorted position of
 // each pair by emission index (the counting sort writes both in k_tile_place).
@@ -1217,7 +1266,7 @@ __device__ __forceinline__ void column_range(const TZones& Z, int64_t K, int c, 
 
 // Per-column tile counts M[c][t]: one block per (region, column), the column's keys read once (coalesced, eight
 // loads in flight per thread) into an LDS histogram.
-__global__ __launch_bounds__(256) void k_tile_count(TZones Z, int tiles) {
+__device__ __forceinline__ void k_tile_count_body(TZones Z, int tiles, const BI blockIdx, const BI gridDim) {
   extern __shared__ int hist[];
   int c;
   const int zone = tzone_of(Z, (int)blockIdx.x, c);
@@ -1238,6 +1287,20 @@ __global__ __launch_bounds__(256) void k_tile_count(TZones Z, int tiles) {
   __syncthreads();
   for (int t = threadIdx.x; t < tiles; t += 256) zz.M[(size_t)c * tiles + t] = hist[t];
 }
+__global__ __launch_bounds__(256) void k_tile_count(TZones Z, int tiles) {
+  k_tile_count_body(Z, tiles, BI{(int)blockIdx.x, (int)blockIdx.y}, BI{(int)gridDim.x, (int)gridDim.y});
+}
+struct k_tile_count_args {
+  TZones Z;
+  int tiles;
+};
+__global__ __launch_bounds__(256) void k_tile_count_views(VBatch<k_tile_count_args> B) {
+  const int vb = vbatch_view(B, (int)blockIdx.x);
+  const k_tile_count_args& a = B.a[vb];
+  const int lb = (int)blockIdx.x - B.first[vb], gx = B.gx[vb];
+  k_tile_count_body(a.Z, a.tiles, BI{lb % gx, lb / gx}, BI{gx, (B.first[vb + 1] - B.first[vb]) / gx});
+}
+
 
 // Column scan of M: S[c][t] = sum of M[c'][t] over c' < c, T[t] = the tile's total.  A block takes
 // CS_T tiles x CS_G column groups; a thread's column run (up to CS_R of them) is loaded at once and kept
@@ -1256,14 +1319,14 @@ __global__ __launch_bounds__(256) void k_tile_count(TZones Z, int tiles) {
 #endif
 constexpr int CS_T = GR_CS_T, CS_G = GR_CS_THREADS / GR_CS_T, CS_R = GR_CS_R;
 
-__device__ __forceinline__ void tile_colscan_block(const TZone& zz, int tiles) {
+__device__ __forceinline__ void tile_colscan_block(const TZone& zz, int tiles, int bx) {
   const int cols = zz.cols;
   const int* __restrict__ M = zz.M;
   int* __restrict__ S = zz.S;
   int* __restrict__ T = zz.T;
   __shared__ int part[CS_G][CS_T + 1];
   const int tl = (int)threadIdx.x % CS_T, g = (int)threadIdx.x / CS_T;
-  const int t = (int)blockIdx.x * CS_T + tl;
+  const int t = bx * CS_T + tl;
   const int per = (cols + CS_G - 1) / CS_G;
   const int c0 = min(cols, g * per), c1 = min(cols, c0 + per);
   const bool regs = per <= CS_R;  // uniform
@@ -1319,18 +1382,39 @@ __device__ void work_items_zones(int tiles, int Kc, const int* __restrict__ Tc, 
                                  int* __restrict__ tile_item0, int* __restrict__ ticket, int ch);
 // ... and the block that finishes last (arrive_last_of over the grid) scans the tile totals into the per-virtual-tile
 // ranges and cuts the work items (work_items_zones): no launch of its own between the scan and the placement.
-__global__ __launch_bounds__(GR_CS_THREADS) void k_tile_colscan(TZones Z, int tiles, int2* __restrict__ ranges,
+__device__ __forceinline__ void k_tile_colscan_body(TZones Z, int tiles, int2* __restrict__ ranges,
                                                              int4* __restrict__ items, int* __restrict__ num_items,
-                                                             int* __restrict__ tile_item0, int* __restrict__ ticket) {
+                                                             int* __restrict__ tile_item0, int* __restrict__ ticket, const BI blockIdx, const BI gridDim) {
   __shared__ int last;
   const TZone zz = zone_at(Z, (int)blockIdx.y);
-  if (zz.K > 0) tile_colscan_block(zz, tiles);  // (an empty region: no counts, and the work items get no totals for it)
+  if (zz.K > 0) tile_colscan_block(zz, tiles, (int)blockIdx.x);  // (an empty region: no counts, and the work items get no totals for it)
   const int nb = (int)(gridDim.x * gridDim.y);
   if (!arrive_last_of(ticket + fan_offset(tiles), nb, (int)(blockIdx.y * gridDim.x + blockIdx.x), &last)) return;
   const TZone z0 = zone_at(Z, 0), z1 = zone_at(Z, 1);
   work_items_zones<true, GR_CS_THREADS>(tiles, z1.zbase, z0.K > 0 ? z0.T : nullptr, z1.K > 0 ? z1.T : nullptr,
                                   ranges, items, num_items, tile_item0, ticket, Z.ch);
 }
+__global__ __launch_bounds__(GR_CS_THREADS) void k_tile_colscan(TZones Z, int tiles, int2* __restrict__ ranges,
+                                                             int4* __restrict__ items, int* __restrict__ num_items,
+                                                             int* __restrict__ tile_item0, int* __restrict__ ticket) {
+  k_tile_colscan_body(Z, tiles, ranges, items, num_items, tile_item0, ticket, BI{(int)blockIdx.x, (int)blockIdx.y}, BI{(int)gridDim.x, (int)gridDim.y});
+}
+struct k_tile_colscan_args {
+  TZones Z;
+  int tiles;
+  int2* ranges;
+  int4* items;
+  int* num_items;
+  int* tile_item0;
+  int* ticket;
+};
+__global__ __launch_bounds__(GR_CS_THREADS) void k_tile_colscan_views(VBatch<k_tile_colscan_args> B) {
+  const int vb = vbatch_view(B, (int)blockIdx.x);
+  const k_tile_colscan_args& a = B.a[vb];
+  const int lb = (int)blockIdx.x - B.first[vb], gx = B.gx[vb];
+  k_tile_colscan_body(a.Z, a.tiles, a.ranges, a.items, a.num_items, a.tile_item0, a.ticket, BI{lb % gx, lb / gx}, BI{gx, (B.first[vb + 1] - B.first[vb]) / gx});
+}
+
 
 
 __device__ __forceinline__ void ts_load(int64_t kb, int64_t k1, int64_t klast, int lane, const uint16_t* __restrict__ keys,
@@ -1469,9 +1553,9 @@ __device__ void work_items_zones(int tiles, int Kc, const int* __restrict__ Tc, 
 #endif
 constexpr int TS_CQ = 8;  // tiles per thread per round of k_tile_place's cursor pass
 template <int WAVES>
-__global__ __launch_bounds__(64 * WAVES, GR_PLACE_WAVES) void k_tile_place(TZones Z, int tiles, int bits,
+__device__ __forceinline__ void k_tile_place_body(TZones Z, int tiles, int bits,
                                                                     const int2* __restrict__ ranges,
-                                                                    int* __restrict__ pairs_out, int* __restrict__ pos_of) {
+                                                                    int* __restrict__ pairs_out, int* __restrict__ pos_of, const BI blockIdx, const BI gridDim) {
   extern __shared__ int cur[];  // [WAVES][tiles]
   constexpr int NT = 64 * WAVES;
   int c;
@@ -1542,6 +1626,28 @@ __global__ __launch_bounds__(64 * WAVES, GR_PLACE_WAVES) void k_tile_place(TZone
     }
   }
 }
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES, GR_PLACE_WAVES) void k_tile_place(TZones Z, int tiles, int bits,
+                                                                    const int2* __restrict__ ranges,
+                                                                    int* __restrict__ pairs_out, int* __restrict__ pos_of) {
+  k_tile_place_body<WAVES>(Z, tiles, bits, ranges, pairs_out, pos_of, BI{(int)blockIdx.x, (int)blockIdx.y}, BI{(int)gridDim.x, (int)gridDim.y});
+}
+struct k_tile_place_args {
+  TZones Z;
+  int tiles;
+  int bits;
+  const int2* ranges;
+  int* pairs_out;
+  int* pos_of;
+};
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES, GR_PLACE_WAVES) void k_tile_place_views(VBatch<k_tile_place_args> B) {
+  const int vb = vbatch_view(B, (int)blockIdx.x);
+  const k_tile_place_args& a = B.a[vb];
+  const int lb = (int)blockIdx.x - B.first[vb], gx = B.gx[vb];
+  k_tile_place_body<WAVES>(a.Z, a.tiles, a.bits, a.ranges, a.pairs_out, a.pos_of, BI{lb % gx, lb / gx}, BI{gx, (B.first[vb + 1] - B.first[vb]) / gx});
+}
+
 
 // Exact three-way bf16 split: x = hi + mid + lo, each a truncated bf16 (hi keeps 8 significant bits,
 // the f32 remainders are exact), returned as f32 values whose low 16 bits are zero.
@@ -2060,9 +2166,9 @@ __device__ __forceinline__ float saved_depth(const float4* __restrict__ saved4, 
 }
 
 // Per tile the depth maximum; the last tile to finish (arrive_last_tile) takes the image's.
-__global__ __launch_bounds__(256) void k_depth_tile_max(ViewK v, const float4* __restrict__ saved4,
+__device__ __forceinline__ void k_depth_tile_max_body(ViewK v, const float4* __restrict__ saved4,
                                                         const float* __restrict__ savedD, float* __restrict__ tile_aux,
-                                                        float* __restrict__ dscal, int* __restrict__ ticket) {
+                                                        float* __restrict__ dscal, int* __restrict__ ticket, const BI blockIdx, const BI gridDim) {
   const int tile = blockIdx.x, tid = threadIdx.x, tiles = v.tiles_x * v.tiles_y;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
@@ -2083,16 +2189,36 @@ __global__ __launch_bounds__(256) void k_depth_tile_max(ViewK v, const float4* _
   __syncthreads();
   if (tid == 0) dscal[0] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
 }
+__global__ __launch_bounds__(256) void k_depth_tile_max(ViewK v, const float4* __restrict__ saved4,
+                                                        const float* __restrict__ savedD, float* __restrict__ tile_aux,
+                                                        float* __restrict__ dscal, int* __restrict__ ticket) {
+  k_depth_tile_max_body(v, saved4, savedD, tile_aux, dscal, ticket, BI{(int)blockIdx.x, (int)blockIdx.y}, BI{(int)gridDim.x, (int)gridDim.y});
+}
+struct k_depth_tile_max_args {
+  ViewK v;
+  const float4* saved4;
+  const float* savedD;
+  float* tile_aux;
+  float* dscal;
+  int* ticket;
+};
+__global__ __launch_bounds__(256) void k_depth_tile_max_views(VBatch<k_depth_tile_max_args> B) {
+  const int vb = vbatch_view(B, (int)blockIdx.x);
+  const k_depth_tile_max_args& a = B.a[vb];
+  const int lb = (int)blockIdx.x - B.first[vb], gx = B.gx[vb];
+  k_depth_tile_max_body(a.v, a.saved4, a.savedD, a.tile_aux, a.dscal, a.ticket, BI{lb % gx, lb / gx}, BI{gx, (B.first[vb + 1] - B.first[vb]) / gx});
+}
+
 
 __device__ void depth_final(const float* __restrict__ tile_loss, const float* __restrict__ tile_aux, int tiles, int64_t HW,
                             float w_depth, float g_scale, float* __restrict__ dscal, double (*r)[256]);
 // Per tile the depth loss's sums; the last tile to finish (arrive_last_tile) turns them into the max's
 // gradient per arg-max pixel (depth_final).
-__global__ __launch_bounds__(256) void k_depth_tile_sums(ViewK v, const float4* __restrict__ saved4,
+__device__ __forceinline__ void k_depth_tile_sums_body(ViewK v, const float4* __restrict__ saved4,
                                                          const float* __restrict__ savedD, const float* __restrict__ t_depth,
                                                          float* __restrict__ dscal, float* __restrict__ tile_loss,
                                                          float* __restrict__ tile_aux, int64_t HW, float w_depth,
-                                                         float g_scale, int* __restrict__ ticket) {
+                                                         float g_scale, int* __restrict__ ticket, const BI blockIdx, const BI gridDim) {
   const int tile = blockIdx.x, tid = threadIdx.x;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
@@ -2129,6 +2255,33 @@ __global__ __launch_bounds__(256) void k_depth_tile_sums(ViewK v, const float4* 
   if (!arrive_last_tile(ticket, tiles, tile, &last)) return;
   depth_final(tile_loss, tile_aux, tiles, HW, w_depth, g_scale, dscal, r);
 }
+__global__ __launch_bounds__(256) void k_depth_tile_sums(ViewK v, const float4* __restrict__ saved4,
+                                                         const float* __restrict__ savedD, const float* __restrict__ t_depth,
+                                                         float* __restrict__ dscal, float* __restrict__ tile_loss,
+                                                         float* __restrict__ tile_aux, int64_t HW, float w_depth,
+                                                         float g_scale, int* __restrict__ ticket) {
+  k_depth_tile_sums_body(v, saved4, savedD, t_depth, dscal, tile_loss, tile_aux, HW, w_depth, g_scale, ticket, BI{(int)blockIdx.x, (int)blockIdx.y}, BI{(int)gridDim.x, (int)gridDim.y});
+}
+struct k_depth_tile_sums_args {
+  ViewK v;
+  const float4* saved4;
+  const float* savedD;
+  const float* t_depth;
+  float* dscal;
+  float* tile_loss;
+  float* tile_aux;
+  int64_t HW;
+  float w_depth;
+  float g_scale;
+  int* ticket;
+};
+__global__ __launch_bounds__(256) void k_depth_tile_sums_views(VBatch<k_depth_tile_sums_args> B) {
+  const int vb = vbatch_view(B, (int)blockIdx.x);
+  const k_depth_tile_sums_args& a = B.a[vb];
+  const int lb = (int)blockIdx.x - B.first[vb], gx = B.gx[vb];
+  k_depth_tile_sums_body(a.v, a.saved4, a.savedD, a.t_depth, a.dscal, a.tile_loss, a.tile_aux, a.HW, a.w_depth, a.g_scale, a.ticket, BI{lb % gx, lb / gx}, BI{gx, (B.first[vb + 1] - B.first[vb]) / gx});
+}
+
 
 // dscal[1] = -(w_depth g_scale / HW) sum_p sign(.) (d_p / dm) / dm / (number of arg-max pixels), from the tiles'
 // write-through sums (the last tile of k_depth_tile_sums)
@@ -2214,11 +2367,11 @@ __device__ __forceinline__ void tile_fragments(const float (*sU)[TP], uint4* __r
 }
 
 // With the fit loss (l1.t_rgb) the last tile to finish (arrive_last_tile) also writes the view loss.
-__global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __restrict__ saved4,
+__device__ __forceinline__ void k_pixel_grads_body(ViewK v, const float4* __restrict__ saved4,
                                                      const float* __restrict__ savedD, const float* __restrict__ g_rgb,
                                                      const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
                                                      uint4* __restrict__ UF, int pieces, L1Args l1, bool depth,
-                                                     int* __restrict__ ticket) {
+                                                     int* __restrict__ ticket, const BI blockIdx, const BI gridDim) {
   const int tile = blockIdx.x, tid = threadIdx.x;
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
@@ -2244,6 +2397,33 @@ __global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __re
                             l1.loss_out, reinterpret_cast<double (*)[256]>(&sU[0][0]));
   }
 }
+__global__ __launch_bounds__(256) void k_pixel_grads(ViewK v, const float4* __restrict__ saved4,
+                                                     const float* __restrict__ savedD, const float* __restrict__ g_rgb,
+                                                     const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
+                                                     uint4* __restrict__ UF, int pieces, L1Args l1, bool depth,
+                                                     int* __restrict__ ticket) {
+  k_pixel_grads_body(v, saved4, savedD, g_rgb, g_alpha, g_depth, UF, pieces, l1, depth, ticket, BI{(int)blockIdx.x, (int)blockIdx.y}, BI{(int)gridDim.x, (int)gridDim.y});
+}
+struct k_pixel_grads_args {
+  ViewK v;
+  const float4* saved4;
+  const float* savedD;
+  const float* g_rgb;
+  const float* g_alpha;
+  const float* g_depth;
+  uint4* UF;
+  int pieces;
+  L1Args l1;
+  bool depth;
+  int* ticket;
+};
+__global__ __launch_bounds__(256) void k_pixel_grads_views(VBatch<k_pixel_grads_args> B) {
+  const int vb = vbatch_view(B, (int)blockIdx.x);
+  const k_pixel_grads_args& a = B.a[vb];
+  const int lb = (int)blockIdx.x - B.first[vb], gx = B.gx[vb];
+  k_pixel_grads_body(a.v, a.saved4, a.savedD, a.g_rgb, a.g_alpha, a.g_depth, a.UF, a.pieces, a.l1, a.depth, a.ticket, BI{lb % gx, lb / gx}, BI{gx, (B.first[vb + 1] - B.first[vb]) / gx});
+}
+
 
 // gr_fwd_render_l1: a finished tile's pixel sums -> the fit loss's upstream fragments (the backward's
 // A operands, two pieces, no depth gradient) and the tile's L1 sums, in the forward's epilogue instead
@@ -2281,7 +2461,7 @@ __device__ __forceinline__ void l1_tile_epilogue(const ViewK& v, int tile, int t
 #define GR_FWD_WAVES3 6
 #endif
 template <int MODE>
-__global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void k_raster_fwd_mfma(ViewK v, int n, const int4* __restrict__ items,
+__device__ __forceinline__ void k_raster_fwd_mfma_body(ViewK v, int n, const int4* __restrict__ items,
                                                          const int* __restrict__ num_items, const int2* __restrict__ ranges,
                                                          const int* __restrict__ pairs, const float4* __restrict__ rec,
                                                          float* __restrict__ fwd_part, float* __restrict__ out_rgb,
@@ -2289,7 +2469,7 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
                                                          float4* __restrict__ saved4, float* __restrict__ savedD,
                                                          L1Args l1, uint4* __restrict__ UF, const int* __restrict__ f16_sa,
                                                          const int* __restrict__ tile_item0, int* __restrict__ ticket,
-                                                         int ch) {
+                                                         int ch, const BI blockIdx, const BI gridDim) {
   // LDS: two staged record buffers (2 x 9 KiB) during the loop, then the 4-wave reduction (20 KiB).
   __shared__ __attribute__((aligned(16))) float smem[4 * 5 * TP];
   __shared__ int last_flag;
@@ -2365,6 +2545,47 @@ __global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void
                             reinterpret_cast<double (*)[256]>(smem));
   }
 }
+template <int MODE>
+__global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void k_raster_fwd_mfma(ViewK v, int n, const int4* __restrict__ items,
+                                                         const int* __restrict__ num_items, const int2* __restrict__ ranges,
+                                                         const int* __restrict__ pairs, const float4* __restrict__ rec,
+                                                         float* __restrict__ fwd_part, float* __restrict__ out_rgb,
+                                                         float* __restrict__ out_alpha, float* __restrict__ out_depth,
+                                                         float4* __restrict__ saved4, float* __restrict__ savedD,
+                                                         L1Args l1, uint4* __restrict__ UF, const int* __restrict__ f16_sa,
+                                                         const int* __restrict__ tile_item0, int* __restrict__ ticket,
+                                                         int ch) {
+  k_raster_fwd_mfma_body<MODE>(v, n, items, num_items, ranges, pairs, rec, fwd_part, out_rgb, out_alpha, out_depth, saved4, savedD, l1, UF, f16_sa, tile_item0, ticket, ch, BI{(int)blockIdx.x, (int)blockIdx.y}, BI{(int)gridDim.x, (int)gridDim.y});
+}
+struct k_raster_fwd_mfma_args {
+  ViewK v;
+  int n;
+  const int4* items;
+  const int* num_items;
+  const int2* ranges;
+  const int* pairs;
+  const float4* rec;
+  float* fwd_part;
+  float* out_rgb;
+  float* out_alpha;
+  float* out_depth;
+  float4* saved4;
+  float* savedD;
+  L1Args l1;
+  uint4* UF;
+  const int* f16_sa;
+  const int* tile_item0;
+  int* ticket;
+  int ch;
+};
+template <int MODE>
+__global__ __launch_bounds__(256, MODE >= 3 ? GR_FWD_WAVES3 : GR_FWD_WAVES) void k_raster_fwd_mfma_views(VBatch<k_raster_fwd_mfma_args> B) {
+  const int vb = vbatch_view(B, (int)blockIdx.x);
+  const k_raster_fwd_mfma_args& a = B.a[vb];
+  const int lb = (int)blockIdx.x - B.first[vb], gx = B.gx[vb];
+  k_raster_fwd_mfma_body<MODE>(a.v, a.n, a.items, a.num_items, a.ranges, a.pairs, a.rec, a.fwd_part, a.out_rgb, a.out_alpha, a.out_depth, a.saved4, a.savedD, a.l1, a.UF, a.f16_sa, a.tile_item0, a.ticket, a.ch, BI{lb % gx, lb / gx}, BI{gx, (B.first[vb + 1] - B.first[vb]) / gx});
+}
+
 
 // Sum over the 4 lane rows (lanes l, l+16, l+32, l+48) of a pair of values with one
 // v_permlane16_swap: returns rows {a01, b01, a23, b23} (row r of the result holds the named sum).
@@ -2660,10 +2881,10 @@ __device__ __forceinline__ void bwd_item_bf16(int n, int k0, int k1, int tid, in
 // register budget is not set by the 5-channel form's.
 // PIECES = 2: no_depth_grad views (two round-to-nearest pieces per operand, three products).
 template <bool DEPTH, int PIECES>
-__global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void k_raster_bwd_bf16(ViewK v, int n, const int4* __restrict__ items,
+__device__ __forceinline__ void k_raster_bwd_bf16_body(ViewK v, int n, const int4* __restrict__ items,
                                                            const int* __restrict__ num_items, const int* __restrict__ pairs,
                                                            const float4* __restrict__ rec, const uint4* __restrict__ UF,
-                                                           float* __restrict__ partials, float* __restrict__ depth3) {
+                                                           float* __restrict__ partials, float* __restrict__ depth3, const BI blockIdx, const BI gridDim) {
   using UL = UFLayout<DEPTH, PIECES>;
   __shared__ __attribute__((aligned(16))) float4 sA[2][TP];
   __shared__ __attribute__((aligned(16))) float4 sB[2][TP];
@@ -2697,6 +2918,32 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
   else
     bwd_item_bf16<false, true, PIECES>(n, k0, k1, tid, wave, tx, ty, pairs, rec, partials, sA, sB, &sZ[0][0], sUF, depth3);
 }
+template <bool DEPTH, int PIECES>
+__global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void k_raster_bwd_bf16(ViewK v, int n, const int4* __restrict__ items,
+                                                           const int* __restrict__ num_items, const int* __restrict__ pairs,
+                                                           const float4* __restrict__ rec, const uint4* __restrict__ UF,
+                                                           float* __restrict__ partials, float* __restrict__ depth3) {
+  k_raster_bwd_bf16_body<DEPTH, PIECES>(v, n, items, num_items, pairs, rec, UF, partials, depth3, BI{(int)blockIdx.x, (int)blockIdx.y}, BI{(int)gridDim.x, (int)gridDim.y});
+}
+struct k_raster_bwd_bf16_args {
+  ViewK v;
+  int n;
+  const int4* items;
+  const int* num_items;
+  const int* pairs;
+  const float4* rec;
+  const uint4* UF;
+  float* partials;
+  float* depth3;
+};
+template <bool DEPTH, int PIECES>
+__global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void k_raster_bwd_bf16_views(VBatch<k_raster_bwd_bf16_args> B) {
+  const int vb = vbatch_view(B, (int)blockIdx.x);
+  const k_raster_bwd_bf16_args& a = B.a[vb];
+  const int lb = (int)blockIdx.x - B.first[vb], gx = B.gx[vb];
+  k_raster_bwd_bf16_body<DEPTH, PIECES>(a.v, a.n, a.items, a.num_items, a.pairs, a.rec, a.UF, a.partials, a.depth3, BI{lb % gx, lb / gx}, BI{gx, (B.first[vb + 1] - B.first[vb]) / gx});
+}
+
 
 #ifndef GR_FWD32_WAVES
 #define GR_FWD32_WAVES 3
@@ -2757,14 +3004,14 @@ __device__ __forceinline__ constexpr int kslot_off(int j) { return j < 4 ? j : j
 // accumulators per lane.  The four waves' sums meet in LDS (fixed wave order), a split tile's items through the
 // write-through partials of the last item to arrive (item order), then the L1 epilogue per pixel (four pixels per
 // thread), the backward's upstream fragments (UF32) and the view loss by the last tile (as k_raster_fwd_mfma<4>).
-__global__ __launch_bounds__(256, GR_FWD32_WAVES) void k_fwd32_l1(ViewK v, int n, const int4* __restrict__ items,
+__device__ __forceinline__ void k_fwd32_l1_body(ViewK v, int n, const int4* __restrict__ items,
                                                                  const int* __restrict__ num_items,
                                                                  const int2* __restrict__ ranges, const int* __restrict__ pairs,
                                                                  const float4* __restrict__ rec, float* __restrict__ fwd_part,
                                                                  float* __restrict__ out_rgb, float* __restrict__ out_alpha,
                                                                  L1Args l1, uint4* __restrict__ UF, const int* __restrict__ f16_sa,
                                                                  const int* __restrict__ tile_item0, int* __restrict__ ticket,
-                                                                 int ch) {
+                                                                 int ch, const BI blockIdx, const BI gridDim) {
   // LDS: the staged batches (2 x 8 planes x 256 floats) during the loop; then the waves' sums of two channels
   // (4 waves x 2 x 32 x 33); then the tile's upstream vectors (4 x 32 x 33); then the view loss's double[3][256]
   __shared__ __attribute__((aligned(16))) float smem[4 * 2 * T32 * F32_LD];
@@ -2956,6 +3203,41 @@ __global__ __launch_bounds__(256, GR_FWD32_WAVES) void k_fwd32_l1(ViewK v, int n
     tile_loss_total<true>(l1.tile_loss, tiles, l1.n1, l1.n2, l1.w_sil, 0, 0.0f, l1.loss_out,
                           reinterpret_cast<double (*)[256]>(smem));
 }
+__global__ __launch_bounds__(256, GR_FWD32_WAVES) void k_fwd32_l1(ViewK v, int n, const int4* __restrict__ items,
+                                                                 const int* __restrict__ num_items,
+                                                                 const int2* __restrict__ ranges, const int* __restrict__ pairs,
+                                                                 const float4* __restrict__ rec, float* __restrict__ fwd_part,
+                                                                 float* __restrict__ out_rgb, float* __restrict__ out_alpha,
+                                                                 L1Args l1, uint4* __restrict__ UF, const int* __restrict__ f16_sa,
+                                                                 const int* __restrict__ tile_item0, int* __restrict__ ticket,
+                                                                 int ch) {
+  k_fwd32_l1_body(v, n, items, num_items, ranges, pairs, rec, fwd_part, out_rgb, out_alpha, l1, UF, f16_sa, tile_item0, ticket, ch, BI{(int)blockIdx.x, (int)blockIdx.y}, BI{(int)gridDim.x, (int)gridDim.y});
+}
+struct k_fwd32_l1_args {
+  ViewK v;
+  int n;
+  const int4* items;
+  const int* num_items;
+  const int2* ranges;
+  const int* pairs;
+  const float4* rec;
+  float* fwd_part;
+  float* out_rgb;
+  float* out_alpha;
+  L1Args l1;
+  uint4* UF;
+  const int* f16_sa;
+  const int* tile_item0;
+  int* ticket;
+  int ch;
+};
+__global__ __launch_bounds__(256, GR_FWD32_WAVES) void k_fwd32_l1_views(VBatch<k_fwd32_l1_args> B) {
+  const int vb = vbatch_view(B, (int)blockIdx.x);
+  const k_fwd32_l1_args& a = B.a[vb];
+  const int lb = (int)blockIdx.x - B.first[vb], gx = B.gx[vb];
+  k_fwd32_l1_body(a.v, a.n, a.items, a.num_items, a.ranges, a.pairs, a.rec, a.fwd_part, a.out_rgb, a.out_alpha, a.l1, a.UF, a.f16_sa, a.tile_item0, a.ticket, a.ch, BI{lb % gx, lb / gx}, BI{gx, (B.first[vb + 1] - B.first[vb]) / gx});
+}
+
 
 // Backward of one work item of a 32-pixel tile (no upstream depth gradient, two-piece bf16 operands as
 // k_raster_bwd_bf16<false, 2>): per group of 32 Gaussians (lane r = l & 31 owns Gaussian r, half h = l >> 5 its
@@ -2964,10 +3246,10 @@ __global__ __launch_bounds__(256, GR_FWD32_WAVES) void k_fwd32_l1(ViewK v, int n
 // each 2 K-steps x 3 piece products on v_mfma_f32_32x32x16_bf16, then the per-Gaussian epilogue over the lane's 16
 // rows (the same sums as the 16-pixel kernel, moments about the first slot of each K-step) and the 8-float row
 // [o S0, o S2, S4, S6 | o S1, S8, S5, S7] at the pair's sorted position (the gather is unchanged).
-__global__ __launch_bounds__(256, GR_BWD32_WAVES) void k_bwd32(ViewK v, int n, const int4* __restrict__ items,
+__device__ __forceinline__ void k_bwd32_body(ViewK v, int n, const int4* __restrict__ items,
                                                               const int* __restrict__ num_items, const int* __restrict__ pairs,
                                                               const float4* __restrict__ rec, const uint4* __restrict__ UF,
-                                                              float* __restrict__ partials) {
+                                                              float* __restrict__ partials, const BI blockIdx, const BI gridDim) {
   constexpr int NB = GR_BWD32_BATCH;  // Gaussians staged per batch (NB / 4 per wave)
   constexpr int WG = NB / 4;          // per wave: one or two groups of 32
   __shared__ __attribute__((aligned(16))) float4 sA[2][NB];
@@ -3127,6 +3409,29 @@ __global__ __launch_bounds__(256, GR_BWD32_WAVES) void k_bwd32(ViewK v, int n, c
     }
   }
 }
+__global__ __launch_bounds__(256, GR_BWD32_WAVES) void k_bwd32(ViewK v, int n, const int4* __restrict__ items,
+                                                              const int* __restrict__ num_items, const int* __restrict__ pairs,
+                                                              const float4* __restrict__ rec, const uint4* __restrict__ UF,
+                                                              float* __restrict__ partials) {
+  k_bwd32_body(v, n, items, num_items, pairs, rec, UF, partials, BI{(int)blockIdx.x, (int)blockIdx.y}, BI{(int)gridDim.x, (int)gridDim.y});
+}
+struct k_bwd32_args {
+  ViewK v;
+  int n;
+  const int4* items;
+  const int* num_items;
+  const int* pairs;
+  const float4* rec;
+  const uint4* UF;
+  float* partials;
+};
+__global__ __launch_bounds__(256, GR_BWD32_WAVES) void k_bwd32_views(VBatch<k_bwd32_args> B) {
+  const int vb = vbatch_view(B, (int)blockIdx.x);
+  const k_bwd32_args& a = B.a[vb];
+  const int lb = (int)blockIdx.x - B.first[vb], gx = B.gx[vb];
+  k_bwd32_body(a.v, a.n, a.items, a.num_items, a.pairs, a.rec, a.UF, a.partials, BI{lb % gx, lb / gx}, BI{gx, (B.first[vb + 1] - B.first[vb]) / gx});
+}
+
 
 
 // k_bwd32 on v_mfma_f32_16x16x32_bf16 (GR_BWD32_M16): groups of 16 Gaussians; lane l owns Gaussian n = l & 15 of the
@@ -3609,9 +3914,9 @@ __device__ __forceinline__ void add4(float4& x, const float4 a) {
 // tail pairs q, q+4, ... after its core pairs, and the depth sums o S3 (depth3, by sorted position) of
 // both, written to sums3[i].
 template <bool DEPTH>
-__global__ __launch_bounds__(256) void k_gather_view(int n, const Cnt2* __restrict__ offsets, const int* __restrict__ pos_of,
+__device__ __forceinline__ void k_gather_view_body(int n, const Cnt2* __restrict__ offsets, const int* __restrict__ pos_of,
                                                      const float4* __restrict__ rows, float2* __restrict__ sums,
-                                                     const float* __restrict__ depth3, float* __restrict__ sums3) {
+                                                     const float* __restrict__ depth3, float* __restrict__ sums3, const BI blockIdx, const BI gridDim) {
   const int tid = threadIdx.x, q4 = tid & 3;
   const int i = blockIdx.x * 64 + (tid >> 2);
   float4 x = {-0.f, -0.f, -0.f, -0.f}, y = x;
@@ -3655,6 +3960,29 @@ __global__ __launch_bounds__(256) void k_gather_view(int n, const Cnt2* __restri
     sums[4 * (size_t)i + q4] = o;
   }
 }
+template <bool DEPTH>
+__global__ __launch_bounds__(256) void k_gather_view(int n, const Cnt2* __restrict__ offsets, const int* __restrict__ pos_of,
+                                                     const float4* __restrict__ rows, float2* __restrict__ sums,
+                                                     const float* __restrict__ depth3, float* __restrict__ sums3) {
+  k_gather_view_body<DEPTH>(n, offsets, pos_of, rows, sums, depth3, sums3, BI{(int)blockIdx.x, (int)blockIdx.y}, BI{(int)gridDim.x, (int)gridDim.y});
+}
+struct k_gather_view_args {
+  int n;
+  const Cnt2* offsets;
+  const int* pos_of;
+  const float4* rows;
+  float2* sums;
+  const float* depth3;
+  float* sums3;
+};
+template <bool DEPTH>
+__global__ __launch_bounds__(256) void k_gather_view_views(VBatch<k_gather_view_args> B) {
+  const int vb = vbatch_view(B, (int)blockIdx.x);
+  const k_gather_view_args& a = B.a[vb];
+  const int lb = (int)blockIdx.x - B.first[vb], gx = B.gx[vb];
+  k_gather_view_body<DEPTH>(a.n, a.offsets, a.pos_of, a.rows, a.sums, a.depth3, a.sums3, BI{lb % gx, lb / gx}, BI{gx, (B.first[vb + 1] - B.first[vb]) / gx});
+}
+
 
 // Chain rule of up to GR_REDUCE_MAX_VIEWS views' gathered sums: one lane per Gaussian; the crw waves of a
 // Gaussian group take views u, u + crw, ... (crw = 4 from three views, else the view count, so that no
@@ -5145,6 +5473,221 @@ gr_status gr_bwd_l1(const gr_view* v, int n, const gr_plan* plan, const float* m
   return bwd_impl(v, n, plan, means, scales, colors, color_dim, opacities, geom, bins, saved, nullptr, nullptr, nullptr,
                   target_rgb, target_mask, w_sil, g_scale, loss_out, d_means, d_scales, d_colors, d_opacities,
                   accumulate, ws, ws_bytes, stream);
+}
+
+}  // extern "C" (the batching helpers are templates)
+
+// ---- gr_fit_views_batched: the fused fit path's per-view chain for several views, one launch per kernel -----------
+template <class A>
+static void vb_add(VBatch<A>& B, const A& a, int blocks, int gx = 0) {
+  B.a[B.nv] = a;
+  B.gx[B.nv] = gx > 0 ? gx : (blocks > 0 ? blocks : 1);
+  B.first[B.nv + 1] = B.first[B.nv] + (blocks > 0 ? blocks : 0);
+  ++B.nv;
+}
+template <class A>
+static VBatch<A> vb_new() {
+  static_assert(sizeof(VBatch<A>) <= 4096, "batched kernel arguments exceed 4 KiB");
+  VBatch<A> B;
+  B.nv = 0;
+  B.first[0] = 0;
+  return B;
+}
+#define GR_VB_LAUNCH(kern, B, threads, lds, s)                                                   \
+  do {                                                                                           \
+    if ((B).first[(B).nv] > 0) {                                                                 \
+      hipLaunchKernelGGL(kern, dim3((unsigned)(B).first[(B).nv]), dim3(threads), lds, s, (B));   \
+      GR_HIP_TRY(hipGetLastError());                                                             \
+    }                                                                                            \
+  } while (0)
+
+extern "C" {
+
+gr_status gr_fit_views_batched(int num_views, const gr_batch_view* bv, int n, float w_sil, float w_depth,
+                                          float g_scale, void* stream) {
+  if (num_views < 1 || num_views > GR_BATCH_MAX_VIEWS || !bv)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views_batched: num_views must be in [1, GR_BATCH_MAX_VIEWS]");
+  if (n <= 0) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views_batched: n must be > 0");
+  static_assert(GR_BATCH_MAX_VIEWS == GR_BATCH_MAX, "gr_hip.h GR_BATCH_MAX_VIEWS");
+  const gr_view& v0 = bv[0].view;
+  const bool depth = bv[0].target_depth != nullptr;
+  for (int j = 0; j < num_views; ++j) {
+    const gr_batch_view& b = bv[j];
+    gr_status st = check_view(&b.view);
+    if (st != GR_OK) return st;
+    if (b.view.width != v0.width || b.view.height != v0.height || tile_of(&b.view) != tile_of(&v0) ||
+        b.view.no_depth_grad != v0.no_depth_grad || b.view.cutoff != v0.cutoff || b.view.core_cutoff != v0.core_cutoff ||
+        b.view.device_counts != v0.device_counts || (b.target_depth != nullptr) != depth)
+      return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views_batched: the views differ in size, tile, footprint or mode");
+    if (b.plan.num_pairs <= 0 || b.plan.num_slots < b.plan.num_pairs)
+      return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views_batched: every view needs pairs (or capacities)");
+    if (!b.geom || !b.bins || !b.scratch || !b.ws || !b.target_rgb || !b.sums || !b.loss || (depth && (!b.saved || !b.sums3)))
+      return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views_batched: null pointer");
+    if (b.bins_bytes < gr_bins_bytes(&b.view, n, &b.plan) || b.scratch_bytes < gr_fwd_scratch_bytes(&b.view, n, &b.plan) ||
+        b.ws_bytes < gr_bwd_bytes(&b.view, n, &b.plan))
+      return set_error(GR_ERR_WORKSPACE, "gr_fit_views_batched: a workspace is too small");
+  }
+  if (!short_keys(vtiles_of(&v0)))
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views_batched: more than 8,192 screen tiles");
+  if (depth ? v0.no_depth_grad != 0 : v0.no_depth_grad != 1)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views_batched: depth loss needs no_depth_grad = 0, the L1 path 1");
+  if (depth && tile_of(&v0) != T)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views_batched: the depth-loss path runs at 16-pixel tiles");
+  hipStream_t s = (hipStream_t)stream;
+  const int tiles = vtiles_of(&v0) / 2;
+  const size_t HW = (size_t)v0.width * v0.height;
+  const int waves = tsort_waves(tiles), bits = bits_for((uint32_t)tiles);
+  auto Be = vb_new<k_emit_offsets_args>();
+  auto Bc = vb_new<k_tile_count_args>();
+  auto Bs = vb_new<k_tile_colscan_args>();
+  auto Bp = vb_new<k_tile_place_args>();
+  for (int j = 0; j < num_views; ++j) {  // the binning (bin_impl's counting-sort path, per view)
+    const gr_batch_view& b = bv[j];
+    const ViewK vk = make_viewk(&b.view);
+    const TileCfg tc = tile_cfg(&b.view, b.plan.num_pairs);
+    const Bins bn = bins_view(b.bins, 2 * tiles, b.plan.num_pairs, tc.ch);
+    const Scratch sc = scratch_view(b.scratch, 2 * tiles, b.plan.num_pairs, tc.ch, tc.part_floats);
+    Geom g = geom_view((void*)b.geom, n);
+    const int64_t K = b.plan.num_pairs, Kc = b.plan.num_core_pairs, Kr[2] = {Kc, K - Kc};
+    TZones Z;
+    Z.cw = col_width(K, tiles);
+    Z.ch = tc.ch;
+    Z.kdev = b.view.device_counts ? (const unsigned long long*)(g.offsets + n) : nullptr;
+    const size_t cells = (size_t)tiles * cols_of(K, Z.cw);
+    char* q = (char*)sc.sort_tmp;
+    for (int z = 0; z < 2; ++z) {
+      TZone& zz = Z.z[z];
+      zz.K = Kr[z];
+      zz.cols = cols_of(Kr[z], Z.cw);
+      zz.zbase = z == 0 ? 0 : (int)Kc;
+      zz.keys = (const uint16_t*)sc.keys_in + (z == 0 ? 0 : Kc);
+      zz.ids = sc.ids_in + (z == 0 ? 0 : Kc);
+      zz.M = (int*)q;
+      q += align_up(cells * sizeof(int));
+      zz.S = (int*)q;
+      q += align_up(cells * sizeof(int));
+      zz.T = (int*)q;
+      q += align_up((size_t)tiles * sizeof(int));
+    }
+    const int cols = Z.z[0].cols + Z.z[1].cols;
+    vb_add(Be, k_emit_offsets_args{vk, n, (const int4*)g.rect, (const Cnt2*)g.counts, (const unsigned long long*)g.total,
+                                   (Cnt2*)g.offsets, (const float4*)g.rec, (uint16_t*)sc.keys_in, sc.ids_in,
+                                   bn.ticket + fan_offset(tiles)},
+           blocks_for(n));
+    vb_add(Bc, k_tile_count_args{Z, tiles}, cols);
+    const int gxs = (tiles + CS_T - 1) / CS_T;
+    vb_add(Bs, k_tile_colscan_args{Z, tiles, bn.ranges, bn.items, bn.num_items, bn.tile_item0, bn.ticket}, 2 * gxs, gxs);
+    vb_add(Bp, k_tile_place_args{Z, tiles, bits, (const int2*)bn.ranges, bn.pairs, bn.pos_of}, cols);
+  }
+  GR_VB_LAUNCH(k_emit_offsets_views, Be, 256, 0, s);
+  GR_VB_LAUNCH(k_tile_count_views, Bc, 256, (size_t)tiles * sizeof(int), s);
+  GR_VB_LAUNCH(k_tile_colscan_views, Bs, CS_T * CS_G, 0, s);
+  const size_t lds = (size_t)tiles * sizeof(int) * waves;
+  if (waves == 8) GR_VB_LAUNCH(k_tile_place_views<8>, Bp, 512, lds, s);
+  else if (waves == 4) GR_VB_LAUNCH(k_tile_place_views<4>, Bp, 256, lds, s);
+  else if (waves == 2) GR_VB_LAUNCH(k_tile_place_views<2>, Bp, 128, lds, s);
+  else GR_VB_LAUNCH(k_tile_place_views<1>, Bp, 64, lds, s);
+
+  auto Bg = vb_new<k_gather_view_args>();
+  if (!depth) {  // the fused fit path: forward with the L1 epilogue, backward splat, gather
+    auto Bf = vb_new<k_fwd32_l1_args>();
+    auto Bf16 = vb_new<k_raster_fwd_mfma_args>();
+    auto Bb = vb_new<k_bwd32_args>();
+    auto Bb16 = vb_new<k_raster_bwd_bf16_args>();
+    for (int j = 0; j < num_views; ++j) {
+      const gr_batch_view& b = bv[j];
+      const ViewK vk = make_viewk(&b.view);
+      const TileCfg tc = tile_cfg(&b.view, b.plan.num_pairs);
+      const Bins bn = bins_view(b.bins, 2 * tiles, b.plan.num_pairs, tc.ch);
+      const Scratch sc = scratch_view(b.scratch, 2 * tiles, b.plan.num_pairs, tc.ch, tc.part_floats);
+      const Geom g = geom_view((void*)b.geom, n);
+      const BwdWs w = bwd_ws(&b.view, n, &b.plan, b.ws);
+      L1Args la{b.target_rgb, b.target_mask, w_sil, g_scale, w.tile_loss};
+      la.pieces = 2;
+      la.loss_out = b.loss;
+      la.n1 = (int64_t)(3 * HW);
+      la.n2 = (int64_t)(b.target_mask ? HW : 0);
+      const int cap = (int)item_cap(2 * tiles, b.plan.num_pairs, tc.ch);
+      if (tc.T == T32) {
+        vb_add(Bf, k_fwd32_l1_args{vk, n, (const int4*)bn.items, (const int*)bn.num_items, (const int2*)bn.ranges,
+                                   (const int*)bn.pairs, (const float4*)g.rec, sc.fwd_part, nullptr, nullptr, la, w.UF,
+                                   (const int*)g.f16_sa, (const int*)bn.tile_item0, bn.ticket, tc.ch},
+               cap);
+        vb_add(Bb, k_bwd32_args{vk, n, (const int4*)bn.items, (const int*)bn.num_items, (const int*)bn.pairs,
+                                (const float4*)g.rec, (const uint4*)w.UF, w.partials},
+               cap);
+      } else {
+        vb_add(Bf16, k_raster_fwd_mfma_args{vk, n, (const int4*)bn.items, (const int*)bn.num_items, (const int2*)bn.ranges,
+                                            (const int*)bn.pairs, (const float4*)g.rec, sc.fwd_part, nullptr, nullptr,
+                                            nullptr, nullptr, nullptr, la, w.UF, (const int*)g.f16_sa,
+                                            (const int*)bn.tile_item0, bn.ticket, tc.ch},
+               cap);
+        vb_add(Bb16, k_raster_bwd_bf16_args{vk, n, (const int4*)bn.items, (const int*)bn.num_items, (const int*)bn.pairs,
+                                            (const float4*)g.rec, (const uint4*)w.UF, w.partials, nullptr},
+               cap);
+      }
+      vb_add(Bg, k_gather_view_args{n, (const Cnt2*)g.offsets, (const int*)bn.pos_of, (const float4*)w.partials,
+                                    (float2*)b.sums, nullptr, nullptr},
+             (n + 63) / 64);
+    }
+    GR_VB_LAUNCH(k_fwd32_l1_views, Bf, 256, 0, s);
+    GR_VB_LAUNCH(k_raster_fwd_mfma_views<4>, Bf16, 256, 0, s);
+    GR_VB_LAUNCH(k_bwd32_views, Bb, 256, 0, s);
+    GR_VB_LAUNCH((k_raster_bwd_bf16_views<false, 2>), Bb16, 256, 0, s);
+    GR_VB_LAUNCH(k_gather_view_views<false>, Bg, 256, 0, s);
+    return GR_OK;
+  }
+  // the depth-loss path (gr_fwd_render + gr_bwd_fit_gather per view): forward into saved sums, the depth loss's max
+  // and sums, the upstream fragments and view loss, the three-piece backward with the tail pairs, the gather
+  auto Bf = vb_new<k_raster_fwd_mfma_args>();
+  auto Bm = vb_new<k_depth_tile_max_args>();
+  auto Bd = vb_new<k_depth_tile_sums_args>();
+  auto Bu = vb_new<k_pixel_grads_args>();
+  auto Bb = vb_new<k_raster_bwd_bf16_args>();
+  for (int j = 0; j < num_views; ++j) {
+    const gr_batch_view& b = bv[j];
+    const ViewK vk = make_viewk(&b.view);
+    const TileCfg tc = tile_cfg(&b.view, b.plan.num_pairs);
+    const Bins bn = bins_view(b.bins, 2 * tiles, b.plan.num_pairs, tc.ch);
+    const Scratch sc = scratch_view(b.scratch, 2 * tiles, b.plan.num_pairs, tc.ch, tc.part_floats);
+    const Geom g = geom_view((void*)b.geom, n);
+    const BwdWs w = bwd_ws(&b.view, n, &b.plan, b.ws);
+    float4* s4 = (float4*)b.saved;
+    float* sD = b.saved + 4 * HW;
+    const int cap = (int)item_cap(2 * tiles, b.plan.num_pairs, tc.ch);
+    L1Args none{nullptr, nullptr, 0.f, 0.f, nullptr};
+    vb_add(Bf, k_raster_fwd_mfma_args{vk, n, (const int4*)bn.items, (const int*)bn.num_items, (const int2*)bn.ranges,
+                                      (const int*)bn.pairs, (const float4*)g.rec, sc.fwd_part, nullptr, nullptr, nullptr,
+                                      s4, sD, none, nullptr, (const int*)g.f16_sa, (const int*)bn.tile_item0, bn.ticket,
+                                      tc.ch},
+           cap);
+    vb_add(Bm, k_depth_tile_max_args{vk, s4, sD, w.tile_aux, w.dscal, bn.ticket}, tiles);
+    vb_add(Bd, k_depth_tile_sums_args{vk, s4, sD, b.target_depth, w.dscal, w.tile_loss, w.tile_aux, (int64_t)HW, w_depth,
+                                      g_scale, bn.ticket},
+           tiles);
+    L1Args l1{b.target_rgb, b.target_mask, w_sil, g_scale, w.tile_loss};
+    l1.loss_out = b.loss;
+    l1.n1 = (int64_t)(3 * HW);
+    l1.n2 = (int64_t)(b.target_mask ? HW : 0);
+    l1.t_depth = b.target_depth;
+    l1.w_depth = w_depth;
+    l1.dscal = w.dscal;
+    vb_add(Bu, k_pixel_grads_args{vk, s4, sD, nullptr, nullptr, nullptr, w.UF, 3, l1, true, bn.ticket}, tiles);
+    vb_add(Bb, k_raster_bwd_bf16_args{vk, n, (const int4*)bn.items, (const int*)bn.num_items, (const int*)bn.pairs,
+                                      (const float4*)g.rec, (const uint4*)w.UF, w.partials,
+                                      w.partials + 8 * (size_t)b.plan.num_slots},
+           cap);
+    vb_add(Bg, k_gather_view_args{n, (const Cnt2*)g.offsets, (const int*)bn.pos_of, (const float4*)w.partials,
+                                  (float2*)b.sums, (const float*)(w.partials + 8 * (size_t)b.plan.num_slots), b.sums3},
+           (n + 63) / 64);
+  }
+  GR_VB_LAUNCH(k_raster_fwd_mfma_views<1>, Bf, 256, 0, s);
+  GR_VB_LAUNCH(k_depth_tile_max_views, Bm, 256, 0, s);
+  GR_VB_LAUNCH(k_depth_tile_sums_views, Bd, 256, 0, s);
+  GR_VB_LAUNCH(k_pixel_grads_views, Bu, 256, 0, s);
+  GR_VB_LAUNCH((k_raster_bwd_bf16_views<true, 3>), Bb, 256, 0, s);
+  GR_VB_LAUNCH(k_gather_view_views<true>, Bg, 256, 0, s);
+  return GR_OK;
 }
 
 gr_status gr_bwd_splat(const gr_view* v, int n, const gr_plan* plan, const void* geom, const void* bins, void* ws,

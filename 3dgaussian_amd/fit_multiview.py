@@ -110,15 +110,21 @@ F32_GRADE = os.environ.get("GR_F32_GRADE", "0") != "0"
 # ~3-pixel-sigma C4 scene (7.8 -> 3.7 per Gaussian), so the binning and the per-pair gradient rows and their gather
 # (DESIGN.md §5); 16 = the drop-in op's tiles.  The f32-grade reference mode (F32_GRADE) keeps 16.
 FIT_TILE = int(os.environ.get("GR_FIT_TILE", "32"))
-# the fused step captured once as a HIP graph and replayed (world size 1; ViewShardedFitter._graph_step): the views are
-# prepared against per-view pair capacities (gr_fwd_prepare_views_sized: the counts stay on the device, nothing in
-# the step waits for the host), the Adam scalars come from a device table indexed by a device step counter, and a
-# step whose views exceed their capacities updates nothing and is redone with larger ones.  1 = on, 0 = eager steps.
-GRAPH_MODE = os.environ.get("GR_GRAPH", "0")
-GRAPH = GRAPH_MODE != "0"
-# "sized": the same device-sized step enqueued eagerly every step (no capture); "exec": likewise through the native
-# executor (gr_fit_views with capacities); "1": captured once and replayed
-GRAPH_CAPTURE = GRAPH_MODE not in ("sized", "exec")
+# How the fused step is enqueued (world size 1; ViewShardedFitter._graph_step): the views are prepared against per-view
+# pair capacities (gr_fwd_prepare_views_sized: the counts stay on the device, nothing in the step waits for the host),
+# the Adam scalars come from a device table indexed by a device step counter, and a step whose views exceed their
+# capacities updates nothing and is redone with larger ones.  Modes (GR_GRAPH):
+#   batch       every kernel launched once per batch of up to 8 views (gr_fit_views_batched), one stream: small views
+#               fill the GPU (C3 580 -> 765, C2 2,020 -> 2,720 Mpx/s, profiles/r05_batched.txt)
+#   batchgraph  that step captured once as a HIP graph and replayed
+#   1           the multi-stream step captured and replayed (ROCm runs a captured graph's branches at most two at a
+#               time here: slower than eager, profiles/r05_graph_ab.txt)
+#   sized/exec  the device-sized multi-stream step enqueued eagerly, Python / native executor (diagnostics)
+#   0           the eager multi-stream step, host-sized
+#   auto        (default) batch for views of at most GRAPH_AUTO_PIXELS, else 0: at 800x800 the per-view launches already
+#               fill the GPU and the eager step's stream overlap wins (C4 1,557 eager vs 1,446 batched)
+GRAPH_MODE = os.environ.get("GR_GRAPH", "auto")
+GRAPH_AUTO_PIXELS = 512 * 512
 GRAPH_MARGIN = float(os.environ.get("GR_GRAPH_MARGIN", "1.25"))  # capacity over the counts seen (+ 4096 pairs)
 
 
@@ -1038,12 +1044,21 @@ class ViewShardedFitter:
     def _graph_ok(self, device) -> bool:
         """The graph applies: the fused path with its one-launch parameter update (world size 1), the Python
         schedule without a separate binning stream, and the optimizer state made by an eager step."""
-        if not (GRAPH and self.world == 1 and device.type == "cuda" and BIN_STREAM == "" and self._direct(device)
+        mode = self._graph_mode()
+        if not (mode != "0" and self.world == 1 and device.type == "cuda" and BIN_STREAM == "" and self._direct(device)
                 and self.params["means"].shape[0] > 0 and self._fused_step_ok()):
+            return False
+        if mode in ("batch", "batchgraph") and F32_GRADE:  # (the batched L1 path runs the two-piece mode only)
             return False
         if min(NUM_STREAMS, len(self.my_views)) > tr._native.FIT_MAX_ACC or len(self.params) > tr._native.FIT_MAX_PARAMS:
             return False
         return all(bool(self.opt.state.get(p)) for p in self.params.values())
+
+    def _graph_mode(self) -> str:
+        """The effective GR_GRAPH mode of this fit (auto: batch for small views, else 0)."""
+        if GRAPH_MODE == "auto":
+            return "batch" if self.width * self.height <= GRAPH_AUTO_PIXELS and len(self.my_views) >= 2 else "0"
+        return GRAPH_MODE
 
     def _graph_key(self) -> tuple:
         g = self.opt.param_groups[0]
@@ -1101,7 +1116,11 @@ class ViewShardedFitter:
             means, scales, colors, opacities = activations(self.params)
             reg_fn = ((lambda: self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean())
                       if self.rank == 0 else None)
-            if GRAPH_MODE == "exec":  # the native executor with capacities (as step()'s executor branch)
+            mode = self._graph_mode()
+            if mode in ("batch", "batchgraph"):  # one launch per kernel for up to 8 views (gr_fit_views_batched), one stream
+                reg = reg_fn() if reg_fn else None
+                total = self._views_batched(means, scales, colors, opacities, gs)
+            elif mode == "exec":  # the native executor with capacities (as step()'s executor branch)
                 total = self._views_native(means, scales, colors, opacities, self._depth_grad(), sized=gs)
                 rs = getattr(self, "_prep", None) if EXEC_STREAMS else None
                 reg = None
@@ -1145,7 +1164,7 @@ class ViewShardedFitter:
             gs.sched_key = self._graph_key()[2:5]
         gs.done_host = t0
         torch.cuda.synchronize(device)
-        if GRAPH_CAPTURE:
+        if self._graph_mode() in ("1", "batchgraph"):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode="relaxed"):
                 gs.loss = self._graph_body(gs)
@@ -1208,6 +1227,106 @@ class ViewShardedFitter:
                     self.opt.state[p]["step"] += 1
             torch.cuda.synchronize(device)
             gs.inflight = inflight
+
+    def _views_batched(self, means, scales, colors, opacities, gs) -> torch.Tensor:
+        """The step's views on the current stream, every kernel launched once per batch of up to 8 views
+        (gr_fit_views_batched) on device-sized views: the preparations (gr_fwd_prepare_views_sized, 4 views each), the
+        batched chain (binning, forward with the loss epilogue or the depth-loss forward, backward, gather), then the
+        chain rules of up to 16 views per gr_reduce_sums into one accumulator set.  Per-view workspaces sized by the
+        capacities are kept in the graph state across steps."""
+        device = means.device
+        L = tr._native.lib()
+        nat = tr._native
+        m, s, c, o = (t.detach().float().contiguous() for t in (means, scales, colors, opacities))
+        n = int(m.shape[0])
+        views = self.my_views
+        depth = self._depth_grad()
+        w_sil = self.w_sil if (self.masks is not None and self.w_sil > 0.0) else 0.0
+        g_scale = 1.0 / len(self.targets)
+        bkey = (n, depth, tuple((int(cp.num_pairs), int(cp.num_core_pairs)) for cp in gs.caps), str(device))
+        bw = getattr(gs, "batch_ws", None)
+        if bw is None or bw[0] != bkey:
+            gvs = []
+            for i in views:
+                if depth:
+                    cam = self.cams[i]
+                    gvd = getattr(self, "_gvd_cache", None)
+                    if gvd is None:
+                        self._gvd_cache = gvd = {}
+                    if i not in gvd:
+                        gvd[i] = tr.make_view(cam.view, cam.proj, self.width, self.height, self._background(device),
+                                              depth_grad=True)
+                    gvs.append(tr.sized_view(gvd[i]))
+                else:
+                    gvs.append(tr.sized_view(self._fit_view(i, device)))
+            u8 = dict(dtype=torch.uint8, device=device)
+            gb = int(L.gr_geom_bytes(n))
+            ws = []
+            for j, gv in enumerate(gvs):
+                cp = gs.caps[j]
+                ws.append(dict(
+                    geom=torch.empty((gb,), **u8),
+                    bins=torch.empty((int(L.gr_bins_bytes(ctypes.byref(gv), n, ctypes.byref(cp))),), **u8),
+                    scratch=torch.empty((int(L.gr_fwd_scratch_bytes(ctypes.byref(gv), n, ctypes.byref(cp))),), **u8),
+                    ws=torch.empty((int(L.gr_bwd_bytes(ctypes.byref(gv), n, ctypes.byref(cp))),), **u8),
+                    saved=(torch.empty((int(L.gr_saved_floats(ctypes.byref(gv))),), dtype=torch.float32, device=device)
+                           if depth else None),
+                    sums=torch.empty((n, 8), dtype=torch.float32, device=device),
+                    sums3=torch.empty((n,), dtype=torch.float32, device=device) if depth else None))
+            gs.batch_ws = bw = (bkey, gvs, ws)
+        _, gvs, ws = bw
+        losses_v = torch.empty(max(1, len(views)), dtype=torch.float32, device=device)
+        # the chain rules in the single-stream schedule's grouping (one accumulator set, batches of up to
+        # REDUCE_BATCH views with the short REDUCE_TAIL batch last): the same sums in the same order as
+        # _views_direct / _views_direct_depth with GR_STREAMS=1, so the same parameters bit for bit (fewer chain-rule
+        # launches and one accumulator for the update to read instead of one per stream)
+        ns = 1
+        shapes = (ns,) + tuple(tuple(t.shape) for t in (m, s, c, o))
+        cached = getattr(self, "_direct_acc", None)
+        if cached is None or cached[0] != shapes or cached[1][0][0].device != device:
+            self._direct_acc = cached = (shapes, [tuple(torch.empty_like(t) for t in (m, s, c, o)) for _ in range(ns)])
+        acc = cached[1]
+        stream = ctypes_stream(device)
+        cd = tr._color_dim(c)
+        for j0 in range(0, len(views), nat.PREPARE_MAX_VIEWS):
+            js = range(j0, min(len(views), j0 + nat.PREPARE_MAX_VIEWS))
+            k = len(js)
+            nat.check(L.gr_fwd_prepare_views_sized(
+                k, (nat.GrView * k)(*[gvs[q] for q in js]), n, nat.ptr(m), nat.ptr(s), nat.ptr(c), cd, nat.ptr(o),
+                (ctypes.c_void_p * k)(*[ws[q]["geom"].data_ptr() for q in js]), ws[js[0]]["geom"].numel(),
+                (nat.GrPlan * k)(*[gs.caps[q] for q in js]),
+                (ctypes.c_void_p * k)(*[gs.observed[q].data_ptr() for q in js]), nat.ptr(gs.ovf), stream),
+                "gr_fwd_prepare_views_sized")
+        for j0 in range(0, len(views), nat.BATCH_MAX_VIEWS):
+            js = range(j0, min(len(views), j0 + nat.BATCH_MAX_VIEWS))
+            arr = (nat.GrBatchView * len(js))()
+            for e, q in zip(arr, js):
+                w, i = ws[q], views[q]
+                e.view, e.plan = gvs[q], gs.caps[q]
+                e.geom, e.bins, e.bins_bytes = w["geom"].data_ptr(), w["bins"].data_ptr(), w["bins"].numel()
+                e.scratch, e.scratch_bytes = w["scratch"].data_ptr(), w["scratch"].numel()
+                e.ws, e.ws_bytes = w["ws"].data_ptr(), w["ws"].numel()
+                e.saved = w["saved"].data_ptr() if depth else None
+                e.target_rgb = self.targets[i].data_ptr()
+                e.target_mask = self.masks[i].data_ptr() if w_sil > 0.0 else None
+                e.target_depth = self.depths[i].data_ptr() if depth else None
+                e.sums, e.sums3 = w["sums"].data_ptr(), (w["sums3"].data_ptr() if depth else None)
+                e.loss = losses_v[q:q + 1].data_ptr()
+            nat.check(L.gr_fit_views_batched(len(js), arr, n, ctypes.c_float(w_sil), ctypes.c_float(self.w_depth if depth else 0.0),
+                                             ctypes.c_float(g_scale), stream), "gr_fit_views_batched")
+        for k, sizes in enumerate(_batch_sizes(ns, len(views))):
+            mine = list(range(k, len(views), ns))
+            at = 0
+            for b in sizes:
+                js = mine[at:at + b]
+                if js:
+                    tr.reduce_sums_native(m, s, c, o,
+                                          [(gvs[q], ws[q]["sums"]) + ((ws[q]["sums3"],) if depth else ()) for q in js],
+                                          acc[k], accumulate=at > 0)
+                at += b
+        self._acc_parts = acc[:min(ns, len(views))] if views else [tuple(torch.zeros_like(t) for t in (m, s, c, o))]
+        self._native_keep = (m, s, c, o)
+        return losses_v[:len(views)].sum() if views else torch.zeros((), device=device)
 
     def graph_sync(self) -> None:
         """Wait for the replayed steps and redo any that overflowed (densify, the parameters' readers and the end of a

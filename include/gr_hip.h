@@ -146,7 +146,7 @@ gr_status gr_fwd_prepare_async(const gr_view* v, int n, const float* means, cons
 /* gr_fwd_prepare_async for up to GR_PREPARE_MAX_VIEWS views of the same Gaussians in one pass: the
  * parameters are read once per Gaussian, each view's geom (geom_bytes each) and plan are exactly what
  * gr_fwd_prepare_async writes for that view.  All plans are valid once the stream has completed. */
-#define GR_PREPARE_MAX_VIEWS 4
+#define GR_PREPARE_MAX_VIEWS 8
 gr_status gr_fwd_prepare_views_async(int num_views, const gr_view* views, int n, const float* means,
                                      const float* scales, const float* colors, int color_dim,
                                      const float* opacities, void* const* geoms, size_t geom_bytes,
@@ -448,6 +448,37 @@ gr_status gr_fit_param_steps(int num, const gr_param_step* steps, double beta1, 
  * it), mirrors *step_dev to host_flags[1] and clears *overflow for the next step.  host_flags: pinned host int[2]. */
 gr_status gr_fit_param_steps_sched(int num, const gr_param_step* steps, double beta1, double beta2, float eps,
                                    const float* sched, int* step_dev, int* overflow, int* host_flags, void* stream);
+
+/* The fused fit path for up to GR_BATCH_MAX_VIEWS views of one image size in one launch per kernel: per view what
+ * gr_fwd_render_l1 + gr_bwd_splat + gr_gather_view do (no_depth_grad = 1; 16- or 32-pixel tiles), or with
+ * target_depth what gr_fwd_render (saved sums) + gr_bwd_fit_gather do (no_depth_grad = 0, 16-pixel tiles), each
+ * kernel's blocks of every view in one grid.  For small views (C2, C3: a few hundred work items per splat) one view
+ * per launch leaves most of the 256 CUs idle; the views of a batch fill them.  The views were prepared (geom, plan)
+ * and may be device-sized (device_counts = 1, plan = capacities); bins / scratch / ws (/ saved: 5 floats per
+ * pixel, depth path) are the single-view calls' workspaces, sums (n x 8) and sums3 (n, depth path) receive what
+ * gr_gather_view / gr_bwd_fit_gather write, loss the view loss.  Then gr_reduce_sums as usual.  Same results as the
+ * single-view calls, bit for bit (every block computes what it computes in its own view's launch). */
+#define GR_BATCH_MAX_VIEWS 8
+typedef struct gr_batch_view {
+  gr_view view;
+  gr_plan plan;
+  const void* geom;
+  void* bins;
+  size_t bins_bytes;
+  void* scratch;
+  size_t scratch_bytes;
+  void* ws;
+  size_t ws_bytes;
+  float* saved;
+  const float* target_rgb;
+  const float* target_mask;
+  const float* target_depth;
+  float* sums;
+  float* sums3;
+  float* loss;
+} gr_batch_view;
+gr_status gr_fit_views_batched(int num_views, const gr_batch_view* views, int n, float w_sil, float w_depth,
+                               float g_scale, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Introspection (host-only, no GPU needed).                                                  */

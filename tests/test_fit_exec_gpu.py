@@ -24,15 +24,16 @@ def test_native_executor_matches_python_schedule(cuda, streams, depth):
     masks = [(t.mean(dim=2) > 0.5).float() for t in targets]
     depths = [torch.rand((H, W), generator=g, device=cuda) for _ in range(V)] if depth else None
     res = {}
-    saved = fm.NATIVE_EXEC, fm.NUM_STREAMS
+    saved = fm.NATIVE_EXEC, fm.NUM_STREAMS, fm.GRAPH_MODE
     try:
         for native in (False, True):
-            fm.NATIVE_EXEC, fm.NUM_STREAMS = ("1" if native else "0"), streams
+            # the eager schedules every step (not the default's batched steps for views this small)
+            fm.NATIVE_EXEC, fm.NUM_STREAMS, fm.GRAPH_MODE = ("1" if native else "0"), streams, "0"
             f = fm.ViewShardedFitter(bench.synthetic_params(50_000, cuda), cams, targets, W, H, masks=masks, depths=depths)
             losses = [float(f.step()) for _ in range(2)]
             res[native] = (losses, {k: v.detach().clone() for k, v in f.params.items()})
     finally:
-        fm.NATIVE_EXEC, fm.NUM_STREAMS = saved
+        fm.NATIVE_EXEC, fm.NUM_STREAMS, fm.GRAPH_MODE = saved
     assert res[True][0] == res[False][0]
     # the default ("auto") takes the native executor for views this small
     f = fm.ViewShardedFitter(bench.synthetic_params(1000, cuda), cams, targets, W, H)
@@ -88,7 +89,7 @@ def test_native_executor_rejects_out_of_range_config(pkg, cuda):
     accp = (ctypes.c_void_p * 4)(*[t.data_ptr() for t in acc])
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     losses = torch.empty(1, device=cuda)
-    bad = [dict(reduce_tail=17), dict(reduce_tail=5, reduce_batch=4), dict(prep_first=5), dict(prep_group=5),
+    bad = [dict(reduce_tail=17), dict(reduce_tail=5, reduce_batch=4), dict(prep_first=9), dict(prep_group=9),
            dict(reduce_batch=17)]
     for b in bad:
         c = dict(num_streams=1, prep_ahead=2, prep_group=2, prep_first=1, reduce_batch=4, reduce_tail=0)

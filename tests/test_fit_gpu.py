@@ -301,7 +301,7 @@ def test_fused_param_step_matches_torch_adam(cuda):
 
 @pytest.mark.parametrize("sh", [False, True])
 def test_grouped_prepare_matches_single_view_prepare(cuda, sh):
-    """gr_fwd_prepare_views_async (parameters read once for up to 4 views) writes, per view, exactly the geom
+    """gr_fwd_prepare_views_async (parameters read once for up to 8 views) writes, per view, exactly the geom
     workspace (records, depths, rectangles, counts, the pair totals, plan) and the pinned-host plan that
     gr_fwd_prepare_async writes for that view alone (the Gaussians' offsets are the binning's: k_emit_cols)."""
     import torch
@@ -317,13 +317,13 @@ def test_grouped_prepare_matches_single_view_prepare(cuda, sh):
         del params["colors_raw"]
     with torch.no_grad():
         acts = [a.contiguous() for a in fm.activations(params)]
-    cams = fm.orbit_cameras(4, W, H, cuda)
+    cams = fm.orbit_cameras(8, W, H, cuda)
     gvs = [tr.make_view(c.view, c.proj, W, H, None, cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF, depth_grad=False)
            for c in cams]
-    pins = torch.zeros((8, 3), dtype=torch.int64, pin_memory=True)
-    for k in (4, 3, 2):
+    pins = torch.zeros((16, 3), dtype=torch.int64, pin_memory=True)
+    for k in (8, 5, 4, 3, 2):
         grouped = tr.prepare_views_native(*acts, gvs[:k], [pins[q] for q in range(k)])
-        single = [tr.prepare_native(*acts, gv, plan_host=pins[4 + (q % 4)]) for q, gv in enumerate(gvs[:k])]
+        single = [tr.prepare_native(*acts, gv, plan_host=pins[8 + q]) for q, gv in enumerate(gvs[:k])]
         for q, (a, b) in enumerate(zip(grouped, single)):
             pa, pb = a.plan(), b.plan()
             assert (pa.num_pairs, pa.num_slots, pa.num_core_pairs) == (pb.num_pairs, pb.num_slots, pb.num_core_pairs)

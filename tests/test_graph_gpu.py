@@ -10,6 +10,10 @@ graph and replayed (fit_multiview.GRAPH, ViewShardedFitter._graph_step; VERDICT 
   the depth term, and across an in-place Morton re-sort.
 * test_graph_overflow_and_redo: capacities forced below the counts at capture: the replayed step overflows, updates
   nothing, and is redone with grown capacities; the fit stays bit-identical to the eager one.
+* test_batched_steps_bit_identical_to_eager: the views' kernels launched once per batch of up to 8 views
+  (gr_fit_views_batched, GR_GRAPH=batch, and that step captured, batchgraph) give the eager schedule's parameters,
+  moments, gradients and losses bit for bit (every block computes what it computes in its own view's launch; the chain
+  rules run in the single-stream schedule's grouping), for the fit path at 32- and 16-pixel tiles and the depth loss.
 """
 from __future__ import annotations
 
@@ -92,9 +96,15 @@ def test_sized_view_matches_host_sized(cuda, mode):
     assert over[0] > 0.0 and torch.isfinite(torch.tensor(over[0]))
 
 
+def _set_mode(fm, mode):
+    """fit_multiview's GR_GRAPH mode ("0", "1", "sized", "exec", "batch", "batchgraph", "auto")."""
+    fm.GRAPH_MODE = mode
+
+
 def _run(fm, params_fn, cams, targets, masks, depths, W, H, steps, graph, resort=0):
-    saved = fm.GRAPH, fm.RESORT_EVERY
-    fm.GRAPH, fm.RESORT_EVERY = graph, resort
+    saved = fm.GRAPH_MODE, fm.RESORT_EVERY
+    _set_mode(fm, graph if isinstance(graph, str) else ("1" if graph else "0"))
+    fm.RESORT_EVERY = resort
     try:
         f = fm.ViewShardedFitter(params_fn(), cams, targets, W, H, lr=0.02, masks=masks, depths=depths)
         losses = [f.step() for _ in range(steps)]
@@ -107,7 +117,8 @@ def _run(fm, params_fn, cams, targets, masks, depths, W, H, steps, graph, resort
         gs = getattr(f, "_gs", None)
         return [float(x) for x in losses], out, mom, grads, f.perm.clone() if f.perm is not None else None, gs
     finally:
-        fm.GRAPH, fm.RESORT_EVERY = saved
+        _set_mode(fm, saved[0])
+        fm.RESORT_EVERY = saved[1]
 
 
 def _assert_same(a, b):
@@ -172,3 +183,25 @@ def test_graph_overflow_and_redo(cuda, monkeypatch):
     _assert_same(eager, graph)
     print(f"overflow and redo: {gs.overflows} redo(s), capacities grown to "
           f"{[int(c.num_pairs) for c in gs.caps]}; bit-identical to eager")
+
+
+@pytest.mark.parametrize("case", ["fit32", "fit16", "depth_sh3", "fit32_graph", "depth_graph"])
+def test_batched_steps_bit_identical_to_eager(cuda, case, monkeypatch):
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    bench = importlib.import_module("bench")
+    W, H = 192, 160
+    depth = case.startswith("depth")
+    if case == "fit16":
+        monkeypatch.setattr(fm, "FIT_TILE", 16)
+    V = 11  # two batches of views (8 + 3), three streams' reduction groupings
+    _, cams, targets, masks, depths = _scene(bench, fm, cuda, 40_000, V, W, H, depth=depth, sh=depth)
+
+    def params_fn():
+        return _scene(bench, fm, cuda, 40_000, V, W, H, depth=depth, sh=depth)[0]
+
+    monkeypatch.setattr(fm, "NUM_STREAMS", 1)  # the batched step reduces in the single-stream schedule's grouping
+    eager = _run(fm, params_fn, cams, targets, masks, depths, W, H, 5, False)
+    batched = _run(fm, params_fn, cams, targets, masks, depths, W, H, 5, "batchgraph" if case.endswith("graph") else "batch")
+    assert batched[5] is not None and batched[5].overflows == 0
+    _assert_same(eager, batched)
+    print(f"{case}: 5 steps of {V} views batched, bit-identical to eager; losses {batched[0]}")

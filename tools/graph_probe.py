@@ -27,7 +27,7 @@ def fitter():
 
 
 for graph in [m == "1" for m in os.environ.get("PROBE_MODES", "01")]:
-    fm.GRAPH = graph
+    fm.GRAPH_MODE = os.environ.get("GR_GRAPH", "1") if graph else "0"
     f = fitter()
     f.step(); f.step()
     torch.cuda.synchronize()
