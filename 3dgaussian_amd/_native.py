@@ -46,6 +46,8 @@ class GrView(ctypes.Structure):
         ("tile", ctypes.c_int),  # screen tile edge: 0/16 (default) or 32 (fused fit path)
         ("device_counts", ctypes.c_int),  # 1: plans are capacities, the counts stay on the device (sized preparation)
         ("chunk", ctypes.c_int),  # work-item length in pairs (0: the default 2048)
+        ("row0", ctypes.c_int),  # a band of tile rows [row0, row0 + rows) (rows 0: the whole view)
+        ("rows", ctypes.c_int),
     ]
 
 

@@ -113,6 +113,7 @@ int bits_for(uint32_t maxval) {
 struct ViewK {
   int W, H, tiles_x, tiles_y;
   int T, ts;          // tile edge and its log2 (the preparation and binning; the splat kernels are per tile size)
+  int ty0, ty1;       // the band of tile rows rendered (gr_view.row0 / rows; the whole view: 0, tiles_y)
   float V[16], P[16];
   float bg[3];
   float cam[3];
@@ -133,6 +134,8 @@ ViewK make_viewk(const gr_view* v) {
   static_assert(T == 16, "ViewK::ts");
   k.tiles_x = tiles_x_of(v->width, k.T);
   k.tiles_y = tiles_y_of(v->height, k.T);
+  k.ty0 = v->rows > 0 ? v->row0 : 0;
+  k.ty1 = v->rows > 0 ? std::min(v->row0 + v->rows, k.tiles_y) : k.tiles_y;
   std::memcpy(k.V, v->view, sizeof(k.V));
   std::memcpy(k.P, v->proj, sizeof(k.P));
   std::memcpy(k.bg, v->background, sizeof(k.bg));
@@ -265,6 +268,12 @@ __device__ __forceinline__ int tile_rect(const ViewK& v, const Proj& p, float op
   const int y0 = (loy <= 0.0f) ? 0 : (int)floorf(loy);
   const int y1 = (hiy >= hm1) ? (v.H - 1) : (int)ceilf(hiy);
   r = make_int4(x0 >> v.ts, y0 >> v.ts, x1 >> v.ts, y1 >> v.ts);  // (x0, y0 >= 0: the oracle's x0 / T)
+  r.y = max(r.y, v.ty0);  // a band of tile rows (gr_view.rows): the tiles outside it get no pair
+  r.w = min(r.w, v.ty1 - 1);
+  if (r.y > r.w) {
+    r = make_int4(0, 0, -1, -1);
+    return 0;
+  }
   return (r.z - r.x + 1) * (r.w - r.y + 1);
 }
 
@@ -2533,7 +2542,7 @@ __device__ __forceinline__ void k_raster_fwd_mfma_body(ViewK v, int n, const int
     if (tid == 0) ticket[tile] = 0;  // left zero for a later render of the same bins
   }
   const int x = tx * T + (tid & (T - 1)), y = ty * T + (tid >> 4);
-  const bool inside = x < v.W && y < v.H;
+  const bool inside = x < v.W && y < v.H && ty >= v.ty0 && ty < v.ty1;  // (a band view: its rows only)
   if (inside) write_pixel(v, y * v.W + x, acc, out_rgb, out_alpha, out_depth, saved4, savedD);
   if constexpr (MODE == 4 || MODE == 5) {
     // an empty tile has no backward work item: only its loss terms are needed, not its fragments
@@ -3149,7 +3158,7 @@ __device__ __forceinline__ void k_fwd32_l1_body(ViewK v, int n, const int4* __re
     const int x = tx * T32 + px0, y = ty * T32 + py0 + 8 * q;
 #pragma unroll
     for (int c = 0; c < 5; ++c) u[q][c] = 0.f;
-    if (x < v.W && y < v.H) {
+    if (x < v.W && y < v.H && ty >= v.ty0 && ty < v.ty1) {  // (a band view: its rows only)
       const int p = y * v.W + x;
       const float a5[5] = {acc[q][0], acc[q][1], acc[q][2], acc[q][3], 0.0f};
       write_pixel(v, p, a5, out_rgb, out_alpha, nullptr, nullptr, nullptr);
@@ -4657,6 +4666,8 @@ gr_status check_view(const gr_view* v) {
   if (v->width <= 0 || v->height <= 0) return set_error(GR_ERR_INVALID_ARGUMENT, "width/height must be positive");
   if ((int64_t)v->width * v->height > (1ll << 30)) return set_error(GR_ERR_INVALID_ARGUMENT, "image too large");
   if (v->tile != 0 && v->tile != T && v->tile != T32) return set_error(GR_ERR_INVALID_ARGUMENT, "tile must be 0, 16 or 32");
+  if (v->rows < 0 || (v->rows > 0 && (v->row0 < 0 || v->row0 >= tiles_y_of(v->height, tile_of(v)))))
+    return set_error(GR_ERR_INVALID_ARGUMENT, "row0 / rows: a band of the view's tile rows");
   return GR_OK;
 }
 
@@ -5171,6 +5182,8 @@ static gr_status fwd_impl(const gr_view* v, int n, const gr_plan* plan, const vo
   const ViewK vk = make_viewk(v);
   const int tiles = vk.tiles_x * vk.tiles_y, vtiles = 2 * tiles;
   const TileCfg tc = tile_cfg(v, num_pairs);
+  if (v->rows > 0 && !l1)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "a band of tile rows (gr_view.rows): gr_fwd_render_l1 only (the fit loss)");
   if (tc.T == T32 && (!l1 || v->no_depth_grad != 1))
     return set_error(GR_ERR_INVALID_ARGUMENT, "32-pixel tiles (gr_view.tile = 32): gr_fwd_render_l1 with no_depth_grad = 1 only");
   if (tc.T == T32 && vk.core != vk.cutoff)
@@ -5299,6 +5312,8 @@ static gr_status bwd_impl(const gr_view* v, int n, const gr_plan* plan, const fl
                      "depth gradient for a view rendered with no_depth_grad (render it with depth_grad=True)");
   if (tile_of(v) != T)
     return set_error(GR_ERR_INVALID_ARGUMENT, "32-pixel tiles (gr_view.tile = 32): the fused fit path only (gr_bwd_splat)");
+  if (v->rows > 0)
+    return set_error(GR_ERR_INVALID_ARGUMENT, "a band of tile rows (gr_view.rows): the fused fit path only (gr_bwd_splat)");
   if (!plan) return set_error(GR_ERR_INVALID_ARGUMENT, "plan is null");
   if (color_dim != 3 && color_dim != 12 && color_dim != 48)
     return set_error(GR_ERR_INVALID_ARGUMENT, "colors must be (N,3) or SH coeffs (N,4,3) / (N,16,3)");
@@ -5536,6 +5551,9 @@ gr_status gr_fit_views_batched(int num_views, const gr_batch_view* bv, int n, fl
     return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views_batched: depth loss needs no_depth_grad = 0, the L1 path 1");
   if (depth && tile_of(&v0) != T)
     return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views_batched: the depth-loss path runs at 16-pixel tiles");
+  for (int j = 0; j < num_views && depth; ++j)
+    if (bv[j].view.rows > 0)
+      return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_views_batched: a band of tile rows needs the L1 path (no depth loss)");
   hipStream_t s = (hipStream_t)stream;
   const int tiles = vtiles_of(&v0) / 2;
   const size_t HW = (size_t)v0.width * v0.height;

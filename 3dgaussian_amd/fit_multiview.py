@@ -125,6 +125,15 @@ FIT_TILE = int(os.environ.get("GR_FIT_TILE", "32"))
 #               fill the GPU and the eager step's stream overlap wins (C4 1,557 eager vs 1,446 batched)
 GRAPH_MODE = os.environ.get("GR_GRAPH", "auto")
 GRAPH_AUTO_PIXELS = 512 * 512
+# multi-GPU: the views left over by the even split (V mod R) are cut into R bands of tile rows, one per rank
+# (gr_view.row0 / rows), so every rank renders V / R views' worth of pixels (50 views on 8 ranks: 6 views and two
+# eighths each instead of 7 on two ranks); the fused path without a depth term only (a depth term needs the whole
+# image's depth maximum).  0 = whole views round-robin.
+BAND_SPLIT = os.environ.get("GR_BAND_SPLIT", "1") != "0"
+# a band costs about this fraction of a whole view beyond its share of the pixels (its preparation, emission, gather
+# and chain rule run over every Gaussian): the split is used when the most loaded rank gains more than its bands cost
+# (C4 at 8 ranks: 3.25 -> 3.09 ms for rank 0; at 4 ranks, two half-view bands, 5.90 -> 5.96: not used)
+BAND_OVERHEAD = float(os.environ.get("GR_BAND_OVERHEAD", "0.3"))
 GRAPH_MARGIN = float(os.environ.get("GR_GRAPH_MARGIN", "1.25"))  # capacity over the counts seen (+ 4096 pairs)
 
 
@@ -254,16 +263,17 @@ def _fit_images(name: str, imgs: Optional[list], shape: tuple, device) -> tuple:
     return [torch.as_tensor(t).to(device=device, dtype=torch.float32).contiguous() for t in imgs], True
 
 
-def _batch_sizes(ns: int, nviews: int) -> list:
+def _batch_sizes(ns: int, nviews: int, tail: Optional[int] = None) -> list:
     """Per stream (views j = k, k + ns, ...): its views' reduction batches, near-equal and at most REDUCE_BATCH, in
     the order they fill; a short last batch of REDUCE_TAIL views (the reductions left when the renders end run alone).
     The native executor's schedule() is the same rule."""
     sizes = []
     for k in range(ns):
         p = len(range(k, nviews, ns))
-        tail = min(REDUCE_TAIL, REDUCE_BATCH) if 0 < REDUCE_TAIL < p else 0  # (gr_fit_views: tail <= batch)
-        nb = max(1, -(-(p - tail) // REDUCE_BATCH))
-        sizes.append([(p - tail) // nb + (1 if b < (p - tail) % nb else 0) for b in range(nb)] + ([tail] if tail else []))
+        rt = REDUCE_TAIL if tail is None else tail
+        t = min(rt, REDUCE_BATCH) if 0 < rt < p else 0  # (gr_fit_views: tail <= batch)
+        nb = max(1, -(-(p - t) // REDUCE_BATCH))
+        sizes.append([(p - t) // nb + (1 if b < (p - t) % nb else 0) for b in range(nb)] + ([t] if t else []))
     return sizes
 
 
@@ -353,7 +363,8 @@ class ViewShardedFitter:
         self.distributed = dist.is_available() and dist.is_initialized()
         self.rank = dist.get_rank(group) if self.distributed else 0
         self.world = dist.get_world_size(group) if self.distributed else 1
-        self.my_views = list(range(self.rank, len(targets), self.world))
+        self._rr_views = list(range(self.rank, len(targets), self.world))
+        self._bands = {}  # virtual view id (>= V) -> (view, first tile row, tile rows) of this rank's bands
         self.opt = torch.optim.Adam(list(self.params.values()), lr=lr)
         self.densify_seed = 1234
         self.steps_done = 0
@@ -395,6 +406,39 @@ class ViewShardedFitter:
             self._bg = torch.zeros(3, device=device)
         return self._bg
 
+    @property
+    def my_views(self) -> list:
+        """This rank's views: i = r, r + R, ... (whole views), or with band splitting the first R * (V // R) views
+        round-robin and this rank's band of each of the V mod R others (virtual ids V + i, _vi / _bands)."""
+        if not self._bands_ok():
+            return self._rr_views
+        V, W = len(self.targets), self.world
+        q = V // W
+        whole = list(range(self.rank, q * W, W))
+        tile = (16 if F32_GRADE else FIT_TILE) or 16
+        ty = -(-self.height // tile)
+        lo, hi = ty * self.rank // W, ty * (self.rank + 1) // W
+        if hi <= lo:  # fewer tile rows than ranks: this rank has no band
+            return whole
+        bands = []
+        for i in range(q * W, V):
+            self._bands[V + i] = (i, lo, hi - lo)
+            bands.append(V + i)
+        return whole + bands
+
+    def _bands_ok(self) -> bool:
+        V, W = len(self.targets), self.world
+        r = V % W if W > 1 else 0
+        # the most loaded rank sheds 1 - r / W views and takes r bands
+        if not (BAND_SPLIT and r and (1.0 - r / W) > BAND_OVERHEAD * r and not self._depth_grad()):
+            return False
+        dev = self.params["means"].device
+        return dev.type == "cuda" and self._direct(dev)
+
+    def _vi(self, v: int) -> int:
+        """The view index of a (possibly virtual, band) view id."""
+        return v - len(self.targets) if v >= len(self.targets) else v
+
     def _depth_grad(self) -> bool:
         """The loss differentiates the depth output (a depth term): the views render in the default
         precision mode with the depth-gradient cutoff; otherwise depth_grad=False (gr_view.no_depth_grad)."""
@@ -431,7 +475,18 @@ class ViewShardedFitter:
     def _fit_view(self, i: int, device) -> "tr._native.GrView":
         """The gr_view of view i for the fused path (one FIT_CUTOFF zone, no depth gradient), built once:
         cameras and background do not change during a fit (saves the host's matrix inverse and copies
-        twice per view and step)."""
+        twice per view and step).  A band id (>= V): that view with its band of tile rows."""
+        if i >= len(self.targets):
+            b = getattr(self, "_band_gv", None)
+            if b is None:
+                self._band_gv = b = {}
+            key = (i, F32_GRADE, FIT_TILE) + self._bands[i]
+            gv = b.get(key)
+            if gv is None:
+                base, row0, rows = self._bands[i]
+                gv = b[key] = tr._native.GrView.from_buffer_copy(self._fit_view(base, device))
+                gv.row0, gv.rows = row0, rows
+            return gv
         cache = getattr(self, "_gv_cache", None)
         if cache is None:
             self._gv_cache = cache = {}
@@ -640,8 +695,8 @@ class ViewShardedFitter:
                 else:
                     arr[j].view = self._fit_view(i, device) if sized is None else tr.sized_view(self._fit_view(i, device))
                     arr[j].target_depth = None
-                arr[j].target_rgb = self.targets[i].data_ptr()
-                arr[j].target_mask = self.masks[i].data_ptr() if w_sil > 0.0 else None
+                arr[j].target_rgb = self.targets[self._vi(i)].data_ptr()
+                arr[j].target_mask = self.masks[self._vi(i)].data_ptr() if w_sil > 0.0 else None
             self._native_targets = cache = (key, arr)
         cfg = tr._native.GrFitConfig(NUM_STREAMS, PREP_AHEAD, PREP_GROUP, PREP_FIRST, REDUCE_BATCH, min(REDUCE_TAIL, REDUCE_BATCH))
         if sized is not None:  # device-side sizing: the capacities, the observed counts, the overflow word
@@ -760,8 +815,8 @@ class ViewShardedFitter:
             with torch.cuda.stream(streams[k]):
                 # one zone at the core cutoff and no depth channel: the loss reads neither depth nor the
                 # tail-only part of W's footprint (torch_renderer.FIT_CUTOFF)
-                rs, ws = tr.forward_l1_native(m, s, c, o, pv.gv, pv, self.targets[i],
-                                              self.masks[i] if w_sil > 0.0 else None, w_sil, g_scale, losses_v[j:j + 1],
+                rs, ws = tr.forward_l1_native(m, s, c, o, pv.gv, pv, self.targets[self._vi(i)],
+                                              self.masks[self._vi(i)] if w_sil > 0.0 else None, w_sil, g_scale, losses_v[j:j + 1],
                                               bin_stream=bin_stream)
                 pv = None
                 tr.backward_splat_native(rs, ws)
@@ -1276,10 +1331,10 @@ class ViewShardedFitter:
             gs.batch_ws = bw = (bkey, gvs, ws)
         _, gvs, ws = bw
         losses_v = torch.empty(max(1, len(views)), dtype=torch.float32, device=device)
-        # the chain rules in the single-stream schedule's grouping (one accumulator set, batches of up to
-        # REDUCE_BATCH views with the short REDUCE_TAIL batch last): the same sums in the same order as
-        # _views_direct / _views_direct_depth with GR_STREAMS=1, so the same parameters bit for bit (fewer chain-rule
-        # launches and one accumulator for the update to read instead of one per stream)
+        # the chain rules in one accumulator set, batches of up to REDUCE_BATCH views (every view is gathered before
+        # the first chain rule, so no short tail batch): the same sums in the same order as _views_direct /
+        # _views_direct_depth with GR_STREAMS=1 and GR_REDUCE_TAIL=0, so the same parameters bit for bit (one chain-rule
+        # launch for up to 16 views, one accumulator for the update to read instead of one per stream)
         ns = 1
         shapes = (ns,) + tuple(tuple(t.shape) for t in (m, s, c, o))
         cached = getattr(self, "_direct_acc", None)
@@ -1307,14 +1362,14 @@ class ViewShardedFitter:
                 e.scratch, e.scratch_bytes = w["scratch"].data_ptr(), w["scratch"].numel()
                 e.ws, e.ws_bytes = w["ws"].data_ptr(), w["ws"].numel()
                 e.saved = w["saved"].data_ptr() if depth else None
-                e.target_rgb = self.targets[i].data_ptr()
-                e.target_mask = self.masks[i].data_ptr() if w_sil > 0.0 else None
+                e.target_rgb = self.targets[self._vi(i)].data_ptr()
+                e.target_mask = self.masks[self._vi(i)].data_ptr() if w_sil > 0.0 else None
                 e.target_depth = self.depths[i].data_ptr() if depth else None
                 e.sums, e.sums3 = w["sums"].data_ptr(), (w["sums3"].data_ptr() if depth else None)
                 e.loss = losses_v[q:q + 1].data_ptr()
             nat.check(L.gr_fit_views_batched(len(js), arr, n, ctypes.c_float(w_sil), ctypes.c_float(self.w_depth if depth else 0.0),
                                              ctypes.c_float(g_scale), stream), "gr_fit_views_batched")
-        for k, sizes in enumerate(_batch_sizes(ns, len(views))):
+        for k, sizes in enumerate(_batch_sizes(ns, len(views), tail=0)):
             mine = list(range(k, len(views), ns))
             at = 0
             for b in sizes:

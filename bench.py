@@ -386,6 +386,8 @@ def splat_replay(fitter, device) -> dict:
     w_sil = fitter.w_sil if fitter.masks is not None else 0.0
     preps = []
     for i in fitter.my_views:
+        if i >= V:  # (a band of a view, multi-GPU: the roofline times whole views)
+            continue
         gv = fitter._fit_view(i, device)
         preps.append((i, gv, tr.prepare_native(*acts, gv)))
     torch.cuda.synchronize()
@@ -398,11 +400,11 @@ def splat_replay(fitter, device) -> dict:
         ws = torch.empty((tr._ws_round(L.gr_bwd_bytes(ctypes.byref(gv), n, ctypes.byref(plan))),), dtype=torch.uint8,
                          device=device)
         loss = torch.zeros(1, device=device)
-        mask = fitter.masks[i] if fitter.masks is not None else None
+        mask = fitter.masks[fitter._vi(i)] if fitter.masks is not None else None
         e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         e[0].record(cur)
         nat.check(L.gr_fwd_render_l1(ctypes.byref(bgv), n, ctypes.byref(plan), nat.ptr(prep.geom), nat.ptr(bins),
-                                     bins.numel(), nat.ptr(scratch), scratch.numel(), nat.ptr(fitter.targets[i]),
+                                     bins.numel(), nat.ptr(scratch), scratch.numel(), nat.ptr(fitter.targets[fitter._vi(i)]),
                                      nat.ptr(mask), ctypes.c_float(w_sil), ctypes.c_float(1.0 / V), nat.ptr(loss), None,
                                      None, nat.ptr(ws), ws.numel(), sp), "gr_fwd_render_l1")
         e[1].record(cur)
@@ -452,6 +454,8 @@ def main():
     masks = [(t.mean(dim=2) > 0.5).to(torch.float32) for t in targets]
     fitter = fm.ViewShardedFitter(params, cams, targets, R, R, lr=0.02, masks=masks, reorder=not args.no_reorder)
     views_per_rank = [len(range(r, V, world)) for r in range(world)]
+    if fitter._bands_ok():  # the leftover views in bands of tile rows, one per rank
+        views_per_rank = [round(V / world, 3)] * world
 
     def timed(steps):
         sync()

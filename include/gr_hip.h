@@ -106,6 +106,11 @@ typedef struct gr_view {
                        /* power of two <= num_pairs / 1024 within [512, 2048] (at least ~4 items per CU).    */
                        /* Each item is one workgroup of the splats; the split tiles' partial sums are added */
                        /* in item order, so the value changes float rounding, deterministically.            */
+  int row0;            /* rows > 0: only the band of tile rows [row0, row0 + rows) is rendered: Gaussians are  */
+  int rows;            /* binned to its tiles only and the fit loss and its gradient cover its pixels only    */
+                       /* (normalised by the whole image's pixel count), so the bands of a view add up to    */
+                       /* the view.  The fused fit path only (gr_fwd_render_l1, gr_bwd_splat, gather, reduce, */
+                       /* gr_fit_views_batched without depth): a multi-GPU fit splits views across ranks.     */
 } gr_view;
 
 /* ------------------------------------------------------------------------------------------ */

@@ -43,6 +43,8 @@ class GrView(ctypes.Structure):
         ("tile", ctypes.c_int),  # tile edge of the binned semantics: 0/16 or 32
         ("device_counts", ctypes.c_int),  # (the HIP path's device-side sizing; the oracle ignores it)
         ("chunk", ctypes.c_int),  # (the HIP path's work-item length; the oracle ignores it)
+        ("row0", ctypes.c_int),  # a band of tile rows [row0, row0 + rows) (rows 0: the whole view)
+        ("rows", ctypes.c_int),
     ]
 
 

@@ -58,8 +58,8 @@ def test_struct_sizes_match_header(pkg):
     # gr_view: 2 ints + 16 + 16 + 3 + 3 + 2 floats + 1 int, then the background_dev pointer (8-aligned);
     # gr_render_params: RenderParams' layout
     from oracle import oracle as orc
-    # then binned, tile, device_counts, chunk
-    assert ctypes.sizeof(pkg._native.GrView) == 4 * (2 + 16 + 16 + 3 + 3 + 2 + 1) + 4 + 8 + 16
+    # then binned, tile, device_counts, chunk, row0, rows
+    assert ctypes.sizeof(pkg._native.GrView) == 4 * (2 + 16 + 16 + 3 + 3 + 2 + 1) + 4 + 8 + 24
     assert [f[0] for f in pkg._native.GrView._fields_] == [f[0] for f in orc.GrView._fields_]
     assert ctypes.sizeof(pkg._native.GrRenderParams) == 4 * (2 + 16 + 16 + 3 + 3)
     # gr_param_step: int64, 2 ints, 2 pointers, GR_FIT_MAX_ACC pointers, 2 pointers, 3 floats (+ tail padding)

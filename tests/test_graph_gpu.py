@@ -13,7 +13,7 @@ graph and replayed (fit_multiview.GRAPH, ViewShardedFitter._graph_step; VERDICT 
 * test_batched_steps_bit_identical_to_eager: the views' kernels launched once per batch of up to 8 views
   (gr_fit_views_batched, GR_GRAPH=batch, and that step captured, batchgraph) give the eager schedule's parameters,
   moments, gradients and losses bit for bit (every block computes what it computes in its own view's launch; the chain
-  rules run in the single-stream schedule's grouping), for the fit path at 32- and 16-pixel tiles and the depth loss.
+  rules run in the single-stream schedule's grouping without its tail batch), for the fit path at 32- and 16-pixel tiles and the depth loss.
 """
 from __future__ import annotations
 
@@ -199,9 +199,59 @@ def test_batched_steps_bit_identical_to_eager(cuda, case, monkeypatch):
     def params_fn():
         return _scene(bench, fm, cuda, 40_000, V, W, H, depth=depth, sh=depth)[0]
 
-    monkeypatch.setattr(fm, "NUM_STREAMS", 1)  # the batched step reduces in the single-stream schedule's grouping
+    # the batched step reduces in the single-stream schedule's grouping, without the short tail batch
+    monkeypatch.setattr(fm, "NUM_STREAMS", 1)
+    monkeypatch.setattr(fm, "REDUCE_TAIL", 0)
     eager = _run(fm, params_fn, cams, targets, masks, depths, W, H, 5, False)
     batched = _run(fm, params_fn, cams, targets, masks, depths, W, H, 5, "batchgraph" if case.endswith("graph") else "batch")
     assert batched[5] is not None and batched[5].overflows == 0
     _assert_same(eager, batched)
     print(f"{case}: 5 steps of {V} views batched, bit-identical to eager; losses {batched[0]}")
+
+
+@pytest.mark.parametrize("world", [3, 8])
+@pytest.mark.parametrize("schedule", ["python", "native"])
+def test_band_split_adds_up_to_the_views(cuda, world, schedule, monkeypatch):
+    """Multi-GPU view sharding with the leftover views cut into bands of tile rows (BAND_SPLIT, gr_view.row0 / rows):
+    every emulated rank's loss and gradient (this process playing each rank in turn, no collective) sum to the
+    single-process step's, within float summation order; each band renders only its rows (a band's pairs are those
+    of its tile rows)."""
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    bench = importlib.import_module("bench")
+    monkeypatch.setattr(fm, "BAND_OVERHEAD", 0.0)  # bands whatever they cost
+    W, H, V = 256, 224, 11  # 7 tile rows of 32 pixels
+    params, cams, targets, masks, _ = _scene(bench, fm, cuda, 50_000, V, W, H)
+    f = fm.ViewShardedFitter(params, cams, targets, W, H, lr=0.02, masks=masks)
+    acts = [a.detach().float().contiguous() for a in fm.activations(f.params)]
+
+    def run():
+        with torch.no_grad():
+            if schedule == "native":
+                total = f._views_native(*acts, False)
+            else:
+                total, _ = f._views_direct(*acts)
+            parts = f._acc_parts
+            acc = [sum(p[q] for p in parts[1:]) + parts[0][q] if len(parts) > 1 else parts[0][q].clone() for q in range(4)]
+        torch.cuda.synchronize()
+        return float(total), acc
+
+    ref_loss, ref = run()
+    tot_loss, tot = 0.0, [torch.zeros_like(a) for a in ref]
+    seen = []
+    for r in range(world):
+        f.rank, f.world = r, world
+        f._rr_views = list(range(r, V, world))
+        views = f.my_views
+        assert len([v for v in views if v >= V]) == (V % world if (7 * (r + 1)) // world > (7 * r) // world else 0)
+        seen += views
+        loss, acc = run()
+        tot_loss += loss
+        tot = [a + b for a, b in zip(tot, acc)]
+    f.rank, f.world = 0, 1
+    assert sorted(v for v in seen if v < V) == list(range(V - V % world))
+    assert abs(tot_loss - ref_loss) <= 1e-6 * abs(ref_loss), (tot_loss, ref_loss)
+    for k, (a, b) in enumerate(zip(tot, ref)):
+        err = float((a - b).norm() / b.norm())
+        assert err <= 1e-5, (k, err)
+    print(f"world {world} ({schedule}): bands of views {list(range(V - V % world, V))} add up: loss {tot_loss:.7f} "
+          f"vs {ref_loss:.7f}")
