@@ -768,7 +768,8 @@ __global__ __launch_bounds__(256) void k_preprocess_views(PrepBatch B, int n, co
   }
   __shared__ unsigned long long wsum[PREP_MAX_VIEWS][4];
   __shared__ float wmax[PREP_MAX_VIEWS][4];
-  for (int k = 0; k < B.nv; ++k) {
+  // views k = blockIdx.y, blockIdx.y + gridDim.y, ... (a grid of several view rows when few Gaussians fill it)
+  for (int k = blockIdx.y; k < B.nv; k += gridDim.y) {
     const Geom& g = B.g[k];
     if (i == n) {
       g.counts[n] = 0ull;
@@ -791,7 +792,7 @@ __global__ __launch_bounds__(256) void k_preprocess_views(PrepBatch B, int n, co
     }
   }
   __syncthreads();
-  if ((int)threadIdx.x < B.nv) {
+  if ((int)threadIdx.x < B.nv && (int)threadIdx.x % (int)gridDim.y == (int)blockIdx.y) {
     const int k = threadIdx.x;
     B.g[k].total[blockIdx.x] = (wsum[k][0] + wsum[k][1]) + (wsum[k][2] + wsum[k][3]);
     B.g[k].omax[blockIdx.x] = fmaxf(fmaxf(wmax[k][0], wmax[k][1]), fmaxf(wmax[k][2], wmax[k][3]));
@@ -4009,7 +4010,7 @@ struct SBatch {
   SViewK r[GR_REDUCE_MAX_VIEWS];
 };
 // waves per Gaussian group of k_reduce_sums (host and device)
-__host__ __device__ constexpr int reduce_sums_crw(int nv, int cd) { return cd == 48 ? 1 : (nv >= 3 ? 4 : (nv >= 1 ? nv : 1)); }
+__host__ __device__ constexpr int reduce_sums_crw(int nv, int cd) { return nv >= 3 ? 4 : (nv >= 1 ? nv : 1); }
 
 template <int CD>
 __global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const float* __restrict__ means,
@@ -4020,7 +4021,7 @@ __global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const floa
   // sum_index (gr_bwd_indexed): Gaussian gi's sums are row sum_index[gi] of the views' sums (a render of a permuted
   // copy); its parameters and gradients stay row gi
   constexpr int NG = 6 + CD;
-  __shared__ float sG[CD == 48 ? 1 : 4][64][NG + 1];
+  __shared__ float sG[4][64][NG + 1];
   const int crw = reduce_sums_crw(B.nv, CD);
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int gw = w / crw, u = w - gw * crw;
@@ -4038,7 +4039,7 @@ __global__ __launch_bounds__(256) void k_reduce_sums(SBatch B, int n, const floa
       chain_rule<CD, float>(B.r[vi].v, gi, Sf, on, means, scales, colors, opac, gr);
     }
   }
-  if constexpr (CD != 48) {
+  {
     if (crw > 1) {  // uniform per launch
       float* mine = sG[w][lane];
 #pragma unroll
@@ -4566,8 +4567,28 @@ __global__ __launch_bounds__(256) void k_fit_param_step(int64_t count, int act, 
 struct ParamSteps {
   gr_param_step s[GR_FIT_MAX_PARAMS];
   int first[GR_FIT_MAX_PARAMS + 1];
+  int vec4[GR_FIT_MAX_PARAMS];  // 1: count % 4 == 0 and every array 16-byte aligned (float4 loads and stores)
   int num;
 };
+// One element of k_fit_param_steps: the activation's backward on the summed gradient, then Adam (torch's
+// single-tensor update order).  Returns the gradient; m, v and x are updated in place.
+__device__ __forceinline__ float fit_param_elem(int act, float gact, float& x, float& m, float& v, float neg_step,
+                                                float bc2s, float b1, float b2, float b2_c, float eps) {
+  float g;
+  if (act == 1) {  // softplus backward: g z / (z + 1), z = exp(x) (x <= 20), else g
+    const float z = expf(x);
+    g = x > 20.0f ? gact : gact * z / (z + 1.0f);
+  } else if (act == 2) {  // sigmoid backward: g (1 - y) y
+    const float y = 1.0f / (1.0f + expf(-x));
+    g = gact * (1.0f - y) * y;
+  } else {
+    g = gact;
+  }
+  m = fmaf(b1, g - m, m);
+  v = fmaf(b2_c, g * g, v * b2);
+  x = fmaf(neg_step, m / (sqrtf(v) / bc2s + eps), x);
+  return g;
+}
 // sched (gr_fit_param_steps_sched): the step's (neg_step_size, bias_correction2_sqrt) are sched[2 *step_dev + 0/1], and a
 // step whose views overflowed their capacities (*ovf) updates nothing.
 __global__ __launch_bounds__(256) void k_fit_param_steps(ParamSteps P, float b1, float b2, float b2_c, float eps,
@@ -4583,27 +4604,38 @@ __global__ __launch_bounds__(256) void k_fit_param_steps(ParamSteps P, float b1,
   float* __restrict__ p = q.param;
   float* __restrict__ m = q.exp_avg;
   float* __restrict__ v = q.exp_avg_sq;
-  for (int64_t e = (int64_t)(blockIdx.x - P.first[t]) * 256 + threadIdx.x; e < q.count; e += (int64_t)nb * 256) {
+  const int64_t e0 = (int64_t)(blockIdx.x - P.first[t]) * 256 + threadIdx.x, stride = (int64_t)nb * 256;
+  if (P.vec4[t]) {  // the same per-element arithmetic, four elements per thread
+    for (int64_t e = e0; e < q.count / 4; e += stride) {
+      float4 ga = q.num_accs > 0 ? ((const float4*)q.accs[0])[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int a = 1; a < q.num_accs; ++a) {  // in stream order
+        const float4 u = ((const float4*)q.accs[a])[e];
+        ga.x = ga.x + u.x;
+        ga.y = ga.y + u.y;
+        ga.z = ga.z + u.z;
+        ga.w = ga.w + u.w;
+      }
+      float4 x = ((float4*)p)[e], mm = ((float4*)m)[e], vv = ((float4*)v)[e], g;
+      g.x = fit_param_elem(q.act, ga.x + q.reg, x.x, mm.x, vv.x, neg_step, bc2s, b1, b2, b2_c, eps);
+      g.y = fit_param_elem(q.act, ga.y + q.reg, x.y, mm.y, vv.y, neg_step, bc2s, b1, b2, b2_c, eps);
+      g.z = fit_param_elem(q.act, ga.z + q.reg, x.z, mm.z, vv.z, neg_step, bc2s, b1, b2, b2_c, eps);
+      g.w = fit_param_elem(q.act, ga.w + q.reg, x.w, mm.w, vv.w, neg_step, bc2s, b1, b2, b2_c, eps);
+      if (q.grad) ((float4*)q.grad)[e] = g;
+      ((float4*)m)[e] = mm;
+      ((float4*)v)[e] = vv;
+      ((float4*)p)[e] = x;
+    }
+    return;
+  }
+  for (int64_t e = e0; e < q.count; e += stride) {
     float gact = q.num_accs > 0 ? q.accs[0][e] : 0.0f;
     for (int a = 1; a < q.num_accs; ++a) gact = gact + q.accs[a][e];  // in stream order
-    gact = gact + q.reg;
-    const float x = p[e];
-    float g;
-    if (q.act == 1) {
-      const float z = expf(x);
-      g = x > 20.0f ? gact : gact * z / (z + 1.0f);
-    } else if (q.act == 2) {
-      const float y = 1.0f / (1.0f + expf(-x));
-      g = gact * (1.0f - y) * y;
-    } else {
-      g = gact;
-    }
+    float x = p[e], mm = m[e], vv = v[e];
+    const float g = fit_param_elem(q.act, gact + q.reg, x, mm, vv, neg_step, bc2s, b1, b2, b2_c, eps);
     if (q.grad) q.grad[e] = g;
-    const float mm = fmaf(b1, g - m[e], m[e]);
-    const float vv = fmaf(b2_c, g * g, v[e] * b2);
     m[e] = mm;
     v[e] = vv;
-    p[e] = fmaf(neg_step, mm / (sqrtf(vv) / bc2s + eps), x);
+    p[e] = x;
   }
 }
 
@@ -4981,13 +5013,15 @@ static gr_status prepare_views_impl(int num_views, const gr_view* views, int n, 
     all_mapped = all_mapped && (hp.p[k] || caps);
   }
   const int blocks = blocks_for(n + 1);
+  // rows of views: at least ~1024 blocks (4 per CU) when the views allow, each view still run by one row alone
+  const dim3 pgrid(blocks, std::max(1, std::min(num_views, (1024 + blocks - 1) / blocks)));
   for (int rep = 0; rep < GR_DEBUG_PREP_REPS; ++rep) {  // > 1: timing experiments only (idempotent repeats)
   if (color_dim == 3)
-    hipLaunchKernelGGL(k_preprocess_views<3>, dim3(blocks), dim3(256), 0, s, B, n, means, scales, colors, opacities);
+    hipLaunchKernelGGL(k_preprocess_views<3>, pgrid, dim3(256), 0, s, B, n, means, scales, colors, opacities);
   else if (color_dim == 12)
-    hipLaunchKernelGGL(k_preprocess_views<12>, dim3(blocks), dim3(256), 0, s, B, n, means, scales, colors, opacities);
+    hipLaunchKernelGGL(k_preprocess_views<12>, pgrid, dim3(256), 0, s, B, n, means, scales, colors, opacities);
   else
-    hipLaunchKernelGGL(k_preprocess_views<48>, dim3(blocks), dim3(256), 0, s, B, n, means, scales, colors, opacities);
+    hipLaunchKernelGGL(k_preprocess_views<48>, pgrid, dim3(256), 0, s, B, n, means, scales, colors, opacities);
   GR_HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_plan_views, dim3(num_views), dim3(PLAN_THREADS), 0, s, B, n, hp);
   GR_HIP_TRY(hipGetLastError());
@@ -6084,8 +6118,13 @@ static gr_status param_steps_impl(int num, const gr_param_step* steps, double be
     for (int a = 0; a < q.num_accs; ++a)
       if (!q.accs[a]) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_param_steps: null accumulator");
     if (q.count == 0) continue;
+    auto al = [](const void* a) { return a == nullptr || ((uintptr_t)a & 15u) == 0; };
+    bool v4 = q.count % 4 == 0 && al(q.param) && al(q.grad) && al(q.exp_avg) && al(q.exp_avg_sq);
+    for (int a = 0; a < q.num_accs; ++a) v4 = v4 && al(q.accs[a]);
     P.s[P.num] = q;
-    P.first[P.num + 1] = P.first[P.num] + (int)std::min<int64_t>((q.count + 255) / 256, 1024);
+    P.vec4[P.num] = v4 ? 1 : 0;
+    // one element (or float4) per thread up to 16384 blocks per tensor: the loads of one pass are all in flight
+    P.first[P.num + 1] = P.first[P.num] + (int)std::min<int64_t>(((v4 ? q.count / 4 : q.count) + 255) / 256, 16384);
     ++P.num;
   }
   if (P.num == 0 && !sched) return GR_OK;

@@ -1,5 +1,6 @@
 """GPU: gr_fit_param_steps (every parameter tensor's gradient and Adam update in one launch) gives exactly what one
-gr_fit_param_step per tensor gives, for each activation and with one to three stream accumulators."""
+gr_fit_param_step per tensor gives, for each activation and with one to three stream accumulators, on both of its
+paths (float4 when the count is a multiple of 4 and every array 16-byte aligned, scalar otherwise)."""
 from __future__ import annotations
 
 import ctypes
@@ -12,19 +13,21 @@ import torch
 def test_param_steps_equal_per_tensor_steps(pkg, cuda):
     nat = pkg._native
     L = nat.lib()
-    # (count, activation, accumulators, regulariser): identity / softplus / sigmoid, sizes across block boundaries
-    specs = [(3 * 1000, 0, 3, 0.0), (3 * 777, 1, 2, 1e-4), (1_000_003, 2, 1, 2e-6), (255, 2, 0, 0.0)]
+    # (count, activation, accumulators, regulariser, element offset of every array): identity / softplus / sigmoid,
+    # sizes across block boundaries; offset 1 misaligns a count that is a multiple of 4 (the scalar path)
+    specs = [(3 * 1000, 0, 3, 0.0, 0), (3 * 777, 1, 2, 1e-4, 0), (1_000_003, 2, 1, 2e-6, 0), (255, 2, 0, 0.0, 0),
+             (4_000_000, 1, 3, 1e-5, 0), (4096, 2, 2, 0.0, 1), (48 * 50_000, 0, 1, 0.0, 0)]
     b1, b2, eps = 0.9, 0.999, 1e-15
     runs = []
     for fused in (False, True):
         state = []
-        for q, (n, act, na, reg) in enumerate(specs):
+        for q, (n, act, na, reg, off) in enumerate(specs):
             gg = torch.Generator(device=cuda).manual_seed(10 + q)
-            p = torch.randn(n, generator=gg, device=cuda) * 3.0
-            m = torch.randn(n, generator=gg, device=cuda) * 1e-3
-            v = torch.rand(n, generator=gg, device=cuda) * 1e-6
-            accs = [torch.randn(n, generator=gg, device=cuda) for _ in range(na)]
-            state.append((p, torch.empty_like(p), accs, m, v, act, reg, -(1e-3 / (1 - b1 ** (q + 2))),
+            p = (torch.randn(n + off, generator=gg, device=cuda) * 3.0)[off:]
+            m = (torch.randn(n + off, generator=gg, device=cuda) * 1e-3)[off:]
+            v = (torch.rand(n + off, generator=gg, device=cuda) * 1e-6)[off:]
+            accs = [torch.randn(n + off, generator=gg, device=cuda)[off:] for _ in range(na)]
+            state.append((p, torch.empty(n + off, device=cuda)[off:], accs, m, v, act, reg, -(1e-3 / (1 - b1 ** (q + 2))),
                           (1 - b2 ** (q + 2)) ** 0.5))
         stream = ctypes.c_void_p(torch.cuda.current_stream(cuda).cuda_stream)
         if fused:

@@ -36,6 +36,10 @@ for step in "$@"; do
       (cd $R && timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1) ;;
     configs)
       (cd $R && timeout -k 10 300 python tools/bench_configs.py C2 C3 > $O/configs.txt 2>$O/configs.err) ;;
+    c3prof)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c3 -o run --output-format csv -- \
+        python3 $R/tools/bench_configs.py C3 > $O/c3prof.log 2>&1)
+      (cd $R && python tools/kstats.py $O/c3 > $O/kernel_stats_c3.txt) ;;
     pmc)
       (cd $R && bash tools/pmc_profile.sh gpurun_out/$TAG/pmc && cp $O/pmc/pmc.json $R/profiles/pmc_traffic.json) ;;
     ab:*)  # ab:<rounds>:<dir>,<dir>... same-box bench A/B of tree copies (tools/ab_bench.sh)
