@@ -184,6 +184,9 @@ _SIG = {
                                           ctypes.c_float, _P]),
     "gr_fit_param_steps_sched": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(GrParamStep), ctypes.c_double, ctypes.c_double,
                                                 ctypes.c_float, _P, _P, _P, _P, _P]),
+    "gr_fit_activations_ws_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
+    "gr_fit_activations": (ctypes.c_int, [ctypes.c_int64, _P, _P, _P, ctypes.c_int64, _P, _P, _P, ctypes.c_float,
+                                          ctypes.c_float, _P, _P, ctypes.c_size_t, _P]),
     "gr_fwd_render_l1": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P, _P,
                                         ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, ctypes.c_size_t, _P]),
     "gr_bwd_splat": (ctypes.c_int, [_VP, ctypes.c_int, _PP, _P, _P, _P, ctypes.c_size_t, _P]),

@@ -4652,6 +4652,71 @@ __global__ void k_step_advance(int* __restrict__ step_dev, int* __restrict__ ovf
   __threadfence_system();
 }
 
+// The fit loop's activations (gr_fit_activations) with torch's float formulas (softplus: x > 20 ? x : log1p(exp(x));
+// sigmoid: 1 / (1 + exp(-x))), and optionally the regulariser's two sums: per block in double, the last block to
+// arrive adds the blocks' sums in block order.
+constexpr int ACT_BLOCKS = 1024;
+__global__ __launch_bounds__(256) void k_fit_activations(int64_t n, const float* __restrict__ s_raw,
+                                                         const float* __restrict__ o_raw, const float* __restrict__ c_raw,
+                                                         int64_t nc, float* __restrict__ s, float* __restrict__ o,
+                                                         float* __restrict__ c, float w_s, float w_o,
+                                                         float* __restrict__ reg_out, double* __restrict__ part,
+                                                         int* __restrict__ ticket) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  double ss = 0.0, so = 0.0;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < 3 * n; e += stride) {
+    const float x = s_raw[e];
+    const float y = (x > 20.0f ? x : log1pf(expf(x))) + 1e-3f;
+    s[e] = y;
+    ss += (double)y;
+  }
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += stride) {
+    const float y = 1.0f / (1.0f + expf(-o_raw[e]));
+    o[e] = y;
+    so += (double)y;
+  }
+  if (c_raw)
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nc; e += stride) c[e] = 1.0f / (1.0f + expf(-c_raw[e]));
+  if (!reg_out) return;  // (uniform)
+  __shared__ double sh[2][4];
+  __shared__ int last;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    ss += __shfl_xor(ss, m);
+    so += __shfl_xor(so, m);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][threadIdx.x >> 6] = ss;
+    sh[1][threadIdx.x >> 6] = so;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) st_through(&part[2 * blockIdx.x + threadIdx.x], (sh[threadIdx.x][0] + sh[threadIdx.x][1]) + (sh[threadIdx.x][2] + sh[threadIdx.x][3]));
+  if (!arrive_last(ticket, (int)gridDim.x, &last)) return;
+  // the last block: thread t sums blocks t, t + 256, ... in order, then the 256 partial sums in a fixed tree
+  double ts = 0.0, to = 0.0;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += 256) {
+    ts += ld_through(&part[2 * b]);
+    to += ld_through(&part[2 * b + 1]);
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    ts += __shfl_xor(ts, m);
+    to += __shfl_xor(to, m);
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][threadIdx.x >> 6] = ts;
+    sh[1][threadIdx.x >> 6] = to;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double ms = ((sh[0][0] + sh[0][1]) + (sh[0][2] + sh[0][3])) / (double)(3 * n);
+    const double mo = ((sh[1][0] + sh[1][1]) + (sh[1][2] + sh[1][3])) / (double)n;
+    *reg_out = w_o * (float)mo + w_s * (float)ms;
+    *ticket = 0;
+  }
+}
+
 // Adam alone on an assembled (e.g. all-reduced) gradient.
 __global__ __launch_bounds__(256) void k_adam_step(int64_t count, float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, float neg_step,
@@ -6144,6 +6209,35 @@ static gr_status param_steps_impl(int num, const gr_param_step* steps, double be
     hipLaunchKernelGGL(k_step_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, step_dev, overflow, mapped);
     GR_HIP_TRY(hipGetLastError());
   }
+  return GR_OK;
+}
+
+size_t gr_fit_activations_ws_bytes(int64_t n) {
+  (void)n;
+  return 2 * ACT_BLOCKS * sizeof(double) + 256;
+}
+
+gr_status gr_fit_activations(int64_t n, const float* scales_raw, const float* opacities_raw, const float* colors_raw,
+                             int64_t color_count, float* scales, float* opacities, float* colors, float reg_scale,
+                             float reg_opacity, float* reg_out, void* ws, size_t ws_bytes, void* stream) {
+  if (n < 0 || color_count < 0) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_activations: negative count");
+  if (n > 0 && (!scales_raw || !opacities_raw || !scales || !opacities))
+    return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_activations: null pointer");
+  if (colors_raw && color_count > 0 && !colors) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_activations: null colors");
+  if (reg_out && (!ws || ws_bytes < gr_fit_activations_ws_bytes(n)))
+    return set_error(GR_ERR_WORKSPACE, "gr_fit_activations: workspace too small");
+  if (n == 0) {
+    if (reg_out) return set_error(GR_ERR_INVALID_ARGUMENT, "gr_fit_activations: the regulariser of no Gaussians");
+    return GR_OK;
+  }
+  const int64_t most = std::max<int64_t>(3 * n, colors_raw ? color_count : 0);
+  const int blocks = (int)std::min<int64_t>(ACT_BLOCKS, (most + 255) / 256);
+  double* part = (double*)ws;
+  int* ticket = ws ? (int*)((char*)ws + 2 * ACT_BLOCKS * sizeof(double)) : nullptr;
+  hipLaunchKernelGGL(k_fit_activations, dim3(blocks), dim3(256), 0, (hipStream_t)stream, n, scales_raw, opacities_raw,
+                     colors_raw, colors_raw ? color_count : 0, scales, opacities, colors, reg_scale, reg_opacity, reg_out,
+                     part, ticket);
+  GR_HIP_TRY(hipGetLastError());
   return GR_OK;
 }
 

@@ -167,6 +167,31 @@ def activations(params: dict):
     return means, scales, colors, opacities
 
 
+def activations_native(params: dict, reg=None, ws=None):
+    """activations() in one HIP launch (gr_fit_activations: the same float formulas as torch's softplus and
+    sigmoid), for the fused step, which needs no autograd graph; with reg = (reg_opacity, reg_scale) also the
+    regulariser reg_opacity * mean(opacities) + reg_scale * mean(scales) (fit_multiview_stub.py:307-308) as a 0-d
+    device tensor, summed in the same launch (ws: a zeroed uint8 tensor of gr_fit_activations_ws_bytes).
+    Returns (means, scales, colors, opacities, reg or None)."""
+    nat = tr._native
+    L = nat.lib()
+    means = params["means"].detach()
+    sr, orw = params["scales_raw"].detach().contiguous(), params["opacities_raw"].detach().contiguous()
+    cr = params["colors_raw"].detach().contiguous() if "colors_raw" in params else None
+    n = int(means.shape[0])
+    scales, opacities = torch.empty_like(sr), torch.empty_like(orw)
+    colors = torch.empty_like(cr) if cr is not None else params["sh_raw"].detach()
+    out = torch.empty((), dtype=torch.float32, device=means.device) if reg is not None and n > 0 else None
+    nat.check(L.gr_fit_activations(n, nat.ptr(sr), nat.ptr(orw), nat.ptr(cr) if cr is not None else None,
+                                   int(cr.numel()) if cr is not None else 0, nat.ptr(scales), nat.ptr(opacities),
+                                   nat.ptr(colors) if cr is not None else None,
+                                   ctypes.c_float(reg[1] if reg else 0.0), ctypes.c_float(reg[0] if reg else 0.0),
+                                   nat.ptr(out) if out is not None else None,
+                                   ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0,
+                                   ctypes_stream(means.device)), "gr_fit_activations")
+    return means, scales, colors, opacities, out
+
+
 def densify_and_prune(params: dict, max_gaussians: int, densify_ratio: float, prune_opacity: float) -> dict:
     """fit_multiview_stub.py:140-197, evaluated on the host (CPU RNG for the jitter) so that every
     rank that calls it with the same RNG state gets identical parameters."""
@@ -550,9 +575,8 @@ class ViewShardedFitter:
         self.opt.zero_grad(set_to_none=True)
         if self._direct(device) and self.params["means"].shape[0] > 0 and self._fused_step_ok():
             with torch.no_grad():
-                means, scales, colors, opacities = activations(self.params)
-                reg_fn = ((lambda: self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean())
-                          if self.rank == 0 else None)
+                means, scales, colors, opacities, reg_t = self._activations_fused(device)
+                reg_fn = (lambda: reg_t) if reg_t is not None else None
                 reg = None
                 if self._native_exec() and GATHER:
                     total = self._views_native(means, scales, colors, opacities, self._depth_grad())
@@ -1165,12 +1189,27 @@ class ViewShardedFitter:
             tab[t, 1] = (1.0 - b2 ** u) ** 0.5
         return torch.from_numpy(tab.reshape(-1)).to(device), T
 
+    def _act_ws_for(self, device) -> torch.Tensor:
+        """activations_native's workspace, kept per fitter (made outside any capture: _graph_build asks first)."""
+        ws = getattr(self, "_act_ws", None)
+        if ws is None or ws.device != device:
+            self._act_ws = ws = torch.zeros(int(tr._native.lib().gr_fit_activations_ws_bytes(0)), dtype=torch.uint8,
+                                            device=device)
+        return ws
+
+    def _activations_fused(self, device):
+        """The fused step's activations and (rank 0) regulariser in one launch (activations_native)."""
+        ws = self._act_ws_for(device)
+        if self.params["means"].shape[0] == 0:
+            means, scales, colors, opacities = activations(self.params)
+            return means, scales, colors, opacities, None
+        return activations_native(self.params, (self.reg_opacity, self.reg_scale) if self.rank == 0 else None, ws)
+
     def _graph_body(self, gs):
         """The fused step (step()'s first branch, eager) on device-sized views, for capture."""
         with torch.no_grad():
-            means, scales, colors, opacities = activations(self.params)
-            reg_fn = ((lambda: self.reg_opacity * opacities.mean() + self.reg_scale * scales.mean())
-                      if self.rank == 0 else None)
+            means, scales, colors, opacities, reg_t = self._activations_fused(self.params["means"].device)
+            reg_fn = (lambda: reg_t) if reg_t is not None else None
             mode = self._graph_mode()
             if mode in ("batch", "batchgraph"):  # one launch per kernel for up to 8 views (gr_fit_views_batched), one stream
                 reg = reg_fn() if reg_fn else None
@@ -1218,6 +1257,7 @@ class ViewShardedFitter:
             gs.sched, gs.sched_len = self._graph_sched(device, t0)
             gs.sched_key = self._graph_key()[2:5]
         gs.done_host = t0
+        self._act_ws_for(device)  # (made before any capture)
         torch.cuda.synchronize(device)
         if self._graph_mode() in ("1", "batchgraph"):
             g = torch.cuda.CUDAGraph()

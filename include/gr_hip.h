@@ -453,6 +453,16 @@ gr_status gr_fit_param_steps(int num, const gr_param_step* steps, double beta1, 
  * it), mirrors *step_dev to host_flags[1] and clears *overflow for the next step.  host_flags: pinned host int[2]. */
 gr_status gr_fit_param_steps_sched(int num, const gr_param_step* steps, double beta1, double beta2, float eps,
                                    const float* sched, int* step_dev, int* overflow, int* host_flags, void* stream);
+/* gr_fit_activations: the fit loop's activations (fit_multiview_stub.py:268-275) in one launch, torch's float formulas:
+ * scales = softplus(scales_raw) + 1e-3 (3n floats; x > 20: x), opacities = sigmoid(opacities_raw) (n), and with
+ * colors_raw colors = sigmoid(colors_raw) (color_count floats; NULL for SH coefficients, used as they are).  With
+ * reg_out, also the regulariser of :307-308, reg_opacity * mean(opacities) + reg_scale * mean(scales), as a device
+ * float (the means in double over a fixed block order, then rounded): ws of gr_fit_activations_ws_bytes(n), whose
+ * counter must be zero on the first call and is left zero. */
+size_t gr_fit_activations_ws_bytes(int64_t n);
+gr_status gr_fit_activations(int64_t n, const float* scales_raw, const float* opacities_raw, const float* colors_raw,
+                             int64_t color_count, float* scales, float* opacities, float* colors, float reg_scale,
+                             float reg_opacity, float* reg_out, void* ws, size_t ws_bytes, void* stream);
 
 /* The fused fit path for up to GR_BATCH_MAX_VIEWS views of one image size in one launch per kernel: per view what
  * gr_fwd_render_l1 + gr_bwd_splat + gr_gather_view do (no_depth_grad = 1; 16- or 32-pixel tiles), or with

@@ -4,6 +4,7 @@ paths (float4 when the count is a multiple of 4 and every array 16-byte aligned,
 from __future__ import annotations
 
 import ctypes
+import importlib
 
 import pytest
 import torch
@@ -53,3 +54,36 @@ def test_param_steps_equal_per_tensor_steps(pkg, cuda):
     for a, b in zip(*runs):
         for x, y in zip(a, b):
             assert torch.equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,rgb", [(1, True), (1000, True), (300_001, False), (2_000_000, True)])
+def test_fit_activations_match_torch(pkg, cuda, n, rgb):
+    """gr_fit_activations (the fused step's activations, one launch) gives torch's softplus + 1e-3 and sigmoid bit for
+    bit, across softplus's threshold (x > 20) and both tails of the sigmoid; its regulariser (reg_opacity * mean(o) +
+    reg_scale * mean(s), the means in double) is torch's float32 value within 1e-6; the workspace counter is left
+    zero (a second call, same results)."""
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    gg = torch.Generator(device=cuda).manual_seed(n)
+    params = {"means": torch.randn((n, 3), generator=gg, device=cuda),
+              "scales_raw": torch.randn((n, 3), generator=gg, device=cuda) * 12.0,
+              "opacities_raw": torch.randn((n,), generator=gg, device=cuda) * 40.0}
+    if rgb:
+        params["colors_raw"] = torch.randn((n, 3), generator=gg, device=cuda) * 30.0
+    else:
+        params["sh_raw"] = torch.randn((n, 16, 3), generator=gg, device=cuda)
+    if n >= 4:  # the thresholds and tails exactly
+        params["scales_raw"].view(-1)[:4] = torch.tensor([20.0, 20.000002, -104.0, 88.0], device=cuda)
+        params["opacities_raw"][:4] = torch.tensor([-88.0, 104.0, 0.0, -1e-8], device=cuda)
+    ws = torch.zeros(int(pkg._native.lib().gr_fit_activations_ws_bytes(n)), dtype=torch.uint8, device=cuda)
+    w_o, w_s = 1e-3, 2.5e-4
+    ref = fm.activations(params)
+    ref_reg = float(w_o * ref[3].mean() + w_s * ref[1].mean())
+    for _ in range(2):
+        m, s, c, o, reg = fm.activations_native(params, (w_o, w_s), ws)
+        torch.cuda.synchronize()
+        assert m.data_ptr() == params["means"].data_ptr()
+        assert torch.equal(s, ref[1]) and torch.equal(o, ref[3]) and torch.equal(c, ref[2])
+        assert abs(float(reg) - ref_reg) <= 1e-6 * abs(ref_reg), (float(reg), ref_reg)
+    _, s2, _, o2, none = fm.activations_native(params)  # no regulariser, no workspace
+    assert none is None and torch.equal(s2, ref[1]) and torch.equal(o2, ref[3])

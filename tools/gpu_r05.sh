@@ -35,11 +35,15 @@ for step in "$@"; do
     smoke)
       (cd $R && timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1) ;;
     configs)
-      (cd $R && timeout -k 10 300 python tools/bench_configs.py C2 C3 > $O/configs.txt 2>$O/configs.err) ;;
+      (cd $R && timeout -k 10 300 python tools/bench_configs.py C2 C3 --steps 20 > $O/configs.txt 2>$O/configs.err) ;;
     c3prof)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c3 -o run --output-format csv -- \
         python3 $R/tools/bench_configs.py C3 > $O/c3prof.log 2>&1)
       (cd $R && python tools/kstats.py $O/c3 > $O/kernel_stats_c3.txt) ;;
+    c4dprof)
+      (cd /tmp && GR_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c4d -o run --output-format csv -- \
+        python3 $R/tools/bench_configs.py C4d --steps 2 --warmup 1 > $O/c4dprof.log 2>&1)
+      (cd $R && python tools/kstats.py $O/c4d > $O/kernel_stats_c4d.txt) ;;
     pmc)
       (cd $R && bash tools/pmc_profile.sh gpurun_out/$TAG/pmc && cp $O/pmc/pmc.json $R/profiles/pmc_traffic.json) ;;
     ab:*)  # ab:<rounds>:<dir>,<dir>... same-box bench A/B of tree copies (tools/ab_bench.sh)
