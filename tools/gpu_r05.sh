@@ -44,6 +44,10 @@ for step in "$@"; do
       (cd /tmp && GR_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c4d -o run --output-format csv -- \
         python3 $R/tools/bench_configs.py C4d --steps 2 --warmup 1 > $O/c4dprof.log 2>&1)
       (cd $R && python tools/kstats.py $O/c4d > $O/kernel_stats_c4d.txt) ;;
+    c4dstreams)  # the depth-loss mode at 1, 2 and 4 HIP streams
+      for ns in 1 2 4; do
+        (cd $R && GR_STREAMS=$ns timeout -k 10 300 python tools/bench_configs.py C4d --steps 4 --warmup 2 >> $O/c4d_streams.txt 2>>$O/c4d_streams.err)
+      done ;;
     pmc)
       (cd $R && bash tools/pmc_profile.sh gpurun_out/$TAG/pmc && cp $O/pmc/pmc.json $R/profiles/pmc_traffic.json) ;;
     ab:*)  # ab:<rounds>:<dir>,<dir>... same-box bench A/B of tree copies (tools/ab_bench.sh)
