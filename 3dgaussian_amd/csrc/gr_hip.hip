@@ -3996,7 +3996,7 @@ __global__ __launch_bounds__(256) void k_gather_view_views(VBatch<k_gather_view_
 
 // Chain rule of up to GR_REDUCE_MAX_VIEWS views' gathered sums: one lane per Gaussian; the crw waves of a
 // Gaussian group take views u, u + crw, ... (crw = 4 from three views, else the view count, so that no
-// wave idles: a block holds 4 / crw groups of 64 Gaussians; SH degree 3: crw = 1), the wave totals are
+// wave idles: a block holds 4 / crw groups of 64 Gaussians; SH degree 3 too: 240 VGPRs, 56 KiB LDS), the wave totals are
 // combined in wave order and written (or added, acc) once.  A Gaussian whose eight sums are all zero
 // touched no tile of that view (its chain rule would add zero).  Deterministic; for a given view count
 // the summation order is fixed (1 or 2 views: the sums a 4-wave group gives, without its idle waves' zeros).
