@@ -20,7 +20,7 @@ for step in "$@"; do
       (cd $R && timeout -k 10 300 python bench.py --no-cpu-baseline --no-psnr > $O/benchq.log 2>&1) ;;
     stats1)
       (cd /tmp && GR_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats1 -o run --output-format csv -- \
-        python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extra-modes --no-dropin --no-psnr > $O/bench_prof1.log 2>&1)
+        python3 $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-extra-modes --no-dropin --no-psnr > $O/bench_prof1.log 2>&1)
       (cd $R && python tools/kstats.py $O/stats1 > $O/kernel_stats_1stream.txt) ;;
     stats4)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats4 -o run --output-format csv -- \
