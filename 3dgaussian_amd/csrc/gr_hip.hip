@@ -2955,8 +2955,14 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
 }
 
 
+// k_fwd32_l1 at 4 waves/SIMD with its record fields loaded axis by axis (GR_FWD32_STREAM: 116 VGPRs, no spill);
+// loading all five fields up front needs 124 VGPRs (3 waves; 15 spilled at 4).  Same box, three rounds each:
+// forward 161-165 -> 160-162 us, step +0.6% (profiles/r05_ab_fwd32_stream.txt)
 #ifndef GR_FWD32_WAVES
-#define GR_FWD32_WAVES 3
+#define GR_FWD32_WAVES 4
+#endif
+#ifndef GR_FWD32_STREAM
+#define GR_FWD32_STREAM 1
 #endif
 #ifndef GR_BWD32_WAVES
 #define GR_BWD32_WAVES 3
@@ -3060,13 +3066,42 @@ __device__ __forceinline__ void k_fwd32_l1_body(ViewK v, int n, const int4* __re
           q[2] = f32x2_t{u1.x, u1.y};
           q[3] = f32x2_t{u1.z, u1.w};
         };
+        f32x2_t oe[4], bv[4];
+#if GR_FWD32_STREAM
+        // the record fields loaded axis by axis behind scheduling fences (fewer live registers: 4 waves/SIMD)
+        {
+          f32x2_t px[4], qx[4], o[4];
+          ld(0, px);
+          ld(2, qx);
+          ld(4, o);
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const f32x2_t dx = X - px[p];
+            const f32x2_t ax = __builtin_elementwise_fma(dx * qx[p], dx, SA);
+            const f32x2_t ex = {__builtin_amdgcn_exp2f(ax.x), __builtin_amdgcn_exp2f(ax.y)};
+            oe[p] = o[p] * ex;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        {
+          f32x2_t py[4], qy[4];
+          ld(1, py);
+          ld(3, qy);
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const f32x2_t dy = Y - py[p];
+            const f32x2_t ay = __builtin_elementwise_fma(dy * qy[p], dy, SB);
+            bv[p] = f32x2_t{__builtin_amdgcn_exp2f(ay.x), __builtin_amdgcn_exp2f(ay.y)};
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#else
         f32x2_t px[4], py[4], qx[4], qy[4], o[4];
         ld(0, px);
         ld(1, py);
         ld(2, qx);
         ld(3, qy);
         ld(4, o);
-        f32x2_t oe[4], bv[4];
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
           const f32x2_t dx = X - px[p], dy = Y - py[p];
@@ -3076,6 +3111,7 @@ __device__ __forceinline__ void k_fwd32_l1_body(ViewK v, int n, const int4* __re
           bv[p] = f32x2_t{__builtin_amdgcn_exp2f(ay.x), __builtin_amdgcn_exp2f(ay.y)};
           oe[p] = o[p] * ex;
         }
+#endif
         s16x8 fb[2], fa[2];
         split2h_frag2(bv, fb);
         split2h_frag2(oe, fa);
