@@ -53,6 +53,14 @@ for step in "$@"; do
     ab:*)  # ab:<rounds>:<dir>,<dir>... same-box bench A/B of tree copies (tools/ab_bench.sh)
       IFS=: read -r _ n dirs <<< "$step"
       (cd $R && bash tools/ab_bench.sh $TAG $n ${dirs//,/ } > $O/ab.txt 2>&1) ;;
+    abdrop:*)  # abdrop:<rounds>:<dir>,<dir>... same-box A/B of the drop-in loop (tools/dropin_run.py) between tree copies
+      IFS=: read -r _ n dirs <<< "$step"
+      for r in $(seq 1 $n); do
+        for d in ${dirs//,/ }; do
+          (cd $R/$d && timeout -k 10 240 python tools/dropin_run.py 3 1 > $O/abdrop_$(basename $(cd $R/$d && pwd))_$r.log 2>&1)
+          echo "$(basename $(cd $R/$d && pwd)) round $r: $(grep '^{' $O/abdrop_$(basename $(cd $R/$d && pwd))_$r.log)" >> $O/abdrop.txt
+        done
+      done ;;
     testk:*)  # testk:<pytest -k expression> a subset of the GPU tests
       (cd $R && timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -s -k "${step#testk:}" > $O/pytest_gpu_k.log 2>&1) ;;
     *)
