@@ -36,6 +36,8 @@ for step in "$@"; do
       (cd $R && timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1) ;;
     configs)
       (cd $R && timeout -k 10 300 python tools/bench_configs.py C2 C3 --steps 20 > $O/configs.txt 2>$O/configs.err) ;;
+    configs5)
+      (cd $R && timeout -k 10 400 python tools/bench_configs.py C5 C5d --steps 6 > $O/configs5.txt 2>$O/configs5.err) ;;
     c3prof)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c3 -o run --output-format csv -- \
         python3 $R/tools/bench_configs.py C3 > $O/c3prof.log 2>&1)
