@@ -2955,30 +2955,17 @@ __global__ __launch_bounds__(256, DEPTH ? GR_BF16_WAVES : GR_BF16_WAVES_ND) void
 }
 
 
-// k_fwd32_l1 at 4 waves/SIMD with its record fields loaded axis by axis (GR_FWD32_STREAM: 116 VGPRs, no spill);
+// k_fwd32_l1 at 4 waves/SIMD with its record fields loaded axis by axis (116 VGPRs, no spill);
 // loading all five fields up front needs 124 VGPRs (3 waves; 15 spilled at 4).  Same box, three rounds each:
 // forward 161-165 -> 160-162 us, step +0.6% (profiles/r05_ab_fwd32_stream.txt)
 #ifndef GR_FWD32_WAVES
 #define GR_FWD32_WAVES 4
-#endif
-#ifndef GR_FWD32_STREAM
-#define GR_FWD32_STREAM 1
 #endif
 #ifndef GR_BWD32_WAVES
 #define GR_BWD32_WAVES 3
 #endif
 #ifndef GR_BWD32_BATCH
 #define GR_BWD32_BATCH 256
-#endif
-// timing diagnostics only (results wrong): 1 = two piece products per K-step instead of three (32 MFMAs per group),
-// 2 = no exponentials (VALU), 4 = no T-side epilogue
-#ifndef GR_BWD32_DIAG
-#define GR_BWD32_DIAG 0
-#endif
-// GR_BWD32_M16 = 1: k_bwd32 on v_mfma_f32_16x16x32_bf16 with groups of 16 Gaussians (four lanes per Gaussian, each 8
-// consecutive pixels of the 32 on both axes; half the accumulators and exponentials per lane of the 32x32x16 form)
-#ifndef GR_BWD32_M16
-#define GR_BWD32_M16 0
 #endif
 // phase fences of k_bwd32 (GR_BWD32_FENCE = 1): the compiler may not move instructions across them, so a pass's
 // MFMAs are not hoisted above the previous pass's epilogue (which would keep every accumulator live at once)
@@ -3067,7 +3054,6 @@ __device__ __forceinline__ void k_fwd32_l1_body(ViewK v, int n, const int4* __re
           q[3] = f32x2_t{u1.z, u1.w};
         };
         f32x2_t oe[4], bv[4];
-#if GR_FWD32_STREAM
         // the record fields loaded axis by axis behind scheduling fences (fewer live registers: 4 waves/SIMD)
         {
           f32x2_t px[4], qx[4], o[4];
@@ -3095,23 +3081,6 @@ __device__ __forceinline__ void k_fwd32_l1_body(ViewK v, int n, const int4* __re
           }
         }
         __builtin_amdgcn_sched_barrier(0);
-#else
-        f32x2_t px[4], py[4], qx[4], qy[4], o[4];
-        ld(0, px);
-        ld(1, py);
-        ld(2, qx);
-        ld(3, qy);
-        ld(4, o);
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const f32x2_t dx = X - px[p], dy = Y - py[p];
-          const f32x2_t ax = __builtin_elementwise_fma(dx * qx[p], dx, SA);
-          const f32x2_t ay = __builtin_elementwise_fma(dy * qy[p], dy, SB);
-          const f32x2_t ex = {__builtin_amdgcn_exp2f(ax.x), __builtin_amdgcn_exp2f(ax.y)};
-          bv[p] = f32x2_t{__builtin_amdgcn_exp2f(ay.x), __builtin_amdgcn_exp2f(ay.y)};
-          oe[p] = o[p] * ex;
-        }
-#endif
         s16x8 fb[2], fa[2];
         split2h_frag2(bv, fb);
         split2h_frag2(oe, fa);
@@ -3220,23 +3189,12 @@ __device__ __forceinline__ void k_fwd32_l1_body(ViewK v, int n, const int4* __re
     for (int e = tid; e < 16 * 64; e += 256) {
       const int set = e >> 6, l = e & 63, side = set >> 3, c = (set >> 1) & 3, s = set & 1;
       float val[8];
-#if GR_BWD32_M16
-      // k_bwd32 on v_mfma_f32_16x16x32_bf16: set (side, channel, M-block s), lane l supplies A[m = l & 15][k = 8 (l >> 4) + j]
-      // with pixel k on the contracted axis and row m at pixel 8 (m >> 2) + 4 s + (m & 3) on the other
-      const int m = l & 15, r = 8 * (m >> 2) + 4 * s + (m & 3);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * (l >> 4) + j;
-        val[j] = side == 0 ? sU[c * T32 * F32_LD + k * F32_LD + r] : sU[c * T32 * F32_LD + r * F32_LD + k];
-      }
-#else
       const int m = l & 31, hh = l >> 5;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = 16 * s + kslot_pixel(hh, j);
         val[j] = side == 0 ? sU[c * T32 * F32_LD + k * F32_LD + m] : sU[c * T32 * F32_LD + m * F32_LD + k];
       }
-#endif
       s16x8 f2[2];
       split2_frag(val, f2);
       __builtin_memcpy(&fr[(set * 2 + 0) * 64 + l], &f2[0], 16);
@@ -3354,13 +3312,8 @@ __device__ __forceinline__ void k_bwd32_body(ViewK v, int n, const int4* __restr
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const float oq = (float)kslot_off(q);
-#if GR_BWD32_DIAG & 2
-          ex[s][q] = (q == 0 ? cX : fmaf(tX, 2.0f * oq, fmaf(a.z, oq * oq, cX)));
-          ey[s][q] = (q == 0 ? cY : fmaf(tY, 2.0f * oq, fmaf(a.w, oq * oq, cY)));
-#else
           ex[s][q] = __builtin_amdgcn_exp2f(q == 0 ? cX : fmaf(tX, 2.0f * oq, fmaf(a.z, oq * oq, cX)));
           ey[s][q] = __builtin_amdgcn_exp2f(q == 0 ? cY : fmaf(tY, 2.0f * oq, fmaf(a.w, oq * oq, cY)));
-#endif
         }
       }
       float S[NPART] = {-0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f};
@@ -3376,7 +3329,7 @@ __device__ __forceinline__ void k_bwd32_body(ViewK v, int n, const int4* __restr
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const s16x8 a0 = as_frag(A0[(s * 2) * 64 + lane]);
-          if (!(GR_BWD32_DIAG & 1)) d = mfma32b(a0, B[s][1], d);
+          d = mfma32b(a0, B[s][1], d);
           d = mfma32b(a0, B[s][0], d);
         }
         return d;
@@ -3480,145 +3433,6 @@ __global__ __launch_bounds__(256, GR_BWD32_WAVES) void k_bwd32_views(VBatch<k_bw
 
 
 
-// k_bwd32 on v_mfma_f32_16x16x32_bf16 (GR_BWD32_M16): groups of 16 Gaussians; lane l owns Gaussian n = l & 15 of the
-// group and the 8 consecutive pixels 8 g + j (g = l >> 4) of the tile's 32 on each axis: its B operands are ex at
-// x = 8 g + j (T, K = 32 x in one instruction) and ey at y = 8 g + j (R), and the A operands' rows are laid out (the
-// forward's fragment builder) so that M-block s's register r is pixel 8 g + 4 s + r of the other axis - again one of
-// the lane's own slots.  Per group and side: 4 channels x 2 M-blocks x 3 piece products; 8 accumulator registers per
-// channel.  The 8-float row of a pair is reduced over its four lanes (pair16 + pair32) and written as two dwords
-// per lane.
-__global__ __launch_bounds__(256, GR_BWD32_WAVES) void k_bwd32m(ViewK v, int n, const int4* __restrict__ items,
-                                                               const int* __restrict__ num_items, const int* __restrict__ pairs,
-                                                               const float4* __restrict__ rec, const uint4* __restrict__ UF,
-                                                               float* __restrict__ partials) {
-  constexpr int NB = GR_BWD32_BATCH;  // Gaussians staged per batch (NB / 4 per wave)
-  constexpr int WG = NB / 4;
-  static_assert(WG % 16 == 0 && WG <= 64, "k_bwd32m batch");
-  __shared__ __attribute__((aligned(16))) float4 sA[2][NB];
-  __shared__ __attribute__((aligned(16))) float4 sB[2][NB];
-  __shared__ __attribute__((aligned(16))) uint4 sUF[2 * 4 * 2 * 2 * 64];  // (side, channel, M-block, piece) x 64 lanes
-  const int nitems = num_items[1];
-  if ((int)blockIdx.x >= nitems) return;
-  const int item = xcd_item(blockIdx.x, nitems);
-  const int4 it = items[item];
-  const int tile = it.x >> 1, k0 = it.y, k1 = it.z;
-  if (k1 <= k0) return;
-  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nl = lane & 15, g = lane >> 4;
-  {  // the tile's 32 fragment chunks -> LDS (DMA)
-    const uint4* src = UF + (size_t)tile * UF32_FRAGS;
-    for (int cc = wave; cc < 32; cc += 4) glds16(src + 64 * cc + lane, sUF + 64 * cc);
-  }
-  const float pxb = (float)(tx * T32 + 8 * g) + 0.5f, pyb = (float)(ty * T32 + 8 * g) + 0.5f;
-  if (lane < WG) {  // the first batch: lanes < WG stage this wave's WG Gaussians
-    const int k = k0 + wave * WG + lane;
-    const int gid = stage_pair(stage_id(k, k1, pairs), k, k1);
-    glds16(rec_of(gid, n, rec), &sA[0][WG * wave]);
-    glds16(rec_of(gid, n, rec) + 1, &sB[0][WG * wave]);
-  }
-  int idn = stage_id(k0 + NB + wave * WG + (lane < WG ? lane : 0), k1, pairs);
-  int buf = 0;
-  for (int base = k0; base < k1; base += NB, buf ^= 1) {
-    stage_wait();
-    if (base == k0) __syncthreads();  // the fragment chunks (every wave's DMA) are in LDS
-    if (base + NB < k1 && lane < WG) {
-      const int gid = stage_pair(idn, base + NB + wave * WG + lane, k1);
-      glds16(rec_of(gid, n, rec), &sA[buf ^ 1][WG * wave]);
-      glds16(rec_of(gid, n, rec) + 1, &sB[buf ^ 1][WG * wave]);
-    }
-    idn = stage_id(base + 2 * NB + wave * WG + (lane < WG ? lane : 0), k1, pairs);
-    const int nb = min(NB, k1 - base);
-    for (int gi = 0; gi < WG / 16; ++gi) {
-      const int g0 = wave * WG + gi * 16;
-      if (g0 >= nb) break;  // wave-uniform
-      const int j = g0 + nl;
-      const float4 a = sA[buf][j];
-      const float4 b = sB[buf][j];
-      const int myslot = j < nb ? base + j : -1;
-      float ex[8], ey[8];
-      const float d0x = pxb - a.x, d0y = pyb - a.y;
-      {
-        const float tX = a.z * d0x, tY = a.w * d0y;
-        const float cX = tX * d0x, cY = tY * d0y;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const float oq = (float)q;
-          ex[q] = __builtin_amdgcn_exp2f(q == 0 ? cX : fmaf(tX, 2.0f * oq, fmaf(a.z, oq * oq, cX)));
-          ey[q] = __builtin_amdgcn_exp2f(q == 0 ? cY : fmaf(tY, 2.0f * oq, fmaf(a.w, oq * oq, cY)));
-        }
-      }
-      // one channel on one side, both M-blocks: 3 piece products each (a_lo b_hi, a_hi b_lo, a_hi b_hi)
-      auto contract = [&](int side, int c, const s16x8 (&B)[2], f32x4 (&d)[2]) {
-        const uint4* A0 = sUF + ((side * 4 + c) * 2 + 0) * 2 * 64;  // (side, c, M-block 0, piece 0)
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-          acc = mfma16(as_frag(A0[(mb * 2 + 1) * 64 + lane]), B[0], acc);
-          const s16x8 a0 = as_frag(A0[(mb * 2) * 64 + lane]);
-          acc = mfma16(a0, B[1], acc);
-          acc = mfma16(a0, B[0], acc);
-          d[mb] = acc;
-        }
-      };
-      float S[NPART] = {-0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f, -0.f};
-      float S6c = -0.f, S8c = -0.f, U0 = -0.f, S5c = -0.f, S7c = -0.f;
-      {  // T: contraction over x (B = ex), rows y = 8 g + 4 mb + r <-> ey[4 mb + r]
-        s16x8 BT[2];
-        split2_frag(ex, BT);
-        f32x4 D[4][2];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) contract(0, c, BT, D[c]);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int mb = i >> 2, r = i & 3;
-          const float e = ey[i], oq = (float)i;
-          const float T0 = D[0][mb][r], T1 = D[1][mb][r], T2 = D[2][mb][r], T3 = D[3][mb][r];
-          S[0] = fmaf(e, T0, S[0]);
-          S[1] = fmaf(e, T1, S[1]);
-          S[2] = fmaf(e, T2, S[2]);
-          const float t = e * fmaf(b.w, T2, fmaf(b.z, T1, fmaf(b.y, T0, T3)));
-          S[4] += t;
-          if (i != 0) {
-            S6c = fmaf(t, oq, S6c);
-            S8c = fmaf(t, oq * oq, S8c);
-          }
-        }
-      }
-      GR_BWD32_PHASE();
-      {  // R: contraction over y (B = ey), rows x = 8 g + 4 mb + r <-> ex[4 mb + r]
-        s16x8 BR[2];
-        split2_frag(ey, BR);
-        f32x4 D[4][2];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) contract(1, c, BR, D[c]);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int mb = i >> 2, r = i & 3;
-          const float oq = (float)i;
-          const float u = ex[i] * fmaf(b.w, D[2][mb][r], fmaf(b.z, D[1][mb][r], fmaf(b.y, D[0][mb][r], D[3][mb][r])));
-          U0 += u;
-          if (i != 0) {
-            S5c = fmaf(u, oq, S5c);
-            S7c = fmaf(u, oq * oq, S7c);
-          }
-        }
-      }
-      S[6] = fmaf(d0y, S[4], S6c);
-      S[8] = fmaf(d0y * d0y, S[4], fmaf(2.0f * d0y, S6c, S8c));
-      S[5] = fmaf(d0x, U0, S5c);
-      S[7] = fmaf(d0x * d0x, U0, fmaf(2.0f * d0x, S5c, S7c));
-      // the four lanes of Gaussian nl (rows g = 0..3) hold quarter sums: lane row g ends with row positions g and 4 + g
-      // of [o S0, o S2, S4, S6 | o S1, S8, S5, S7]
-      const float v1 = pair32(pair16(S[0], S[2]), pair16(S[4], S[6]));
-      const float v2 = pair32(pair16(S[1], S[8]), pair16(S[5], S[7]));
-      if (myslot >= 0) {
-        float* row = partials + 8 * (size_t)myslot;
-        row[g] = g < 2 ? b.x * v1 : v1;
-        row[4 + g] = g == 0 ? b.x * v2 : v2;
-      }
-    }
-  }
-}
 
 // ------------------------------------------------------------------------------------------------
 // Per-Gaussian reduction of pair partials + chain rule.  Deterministic.
@@ -5870,7 +5684,7 @@ gr_status gr_bwd_splat(const gr_view* v, int n, const gr_plan* plan, const void*
   if (GR_DEBUG_SKIP & 2) return GR_OK;
   prof_mark(PROF_RASTER_BWD, s);
   if (tc.T == T32)
-    hipLaunchKernelGGL(GR_BWD32_M16 ? k_bwd32m : k_bwd32, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
+    hipLaunchKernelGGL(k_bwd32, dim3((unsigned)cap), dim3(256), 0, s, vk, n, (const int4*)b.items,
                        (const int*)b.num_items, (const int*)b.pairs, (const float4*)g.rec, (const uint4*)w.UF, w.partials);
   else
   hipLaunchKernelGGL((v->no_depth_grad == 1 ? k_raster_bwd_bf16<false, 2> : k_raster_bwd_bf16<false, 3>), dim3((unsigned)cap),
@@ -6045,8 +5859,17 @@ gr_status gr_render_u8(const gr_render_params* p, int n, const float* means, con
   if (!p || !rgba) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");
   if (p->width <= 0 || p->height <= 0) return set_error(GR_ERR_INVALID_ARGUMENT, "width/height must be positive");
   const size_t HW = (size_t)p->width * p->height;
-  if (n <= 0) {  // renderer.cu:279-281
-    std::memset(rgba, 0, HW * 4);
+  if (n <= 0) {
+    if (p->force_cpu) {
+      // force_cpu selects the CPU renderer (renderer_dispatch.cpp:12-13), whose n <= 0 image is the finalized background
+      // with A = 255 in both modes (renderer_cpu.cpp:219-257: zero sums); for n > 0 this path already has its semantics
+      uint8_t px[4];
+      for (int c = 0; c < 3; ++c) px[c] = (uint8_t)(std::min(std::max(p->background[c], 0.0f), 1.0f) * 255.0f + 0.5f);
+      px[3] = 255;
+      for (size_t i = 0; i < HW; ++i) std::memcpy(rgba + 4 * i, px, 4);
+    } else {
+      std::memset(rgba, 0, HW * 4);  // the CUDA renderer's (renderer.cu:279-281)
+    }
     return GR_OK;
   }
   if (!means || !scales || !colors || !opacities) return set_error(GR_ERR_INVALID_ARGUMENT, "null pointer");

@@ -457,6 +457,8 @@ class ViewShardedFitter:
         # the most loaded rank sheds 1 - r / W views and takes r bands
         if not (BAND_SPLIT and r and (1.0 - r / W) > BAND_OVERHEAD * r and not self._depth_grad()):
             return False
+        if self.params["means"].shape[0] == 0:  # (the generic loop renders whole views only)
+            return False
         dev = self.params["means"].device
         return dev.type == "cuda" and self._direct(dev)
 
@@ -572,6 +574,7 @@ class ViewShardedFitter:
         device = self.params["means"].device
         if self._graph_ok(device):
             return self._graph_step(device)
+        self._graph_leave()
         self.opt.zero_grad(set_to_none=True)
         if self._direct(device) and self.params["means"].shape[0] > 0 and self._fused_step_ok():
             with torch.no_grad():
@@ -1146,7 +1149,8 @@ class ViewShardedFitter:
                 tuple((self.opt.state[p]["exp_avg"].data_ptr(), self.opt.state[p]["exp_avg_sq"].data_ptr()) for p in plist),
                 float(g["lr"]), tuple(g["betas"]), float(g["eps"]), tuple(self.my_views), self._depth_grad(),
                 self.w_sil, self.w_depth, self.reg_opacity, self.reg_scale, F32_GRADE, FIT_TILE, NUM_STREAMS,
-                tuple(t.data_ptr() for t in self.targets))
+                tuple(t.data_ptr() for t in self.targets), tuple(m.data_ptr() for m in (self.masks or ())),
+                tuple(d.data_ptr() for d in (self.depths or ())))
 
     def _probe_counts(self, device) -> list:
         """Every view of this rank prepared once with host-read plans: [(pairs, slots, core pairs)] per view."""
@@ -1423,6 +1427,18 @@ class ViewShardedFitter:
         self._native_keep = (m, s, c, o)
         return losses_v[:len(views)].sum() if views else torch.zeros((), device=device)
 
+    def _graph_leave(self) -> None:
+        """The step goes eager while replayed steps may still be in flight (the graph's conditions changed, e.g.
+        F32_GRADE toggled): settle them first (an overflowed one is redone and its loss rewritten, and the host's Adam
+        step count corrected), then drop the graph, so that a later capture counts only its own replays."""
+        gs = getattr(self, "_gs", None)
+        if gs is None or gs.graph is None:
+            return
+        self.graph_sync()
+        gs.graph = None
+        gs.key = None
+        gs.inflight = []
+
     def graph_sync(self) -> None:
         """Wait for the replayed steps and redo any that overflowed (densify, the parameters' readers and the end of a
         fit call this; a no-op without a graph)."""
@@ -1579,11 +1595,17 @@ def main(argv=None) -> None:
                                silhouette_weight=args.silhouette_weight, depth_weight=args.depth_weight,
                                reg_opacity=args.reg_opacity, reg_scale=args.reg_scale)
     loss_log = []
+    pending = []  # the step tensors not yet read: a replayed step found to have overflowed is redone and its loss
+    #               rewritten in place one step later (graph_sync), so the host reads them after that
     for it in range(args.iters):
-        lv = float(fitter.step())
-        loss_log.append(lv)
+        pending.append(fitter.step())
         if rank == 0 and (it == 0 or (it + 1) % 25 == 0):
-            print(f"iter {it+1:4d}  loss={lv:.6f}  N={fitter.params['means'].shape[0]}")
+            fitter.graph_sync()
+            print(f"iter {it+1:4d}  loss={float(pending[-1]):.6f}  N={fitter.params['means'].shape[0]}")
+        if (it + 1) % args.prune_interval == 0 or (it + 1) % args.densify_interval == 0 or it + 1 == args.iters:
+            fitter.graph_sync()
+            loss_log.extend(float(t) for t in pending)
+            pending = []
         if (it + 1) % args.prune_interval == 0 or (it + 1) % args.densify_interval == 0:
             fitter.densify_and_prune(args.max_gaussians,
                                      args.densify_ratio if (it + 1) % args.densify_interval == 0 else 0.0,

@@ -6,7 +6,10 @@ src/renderer_dispatch.cpp and src/renderer.cu).
 background=None) -> np.ndarray (H,W,4) uint8`` with the binding's validation and messages
 (RuntimeError).  Semantics are renderer_cpu.cpp's: 3-sigma box, w < 1e-5 skip, no clamps, uint8
 round-half-up, alpha 255.  ``enable_depth_sort=1`` (an extension argument; RenderParams field at
-gaussian_types.h:37) gives exact per-pixel front-to-back compositing in camera-z order.
+gaussian_types.h:37) gives exact per-pixel front-to-back compositing in camera-z order.  ``force_cpu=1`` (an
+extension argument, RenderParams.force_cpu: renderer_dispatch.cpp:12-13) asks for the CPU renderer's contract, which
+this HIP path already follows except at n == 0: the background with alpha 255 (renderer_cpu.cpp:219-240) instead of
+the CUDA renderer's all-zero image (renderer.cu:279-281).
 """
 from __future__ import annotations
 
@@ -34,7 +37,7 @@ _MISSING = object()
 
 
 def render_gaussians(means, scales, colors, opacities, width=800, height=600, view=_MISSING, proj=_MISSING,
-                     background=None, enable_depth_sort=0):
+                     background=None, enable_depth_sort=0, force_cpu=0):
     if view is _MISSING or proj is _MISSING:
         raise TypeError("render_gaussians() missing required arguments: 'view' and 'proj'")
     _require_contiguous_f32(means, "means")
@@ -74,7 +77,7 @@ def render_gaussians(means, scales, colors, opacities, width=800, height=600, vi
     p.background[:] = bg.reshape(3).tolist()
     p.enable_depth_sort = int(enable_depth_sort)
     p.depth_slices = 16
-    p.force_cpu = 0
+    p.force_cpu = int(force_cpu)
     out = np.empty((int(height), int(width), 4), np.uint8)
     L = _native.lib()
     st = L.gr_render_u8(ctypes.byref(p), n, means.ctypes.data_as(ctypes.c_void_p), scales.ctypes.data_as(ctypes.c_void_p),

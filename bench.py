@@ -339,9 +339,10 @@ def dropin_op(n: int, V: int, R: int, steps: int, warmup: int, device, depth_los
 
 
 def psnr_vs_ref(fitter, cams, R: int, device, npix: int = 2048) -> dict:
-    """Checker leg: view 0 of the current fitted state, rendered by the bench's path (fit footprint, no depth
-    channel, two-piece f16/bf16 splits) and by the drop-in default path, against the exact float64 dense
-    render (oracle/gr_oracle.c: every Gaussian at every pixel, no cutoff) at ``npix`` random pixels."""
+    """Checker leg: view 0 of the current fitted state, rendered by the bench's own forward (gr_fwd_render_l1 on the
+    fitter's gr_view of view 0: the kernel the timed step runs, k_fwd32_l1 at the fit's 32-pixel tiles, with its L1
+    epilogue against view 0's target, images written beside) and by the drop-in default path, against the exact
+    float64 dense render (oracle/gr_oracle.c: every Gaussian at every pixel, no cutoff) at ``npix`` random pixels."""
     from oracle import oracle as orc
 
     with torch.no_grad():
@@ -354,14 +355,24 @@ def psnr_vs_ref(fitter, cams, R: int, device, npix: int = 2048) -> dict:
     d_out, d_a, _ = orc.dense_pixels(v, sc, pix)
     t_dense = time.perf_counter() - t0
     res = {}
-    for name, kw in (("bench_path", dict(cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF, depth_grad=False)),
-                     ("dropin_default", {})):
-        gv = tr.make_view(view, proj, R, R, None, **kw)
-        out, alpha, _, _ = tr.forward_native(*acts, gv, want_depth=False)
+    for name in ("bench_path", "dropin_default"):
+        if name == "bench_path":
+            gv = fitter._fit_view(0, device)
+            out = torch.empty((R, R, 3), device=device)
+            alpha = torch.empty((R, R), device=device)
+            mask = fitter.masks[0] if fitter.masks is not None else None
+            tr.forward_l1_native(*acts, gv, tr.prepare_native(*acts, gv), fitter.targets[0], mask,
+                                 fitter.w_sil if mask is not None else 0.0, 1.0 / len(cams),
+                                 torch.zeros(1, device=device), out=out, alpha=alpha)
+            kernel = f"gr_fwd_render_l1 ({'k_fwd32_l1' if gv.tile == 32 else 'k_raster_fwd_mfma'}, tile {gv.tile or 16})"
+        else:
+            gv = tr.make_view(view, proj, R, R, None)
+            out, alpha, _, _ = tr.forward_native(*acts, gv, want_depth=False)
+            kernel = "gr_fwd_render (drop-in default footprint, 16-pixel tiles)"
         o = out.cpu().numpy().reshape(-1, 3)[pix]
         a = alpha.cpu().numpy().reshape(-1)[pix]
         res[name] = {"psnr_db": round(orc.psnr(o, d_out), 2), "rel_l2_rgb": float(f"{orc.rel_l2(o, d_out):.3e}"),
-                     "rel_l2_alpha": float(f"{orc.rel_l2(a, d_a):.3e}")}
+                     "rel_l2_alpha": float(f"{orc.rel_l2(a, d_a):.3e}"), "kernel": kernel}
     res.update(value=res["bench_path"]["psnr_db"], unit="dB", target=">= 60 dB (north_star)",
                sample=f"view 0 of the final fitted state, {npix} random pixels, exact float64 dense reference "
                       f"({t_dense:.1f} s on the host)")
@@ -385,9 +396,8 @@ def splat_replay(fitter, device) -> dict:
     V = max(len(fitter.targets), 1)
     w_sil = fitter.w_sil if fitter.masks is not None else 0.0
     preps = []
-    for i in fitter.my_views:
-        if i >= V:  # (a band of a view, multi-GPU: the roofline times whole views)
-            continue
+    whole = [i for i in fitter.my_views if i < V]  # (a band of a view, multi-GPU: the roofline times whole views)
+    for i in whole or [0]:  # (a rank with bands only, V < R: one whole view stands in)
         gv = fitter._fit_view(i, device)
         preps.append((i, gv, tr.prepare_native(*acts, gv)))
     torch.cuda.synchronize()

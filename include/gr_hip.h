@@ -61,7 +61,9 @@ typedef struct gr_render_params {
   float background[3];
   int enable_depth_sort; /* 0: OIT weighted average, 1: exact depth-sorted "over" compositing */
   int depth_slices;      /* accepted for ABI compatibility; the HIP path sorts exactly       */
-  int force_cpu;         /* accepted for ABI compatibility; the HIP path is the only path    */
+  int force_cpu;         /* 1: the CPU renderer's contract (renderer_dispatch.cpp:12-13); the HIP */
+                         /* path already has its semantics, except n <= 0: background, A = 255  */
+                         /* (renderer_cpu.cpp:219-240) instead of renderer.cu's all-zero RGBA   */
 } gr_render_params;
 
 /* One camera view for the differentiable path (torch_renderer.py:109-121 arguments). */

@@ -119,3 +119,20 @@ def test_integration_ctypes_example_runs(pkg):
     got = ns["plan"]
     assert (got.num_pairs, got.num_core_pairs) == (int(ref.num_pairs), int(ref.num_core_pairs))
     assert got.num_pairs > 0 and np.isfinite(got.num_pairs)
+
+
+def test_u8_force_cpu_empty_scene_is_the_cpu_background(pkg):
+    """gr_render_u8 with n == 0 runs on the host only (no device call): the CUDA renderer's contract gives an all-zero
+    image (renderer.cu:279-281); RenderParams.force_cpu = 1 the CPU renderer's (renderer_cpu.cpp:219-240: the finalized
+    background, alpha 255), bit-exact against its compiled-reference goldens, both modes."""
+    import numpy as np
+
+    from conftest import golden
+
+    gr = pkg.gaussian_renderer
+    for name in ("u8_n0_17x13_sort0", "u8_n0_17x13_sort1"):
+        d = golden(name)
+        args = (d["means"], d["scales"], d["colors"], d["opacities"], int(d["width"]), int(d["height"]),
+                np.ascontiguousarray(d["view"]), np.ascontiguousarray(d["proj"]), np.ascontiguousarray(d["background"]))
+        assert not gr.render_gaussians(*args, enable_depth_sort=int(d["sort"])).any()
+        np.testing.assert_array_equal(gr.render_gaussians(*args, enable_depth_sort=int(d["sort"]), force_cpu=1), d["rgba"])

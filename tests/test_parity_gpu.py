@@ -260,8 +260,13 @@ def test_legacy_u8_matches_reference_cpu(pkg, cuda, name):
                               np.ascontiguousarray(d["view"]), np.ascontiguousarray(d["proj"]),
                               np.ascontiguousarray(d["background"]), enable_depth_sort=int(d["sort"]))
     if d["means"].shape[0] == 0:
-        # HIP path keeps renderer.cu's n<=0 contract (renderer.cu:279-281): all-zero RGBA
+        # HIP path keeps renderer.cu's n<=0 contract (renderer.cu:279-281): all-zero RGBA; with force_cpu=1 the CPU
+        # renderer's (the golden's: background, alpha 255), bit-exact
         assert not out.any()
+        cpu = gr.render_gaussians(d["means"], d["scales"], d["colors"], d["opacities"], int(d["width"]), int(d["height"]),
+                                  np.ascontiguousarray(d["view"]), np.ascontiguousarray(d["proj"]),
+                                  np.ascontiguousarray(d["background"]), enable_depth_sort=int(d["sort"]), force_cpu=1)
+        np.testing.assert_array_equal(cpu, d["rgba"])
         return
     diff = np.abs(out.astype(np.int32) - d["rgba"].astype(np.int32))
     assert diff.max() <= 1, f"{name}: max diff {diff.max()}"

@@ -11,6 +11,10 @@ two-piece splits) and in the default mode (depth_grad=True, upstream depth gradi
   relL2 <= 1e-4 over the sample.  This ties the tile footprint (7 sigma / 5.5 sigma core) to the dense
   math at the sizes the headline runs.
 
+The "fit32" mode and the tile-32 fitted-state case run the kernels the headline times (k_fwd32_l1, k_bwd32: the
+fused fit path at 32-pixel tiles) with the fit's L1 + silhouette loss; their upstream gradients are the L1 signs of
+the HIP images, handed to the oracle and the dense reference alike.
+
 Scenes: SURVEY.md §8(d)'s synthetic recipe (density-matched scale), Gaussians in the trainer's Morton
 order (bench.py's layout), orbit view 0.  Upstream gradients: seeded standard normal."""
 from __future__ import annotations
@@ -37,6 +41,31 @@ def _scene(n):
     return orc.Scene(sc.means[perm].copy(), sc.scales[perm].copy(), sc.colors[perm].copy(), sc.opacities[perm].copy())
 
 
+def _fused32(tr, t, view, proj, W, H, target, mask, w_sil, g_scale, cuda):
+    """The kernels the headline times, on one view: the fused fit path at the fit's tile size (fm.FIT_TILE = 32:
+    k_fwd32_l1 with its L1 epilogue -> k_bwd32 -> k_gather_view -> k_reduce_sums), images written beside.
+    Returns (loss, out, alpha, grads) as numpy and the L1 upstream (g_rgb, g_a) the references take: the HIP images'
+    own signs sign(out - t), sign(alpha - m) (torch's abs' with sign(0) = 0), scaled as the kernel scales them, so a
+    near-tie at the kink (which the last float bit decides) is the same pixel gradient on both sides."""
+    from test_tile32_gpu import _fused_view
+
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    t = [x.detach().contiguous() for x in t]
+    loss, out, alpha, grads, _ = _fused_view(tr, t, view, proj, W, H, fm.FIT_TILE, target, mask, w_sil, g_scale, cuda)
+    h_out, h_alpha = out.cpu().numpy(), alpha.cpu().numpy()
+    tn, mn = target.cpu().numpy(), mask.cpu().numpy()
+    HW = W * H
+    g_rgb = (np.sign(h_out.astype(np.float64) - tn) * (g_scale / (3 * HW))).astype(np.float32)
+    g_a = (np.sign(h_alpha.astype(np.float64) - mn) * (w_sil * g_scale / HW)).astype(np.float32)
+    return loss, h_out, h_alpha, [g.cpu().numpy() for g in grads], g_rgb, g_a
+
+
+def _l1_target(H, W, seed, cuda):
+    g = torch.Generator(device=cuda).manual_seed(seed)
+    target = torch.rand((H, W, 3), generator=g, device=cuda)
+    return target, (target.mean(dim=2) > 0.5).float().contiguous()
+
+
 def _fit_mode(tr, t, view, proj, W, H, g_rgb, g_a, cuda):
     """The fused fit path's render settings (fit_multiview._views_direct): one zone at FIT_CUTOFF, no
     depth channel, forward_native(want_depth=False) + gr_bwd (generic upstream gradients)."""
@@ -49,12 +78,16 @@ def _fit_mode(tr, t, view, proj, W, H, g_rgb, g_a, cuda):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("mode", ["no_depth_grad", "depth_grad", "fit"])
+@pytest.mark.parametrize("mode", ["no_depth_grad", "depth_grad", "fit", "fit32"])
 @pytest.mark.parametrize("cfg", ["C4", "C5"])
 def test_full_view_vs_oracle(pkg, cuda, cfg, mode):
     """mode: the bench's drop-in mode (depth_grad=False), the default mode (depth_grad=True, with an
-    upstream depth gradient), or the fused fit path's settings (one 5.5-sigma zone, no depth)."""
+    upstream depth gradient), the fit path's settings on the 16-pixel kernels (one FIT_CUTOFF zone, no depth,
+    generic upstream), or "fit32": the headline's own kernels (the fused path at 32-pixel tiles, k_fwd32_l1 /
+    k_bwd32, with the fit's L1 + silhouette loss on a random target; the references take the HIP images' signs)
+    against the float64 binned oracle at tile 32 and the dense sample."""
     tr = pkg.torch_renderer
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
     depth_grad = mode == "depth_grad"
     n, W, H, V = CONFIGS[cfg]
     sc = _scene(n)
@@ -65,7 +98,16 @@ def test_full_view_vs_oracle(pkg, cuda, cfg, mode):
     g_d = rng.standard_normal((H, W)).astype(np.float32) if depth_grad else None
 
     t = [torch.from_numpy(a).to(cuda).requires_grad_(True) for a in sc.arrays()]
-    if mode == "fit":
+    tile, h_loss = 0, None
+    if mode == "fit32":
+        tile = fm.FIT_TILE
+        target, mask = _l1_target(H, W, 5, cuda)
+        h_loss, h_out, h_a, h_grads, g_rgb, g_a = _fused32(tr, t, view, proj, W, H, target, mask, 0.2, 1.0 / V, cuda)
+        hip = {"out": h_out, "alpha": h_a}
+        hip.update(zip(GRADS, h_grads))
+        hip["d_scales"] = hip["d_scales"][:, :2]  # (the fused path's scale gradient has no z column, the reference's either)
+        depth = None
+    elif mode == "fit":
         out, alpha, grads = _fit_mode(tr, t, view, proj, W, H, g_rgb, g_a, cuda)
         depth = None
     else:
@@ -75,22 +117,31 @@ def test_full_view_vs_oracle(pkg, cuda, cfg, mode):
             loss = loss + (depth * torch.from_numpy(g_d).to(cuda)).sum()
         loss.backward()
         grads = [x.grad for x in t]
-    torch.cuda.synchronize()
-    hip = {"out": out.detach().cpu().numpy(), "alpha": alpha.detach().cpu().numpy()}
-    if depth is not None:
-        hip["depth"] = depth.detach().cpu().numpy()
-    for k, x in zip(GRADS, grads):
-        hip[k] = x.cpu().numpy()
+    if mode != "fit32":
+        torch.cuda.synchronize()
+        hip = {"out": out.detach().cpu().numpy(), "alpha": alpha.detach().cpu().numpy()}
+        if depth is not None:
+            hip["depth"] = depth.detach().cpu().numpy()
+        for k, x in zip(GRADS, grads):
+            hip[k] = x.cpu().numpy()
 
     t0 = time.perf_counter()
-    cut = tr.FIT_CUTOFF if mode == "fit" else tr.default_cutoff(depth_grad)
-    core = tr.FIT_CUTOFF if mode == "fit" else tr.DEFAULT_CORE_CUTOFF
-    v = orc.make_view(view, proj, W, H, None, cutoff=cut, core_cutoff=core)
+    fit = mode in ("fit", "fit32")
+    cut = tr.FIT_CUTOFF if fit else tr.default_cutoff(depth_grad)
+    core = tr.FIT_CUTOFF if fit else tr.DEFAULT_CORE_CUTOFF
+    v = orc.make_view(view, proj, W, H, None, cutoff=cut, core_cutoff=core, tile=tile)
     ora = dict(zip(("out", "alpha", "depth"), orc.forward(v, sc, binned=True)))
     if depth is None:
         del ora["depth"]
     ora.update(zip(GRADS, orc.backward(v, sc, g_rgb, g_a, g_d, binned=True)))
+    if mode == "fit32":
+        ora["d_scales"] = ora["d_scales"][:, :2]
+        tn, mn = target.cpu().numpy().astype(np.float64), mask.cpu().numpy().astype(np.float64)
+        # (the kernel's loss value is unscaled; g_scale scales its upstream gradients only)
+        o_loss = np.abs(ora["out"].astype(np.float64) - tn).mean() + 0.2 * np.abs(ora["alpha"].astype(np.float64) - mn).mean()
     errs = {k: orc.rel_l2(hip[k], ora[k]) for k in ora}
+    if h_loss is not None:
+        errs["loss"] = abs(h_loss - o_loss) / o_loss
     t1 = time.perf_counter()
 
     pix = rng.choice(W * H, 1000, replace=False).astype(np.int32)
@@ -102,7 +153,7 @@ def test_full_view_vs_oracle(pkg, cuda, cfg, mode):
     if depth is not None:
         dense["depth"] = orc.rel_l2(hip["depth"].reshape(-1)[pix], d_d)
     for k, gd in zip(GRADS, dense_g):
-        dense[k] = orc.rel_l2(hip[k][sel], gd)
+        dense[k] = orc.rel_l2(hip[k][sel], gd[:, :2] if (k == "d_scales" and mode == "fit32") else gd)
     print(f"{cfg} {mode}: vs binned oracle", {k: f"{e:.2e}" for k, e in errs.items()},
           f"({t1 - t0:.1f} s); vs dense sample", {k: f"{e:.2e}" for k, e in dense.items()},
           f"({time.perf_counter() - t1:.1f} s)")
@@ -111,16 +162,21 @@ def test_full_view_vs_oracle(pkg, cuda, cfg, mode):
             assert errs[k] <= 2e-5, (k, errs[k])
     for k in GRADS:
         assert errs[k] <= 1e-4, (k, errs[k])
+    if "loss" in errs:
+        assert errs["loss"] <= 1e-5, errs["loss"]
     assert orc.psnr(hip["out"], ora["out"]) >= 60.0
     for k, e in dense.items():
         assert e <= 1e-4, (k, e)
 
 
 @pytest.mark.timeout(400)
-def test_fit_path_on_fitted_state_vs_dense(pkg, cuda):
+@pytest.mark.parametrize("tile", [16, 32])
+def test_fit_path_on_fitted_state_vs_dense(pkg, cuda, tile):
     """The bench's own workload after several fit steps (Gaussians moved, scales and opacities changed by
-    Adam): the fused fit path's render settings (one FIT_CUTOFF zone, no depth) against the dense
-    float64 reference on a sample (1000 pixels, 1000 Gaussians), relL2 <= 1e-4."""
+    Adam): the fit footprint (one FIT_CUTOFF zone, no depth) against the dense float64 reference on a sample
+    (1000 pixels, 1000 Gaussians), relL2 <= 1e-4.  tile 16: the 16-pixel kernels with generic upstream gradients;
+    tile 32: the headline's own kernels (the fused path, k_fwd32_l1 / k_bwd32) with the fit's L1 + silhouette loss
+    on that view's target, the dense reference taking the HIP images' signs."""
     import importlib
 
     tr = pkg.torch_renderer
@@ -142,17 +198,23 @@ def test_fit_path_on_fitted_state_vs_dense(pkg, cuda):
     rng = np.random.default_rng(9)
     g_rgb = rng.standard_normal((H, W, 3)).astype(np.float32)
     g_a = rng.standard_normal((H, W)).astype(np.float32)
-    out, alpha, grads = _fit_mode(tr, acts, view, proj, W, H, g_rgb, g_a, cuda)
+    if tile == 32:
+        _, out, alpha, grads, g_rgb, g_a = _fused32(tr, acts, view, proj, W, H, fit.targets[3], fit.masks[3], fit.w_sil,
+                                                    1.0 / V, cuda)
+        grads[1] = grads[1][:, :2]
+    else:
+        out, alpha, grads = _fit_mode(tr, acts, view, proj, W, H, g_rgb, g_a, cuda)
+        out, alpha, grads = out.cpu().numpy(), alpha.cpu().numpy(), [x.cpu().numpy() for x in grads]
     v = orc.make_view(view, proj, W, H, None, cutoff=tr.FIT_CUTOFF, core_cutoff=tr.FIT_CUTOFF)
     pix = rng.choice(W * H, 1000, replace=False).astype(np.int32)
     d_out, d_a, _ = orc.dense_pixels(v, sc, pix)
     sel = np.sort(rng.choice(n, 1000, replace=False)).astype(np.int32)
     dense_g = orc.dense_grads_sel(v, sc, sel, g_rgb, g_a, None)
-    errs = {"out": orc.rel_l2(out.cpu().numpy().reshape(-1, 3)[pix], d_out),
-            "alpha": orc.rel_l2(alpha.cpu().numpy().reshape(-1)[pix], d_a)}
+    errs = {"out": orc.rel_l2(out.reshape(-1, 3)[pix], d_out),
+            "alpha": orc.rel_l2(alpha.reshape(-1)[pix], d_a)}
     for k, x, gd in zip(GRADS, grads, dense_g):
-        errs[k] = orc.rel_l2(x.cpu().numpy()[sel], gd)
-    print("fitted C4 state, fit path vs dense sample:", {k: f"{e:.2e}" for k, e in errs.items()})
+        errs[k] = orc.rel_l2(x[sel], gd[:, : x.shape[1]] if x.ndim == 2 else gd)
+    print(f"fitted C4 state, fit path at {tile}-pixel tiles vs dense sample:", {k: f"{e:.2e}" for k, e in errs.items()})
     for k, e in errs.items():
         assert e <= 1e-4, (k, e)
 
