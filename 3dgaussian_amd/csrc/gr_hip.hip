@@ -456,6 +456,7 @@ inline int64_t item_cap(int tiles, int64_t K, int ch = CH) { return (K + ch - 1)
 // Per tile size: the work-item length, the split-tile partial sums per item (forward channels x pixels) and the
 // backward's upstream fragments per tile.
 constexpr int UF32_FRAGS = 2 * 4 * 2 * 2 * 64;  // uint4 per 32-pixel tile: (side, channel, K-step, piece) x 64 lanes
+constexpr int UF32_STRIDE = UF32_FRAGS + 64;  // + one chunk: the tile's four f16 operand exponents (an int4 at its start)
 struct TileCfg {
   int T, ch;
   size_t part_floats, uf_frags;
@@ -483,7 +484,7 @@ inline int chunk_of(const gr_view* v, int base, int64_t K) {
 }
 // K: the plan's pair count (the work-item length follows it, chunk_of); -1 where only the tile geometry is needed
 inline TileCfg tile_cfg(const gr_view* v, int64_t K = -1) {
-  return tile_of(v) == T32 ? TileCfg{T32, chunk_of(v, CH32, K), (size_t)4 * TP32, (size_t)UF32_FRAGS}
+  return tile_of(v) == T32 ? TileCfg{T32, chunk_of(v, CH32, K), (size_t)4 * TP32, (size_t)UF32_STRIDE}
                            : TileCfg{T, chunk_of(v, CH, K), (size_t)5 * TP, (size_t)UF_FRAGS16};
 }
 
@@ -1769,9 +1770,10 @@ __device__ __forceinline__ void split3_frag2(const f32x2_t (&v)[4], s16x8 (&f)[3
 // exponent arguments) so the footprint's smallest weights stay normal in f16: B = ey by 2^GR_F16_SB
 // (ey <= 1, so B <= 2^12), A = o c ex by 2^GR_F16_SA (finite for opacities up to 4094; colours are
 // clamped to [0, 1]); the accumulators are rescaled by 2^-(SA+SB), exactly.
-// hi = f16(x) truncated (v_cvt_pkrtz), lo = x - hi exact in f32 (one v_fma_mix_f32 per value reads
-// hi's f16 half), truncated to f16: |x - hi - lo| <= 2^-20 |x|; the dropped lo*lo <= 2^-20 of the
-// product.  Four instructions per pair of values instead of five.  Same-box A/B at C4 (fit path):
+// hi = f16(x) rounded to nearest (v_cvt_pk_f16_f32), lo = x - hi exact in f32 (one v_fma_mix_f32 per value reads
+// hi's f16 half), rounded to nearest f16: |x - hi| <= 2^-11 |x| and |x - hi - lo| <= 2^-22 |x| while both pieces
+// are normal, so the three products miss a b by at most 3 * 2^-22 of it (round 6; truncated pieces, as before,
+// left 3 * 2^-20).  Four instructions per pair of values instead of five.  Same-box A/B at C4 (fit path):
 // forward 145/154 -> 140/135 us, step 1369-1380 -> 1403-1408 Mpx/s (A/B at SA = SB = 12); fit-path errors vs the float64 oracle
 // out 1e-7, gradients <= 1.2e-5 (profiles/r02p_ab_f16.txt).
 #ifndef GR_FWD_F16
@@ -1806,15 +1808,46 @@ __device__ __forceinline__ float f16_resid_hi(float x, unsigned h) {  // x - f16
   asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
   return r;
 }
+typedef _Float16 f16x2h_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pk_f16(float a, float b) {  // two f16, round to nearest even: v_cvt_pk_f16_f32
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{a, b}, f16x2h_t));
+}
+#ifndef GR_F16_RNE_FWD
+#define GR_F16_RNE_FWD 1
+#endif
+__device__ __forceinline__ unsigned pk_f16_fwd(float a, float b) {  // (A/B knob: the forward's pieces truncated)
+  if constexpr (GR_F16_RNE_FWD) return pk_f16(a, b);
+  return __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(a, b));
+}
 __device__ __forceinline__ void split2h_frag2(const f32x2_t (&v)[4], s16x8 (&f)[2]) {
   unsigned h[4], l[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    h[p] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(v[p].x, v[p].y));
-    l[p] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(f16_resid_lo(v[p].x, h[p]), f16_resid_hi(v[p].y, h[p])));
+    h[p] = pk_f16_fwd(v[p].x, v[p].y);
+    l[p] = pk_f16_fwd(f16_resid_lo(v[p].x, h[p]), f16_resid_hi(v[p].y, h[p]));
   }
   f[0] = as_frag(make_uint4(h[0], h[1], h[2], h[3]));
   f[1] = as_frag(make_uint4(l[0], l[1], l[2], l[3]));
+}
+// the same split (round to nearest) of 8 values held as a plain array
+__device__ __forceinline__ void split2h_frag(const float (&v)[8], s16x8 (&f)[2]) {
+  unsigned h[4], l[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    h[p] = pk_f16(v[2 * p], v[2 * p + 1]);
+    l[p] = pk_f16(f16_resid_lo(v[2 * p], h[p]), f16_resid_hi(v[2 * p + 1], h[p]));
+  }
+  f[0] = as_frag(make_uint4(h[0], h[1], h[2], h[3]));
+  f[1] = as_frag(make_uint4(l[0], l[1], l[2], l[3]));
+}
+// The 32-pixel backward's A operands (the per-pixel upstream vectors) in f16 pieces: per channel the values are scaled
+// by 2^e with e = 14 - exponent(bound of |u|), so the bound lies in [2^13, 2^14) and values down to 2^-17 of it keep
+// both pieces normal (exact power-of-two scaling, undone on the backward's sums)
+__device__ __forceinline__ int f16_exp_of(float m) {
+  if (!(m > 0.0f) || !(m <= 3.0e38f)) return 0;  // an all-zero channel, or inf / NaN (they propagate either way)
+  int e = 0;
+  (void)frexpf(m, &e);  // m < 2^e
+  return 14 - e;
 }
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ f32x4 mfma16h(const s16x8& a, const s16x8& b, f32x4 c) {
@@ -3183,20 +3216,29 @@ __device__ __forceinline__ void k_fwd32_l1_body(ViewK v, int n, const int4* __re
 #pragma unroll
       for (int c = 0; c < 4; ++c) sU[c * T32 * F32_LD + px0 * F32_LD + py0 + 8 * q] = u[q][c];
     __syncthreads();
+    // the f16 operand scales from the L1 upstream's bounds (pixel_upstream, den = 1 + W >= 1): |dC_c| <= g / (3 HW),
+    // |dW| <= 3 g / (3 HW) + w_sil g / HW; a pixel's value sits 1 / (1 + W) below its bound, so both f16 pieces stay
+    // normal while W < 2^16 (f16_exp_of)
+    const float HWf = (float)v.W * (float)v.H, gC = fabsf(l1.g_scale) / (3.0f * HWf);
+    const int eC = f16_exp_of(gC), eWb = f16_exp_of(3.0f * gC + fabsf(l1.w_sil * l1.g_scale) / HWf);
+    const int ex4[4] = {eC, eC, eC, eWb};
     // fragment set (side, channel, K-step s), lane l: side 0 (T, contraction over x) A[m = y][k] = U[x = 16 s + k][y],
-    // side 1 (R, over y) A[m = x][k] = U[x][y = 16 s + k], k = kslot_pixel(h, j); two round-to-nearest bf16 pieces
-    uint4* fr = UF + (size_t)tile * UF32_FRAGS;
+    // side 1 (R, over y) A[m = x][k] = U[x][y = 16 s + k], k = kslot_pixel(h, j); U * 2^e_c in two round-to-nearest
+    // f16 pieces (split2h_frag), the exponents e_c after the fragments
+    uint4* fr = UF + (size_t)tile * UF32_STRIDE;
+    if (tid == 0) fr[UF32_FRAGS] = make_uint4((unsigned)ex4[0], (unsigned)ex4[1], (unsigned)ex4[2], (unsigned)ex4[3]);
     for (int e = tid; e < 16 * 64; e += 256) {
       const int set = e >> 6, l = e & 63, side = set >> 3, c = (set >> 1) & 3, s = set & 1;
+      const int sc = c == 0 ? ex4[0] : (c == 1 ? ex4[1] : (c == 2 ? ex4[2] : ex4[3]));
       float val[8];
       const int m = l & 31, hh = l >> 5;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = 16 * s + kslot_pixel(hh, j);
-        val[j] = side == 0 ? sU[c * T32 * F32_LD + k * F32_LD + m] : sU[c * T32 * F32_LD + m * F32_LD + k];
+        val[j] = ldexpf(side == 0 ? sU[c * T32 * F32_LD + k * F32_LD + m] : sU[c * T32 * F32_LD + m * F32_LD + k], sc);
       }
       s16x8 f2[2];
-      split2_frag(val, f2);
+      split2h_frag(val, f2);
       __builtin_memcpy(&fr[(set * 2 + 0) * 64 + l], &f2[0], 16);
       __builtin_memcpy(&fr[(set * 2 + 1) * 64 + l], &f2[1], 16);
     }
@@ -3243,13 +3285,15 @@ __global__ __launch_bounds__(256, GR_FWD32_WAVES) void k_fwd32_l1_views(VBatch<k
 }
 
 
-// Backward of one work item of a 32-pixel tile (no upstream depth gradient, two-piece bf16 operands as
-// k_raster_bwd_bf16<false, 2>): per group of 32 Gaussians (lane r = l & 31 owns Gaussian r, half h = l >> 5 its
-// slots kslot_pixel(h, .) of each 16-pixel K-step s) the contractions
+// Backward of one work item of a 32-pixel tile (no upstream depth gradient): per group of 32 Gaussians (lane
+// r = l & 31 owns Gaussian r, half h = l >> 5 its slots kslot_pixel(h, .) of each 16-pixel K-step s) the contractions
 //   T_c[y][g] = sum_x U_c[x][y] ex_g(x)   and   R_c[x][g] = sum_y U_c[x][y] ey_g(y),   c = dC_r, dC_g, dC_b, dW,
-// each 2 K-steps x 3 piece products on v_mfma_f32_32x32x16_bf16, then the per-Gaussian epilogue over the lane's 16
-// rows (the same sums as the 16-pixel kernel, moments about the first slot of each K-step) and the 8-float row
-// [o S0, o S2, S4, S6 | o S1, S8, S5, S7] at the pair's sorted position (the gather is unchanged).
+// each 2 K-steps x 3 piece products on v_mfma_f32_32x32x16_f16 (round 6: two round-to-nearest f16 pieces, U scaled
+// by 2^e_c per channel and ex / ey by 2^SB into f16's normal range, <= 3 * 2^-22 per product; the bf16 pieces before
+// left ~2^-16), then the per-Gaussian epilogue over the lane's 16 rows (the same sums as the 16-pixel kernel, moments
+// about the first slot of each K-step) and the 8-float row [o S0, o S2, S4, S6 | o S1, S8, S5, S7] at the pair's
+// sorted position (the gather is unchanged).  Same-box A/B at C4 vs the bf16 phased form: backward 219-223 ->
+// 212-216 us, step +1.5-2% (profiles/r06_ab_bwd32_f16.txt).
 __device__ __forceinline__ void k_bwd32_body(ViewK v, int n, const int4* __restrict__ items,
                                                               const int* __restrict__ num_items, const int* __restrict__ pairs,
                                                               const float4* __restrict__ rec, const uint4* __restrict__ UF,
@@ -3268,9 +3312,12 @@ __device__ __forceinline__ void k_bwd32_body(ViewK v, int n, const int4* __restr
   const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   {  // the tile's 32 fragment chunks -> LDS (DMA)
-    const uint4* src = UF + (size_t)tile * UF32_FRAGS;
+    const uint4* src = UF + (size_t)tile * UF32_STRIDE;
     for (int cc = wave; cc < 32; cc += 4) glds16(src + 64 * cc + lane, sUF + 64 * cc);
   }
+  // the fragments' per-channel exponents (f16_exp_of): the contractions carry U 2^e_c and the B operands 2^SB
+  const uint4 e4 = UF[(size_t)tile * UF32_STRIDE + UF32_FRAGS];
+  const int eC0 = (int)e4.x, eC1 = (int)e4.y, eC2 = (int)e4.z, eW = (int)e4.w;
   // pixel centres of the lane's first slot per K-step: base + kslot offsets (compile-time)
   const float pxb[2] = {(float)(tx * T32 + 4 * h) + 0.5f, (float)(tx * T32 + 16 + 4 * h) + 0.5f};
   const float pyb[2] = {(float)(ty * T32 + 4 * h) + 0.5f, (float)(ty * T32 + 16 + 4 * h) + 0.5f};
@@ -3308,7 +3355,8 @@ __device__ __forceinline__ void k_bwd32_body(ViewK v, int n, const int4* __restr
         d0x[s] = pxb[s] - a.x;
         d0y[s] = pyb[s] - a.y;
         const float tX = a.z * d0x[s], tY = a.w * d0y[s];
-        const float cX = tX * d0x[s], cY = tY * d0y[s];
+        // ex, ey by 2^SB (the f16 B operands' range, as k_fwd32_l1's ey); the epilogue's weights carry it too
+        const float cX = fmaf(tX, d0x[s], (float)GR_F16_SB), cY = fmaf(tY, d0y[s], (float)GR_F16_SB);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const float oq = (float)kslot_off(q);
@@ -3325,70 +3373,92 @@ __device__ __forceinline__ void k_bwd32_body(ViewK v, int n, const int4* __restr
         const uint4* A0 = sUF + ((side * 4 + c) * 2 + 0) * 2 * 64;  // (side, c, s = 0, piece 0)
         f32x16 d = {};
 #pragma unroll
-        for (int s = 0; s < 2; ++s) d = mfma32b(as_frag(A0[(s * 2 + 1) * 64 + lane]), B[s][0], d);
+        for (int s = 0; s < 2; ++s) d = mfma32h(as_frag(A0[(s * 2 + 1) * 64 + lane]), B[s][0], d);
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const s16x8 a0 = as_frag(A0[(s * 2) * 64 + lane]);
-          d = mfma32b(a0, B[s][1], d);
-          d = mfma32b(a0, B[s][0], d);
+          d = mfma32h(a0, B[s][1], d);
+          d = mfma32h(a0, B[s][0], d);
         }
         return d;
       };
-      // Each side in two passes of two channels, (dC_r, dW) then (dC_g, dC_b): the first pass leaves
-      // p = b_r T_r + T_W per row (the same float operations as fmaf(b_b, T_b, fmaf(b_g, T_g, fmaf(b_r, T_r, T_W)))),
-      // so 32 accumulators and 16 partials are live instead of 64 accumulators.
-      {  // T: contraction over x (B = ex), rows y
-        s16x8 BT[2][2];
-        split2_frag(ex[0], BT[0]);
-        split2_frag(ex[1], BT[1]);
-        float p[16];
-        {
-          const f32x16 D0 = contract(0, 0, BT), D3 = contract(0, 3, BT);
+      // the channel combination p = T_W + b_r T_r + b_g T_g + b_b T_b on the scaled sums: b_c by 2^(e_W - e_c)
+      const float4 bs = make_float4(b.x, ldexpf(b.y, eW - eC0), ldexpf(b.z, eW - eC1), ldexpf(b.w, eW - eC2));
+      // Software-pipelined within the group, one channel per pass: each pass's 6 MFMAs share a scheduling region with
+      // the previous pass's epilogue (which reads only finished accumulators), so the wave's own VALU work issues
+      // between its MFMAs.  The channel combination p = fmaf(b_b, T_b, fmaf(b_g, T_g, fmaf(b_r, T_r, T_W))) is built
+      // one channel at a time in that same order (the phased form's float operations, bit-identical), so only the
+      // running p and two channels' accumulators are live.  Regions: [T_W] [T_r] [T_g | T_r epi] [T_b | T_g epi]
+      // [ey split, R_W | T_b epi + moments] [R_r] [R_g | R_r epi] [R_b | R_g epi] [R_b epi + moments].
+      s16x8 BT[2][2], BR[2][2];
+      split2h_frag(ex[0], BT[0]);
+      split2h_frag(ex[1], BT[1]);
+      float p[16];
+      {
+        const f32x16 D3 = contract(0, 3, BT);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) p[i] = D3[i];
+      }
+      f32x16 Dc = contract(0, 0, BT);
+      GR_BWD32_PHASE();
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {  // channel c's epilogue beside channel c + 1's MFMAs
+        const float bc = c == 0 ? bs.y : (c == 1 ? bs.z : bs.w);
+        f32x16 Dn;
+        if (c < 2) {
+          Dn = contract(0, c + 1, BT);
+        } else {
+          split2h_frag(ey[0], BR[0]);
+          split2h_frag(ey[1], BR[1]);
+          Dn = contract(1, 3, BR);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          S[c] = fmaf(ey[i >> 3][i & 7], Dc[i], S[c]);
+          p[i] = fmaf(bc, Dc[i], p[i]);
+        }
+        if (c == 2) {
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            S[0] = fmaf(ey[i >> 3][i & 7], D0[i], S[0]);
-            p[i] = fmaf(b.y, D0[i], D3[i]);
+            const int s = i >> 3, q = i & 7;
+            const float oq = (float)kslot_off(q);
+            const float t = ey[s][q] * p[i];
+            S4s[s] += t;
+            if (q != 0) {
+              S6c[s] = fmaf(t, oq, S6c[s]);
+              S8c[s] = fmaf(t, oq * oq, S8c[s]);
+            }
           }
         }
-        GR_BWD32_PHASE();  // keeps the second pass's MFMAs (and their accumulators) after the first pass's epilogue
-        const f32x16 D1 = contract(0, 1, BT), D2 = contract(0, 2, BT);
+        Dc = Dn;
+        GR_BWD32_PHASE();
+      }
+      // R side: Dc = R_W
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int s = i >> 3, q = i & 7;
-          const float e = ey[s][q], oq = (float)kslot_off(q);
-          S[1] = fmaf(e, D1[i], S[1]);
-          S[2] = fmaf(e, D2[i], S[2]);
-          const float t = e * fmaf(b.w, D2[i], fmaf(b.z, D1[i], p[i]));
-          S4s[s] += t;
-          if (q != 0) {  // slot 0 of each K-step is the origin of its moments
-            S6c[s] = fmaf(t, oq, S6c[s]);
-            S8c[s] = fmaf(t, oq * oq, S8c[s]);
-          }
+      for (int i = 0; i < 16; ++i) p[i] = Dc[i];
+      Dc = contract(1, 0, BR);
+      GR_BWD32_PHASE();
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float bc = c == 0 ? bs.y : (c == 1 ? bs.z : bs.w);
+        f32x16 Dn;
+        if (c < 2) Dn = contract(1, c + 1, BR);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) p[i] = fmaf(bc, Dc[i], p[i]);
+        if (c < 2) {
+          Dc = Dn;
+          GR_BWD32_PHASE();
         }
       }
-      GR_BWD32_PHASE();
-      {  // R: contraction over y (B = ey), rows x
-        s16x8 BR[2][2];
-        split2_frag(ey[0], BR[0]);
-        split2_frag(ey[1], BR[1]);
-        float p[16];
-        {
-          const f32x16 D0 = contract(1, 0, BR), D3 = contract(1, 3, BR);
 #pragma unroll
-          for (int i = 0; i < 16; ++i) p[i] = fmaf(b.y, D0[i], D3[i]);
-        }
-        GR_BWD32_PHASE();
-        const f32x16 D1 = contract(1, 1, BR), D2 = contract(1, 2, BR);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int s = i >> 3, q = i & 7;
-          const float oq = (float)kslot_off(q);
-          const float u = ex[s][q] * fmaf(b.w, D2[i], fmaf(b.z, D1[i], p[i]));
-          U0[s] += u;
-          if (q != 0) {
-            S5c[s] = fmaf(u, oq, S5c[s]);
-            S7c[s] = fmaf(u, oq * oq, S7c[s]);
-          }
+      for (int i = 0; i < 16; ++i) {
+        const int s = i >> 3, q = i & 7;
+        const float oq = (float)kslot_off(q);
+        const float u = ex[s][q] * p[i];
+        U0[s] += u;
+        if (q != 0) {
+          S5c[s] = fmaf(u, oq, S5c[s]);
+          S7c[s] = fmaf(u, oq * oq, S7c[s]);
         }
       }
       S[4] = S4s[0] + S4s[1];
@@ -3399,6 +3469,12 @@ __device__ __forceinline__ void k_bwd32_body(ViewK v, int n, const int4* __restr
         S[5] += fmaf(d0x[s], U0[s], S5c[s]);
         S[7] += fmaf(d0x[s] * d0x[s], U0[s], fmaf(2.0f * d0x[s], S5c[s], S7c[s]));
       }
+      // undo the scales (exact): the colour sums carry 2^(e_c + 2 SB), the rest 2^(e_W + 2 SB)
+      S[0] = ldexpf(S[0], -(eC0 + 2 * GR_F16_SB));
+      S[1] = ldexpf(S[1], -(eC1 + 2 * GR_F16_SB));
+      S[2] = ldexpf(S[2], -(eC2 + 2 * GR_F16_SB));
+#pragma unroll
+      for (int k = 4; k < 9; ++k) S[k] = ldexpf(S[k], -(eW + 2 * GR_F16_SB));
       // lanes r and r + 32 hold the two halves of Gaussian r's slots (pair32); row as k_raster_bwd_bf16<false, .>
       const float Pa = pair32(S[0], S[1]), Pb = pair32(S[2], S[8]), Pc = pair32(S[4], S[5]);
       const float Pd = pair32(S[6], S[7]);

@@ -440,8 +440,7 @@ class ViewShardedFitter:
         V, W = len(self.targets), self.world
         q = V // W
         whole = list(range(self.rank, q * W, W))
-        tile = (16 if F32_GRADE else FIT_TILE) or 16
-        ty = -(-self.height // tile)
+        ty = -(-self.height // self.views_tile())
         lo, hi = ty * self.rank // W, ty * (self.rank + 1) // W
         if hi <= lo:  # fewer tile rows than ranks: this rank has no band
             return whole
@@ -450,6 +449,11 @@ class ViewShardedFitter:
             self._bands[V + i] = (i, lo, hi - lo)
             bands.append(V + i)
         return whole + bands
+
+    def views_tile(self) -> int:
+        """The tile size the fused path renders this fit's views at: FIT_TILE, or 16 in the f32-grade mode (its
+        three-piece splits have 16-pixel kernels only)."""
+        return (16 if F32_GRADE else FIT_TILE) or 16
 
     def _bands_ok(self) -> bool:
         V, W = len(self.targets), self.world

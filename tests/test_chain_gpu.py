@@ -208,46 +208,83 @@ def test_dropin_loop_speculation_is_exact(cuda):
 
 
 def test_f32_grade_fit_mode(cuda):
+    """The fused path at f32 grade (F32_GRADE: no_depth_grad = 2, the three-piece splits, on its 16-pixel kernels) and in
+    the headline's two-piece mode (k_fwd32_l1 / k_bwd32 at 32-pixel tiles): each against the float64 binned oracle at
+    its own tile size (<= 1e-5) and the two against each other (<= 1e-4: splits plus the 16- vs 32-pixel footprints).
+
+    The L1 loss's upstream is sign(out - t): a pixel whose image lies within a few float ulps of its target takes
+    whichever sign its own run's last bit gives, and one flipped pixel moves the colour gradients of the Gaussians under
+    it by ~1/30 (round 5's 1.9e-4 on d_colors between the two modes at one tile size came from such pixels, each run
+    taking its own signs).  So the targets are moved off the kink first: where the float64 oracle's image is within
+    1e-4 of the target, the target is pushed 2e-4 away from it (on the side it was), which leaves every upstream sign
+    identical in both HIP runs and the oracle (their images agree to ~1e-6), and every gradient comparable term by
+    term.  The number of pixels within 1e-6 of their target before the move (the candidates for a flip) is printed."""
     fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    tr = importlib.import_module("3dgaussian_amd.torch_renderer")
     bench = importlib.import_module("bench")
     Wt = Ht = 256
-    cams = fm.orbit_cameras(6, Wt, Ht, cuda)
+    V = 6
+    cams = fm.orbit_cameras(V, Wt, Ht, cuda)
     g = torch.Generator(device=cuda).manual_seed(8)
     targets = [torch.rand((Ht, Wt, 3), generator=g, device=cuda) for _ in cams]
     masks = [(t.mean(dim=2) > 0.5).float() for t in targets]
+    with torch.no_grad():
+        acts = [a.detach().float().contiguous() for a in fm.activations(bench.synthetic_params(40_000, cuda))]
+    sc = orc.Scene(*(a.cpu().numpy() for a in acts))
+    ocams = orc.orbit_cameras(V, Wt, Ht)
+    near_ties, moved = 0, 0
+    for i, (view, proj) in enumerate(ocams):
+        o_out, _, _ = orc.forward(orc.make_view(view, proj, Wt, Ht, None, cutoff=fit_cutoff(), core_cutoff=fit_cutoff(),
+                                                tile=fm.FIT_TILE), sc, binned=True)
+        t = targets[i].cpu().numpy().astype(np.float64)
+        d = o_out.astype(np.float64) - t
+        near_ties += int((np.abs(d) < 1e-6).sum())
+        close = np.abs(d) < 1e-4
+        moved += int(close.sum())
+        t = np.where(close, t - np.where(d >= 0, 2e-4, -2e-4), t)
+        targets[i] = torch.from_numpy(t.astype(np.float32)).to(cuda)
     out = {}
-    # both modes at 16-pixel tiles (the f32-grade mode's): the two-piece splits are what differs, not the per-tile
-    # culling (the 32-pixel fit path is pinned against the oracle at its own tile size in test_tile32_gpu.py)
     for f32 in (False, True):
-        saved = fm.F32_GRADE, fm.FIT_TILE
-        fm.F32_GRADE, fm.FIT_TILE = f32, 16
+        saved = fm.F32_GRADE
+        fm.F32_GRADE = f32
         try:
             f = fm.ViewShardedFitter(bench.synthetic_params(40_000, cuda), cams, targets, Wt, Ht, masks=masks)
+            assert f.views_tile() == (16 if f32 else fm.FIT_TILE)
             with torch.no_grad():
-                acts = [a.detach().float().contiguous() for a in fm.activations(f.params)]
                 total = float(f._views_direct(*acts)[0])
                 parts = f._acc_parts
                 acc = [sum(p[q] for p in parts[1:]) + parts[0][q] if len(parts) > 1 else parts[0][q] for q in range(4)]
-            out[f32] = (total, [a.cpu().numpy() for a in acc], acts)
+            out[f32] = (total, [a.cpu().numpy() for a in acc])
         finally:
-            fm.F32_GRADE, fm.FIT_TILE = saved
-    sc = orc.Scene(*(a.cpu().numpy() for a in out[True][2]))
-    ora = None
-    for i, (view, proj) in enumerate(orc.orbit_cameras(6, Wt, Ht)):
-        v = orc.make_view(view, proj, Wt, Ht, None, cutoff=fit_cutoff(), core_cutoff=fit_cutoff())
-        o_out, o_a, _ = orc.forward(v, sc, binned=True)
-        t, m = targets[i].cpu().numpy(), masks[i].cpu().numpy()
-        g_rgb = (np.sign(o_out.astype(np.float64) - t) / (6 * 3 * Ht * Wt)).astype(np.float32)
-        g_a = (np.sign(o_a.astype(np.float64) - m) * 0.2 / (6 * Ht * Wt)).astype(np.float32)
-        gk = orc.backward(v, sc, g_rgb, g_a, None, binned=True)
-        ora = [x.astype(np.float64) for x in gk] if ora is None else [a + x for a, x in zip(ora, gk)]
-    e2 = {k: orc.rel_l2(a, b) for k, a, b in zip(("m", "s", "c", "o"), out[False][1], out[True][1])}
-    eo = {k: orc.rel_l2(a, b) for k, a, b in zip(("m", "s", "c", "o"), out[True][1], ora)}
-    print("f32-grade vs two-piece:", {k: f"{e:.1e}" for k, e in e2.items()}, "f32-grade vs oracle:",
-          {k: f"{e:.1e}" for k, e in eo.items()})
+            fm.F32_GRADE = saved
+    res = {}
+    for f32, tile in ((True, 16), (False, fm.FIT_TILE)):
+        ora, o_loss = None, 0.0
+        for i, (view, proj) in enumerate(ocams):
+            v = orc.make_view(view, proj, Wt, Ht, None, cutoff=fit_cutoff(), core_cutoff=fit_cutoff(), tile=tile)
+            o_out, o_a, _ = orc.forward(v, sc, binned=True)
+            t, m = targets[i].cpu().numpy(), masks[i].cpu().numpy()
+            o_loss += np.abs(o_out.astype(np.float64) - t).mean() + 0.2 * np.abs(o_a.astype(np.float64) - m).mean()
+            g_rgb = (np.sign(o_out.astype(np.float64) - t) / (V * 3 * Ht * Wt)).astype(np.float32)
+            g_a = (np.sign(o_a.astype(np.float64) - m) * 0.2 / (V * Ht * Wt)).astype(np.float32)
+            gk = orc.backward(v, sc, g_rgb, g_a, None, binned=True)
+            ora = [x.astype(np.float64) for x in gk] if ora is None else [a + x for a, x in zip(ora, gk)]
+        e = {k: orc.rel_l2(h[:, :2] if k == "s" else h, o[:, :2] if k == "s" else o)
+             for k, h, o in zip(("m", "s", "c", "o"), out[f32][1], ora)}
+        e["loss"] = abs(out[f32][0] - o_loss) / o_loss
+        res[f32] = e
+    e2 = {k: orc.rel_l2(a[:, :2] if k == "s" else a, b[:, :2] if k == "s" else b)
+          for k, a, b in zip(("m", "s", "c", "o"), out[False][1], out[True][1])}
+    print(f"{near_ties} pixels within 1e-6 of their target, {moved} targets moved off the kink;",
+          "f32-grade (16 px) vs oracle:", {k: f"{x:.1e}" for k, x in res[True].items()},
+          f"two-piece ({fm.FIT_TILE} px) vs oracle:", {k: f"{x:.1e}" for k, x in res[False].items()},
+          "f32-grade vs two-piece:", {k: f"{x:.1e}" for k, x in e2.items()})
     assert abs(out[True][0] - out[False][0]) <= 1e-5 * abs(out[True][0])
     for k in e2:
-        assert e2[k] <= 1e-4 and eo[k] <= 1e-5, (k, e2[k], eo[k])
+        assert e2[k] <= 1e-4, (k, e2[k])
+    for f32 in (True, False):
+        for k, x in res[f32].items():
+            assert x <= 1e-5, (f32, k, x)
 
 
 def test_gather_then_reduce_sums_matches_reduce_views(cuda):
