@@ -125,15 +125,19 @@ FIT_TILE = int(os.environ.get("GR_FIT_TILE", "32"))
 #               fill the GPU and the eager step's stream overlap wins (C4 1,557 eager vs 1,446 batched)
 GRAPH_MODE = os.environ.get("GR_GRAPH", "auto")
 GRAPH_AUTO_PIXELS = 512 * 512
-# multi-GPU: the views left over by the even split (V mod R) are cut into R bands of tile rows, one per rank
-# (gr_view.row0 / rows), so every rank renders V / R views' worth of pixels (50 views on 8 ranks: 6 views and two
-# eighths each instead of 7 on two ranks); the fused path without a depth term only (a depth term needs the whole
-# image's depth maximum).  0 = whole views round-robin.
+# multi-GPU: the r = V mod R views left over by the even split are cut into bands of tile rows (gr_view.row0 / rows),
+# the ranks split into r groups, one per leftover view, each group cutting its view into as many bands as it has ranks:
+# every rank renders V // R views and ONE band (50 views on 8 ranks: 6 views and a quarter view each instead of 7 on
+# two ranks; round 5 gave every rank a band of every leftover view, two eighths, each paying a band's fixed cost); the
+# fused path without a depth term only (a depth term needs the whole image's depth maximum).  0 = whole views round-robin.
 BAND_SPLIT = os.environ.get("GR_BAND_SPLIT", "1") != "0"
-# a band costs about this fraction of a whole view beyond its share of the pixels (its preparation, emission, gather
-# and chain rule run over every Gaussian): the split is used when the most loaded rank gains more than its bands cost
-# (C4 at 8 ranks: 3.25 -> 3.09 ms for rank 0; at 4 ranks, two half-view bands, 5.90 -> 5.96: not used)
-BAND_OVERHEAD = float(os.environ.get("GR_BAND_OVERHEAD", "0.3"))
+# a band costs about this fraction of a whole view beyond its share of the view's pairs (its preparation, binning
+# launches, gather and chain rule run over every Gaussian: ~90 of ~560 us single-stream at C4, tools/band_probe.py;
+# more in the overlapped step): the split is used when the most loaded rank's band (this plus its largest share of the
+# pairs) is below a whole view.  Measured per rank (profiles/r06_rank_share.txt): C4 at 8 ranks, quarter-view bands
+# (29% of the pairs): 3.25 -> 3.02-3.10 ms for every rank; at 4 ranks, half-view bands: 5.82 -> 6.13-6.19, so 0.5 keeps
+# whole views there
+BAND_OVERHEAD = float(os.environ.get("GR_BAND_OVERHEAD", "0.5"))
 GRAPH_MARGIN = float(os.environ.get("GR_GRAPH_MARGIN", "1.25"))  # capacity over the counts seen (+ 4096 pairs)
 
 
@@ -302,6 +306,35 @@ def _batch_sizes(ns: int, nviews: int, tail: Optional[int] = None) -> list:
     return sizes
 
 
+def _int_hist(idx: torch.Tensor, wts: torch.Tensor, nb: int) -> torch.Tensor:
+    """Sum of the int64 weights per bin 0..nb-1 (indices in range): sorted indices, prefix sums, bin ends."""
+    srt, order = torch.sort(idx)
+    cw = torch.cumsum(wts[order], 0)
+    ends = torch.searchsorted(srt, torch.arange(nb, device=idx.device, dtype=srt.dtype), right=True)
+    upto = torch.where(ends > 0, cw[(ends - 1).clamp_min(0)], torch.zeros_like(ends))
+    return torch.diff(upto, prepend=torch.zeros(1, dtype=upto.dtype, device=upto.device))
+
+
+def _min_max_cuts(w, g: int) -> list:
+    """Boundaries 0 = c_0 < c_1 < ... < c_g = len(w) of g non-empty contiguous runs of `w` whose largest sum is
+    the smallest possible (dynamic programming over the cut positions; ties to the earliest cut)."""
+    n = len(w)
+    c = np.concatenate([[0.0], np.cumsum(np.asarray(w, np.float64))])
+    best = np.full((g + 1, n + 1), np.inf)
+    arg = np.zeros((g + 1, n + 1), np.int64)
+    best[0, 0] = 0.0
+    for k in range(1, g + 1):
+        for j in range(k, n - (g - k) + 1):
+            for i in range(k - 1, j):
+                v = max(best[k - 1, i], c[j] - c[i])
+                if v < best[k, j]:
+                    best[k, j], arg[k, j] = v, i
+    cuts = [n]
+    for k in range(g, 0, -1):
+        cuts.append(int(arg[k, cuts[-1]]))
+    return cuts[::-1]
+
+
 def bucketed_all_reduce(buckets: list, assemble: Callable[[int], None], finish: Callable[[int], None], group=None) -> None:
     """The step's one real exchange (SUM over ranks) in buckets, one per parameter tensor (plus the loss in
     the last): bucket b is assembled (``assemble(b)``, on the current stream) and its all-reduce issued
@@ -434,21 +467,93 @@ class ViewShardedFitter:
     @property
     def my_views(self) -> list:
         """This rank's views: i = r, r + R, ... (whole views), or with band splitting the first R * (V // R) views
-        round-robin and this rank's band of each of the V mod R others (virtual ids V + i, _vi / _bands)."""
+        round-robin and this rank's band of its group's leftover view (a virtual id V + i, _vi / _bands)."""
         if not self._bands_ok():
             return self._rr_views
         V, W = len(self.targets), self.world
         q = V // W
         whole = list(range(self.rank, q * W, W))
-        ty = -(-self.height // self.views_tile())
-        lo, hi = ty * self.rank // W, ty * (self.rank + 1) // W
-        if hi <= lo:  # fewer tile rows than ranks: this rank has no band
+        band = self._band_of(self.rank)
+        if band is None:  # (more ranks in the group than the view has tile rows: this rank renders no band)
             return whole
-        bands = []
-        for i in range(q * W, V):
-            self._bands[V + i] = (i, lo, hi - lo)
-            bands.append(V + i)
-        return whole + bands
+        i, lo, rows = band
+        self._bands[V + i] = band
+        return whole + [V + i]
+
+    def _band_groups(self) -> list:
+        """[(leftover view, first rank, ranks)]: the R ranks in r = V mod R contiguous groups, one per leftover view."""
+        V, W = len(self.targets), self.world
+        r = V % W
+        return [(V - r + j, j * W // r, (j + 1) * W // r - j * W // r) for j in range(r)]
+
+    def _band_of(self, rank: int):
+        """(view, first tile row, tile rows) of `rank`'s band, or None (its group's view has fewer tile rows than ranks)."""
+        for i, r0, g in self._band_groups():
+            if r0 <= rank < r0 + g:
+                cuts = self._band_cuts(i, g)
+                k = rank - r0
+                return (i, cuts[k], cuts[k + 1] - cuts[k]) if cuts[k + 1] > cuts[k] else None
+        return None
+
+    def _band_cuts(self, i: int, g: int) -> list:
+        """Tile-row boundaries cutting view i into g bands of about equal work: a band's time is a fixed part plus its
+        (Gaussian, tile) pairs (tools/band_probe.py: ~90 us + ~130 us per million pairs at C4, single stream), and a
+        scene's pairs crowd the middle rows (view 48 of C4: rows 6-18 of 25 hold 97% of them), so equal rows left the
+        middle bands twice the edge ones' work.  The pairs per row are estimated from the Gaussians' projected 5-sigma
+        boxes (rows x tile columns touched), recomputed with the Morton re-sort and after densify; every rank computes
+        the same cuts from its identical replica."""
+        tile = self.views_tile()
+        ty = -(-self.height // tile)
+        key = (i, g, tile, int(self.params["means"].shape[0]), self.steps_done // max(1, RESORT_EVERY))
+        cache = self.__dict__.setdefault("_cuts_cache", {})
+        if key in cache:
+            return cache[key]
+        if len(cache) > 64:
+            cache.clear()
+        w = self._row_pairs_cached(i, tile, ty)
+        cuts = _min_max_cuts(w, g) if ty >= g else [ty * k // g for k in range(g + 1)]
+        cache[key] = cuts
+        return cuts
+
+    def _row_pairs_cached(self, i: int, tile: int, ty: int) -> np.ndarray:
+        key = (i, tile, int(self.params["means"].shape[0]), self.steps_done // max(1, RESORT_EVERY))
+        cache = self.__dict__.setdefault("_rows_cache", {})
+        if key not in cache:
+            if len(cache) > 64:
+                cache.clear()
+            cache[key] = self._row_pairs(i, tile, ty)
+        return cache[key]
+
+    def _row_pairs(self, i: int, tile: int, ty: int) -> np.ndarray:
+        """Estimated (Gaussian, tile) pairs per tile row of view i: per Gaussian the tile rows and columns of its
+        FIT_CUTOFF-sigma box (torch_renderer.py:57-78, 146-150's projection and sigma rule; rectangle, not the
+        elliptical test), summed over the rows it spans (a difference array)."""
+        with torch.no_grad():
+            m, sc, _, _ = activations(self.params)
+            cam = self.cams[i]
+            V, P = cam.view.float(), cam.proj.float()
+            pc = m.float() @ V[:3, :3].T + V[:3, 3]
+            clip = pc @ P[:3, :3].T + P[:3, 3]
+            w4 = pc @ P[3, :3] + P[3, 3]
+            ws = torch.where(w4.abs() < 1e-8, torch.ones_like(w4), w4)
+            ndc = clip / ws[:, None]
+            ok = (ndc[:, 2] >= -1) & (ndc[:, 2] <= 1) & (w4 != 0)
+            px = (ndc[:, 0] * 0.5 + 0.5) * (self.width - 1)
+            py = (1 - (ndc[:, 1] * 0.5 + 0.5)) * (self.height - 1)
+            za = pc[:, 2].abs().clamp_min(1e-6)
+            sx = (sc[:, 0].abs() * 0.5 * self.width * P[0, 0].abs() / za).clamp_min(1.0) * tr.FIT_CUTOFF
+            sy = (sc[:, 1].abs() * 0.5 * self.height * P[1, 1].abs() / za).clamp_min(1.0) * tr.FIT_CUTOFF
+            tx = -(-self.width // tile)
+            c0 = ((px - sx) / tile).floor().clamp(0, tx - 1)
+            c1 = ((px + sx) / tile).floor().clamp(0, tx - 1)
+            r0 = ((py - sy) / tile).floor().clamp(0, ty - 1)
+            r1 = ((py + sy) / tile).floor().clamp(0, ty - 1)
+            ok = ok & (px + sx >= 0) & (px - sx <= self.width - 1) & (py + sy >= 0) & (py - sy <= self.height - 1)
+            cols = torch.where(ok, c1 - c0 + 1, torch.zeros_like(c0)).long()
+            # a difference array of integer counts, summed without atomics (a sort, a prefix sum and a search): exact
+            # and the same on every rank (an index_add_ of float64 took 28 ms per view at C4)
+            d = _int_hist(r0.long(), cols, ty + 1) - _int_hist((r1 + 1).long(), cols, ty + 1)
+            return torch.cumsum(d, 0)[:ty].double().cpu().numpy()
 
     def views_tile(self) -> int:
         """The tile size the fused path renders this fit's views at: FIT_TILE, or 16 in the f32-grade mode (its
@@ -458,13 +563,25 @@ class ViewShardedFitter:
     def _bands_ok(self) -> bool:
         V, W = len(self.targets), self.world
         r = V % W if W > 1 else 0
-        # the most loaded rank sheds 1 - r / W views and takes r bands
-        if not (BAND_SPLIT and r and (1.0 - r / W) > BAND_OVERHEAD * r and not self._depth_grad()):
+        if not (BAND_SPLIT and r and not self._depth_grad()):
             return False
         if self.params["means"].shape[0] == 0:  # (the generic loop renders whole views only)
             return False
         dev = self.params["means"].device
-        return dev.type == "cuda" and self._direct(dev)
+        if not (dev.type == "cuda" and self._direct(dev)):
+            return False
+        # the most loaded rank: V // R views and one band, its largest share of its view's pairs plus the band's fixed
+        # cost (a group of one renders its whole view, no band cost): bands only where that beats a whole view
+        load = max((1.0 if g == 1 else BAND_OVERHEAD + self._band_share(i, g)) for i, _, g in self._band_groups())
+        return load < 1.0
+
+    def _band_share(self, i: int, g: int) -> float:
+        """The largest band's share of view i's estimated pairs when cut into g bands (_band_cuts)."""
+        tile = self.views_tile()
+        w = self._row_pairs_cached(i, tile, -(-self.height // tile))
+        cuts = self._band_cuts(i, g)
+        tot = float(w.sum())
+        return max(float(w[cuts[k]:cuts[k + 1]].sum()) for k in range(g)) / tot if tot > 0 else 1.0 / g
 
     def _vi(self, v: int) -> int:
         """The view index of a (possibly virtual, band) view id."""

@@ -209,13 +209,14 @@ def test_batched_steps_bit_identical_to_eager(cuda, case, monkeypatch):
     print(f"{case}: 5 steps of {V} views batched, bit-identical to eager; losses {batched[0]}")
 
 
-@pytest.mark.parametrize("world", [3, 8])
+@pytest.mark.parametrize("world", [5, 8])
 @pytest.mark.parametrize("schedule", ["python", "native"])
 def test_band_split_adds_up_to_the_views(cuda, world, schedule, monkeypatch):
-    """Multi-GPU view sharding with the leftover views cut into bands of tile rows (BAND_SPLIT, gr_view.row0 / rows):
-    every emulated rank's loss and gradient (this process playing each rank in turn, no collective) sum to the
-    single-process step's, within float summation order; each band renders only its rows (a band's pairs are those
-    of its tile rows)."""
+    """Multi-GPU view sharding with the leftover views cut into bands of tile rows (BAND_SPLIT, gr_view.row0 / rows;
+    round 6: the ranks in one group per leftover view, one band per rank): every emulated rank's loss and gradient (this
+    process playing each rank in turn, no collective) sum to the single-process step's, within float summation order;
+    each band renders only its rows (a band's pairs are those of its tile rows).  11 views: 5 ranks cut view 10 in
+    five bands; 8 ranks cut views 8, 9, 10 over groups of 2, 3 and 3."""
     fm = importlib.import_module("3dgaussian_amd.fit_multiview")
     bench = importlib.import_module("bench")
     monkeypatch.setattr(fm, "BAND_OVERHEAD", 0.0)  # bands whatever they cost
@@ -242,7 +243,7 @@ def test_band_split_adds_up_to_the_views(cuda, world, schedule, monkeypatch):
         f.rank, f.world = r, world
         f._rr_views = list(range(r, V, world))
         views = f.my_views
-        assert len([v for v in views if v >= V]) == (V % world if (7 * (r + 1)) // world > (7 * r) // world else 0)
+        assert len([v for v in views if v >= V]) == 1  # one band per rank (7 tile rows >= every group's size)
         seen += views
         loss, acc = run()
         tot_loss += loss

@@ -1,6 +1,7 @@
-"""One rank's share of the multi-GPU C4 step on one GPU: the step time of rank r of R with whole views round-robin
-(7 views for rank 0 of 8) and with the leftover views in bands of tile rows (6 views and two eighths), no collective
-(the step's update runs as at world size 1).   python tools/rank_share.py [R] [r] [steps]"""
+"""Ranks' shares of the multi-GPU C4 step on one GPU: the step time of rank r of R with whole views round-robin
+(7 views for rank 0 of 8) and with the leftover views in bands of tile rows (6 views and one band of a quarter view,
+round 6), no collective (the step's update runs as at world size 1).
+    python tools/rank_share.py [R] [r|all] [steps] [both|whole|bands]"""
 import importlib, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -8,7 +9,8 @@ import torch
 fm = importlib.import_module("3dgaussian_amd.fit_multiview")
 bench = importlib.import_module("bench")
 Rk = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-rk = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+ranks = list(range(int(sys.argv[1]) if len(sys.argv) > 1 else 8)) if (len(sys.argv) > 2 and sys.argv[2] == "all") else \
+    [int(sys.argv[2]) if len(sys.argv) > 2 else 0]
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
 dev = torch.device("cuda:0")
 R, V, N = 800, 50, 1_000_000
@@ -22,7 +24,7 @@ class Share(fm.ViewShardedFitter):
         return self.fixed if self.fixed is not None else super().my_views
 
 
-def run(band):
+def run(band, rk):
     params = bench.synthetic_params(N, dev)
     cams = fm.orbit_cameras(V, R, R, dev)
     g = torch.Generator(device=dev).manual_seed(1)
@@ -50,5 +52,9 @@ def run(band):
     torch.cuda.empty_cache()
 
 
-run(False)
-run(True)
+mode = sys.argv[4] if len(sys.argv) > 4 else "both"
+if mode in ("both", "whole"):
+    run(False, ranks[0])
+if mode in ("both", "bands"):
+    for rk in ranks:
+        run(True, rk)
