@@ -1773,7 +1773,9 @@ __device__ __forceinline__ void split3_frag2(const f32x2_t (&v)[4], s16x8 (&f)[3
 // hi = f16(x) rounded to nearest (v_cvt_pk_f16_f32), lo = x - hi exact in f32 (one v_fma_mix_f32 per value reads
 // hi's f16 half), rounded to nearest f16: |x - hi| <= 2^-11 |x| and |x - hi - lo| <= 2^-22 |x| while both pieces
 // are normal, so the three products miss a b by at most 3 * 2^-22 of it (round 6; truncated pieces, as before,
-// left 3 * 2^-20).  Four instructions per pair of values instead of five.  Same-box A/B at C4 (fit path):
+// left 3 * 2^-20; r06e, profiles/r06_ab_bwd32_f16.txt: the forward even either way, the knob removed).  Four
+// instructions per pair of values instead of five; the lo pair straight from v_fma_mix{lo,hi}_f16 (three) measured
+// slower, forward 160 -> 167 us, backward 202 -> 206 us (profiles/r06_probe_diag.txt).  Same-box A/B at C4 (fit path):
 // forward 145/154 -> 140/135 us, step 1369-1380 -> 1403-1408 Mpx/s (A/B at SA = SB = 12); fit-path errors vs the float64 oracle
 // out 1e-7, gradients <= 1.2e-5 (profiles/r02p_ab_f16.txt).
 #ifndef GR_FWD_F16
@@ -1812,19 +1814,12 @@ typedef _Float16 f16x2h_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned pk_f16(float a, float b) {  // two f16, round to nearest even: v_cvt_pk_f16_f32
   return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{a, b}, f16x2h_t));
 }
-#ifndef GR_F16_RNE_FWD
-#define GR_F16_RNE_FWD 1
-#endif
-__device__ __forceinline__ unsigned pk_f16_fwd(float a, float b) {  // (A/B knob: the forward's pieces truncated)
-  if constexpr (GR_F16_RNE_FWD) return pk_f16(a, b);
-  return __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(a, b));
-}
 __device__ __forceinline__ void split2h_frag2(const f32x2_t (&v)[4], s16x8 (&f)[2]) {
   unsigned h[4], l[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    h[p] = pk_f16_fwd(v[p].x, v[p].y);
-    l[p] = pk_f16_fwd(f16_resid_lo(v[p].x, h[p]), f16_resid_hi(v[p].y, h[p]));
+    h[p] = pk_f16(v[p].x, v[p].y);
+    l[p] = pk_f16(f16_resid_lo(v[p].x, h[p]), f16_resid_hi(v[p].y, h[p]));
   }
   f[0] = as_frag(make_uint4(h[0], h[1], h[2], h[3]));
   f[1] = as_frag(make_uint4(l[0], l[1], l[2], l[3]));
@@ -2147,12 +2142,15 @@ __device__ __forceinline__ void pixel_upstream(const ViewK& v, int p, float4 s, 
                                                const float* __restrict__ g_alpha, const float* __restrict__ g_depth,
                                                const L1Args& l1, float (&u)[5], float& l_rgb, float& l_sil) {
   const float den = 1.0f + s.x, dden = s.x + 1e-6f;
+  // one correctly rounded reciprocal of the finalize's denominator instead of ten divisions (each ~10 VALU): the
+  // quotients below are products with it, within 1 ulp of the divisions (round 6, the L1 epilogue of the fit forwards)
+  const float inv = 1.0f / den;
   float gW = 0.f;
   const float C[3] = {s.y, s.z, s.w};
   const float HWf = (float)v.W * (float)v.H;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const float r = (view_bg(v, k) + C[k]) / den;
+    const float r = (view_bg(v, k) + C[k]) * inv;
     float gk;
     if (l1.t_rgb) {
       const float t = clamp01(r) - l1.t_rgb[3 * p + k];
@@ -2162,10 +2160,10 @@ __device__ __forceinline__ void pixel_upstream(const ViewK& v, int p, float4 s, 
       gk = g_rgb[3 * p + k];
     }
     const float go = (r >= 0.0f && r <= 1.0f) ? gk : 0.0f;
-    u[k] = go / den;
-    gW -= go * r / den;
+    u[k] = go * inv;
+    gW -= (go * r) * inv;
   }
-  const float al = s.x / den;
+  const float al = s.x * inv;
   float ga = 0.0f;
   bool has_a = g_alpha != nullptr;
   if (l1.t_rgb && l1.t_mask) {
@@ -2176,7 +2174,7 @@ __device__ __forceinline__ void pixel_upstream(const ViewK& v, int p, float4 s, 
   } else if (g_alpha) {
     ga = g_alpha[p];
   }
-  if (has_a && al >= 0.0f && al <= 1.0f) gW += ga / (den * den);
+  if (has_a && al >= 0.0f && al <= 1.0f) gW += ga * (inv * inv);
   const bool dfit = l1.t_rgb && l1.t_depth;
   if (g_depth || dfit) {
     const float d = Dp / dden;

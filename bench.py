@@ -643,8 +643,9 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f32 (splat contractions on 16-bit MFMA with two-piece operand splits: forward f16 pieces, "
-                     "<= 3*2^-20 per product; backward bf16 pieces, ~2^-16 per product; no-depth-gradient mode)",
+            "dtype": "f32 (splat contractions on v_mfma_f32_32x32x16_f16 with f32 accumulation; every operand in two "
+                     "round-to-nearest f16 pieces, pre-scaled into f16's normal range, three piece products: "
+                     "<= 3*2^-22 per product, forward and backward; no-depth-gradient mode)",
             "data": "synthetic (seeded Gaussians per SURVEY.md 8(d), random targets)",
             "config": {"workload": f"C4: {n} Gaussians, {V} orbit views {R}x{R}, fwd+bwd+grad all-reduce+Adam per step",
                        "gaussians": n, "views": V, "width": R, "height": R, "cutoff_sigma": tr.FIT_CUTOFF, "core_cutoff_sigma": tr.FIT_CUTOFF,
