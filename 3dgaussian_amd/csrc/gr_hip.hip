@@ -1177,6 +1177,23 @@ template <typename V>
 __device__ __forceinline__ V ld_through(const V* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The 16-byte form (round 6, the 32-pixel forward's split-tile partials): raw buffer stores / loads with the sc1 cache
+// policy (the same write-through as the 4-byte atomics above compile to), through a buffer resource on the hand-off
+// buffer; the compiler tracks them (vmcnt) like any load / store.  A quarter of the memory instructions.
+constexpr int GR_CPOL_SC1 = 16;  // cache-policy immediate: sc1
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t through_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);  // raw, 32-bit data
+}
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_through16(__amdgpu_buffer_rsrc_t r, int byte_off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
+                                                 __float_as_uint(v.w)},
+                                         r, byte_off, 0, GR_CPOL_SC1);
+}
+__device__ __forceinline__ float4 ld_through16(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  const u32x4_t u = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, GR_CPOL_SC1);
+  return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+}
 // Every thread of the block calls this after its write-through stores: true in the block that arrives last of
 // `count` (uniform per block).  `flag`: one LDS word.
 __device__ __forceinline__ bool arrive_last(int* ticket, int count, int* flag) {
@@ -3168,23 +3185,27 @@ __device__ __forceinline__ void k_fwd32_l1_body(ViewK v, int n, const int4* __re
   const int nch = tile_chunks(ranges[2 * tile], ch) + tile_chunks(ranges[2 * tile + 1], ch);
   if (nch > 1) {
     // a tile split over several items: each leaves its partial sums (write-through) and takes the tile's ticket; the
-    // last to arrive sums every item's partials in item order (deterministic) and finishes the tile
-    float* dst = fwd_part + (size_t)item * 4 * TP32;
+    // last to arrive sums every item's partials in item order (deterministic) and finishes the tile.  An item's
+    // partials are four float4 planes (plane q: thread t's four channels of its pixel q at 16 t bytes), so each of a
+    // thread's four 16-byte write-through stores is part of one contiguous 4 KB block per instruction
+    const __amdgpu_buffer_rsrc_t dst = through_rsrc(fwd_part + (size_t)item * 4 * TP32);
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) st_through(dst + c * TP32 + (py0 + 8 * q) * T32 + px0, acc[q][c]);
+    for (int q = 0; q < 4; ++q) st_through16(dst, 16 * (256 * q + tid), make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]));
     if (!arrive_last(&ticket[tile], nch, &last_flag)) return;
-    const float* src = fwd_part + (size_t)tile_item0[2 * tile] * 4 * TP32;
+    const __amdgpu_buffer_rsrc_t src = through_rsrc(fwd_part + (size_t)tile_item0[2 * tile] * 4 * TP32);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int c = 0; c < 4; ++c) acc[q][c] = 0.f;
     for (int e = 0; e < nch; ++e)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[q][c] += ld_through(src + (size_t)e * 4 * TP32 + c * TP32 + (py0 + 8 * q) * T32 + px0);
+      for (int q = 0; q < 4; ++q) {
+        const float4 pv = ld_through16(src, 4 * 4 * TP32 * e + 16 * (256 * q + tid));
+        acc[q][0] += pv.x;
+        acc[q][1] += pv.y;
+        acc[q][2] += pv.z;
+        acc[q][3] += pv.w;
+      }
     if (tid == 0) ticket[tile] = 0;  // left zero for a later render of the same bins
   }
   // per pixel: outputs, the L1 terms and the upstream vector u = (dC_r, dC_g, dC_b, dW)
