@@ -1727,19 +1727,13 @@ typedef float f32x2_t __attribute__((ext_vector_type(2)));
 // a one-signed lo*lo of up to 2^-14).
 __device__ __forceinline__ void split2_frag(const float (&v)[8], s16x8 (&f)[2]) {
   unsigned h[4], l[4];
-  f32x2_t r[4];
-  // in rounds (every hi, every residual, every lo): no instruction reads the one just before it (round 6)
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    const bf16x2_t hb = __builtin_convertvector(f32x2_t{v[2 * p], v[2 * p + 1]}, bf16x2_t);
+    const f32x2_t x = {v[2 * p], v[2 * p + 1]};
+    const bf16x2_t hb = __builtin_convertvector(x, bf16x2_t);
     __builtin_memcpy(&h[p], &hb, 4);
-  }
-#pragma unroll
-  for (int p = 0; p < 4; ++p)
-    r[p] = f32x2_t{v[2 * p] - __uint_as_float(h[p] << 16), v[2 * p + 1] - __uint_as_float(h[p] & 0xffff0000u)};
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const bf16x2_t lb = __builtin_convertvector(r[p], bf16x2_t);
+    const f32x2_t r = {x.x - __uint_as_float(h[p] << 16), x.y - __uint_as_float(h[p] & 0xffff0000u)};
+    const bf16x2_t lb = __builtin_convertvector(r, bf16x2_t);
     __builtin_memcpy(&l[p], &lb, 4);
   }
   f[0] = as_frag(make_uint4(h[0], h[1], h[2], h[3]));
@@ -1839,34 +1833,22 @@ __device__ __forceinline__ unsigned pk_f16(float a, float b) {  // two f16, roun
 }
 __device__ __forceinline__ void split2h_frag2(const f32x2_t (&v)[4], s16x8 (&f)[2]) {
   unsigned h[4], l[4];
-  float r[8];
-  // in three rounds (every hi, every residual, every lo) so that no instruction reads the one just before it (a
-  // v_fma_mix result read by the next VALU costs a wait state, s_nop)
-#pragma unroll
-  for (int p = 0; p < 4; ++p) h[p] = pk_f16(v[p].x, v[p].y);
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    r[2 * p] = f16_resid_lo(v[p].x, h[p]);
-    r[2 * p + 1] = f16_resid_hi(v[p].y, h[p]);
+    h[p] = pk_f16(v[p].x, v[p].y);
+    l[p] = pk_f16(f16_resid_lo(v[p].x, h[p]), f16_resid_hi(v[p].y, h[p]));
   }
-#pragma unroll
-  for (int p = 0; p < 4; ++p) l[p] = pk_f16(r[2 * p], r[2 * p + 1]);
   f[0] = as_frag(make_uint4(h[0], h[1], h[2], h[3]));
   f[1] = as_frag(make_uint4(l[0], l[1], l[2], l[3]));
 }
 // the same split (round to nearest) of 8 values held as a plain array
 __device__ __forceinline__ void split2h_frag(const float (&v)[8], s16x8 (&f)[2]) {
   unsigned h[4], l[4];
-  float r[8];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) h[p] = pk_f16(v[2 * p], v[2 * p + 1]);
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    r[2 * p] = f16_resid_lo(v[2 * p], h[p]);
-    r[2 * p + 1] = f16_resid_hi(v[2 * p + 1], h[p]);
+    h[p] = pk_f16(v[2 * p], v[2 * p + 1]);
+    l[p] = pk_f16(f16_resid_lo(v[2 * p], h[p]), f16_resid_hi(v[2 * p + 1], h[p]));
   }
-#pragma unroll
-  for (int p = 0; p < 4; ++p) l[p] = pk_f16(r[2 * p], r[2 * p + 1]);
   f[0] = as_frag(make_uint4(h[0], h[1], h[2], h[3]));
   f[1] = as_frag(make_uint4(l[0], l[1], l[2], l[3]));
 }
@@ -1980,36 +1962,18 @@ __device__ __forceinline__ void fwd_accumulate_bf16(float* smem, int n, int k0, 
       ld(4, o);
       if constexpr (ZCH) ld(8, z);
       f32x2_t aW[4], aD[4], bv[4], oe[4];
-      // stage by stage over the four pairs (differences, products, exponent arguments, exponentials): no packed op
-      // reads the result of the one just before it, which costs a wait state (s_nop) (round 6; the same values)
-      f32x2_t dx[4], dy[4], tx[4], ty[4];
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-        dx[p] = X - px[p];
-        dy[p] = Y - py[p];
-      }
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        tx[p] = dx[p] * qx[p];
-        ty[p] = dy[p] * qy[p];
-      }
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
+        const f32x2_t dx = X - px[p], dy = Y - py[p];
 #if GR_FWD_F16
-        tx[p] = F16 ? __builtin_elementwise_fma(tx[p], dx[p], SA) : tx[p] * dx[p];
-        ty[p] = F16 ? __builtin_elementwise_fma(ty[p], dy[p], SB) : ty[p] * dy[p];
+        const f32x2_t tx = F16 ? __builtin_elementwise_fma(dx * qx[p], dx, SA) : (dx * qx[p]) * dx;
+        const f32x2_t ty = F16 ? __builtin_elementwise_fma(dy * qy[p], dy, SB) : (dy * qy[p]) * dy;
 #else
-        tx[p] = tx[p] * dx[p];
-        ty[p] = ty[p] * dy[p];
+        const f32x2_t tx = (dx * qx[p]) * dx, ty = (dy * qy[p]) * dy;
 #endif
-      }
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        oe[p] = o[p] * f32x2_t{__builtin_amdgcn_exp2f(tx[p].x), __builtin_amdgcn_exp2f(tx[p].y)};
-        bv[p] = f32x2_t{__builtin_amdgcn_exp2f(ty[p].x), __builtin_amdgcn_exp2f(ty[p].y)};
-      }
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
+        const f32x2_t ex = {__builtin_amdgcn_exp2f(tx.x), __builtin_amdgcn_exp2f(tx.y)};
+        bv[p] = f32x2_t{__builtin_amdgcn_exp2f(ty.x), __builtin_amdgcn_exp2f(ty.y)};
+        oe[p] = o[p] * ex;
         aW[p] = oe[p];
         if constexpr (ZCH) aD[p] = oe[p] * z[p];
       }
@@ -3140,34 +3104,29 @@ __device__ __forceinline__ void k_fwd32_l1_body(ViewK v, int n, const int4* __re
         f32x2_t oe[4], bv[4];
         // the record fields loaded axis by axis behind scheduling fences (fewer live registers: 4 waves/SIMD)
         {
-          // stage by stage over the four pairs (every difference, every product, every fma, every exponential), so
-          // no packed op reads the result of the one just before it (that costs a wait state, s_nop)
-          f32x2_t px[4], qx[4], o[4], d[4], a[4];
+          f32x2_t px[4], qx[4], o[4];
           ld(0, px);
           ld(2, qx);
           ld(4, o);
 #pragma unroll
-          for (int p = 0; p < 4; ++p) d[p] = X - px[p];
-#pragma unroll
-          for (int p = 0; p < 4; ++p) a[p] = d[p] * qx[p];
-#pragma unroll
-          for (int p = 0; p < 4; ++p) a[p] = __builtin_elementwise_fma(a[p], d[p], SA);
-#pragma unroll
-          for (int p = 0; p < 4; ++p) oe[p] = o[p] * f32x2_t{__builtin_amdgcn_exp2f(a[p].x), __builtin_amdgcn_exp2f(a[p].y)};
+          for (int p = 0; p < 4; ++p) {
+            const f32x2_t dx = X - px[p];
+            const f32x2_t ax = __builtin_elementwise_fma(dx * qx[p], dx, SA);
+            const f32x2_t ex = {__builtin_amdgcn_exp2f(ax.x), __builtin_amdgcn_exp2f(ax.y)};
+            oe[p] = o[p] * ex;
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
         {
-          f32x2_t py[4], qy[4], d[4], a[4];
+          f32x2_t py[4], qy[4];
           ld(1, py);
           ld(3, qy);
 #pragma unroll
-          for (int p = 0; p < 4; ++p) d[p] = Y - py[p];
-#pragma unroll
-          for (int p = 0; p < 4; ++p) a[p] = d[p] * qy[p];
-#pragma unroll
-          for (int p = 0; p < 4; ++p) a[p] = __builtin_elementwise_fma(a[p], d[p], SB);
-#pragma unroll
-          for (int p = 0; p < 4; ++p) bv[p] = f32x2_t{__builtin_amdgcn_exp2f(a[p].x), __builtin_amdgcn_exp2f(a[p].y)};
+          for (int p = 0; p < 4; ++p) {
+            const f32x2_t dy = Y - py[p];
+            const f32x2_t ay = __builtin_elementwise_fma(dy * qy[p], dy, SB);
+            bv[p] = f32x2_t{__builtin_amdgcn_exp2f(ay.x), __builtin_amdgcn_exp2f(ay.y)};
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
         s16x8 fb[2], fa[2];
