@@ -946,18 +946,19 @@ __device__ __forceinline__ void k_emit_offsets_body(ViewK v, int n, const int4* 
     return;
   }
   const Cnt2 cn{i < n ? counts[i].v : 0ull};
-  unsigned long long tot;
-  const unsigned long long ex = block_exclusive_scan<4>(cn.v, wsum, tot);
+  // every load the block needs issued before the scan's barriers (their latencies overlap instead of adding up)
   const Cnt2 cb{bsum[b]};
   const int Kc = (int)offsets[n].c();
+  const int4 rc = i < n ? rect[i] : make_int4(0, 0, -1, -1);
+  const float4 a = i < n ? rec[(size_t)REC4 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  unsigned long long tot;
+  const unsigned long long ex = block_exclusive_scan<4>(cn.v, wsum, tot);
   const int c0 = (int)cb.c(), t0 = (int)cb.t();  // the block's first core pair, first tail pair (after Kc)
   const int nc = (int)(tot & 0xffffffffull), nt = (int)(tot >> 32);
   const bool staged = nc + nt <= EWIN_BLK;       // uniform per block
   const unsigned long long run = cb.v + ex;
   if (i < n) offsets[i].v = run;
   if (cn.v != 0) {
-    const int4 rc = rect[i];
-    const float4 a = rec[(size_t)REC4 * i];
     int kc = (int)(run & 0xffffffffull), kt = (int)(run >> 32);
     const float thr_cut = radius_thr(v.cutoff), thr_core = radius_thr(v.core);
     for (int ty = rc.y; ty <= rc.w; ++ty) {
