@@ -99,3 +99,33 @@ def test_native_executor_rejects_out_of_range_config(pkg, cuda):
         st = L.gr_fit_views(nat.executor(0), ctypes.byref(cfg), 1, arr, n, *[nat.ptr(t) for t in p[:3]], 3, nat.ptr(p[3]),
                             0.0, 0.0, 1.0, nat.ptr(losses), accp, stream)
         assert st == nat.GR_ERR_INVALID_ARGUMENT, (b, st)
+
+
+def test_fit_step_is_deterministic_at_c4_size(cuda):
+    """Round 6: the same fused fit step run twice from the same state (1M Gaussians, 13 views of 800x800, two steps,
+    the Python schedule at 4 streams) leaves bit-identical parameters.  A reordering that left an inline-asm
+    v_fma_mix without its wait state made the backward's operands timing-dependent: the losses still agreed, the updated
+    means did not (profiles/r06_determinism.txt)."""
+    fm = importlib.import_module("3dgaussian_amd.fit_multiview")
+    bench = importlib.import_module("bench")
+    R, V = 800, 13
+    cams = fm.orbit_cameras(V, R, R, cuda)
+    g = torch.Generator(device=cuda).manual_seed(4)
+    targets = [torch.rand((R, R, 3), generator=g, device=cuda) for _ in range(V)]
+    masks = [(t.mean(dim=2) > 0.5).float() for t in targets]
+    runs = []
+    saved = fm.NATIVE_EXEC
+    try:
+        fm.NATIVE_EXEC = "0"
+        for _ in range(2):
+            f = fm.ViewShardedFitter(bench.synthetic_params(1_000_000, cuda), cams, targets, R, R, masks=masks)
+            losses = [float(f.step()) for _ in range(2)]
+            torch.cuda.synchronize()
+            runs.append((losses, {k: v.detach().clone() for k, v in f.params.items()}))
+            del f
+            torch.cuda.empty_cache()
+    finally:
+        fm.NATIVE_EXEC = saved
+    assert runs[0][0] == runs[1][0]
+    for k in runs[0][1]:
+        assert torch.equal(runs[0][1][k], runs[1][1][k]), k
